@@ -1,0 +1,204 @@
+/*
+ * ttamm.h — C ABI of libttamm.so, the MI355X (gfx950) two-tower training step.
+ *
+ * The reference (alperkartkaya2-afk/two-tower-augmented-with-adaptive-mimic-mechanism)
+ * is pure Python/PyTorch, so the "FFI" this boundary replaces is the set of Python calls
+ * its training step makes.  Each entry point below names the reference interface it
+ * stands in for (file:line relative to the reference root).  The Python host mirror in
+ * two-tower-augmented-with-adaptive-mimic-mechanism_amd/ttamm binds these with ctypes
+ * (see INTEGRATION.md for the binding a maintainer would add to the reference).
+ *
+ * Conventions
+ *   - Every pointer argument is a DEVICE pointer unless its comment says "host".
+ *   - The caller (PyTorch's caching allocator) owns all memory; the library never
+ *     allocates or frees caller buffers.  Scratch comes from a caller workspace sized by
+ *     the matching *_workspace_size query.
+ *   - `stream` is a hipStream_t passed as void* (torch.cuda.current_stream().cuda_stream).
+ *     All calls are asynchronous on that stream and reentrant.
+ *   - Return value: TTAMM_OK (0) or an error code; ttamm_last_error() gives a
+ *     thread-local message.  The Python wrapper maps TTAMM_E_INVALID to ValueError and
+ *     TTAMM_E_RUNTIME / TTAMM_E_HIP to RuntimeError, mirroring the reference's conventions
+ *     (encoders.py:51-52,203-204,236-252; adaptive_mimic.py:32-33,101-102; samplers.py:25-28,38-42,78-81).
+ *   - Indices are int64 (torch.long), as the reference requires (adaptive_mimic.py:101-102).
+ *   - Floating point is fp32 throughout (the reference computes in fp32).
+ */
+#ifndef TTAMM_H
+#define TTAMM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TTAMM_ABI_VERSION 1
+
+#define TTAMM_OK 0
+#define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
+#define TTAMM_E_RUNTIME 2 /* runtime condition          -> RuntimeError */
+#define TTAMM_E_HIP 3     /* HIP API failure            -> RuntimeError */
+
+#define TTAMM_MAX_LINEAR 4 /* feature-encoder Linear layers per tower (hidden + final) */
+
+/* Fusion strategies of TowerEncoder (encoders.py:194-219). "concat" is not on the hot path. */
+#define TTAMM_FUSION_IDENTITY 0
+#define TTAMM_FUSION_SUM 1
+#define TTAMM_FUSION_GATED 2
+
+/* Which optimizer owns a row table (training.py:276-309, :1311-1350). */
+#define TTAMM_OPT_SPARSE_ADAM 0 /* nn.Embedding(sparse=True) -> torch.optim.SparseAdam      */
+#define TTAMM_OPT_DENSE 1       /* every other parameter       -> AdamW / Adam (dense group) */
+
+/* Device-side status word bits (written by kernels, read by the host at epoch end). */
+#define TTAMM_STATUS_SAMPLER_EXHAUSTED 1u /* samplers.py:78-81 */
+
+/* ---------------------------------------------------------------------------------- */
+/* Parameter descriptors                                                               */
+/* ---------------------------------------------------------------------------------- */
+
+/* nn.Linear(in, out): weight [out, in] row-major, bias [out]; plus its AdamW state. */
+typedef struct ttamm_linear {
+    float* weight;
+    float* bias;
+    float* weight_exp_avg;
+    float* weight_exp_avg_sq;
+    float* bias_exp_avg;
+    float* bias_exp_avg_sq;
+    int32_t in_features;
+    int32_t out_features;
+} ttamm_linear;
+
+/* A row table [rows, dim] (an nn.Embedding weight) and its optimizer state. */
+typedef struct ttamm_table {
+    float* weight;
+    float* exp_avg;
+    float* exp_avg_sq;
+    int64_t rows;
+    int32_t dim;
+    int32_t optimizer; /* TTAMM_OPT_* */
+} ttamm_table;
+
+/* One tower: TowerEncoder (encoders.py:171-255) + its half of AdaptiveMimicMechanism
+ * (adaptive_mimic.py:35-38). */
+typedef struct ttamm_tower {
+    ttamm_table id;        /* TowerEncoder.embedding                                   */
+    ttamm_table mimic;     /* {user,item}_augmented; weight==NULL when mimic disabled  */
+    const float* features; /* [id.rows, feat_ld] feature rows (zero-padded), or NULL   */
+    int64_t feat_ld;       /* row stride in floats, multiple of 4                       */
+    int32_t feat_dim;      /* F (unpadded)                                              */
+    int32_t fusion;        /* TTAMM_FUSION_*                                            */
+    int32_t n_linear;      /* Linear layers in the feature encoder (0 = none)           */
+    float dropout;         /* Dropout p after each hidden ReLU (encoders.py:132-138)    */
+    ttamm_linear linear[TTAMM_MAX_LINEAR];
+    ttamm_linear gate[2];  /* FeatureFusionGate.gate_network.{0,2} (encoders.py:157-162) */
+} ttamm_tower;
+
+/* Optimizer hyper-parameters for one step, as the Python floats torch holds (double).
+ * Derived constants (1-beta, bias corrections, step sizes) are computed on the host in
+ * double precision and rounded to fp32 once, exactly as torch does
+ * (adam.py:527-534, _functional.py:80-82). */
+typedef struct ttamm_hparams {
+    double lr, beta1, beta2, eps, weight_decay; /* dense group (Python floats)       */
+    int32_t decoupled_weight_decay;             /* 1 = AdamW, 0 = Adam (L2 into grad) */
+    double sparse_lr, sparse_beta1, sparse_beta2, sparse_eps; /* SparseAdam group    */
+    int64_t dense_step;  /* dense step count after this step's increment (>= 1)       */
+    int64_t sparse_step; /* SparseAdam per-tensor step after increment (>= 1)         */
+    double lambda_mimic_user; /* loss_weights.mimic_user (training.py:722,800-801)    */
+    double lambda_mimic_item; /* loss_weights.mimic_item (training.py:723,802-803)    */
+} ttamm_hparams;
+
+/* One batch of the training loop (training.py:726-736). */
+typedef struct ttamm_batch {
+    const int64_t* users;     /* [batch]                                              */
+    const int64_t* pos_items; /* [batch]                                              */
+    int64_t* neg_items;       /* [batch*num_neg]: sampler output, or caller input     */
+    int64_t batch;
+    int32_t num_neg;          /* negatives_per_positive                                */
+    int32_t sample_negatives; /* 1 = draw on device (samplers.py:11-85), 0 = given    */
+    const int64_t* pos_offsets; /* CSR of each user's positives: [num_users+1]        */
+    const int64_t* pos_values;  /* sorted item ids per user                           */
+    uint64_t seed;              /* RNG key (negatives + dropout)                      */
+    uint64_t counter;           /* per-step RNG counter                               */
+    /* Optional injected dropout keep-masks (1 = keep), one per hidden layer, row-major
+     * [rows, out_features]: user tower rows = batch, item tower rows = batch*(1+num_neg)
+     * ordered [positives; negatives].  NULL = draw from the RNG. */
+    const uint8_t* user_keep_mask[TTAMM_MAX_LINEAR];
+    const uint8_t* item_keep_mask[TTAMM_MAX_LINEAR];
+} ttamm_batch;
+
+/* Everything one fused training step touches. */
+typedef struct ttamm_step_args {
+    ttamm_tower user;
+    ttamm_tower item;
+    int32_t mimic_enabled;
+    ttamm_hparams hp;
+    ttamm_batch b;
+    float* loss_out;      /* [4]: total, bce, mimic_user, mimic_item of this step     */
+    double* loss_accum;   /* [2]: += total*batch, += batch  (training.py:829-831)      */
+    uint32_t* status;     /* device status word (TTAMM_STATUS_* bits), OR-ed          */
+    void* workspace;
+    size_t workspace_bytes;
+    void* timing_events[2]; /* optional hipEvent_t pair recorded around the dense
+                               mimic-table AdamW sweep (bench roofline); NULL = off   */
+} ttamm_step_args;
+
+/* ---------------------------------------------------------------------------------- */
+/* Entry points                                                                        */
+/* ---------------------------------------------------------------------------------- */
+
+int ttamm_abi_version(void);
+const char* ttamm_last_error(void);
+
+/* Replaces one iteration of `_train_one_epoch` (training.py:726-831): negative sampling,
+ * both tower forwards, mimic augmentation + losses, dot-product scoring, BCE, backward,
+ * AdamW (dense group incl. the full mimic tables) and SparseAdam (ID tables). */
+size_t ttamm_train_step_workspace_size(const ttamm_step_args* args);
+int ttamm_train_step(const ttamm_step_args* args, void* stream);
+
+/* nn.Embedding forward / AdaptiveMimicMechanism._gather_and_reshape
+ * (encoders.py:222-223, adaptive_mimic.py:97-105): out[r, :] = table[idx[r], :]. */
+int ttamm_gather_rows(const float* table, int64_t table_rows, int32_t dim, const int64_t* idx,
+                      int64_t n, float* out, int64_t out_ld, void* stream);
+
+/* TowerEncoder.forward in eval mode (encoders.py:221-255), optionally followed by
+ * AdaptiveMimicMechanism.augment_* (adaptive_mimic.py:70-95) when tower->mimic.weight
+ * is non-NULL and `augment` != 0.  ID (and mimic) rows are idx[r]; feature rows are
+ * tower->features[feat_idx[r]] (feat_idx NULL: row r, i.e. features already gathered by the
+ * caller as in training.py:741-747).  out: [n, dim]. */
+size_t ttamm_tower_forward_workspace_size(const ttamm_tower* tower, int64_t n);
+int ttamm_tower_forward(const ttamm_tower* tower, const int64_t* idx, const int64_t* feat_idx, int64_t n,
+                        int32_t augment, float* out, void* workspace, size_t workspace_bytes,
+                        void* stream);
+
+/* AdaptiveMimicMechanism._apply_aug (adaptive_mimic.py:88-95): out = base + table[idx].
+ * aug_out (optional) receives table[idx]. */
+int ttamm_mimic_augment(const float* table, int64_t table_rows, int32_t dim, const int64_t* idx,
+                        int64_t n, const float* base, float* out, float* aug_out, void* stream);
+
+/* F.mse_loss(input, target) with reduction='mean' (adaptive_mimic.py:97-98): out[0] = mean. */
+int ttamm_mse_loss(const float* input, const float* target, int64_t n, float* out, void* stream);
+
+/* sample_negative_items (samplers.py:11-85) on device: out[b, j] uniform in [0, num_items)
+ * and not among user b's positives (CSR, sorted per user); up to 11 draws per slot, then
+ * the TTAMM_STATUS_SAMPLER_EXHAUSTED bit is set in *status. */
+int ttamm_sample_negatives(const int64_t* users, int64_t batch, int32_t num_neg, int64_t num_items,
+                           const int64_t* pos_offsets, const int64_t* pos_values, uint64_t seed,
+                           uint64_t counter, int64_t* out, uint32_t* status, void* stream);
+
+/* torch.optim.SparseAdam step on one table for already-coalesced rows
+ * (_functional.py:24-84): rows[u] unique, grad [n_rows, dim]. */
+int ttamm_sparse_adam_rows(float* weight, float* exp_avg, float* exp_avg_sq, int32_t dim,
+                           const int64_t* rows, const float* grad, int64_t n_rows, double lr,
+                           double beta1, double beta2, double eps, int64_t step, void* stream);
+
+/* torch.optim.AdamW / Adam single-tensor step over a dense tensor (adam.py:419-547). */
+int ttamm_adamw_dense(float* param, float* exp_avg, float* exp_avg_sq, const float* grad, int64_t n,
+                      double lr, double beta1, double beta2, double eps, double weight_decay,
+                      int32_t decoupled, int64_t step, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TTAMM_H */

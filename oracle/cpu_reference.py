@@ -1,0 +1,394 @@
+"""PyTorch-CPU restatement of the reference training step (TEST INFRASTRUCTURE ONLY).
+
+See oracle/__init__.py for scope and pinning status.  Module classes here mirror the
+reference's parameter layout so ``state_dict`` keys are interchangeable with
+ttamm's modules (and with the reference's checkpoints, training.py:173-181).
+"""
+
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass
+from typing import Any, Iterable, Mapping, Sequence
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+
+# ---------------------------------------------------------------------------------------
+# modules (reference: src/models/encoders.py, adaptive_mimic.py, two_tower.py)
+# ---------------------------------------------------------------------------------------
+class FeatureEncoderWrapper(nn.Module):  # encoders.py:81-90
+    def __init__(self, network: nn.Module, output_dim: int) -> None:
+        super().__init__()
+        self.network = network
+        self.output_dim = output_dim
+
+
+class FeatureFusionGate(nn.Module):  # encoders.py:149-168
+    def __init__(self, dim: int, hidden_dim: int | None = None) -> None:
+        super().__init__()
+        h = hidden_dim or dim
+        self.gate_network = nn.Sequential(nn.Linear(2 * dim, h), nn.ReLU(), nn.Linear(h, dim), nn.Sigmoid())
+
+
+class OracleTower(nn.Module):  # encoders.py:171-219 (constructor) — forward is tower_forward below
+    def __init__(self, embedding: nn.Embedding, feature_encoder, fusion: str, gate) -> None:
+        super().__init__()
+        self.embedding = embedding
+        self.feature_encoder = feature_encoder
+        self.fusion = "identity" if feature_encoder is None else fusion
+        self.adaptive_mimic = gate
+        self.num_embeddings = embedding.num_embeddings
+        self.id_dim = embedding.embedding_dim
+        self.output_dim = self.id_dim
+
+
+class OracleMimic(nn.Module):  # adaptive_mimic.py:20-38
+    def __init__(self, num_users: int, num_items: int, embedding_dim: int, init_std: float = 0.02) -> None:
+        super().__init__()
+        if num_users <= 0 or num_items <= 0:
+            raise ValueError("num_users and num_items must be positive.")
+        self.embedding_dim = embedding_dim
+        self.user_augmented = nn.Embedding(num_users, embedding_dim)
+        self.item_augmented = nn.Embedding(num_items, embedding_dim)
+        nn.init.normal_(self.user_augmented.weight, mean=0.0, std=init_std)
+        nn.init.normal_(self.item_augmented.weight, mean=0.0, std=init_std)
+
+
+class OracleModel(nn.Module):  # two_tower.py:19-38
+    def __init__(self, user_encoder, item_encoder, adaptive_mimic=None) -> None:
+        super().__init__()
+        self.user_encoder = user_encoder
+        self.item_encoder = item_encoder
+        self.similarity = nn.CosineSimilarity(dim=-1)
+        self.adaptive_mimic = adaptive_mimic
+
+
+def build_tower(cfg: Mapping[str, Any], *, num_embeddings: int, feature_dim: int) -> OracleTower:
+    """encoders.py:258-331 with the same parameter construction / init order."""
+    id_cfg = cfg.get("id_embedding", {}) or {}
+    params = id_cfg.get("params", {}) or {}
+    emb = nn.Embedding(num_embeddings, int(params.get("embedding_dim", 64)), sparse=bool(params.get("sparse", False)))
+    init = id_cfg.get("init") or {"type": "normal", "std": 0.02}
+    nn.init.normal_(emb.weight, mean=0.0, std=float(init.get("std", 0.02)))  # encoders.py:25-27
+    fusion = str(cfg.get("fusion", "gated" if feature_dim > 0 else "identity")).lower()
+    fe = None
+    if feature_dim > 0:
+        fcfg = dict(cfg.get("feature_encoder") or {})
+        out = int(fcfg.get("output_dim") or emb.embedding_dim)
+        kind = fcfg.get("type", "linear")
+        if kind == "linear":  # encoders.py:121-124
+            lin = nn.Linear(feature_dim, out)
+            nn.init.xavier_uniform_(lin.weight)
+            fe = FeatureEncoderWrapper(lin, out)
+        elif kind == "mlp":  # encoders.py:126-144
+            mods: list[nn.Module] = []
+            prev = feature_dim
+            act = nn.ReLU()
+            for h in fcfg.get("hidden_dims") or []:
+                lin = nn.Linear(prev, int(h))
+                nn.init.xavier_uniform_(lin.weight)
+                mods += [lin, act]
+                if fcfg.get("dropout"):
+                    mods.append(nn.Dropout(p=float(fcfg["dropout"])))
+                prev = int(h)
+            last = nn.Linear(prev, out)
+            nn.init.xavier_uniform_(last.weight)
+            mods.append(last)
+            fe = FeatureEncoderWrapper(nn.Sequential(*mods), out)
+        else:
+            raise ValueError(f"oracle: unsupported feature encoder {kind}")
+    gate = None
+    if fusion in ("gated", "adaptive_mimic"):
+        gate = FeatureFusionGate(emb.embedding_dim, (cfg.get("adaptive_mimic") or {}).get("hidden_dim"))
+        fusion = "gated"
+    return OracleTower(emb, fe, fusion, gate)
+
+
+def build_model(
+    tower_cfg: Mapping[str, Any], *, num_users: int, num_items: int, user_feature_dim: int, item_feature_dim: int,
+    mimic: bool = True, init_std: float = 0.02,
+) -> OracleModel:
+    """training.py:1266-1301."""
+    ue = build_tower(tower_cfg, num_embeddings=num_users, feature_dim=user_feature_dim)
+    ie = build_tower(tower_cfg, num_embeddings=num_items, feature_dim=item_feature_dim)
+    mm = OracleMimic(num_users, num_items, ue.output_dim, init_std) if mimic else None
+    return OracleModel(ue, ie, mm)
+
+
+# ---------------------------------------------------------------------------------------
+# forward (encoders.py:221-255) with optional injected dropout keep-masks
+# ---------------------------------------------------------------------------------------
+def _dropout(x: torch.Tensor, p: float, keep: torch.Tensor | None, training: bool) -> torch.Tensor:
+    if not training or p == 0.0:
+        return x
+    if keep is None:
+        return F.dropout(x, p=p, training=True)
+    noise = keep.to(torch.float32)
+    noise.div_(1 - p)  # ATen _dropout_impl: noise.bernoulli_(1-p).div_(1-p); input * noise
+    return x * noise
+
+
+def feature_forward(fe: FeatureEncoderWrapper, x: torch.Tensor, keep_masks: Sequence[torch.Tensor] | None,
+                    training: bool) -> torch.Tensor:
+    net = fe.network
+    if isinstance(net, nn.Linear):
+        return net(x)
+    hidden = 0
+    for m in net:
+        if isinstance(m, nn.Dropout):
+            keep = keep_masks[hidden] if keep_masks is not None else None
+            x = _dropout(x, m.p, keep, training)
+            hidden += 1
+        else:
+            x = m(x)
+    return x
+
+
+def tower_forward(tower: OracleTower, idx: torch.Tensor, feats: torch.Tensor | None,
+                  keep_masks: Sequence[torch.Tensor] | None = None, training: bool = True) -> torch.Tensor:
+    e = tower.embedding(idx)  # encoders.py:223
+    if tower.fusion == "identity" or tower.feature_encoder is None or feats is None:
+        return e
+    f = feature_forward(tower.feature_encoder, feats, keep_masks, training)  # :233
+    if tower.fusion == "sum":
+        return e + f  # :240
+    gate = tower.adaptive_mimic.gate_network(torch.cat([e, f], dim=-1))  # :164-168
+    return gate * e + (1.0 - gate) * f
+
+
+def gather_aug(table: nn.Embedding, idx: torch.Tensor, reference: torch.Tensor):
+    """adaptive_mimic.py:88-105: (reference + table[idx], table[idx])."""
+    if idx.dtype != torch.long:
+        raise ValueError("Adaptive mimic indices must be torch.long tensors.")
+    aug = table(idx.reshape(-1)).reshape(reference.shape)
+    return reference + aug, aug
+
+
+# ---------------------------------------------------------------------------------------
+# sampler (samplers.py:11-85)
+# ---------------------------------------------------------------------------------------
+def sample_negative_items(users: torch.Tensor, *, num_items: int, positives: Mapping[int, set[int]],
+                          num_negatives: int) -> torch.Tensor:
+    if num_negatives <= 0:
+        raise ValueError("num_negatives must be greater than zero.")
+    if num_items <= 1:
+        raise ValueError("num_items must be greater than one.")
+    out = torch.empty((users.shape[0], num_negatives), dtype=torch.long)
+    cache: dict[int, torch.Tensor] = {}
+    for row, u in enumerate(users.tolist()):
+        pos = positives.get(int(u), set())
+        if len(pos) >= num_items:
+            raise RuntimeError(f"User {int(u)} interacted with all items; cannot sample negatives.")
+        pt = None
+        if pos:
+            pt = cache.get(int(u))
+            if pt is None:
+                pt = torch.tensor(sorted(pos), dtype=torch.long)
+                cache[int(u)] = pt
+        draw = torch.randint(0, num_items, (num_negatives,), dtype=torch.long)
+        if pt is not None:
+            bad = torch.isin(draw, pt)
+            rounds = 0
+            while bad.any():
+                draw[bad] = torch.randint(0, num_items, (int(bad.sum().item()),), dtype=torch.long)
+                bad = torch.isin(draw, pt)
+                rounds += 1
+                if rounds > 10:
+                    raise RuntimeError("Exceeded resampling attempts while drawing negatives.")
+        out[row] = draw
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# optimizers (training.py:276-309, :1311-1350)
+# ---------------------------------------------------------------------------------------
+def parameter_groups(model: OracleModel) -> tuple[list, list]:
+    dense, sparse, seen = [], [], set()
+
+    def put(p, bucket):
+        if id(p) not in seen:
+            seen.add(id(p))
+            bucket.append(p)
+
+    for tower in (model.user_encoder, model.item_encoder):
+        put(tower.embedding.weight, sparse if tower.embedding.sparse else dense)
+        for name, p in tower.named_parameters():
+            if name != "embedding.weight":
+                put(p, dense)
+    for p in model.parameters():
+        put(p, dense)
+    return dense, sparse
+
+
+def build_optimizers(model: OracleModel, *, lr: float = 1e-3, weight_decay: float = 0.01, betas=(0.9, 0.999),
+                     optimizer: str = "adamw") -> list[torch.optim.Optimizer]:
+    dense, sparse = parameter_groups(model)
+    opts: list[torch.optim.Optimizer] = []
+    if dense:
+        cls = torch.optim.AdamW if optimizer == "adamw" else torch.optim.Adam
+        opts.append(cls(dense, lr=lr, weight_decay=weight_decay, betas=betas))
+    if sparse:
+        opts.append(torch.optim.SparseAdam(sparse, lr=lr, betas=betas))
+    return opts
+
+
+# ---------------------------------------------------------------------------------------
+# one training step (training.py:726-831)
+# ---------------------------------------------------------------------------------------
+@dataclass
+class StepResult:
+    total: float
+    bce: float
+    mimic_user: float
+    mimic_item: float
+
+
+def train_step(
+    model: OracleModel,
+    optimizers: Sequence[torch.optim.Optimizer],
+    users: torch.Tensor,
+    pos_items: torch.Tensor,
+    neg_items: torch.Tensor,
+    *,
+    user_features: torch.Tensor | None,
+    item_features: torch.Tensor | None,
+    loss_weights: Mapping[str, float] | None = None,
+    user_keep_masks: Sequence[torch.Tensor] | None = None,
+    item_keep_masks: Sequence[torch.Tensor] | None = None,
+) -> StepResult:
+    """One iteration of _train_one_epoch's body.  item_keep_masks rows are ordered
+    [positives; negatives] (the two item_encoder calls, training.py:750 and :776)."""
+    model.train()
+    lw = dict(loss_weights or {})
+    lam_u = float(lw.get("mimic_user", 0.0))
+    lam_i = float(lw.get("mimic_item", 0.0))
+    mimic = model.adaptive_mimic
+    B = users.shape[0]
+    N = neg_items.shape[1]
+    for opt in optimizers:  # :738-739
+        opt.zero_grad()
+    uf = user_features.index_select(0, users) if user_features is not None and user_features.numel() else None
+    pf = item_features.index_select(0, pos_items) if item_features is not None and item_features.numel() else None
+    pos_masks = [m[:B] for m in item_keep_masks] if item_keep_masks is not None else None
+    neg_masks = [m[B:] for m in item_keep_masks] if item_keep_masks is not None else None
+    t_u = tower_forward(model.user_encoder, users, uf, user_keep_masks)  # :749
+    t_p = tower_forward(model.item_encoder, pos_items, pf, pos_masks)  # :750
+    loss_u = loss_i = None
+    if mimic is not None:  # :752-763 -> adaptive_mimic.py:40-68
+        u, a_u = gather_aug(mimic.user_augmented, users, t_u)
+        p, a_p = gather_aug(mimic.item_augmented, pos_items, t_p)
+        loss_u = F.mse_loss(a_u, t_p.detach())
+        loss_i = F.mse_loss(a_p, t_u.detach())
+    else:
+        u, p = t_u, t_p
+    pos_logits = (u * p).sum(dim=-1)  # :770
+    neg_flat = neg_items.reshape(-1)
+    nf = item_features.index_select(0, neg_flat) if item_features is not None and item_features.numel() else None
+    t_n = tower_forward(model.item_encoder, neg_flat, nf, neg_masks)  # :776
+    n = gather_aug(mimic.item_augmented, neg_flat, t_n)[0] if mimic is not None else t_n
+    n = n.view(-1, N, u.shape[-1])
+    neg_logits = (u.unsqueeze(1) * n).sum(dim=-1)  # :786-787
+    logits = torch.cat([pos_logits, neg_logits.reshape(-1)], dim=0)
+    labels = torch.cat([torch.ones_like(pos_logits), torch.zeros_like(neg_logits.reshape(-1))], dim=0)
+    bce = nn.BCEWithLogitsLoss()(logits, labels)  # :798, criterion :1366
+    total = bce
+    if loss_u is not None and lam_u > 0:
+        total = total + lam_u * loss_u
+    if loss_i is not None and lam_i > 0:
+        total = total + lam_i * loss_i
+    total.backward()  # :822
+    for opt in optimizers:  # :826-827
+        opt.step()
+    return StepResult(
+        float(total.item()), float(bce.item()),
+        float(loss_u.item()) if loss_u is not None else 0.0,
+        float(loss_i.item()) if loss_i is not None else 0.0,
+    )
+
+
+def train_one_epoch(model, batches: Iterable, optimizers, *, negatives_per_positive: int, num_items: int,
+                    positives: Mapping[int, set[int]], user_features, item_features,
+                    loss_weights: Mapping[str, float] | None = None, max_steps: int | None = None) -> tuple[float, int, float]:
+    """training.py:700-833 with the reference's per-row sampler; returns
+    (mean loss, interactions, seconds)."""
+    running, seen, steps = 0.0, 0, 0
+    t0 = time.perf_counter()
+    for users, pos in batches:
+        neg = sample_negative_items(users, num_items=num_items, positives=positives,
+                                    num_negatives=negatives_per_positive)
+        res = train_step(model, optimizers, users, pos, neg, user_features=user_features,
+                         item_features=item_features, loss_weights=loss_weights)
+        running += res.total * users.shape[0]
+        seen += users.shape[0]
+        steps += 1
+        if max_steps is not None and steps >= max_steps:
+            break
+    return running / max(seen, 1), seen, time.perf_counter() - t0
+
+
+# ---------------------------------------------------------------------------------------
+# ranking metrics (src/evaluation/metrics.py:22-116)
+# ---------------------------------------------------------------------------------------
+def _dcg(rels: Sequence[int]) -> float:
+    return float(sum(r / np.log2(i + 2) for i, r in enumerate(rels)))
+
+
+def user_metrics(predicted: Sequence[int], truth: set[int], ks: Iterable[int]) -> dict[str, float]:
+    ks = sorted(ks)
+    res: dict[str, float] = {}
+    for k in ks:
+        head = list(predicted[:k])
+        hits = len(set(head) & truth)
+        res[f"recall@{k}"] = hits / max(len(truth), 1)
+        res[f"precision@{k}"] = hits / max(k, 1)
+        res[f"hit_rate@{k}"] = 1.0 if hits else 0.0
+        ideal = _dcg([1] * min(k, len(truth)))
+        res[f"ndcg@{k}"] = _dcg([1 if x in truth else 0 for x in head]) / ideal if ideal else 0.0
+        h, acc = 0, 0.0
+        for i, x in enumerate(head, start=1):
+            if x in truth:
+                h += 1
+                acc += h / i
+        res[f"map@{k}"] = acc / min(len(truth), k) if truth else 0.0
+    rr = 0.0
+    for i, x in enumerate(predicted[: (ks[-1] if ks else len(predicted))], start=1):
+        if x in truth:
+            rr = 1.0 / i
+            break
+    res["mrr"] = rr
+    return res
+
+
+@dataclass(frozen=True)
+class RankingMetrics:
+    recall: dict
+    precision: dict
+    ndcg: dict
+    hit_rate: dict
+    map: dict
+    mrr: float
+
+
+def ranking_metrics(predictions: Mapping[int, Sequence[int]], truth: Mapping[int, set[int]], ks: Iterable[int]) -> RankingMetrics:
+    ks = list(ks)
+    acc = {name: {k: [] for k in ks} for name in ("recall", "precision", "ndcg", "hit_rate", "map")}
+    mrr = []
+    for u, pred in predictions.items():
+        gt = truth.get(u, set())
+        if not gt:
+            continue
+        m = user_metrics(pred, gt, ks)
+        for name in acc:
+            for k in ks:
+                acc[name][k].append(m[f"{name}@{k}"])
+        mrr.append(m["mrr"])
+
+    def mean(v):
+        return float(np.mean(v)) if v else 0.0
+
+    return RankingMetrics(**{name: {k: mean(acc[name][k]) for k in ks} for name in acc}, mrr=mean(mrr))

@@ -1,0 +1,97 @@
+// extern "C" surface of libttamm.so (declared in include/ttamm.h).
+#include <cstdio>
+#include <cstring>
+
+#include "kernels.h"
+
+namespace ttamm {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+size_t train_step_workspace_size(const ttamm_step_args& A);
+int train_step(const ttamm_step_args& A, hipStream_t s);
+size_t tower_forward_workspace_size(const ttamm_tower& T, int64_t n);
+int tower_forward_eval(const ttamm_tower& T, const int64_t* idx, const int64_t* fidx, int64_t n, int augment,
+                       float* out, void* ws, size_t ws_bytes, hipStream_t s);
+
+}  // namespace ttamm
+
+using namespace ttamm;
+
+#define TTAMM_API extern "C" __attribute__((visibility("default")))
+
+TTAMM_API int ttamm_abi_version(void) { return TTAMM_ABI_VERSION; }
+
+TTAMM_API const char* ttamm_last_error(void) { return g_last_error.c_str(); }
+
+TTAMM_API size_t ttamm_train_step_workspace_size(const ttamm_step_args* args) {
+    if (!args) return 0;
+    return train_step_workspace_size(*args);
+}
+
+TTAMM_API int ttamm_train_step(const ttamm_step_args* args, void* stream) {
+    if (!args) return fail(TTAMM_E_INVALID, "null step args");
+    g_last_error.clear();
+    return train_step(*args, (hipStream_t)stream);
+}
+
+TTAMM_API int ttamm_gather_rows(const float* table, int64_t table_rows, int32_t dim, const int64_t* idx, int64_t n,
+                                float* out, int64_t out_ld, void* stream) {
+    if (n < 0 || dim <= 0 || out_ld < dim || table_rows <= 0) return fail(TTAMM_E_INVALID, "gather_rows: bad shape");
+    return launch_gather_rows(table, dim, idx, n, out, out_ld, (hipStream_t)stream);
+}
+
+TTAMM_API size_t ttamm_tower_forward_workspace_size(const ttamm_tower* tower, int64_t n) {
+    if (!tower) return 0;
+    return tower_forward_workspace_size(*tower, n);
+}
+
+TTAMM_API int ttamm_tower_forward(const ttamm_tower* tower, const int64_t* idx, const int64_t* feat_idx, int64_t n,
+                                  int32_t augment, float* out, void* workspace, size_t workspace_bytes, void* stream) {
+    if (!tower) return fail(TTAMM_E_INVALID, "null tower");
+    return tower_forward_eval(*tower, idx, feat_idx, n, augment, out, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+TTAMM_API int ttamm_mimic_augment(const float* table, int64_t table_rows, int32_t dim, const int64_t* idx, int64_t n,
+                                  const float* base, float* out, float* aug_out, void* stream) {
+    if (n < 0 || dim <= 0 || table_rows <= 0) return fail(TTAMM_E_INVALID, "mimic_augment: bad shape");
+    return launch_combine(base, dim, nullptr, 0, table, idx, n, dim, nullptr, aug_out, out, (hipStream_t)stream);
+}
+
+TTAMM_API int ttamm_mse_loss(const float* input, const float* target, int64_t n, float* out, void* stream) {
+    return launch_mse(input, target, n, out, (hipStream_t)stream);
+}
+
+TTAMM_API int ttamm_sample_negatives(const int64_t* users, int64_t batch, int32_t num_neg, int64_t num_items,
+                                     const int64_t* pos_offsets, const int64_t* pos_values, uint64_t seed,
+                                     uint64_t counter, int64_t* out, uint32_t* status, void* stream) {
+    return launch_sample_negatives(users, batch, num_neg, num_items, pos_offsets, pos_values, seed, counter, out,
+                                   status, (hipStream_t)stream);
+}
+
+TTAMM_API int ttamm_sparse_adam_rows(float* weight, float* exp_avg, float* exp_avg_sq, int32_t dim,
+                                     const int64_t* rows, const float* grad, int64_t n_rows, double lr, double beta1,
+                                     double beta2, double eps, int64_t step, void* stream) {
+    if (step < 1 || dim <= 0 || n_rows < 0) return fail(TTAMM_E_INVALID, "sparse_adam_rows: bad arguments");
+    const SparseConsts c = make_sparse_consts(lr, beta1, beta2, eps, step);
+    return launch_sparse_adam_rows(weight, exp_avg, exp_avg_sq, dim, rows, grad, n_rows, c, (hipStream_t)stream);
+}
+
+TTAMM_API int ttamm_adamw_dense(float* param, float* exp_avg, float* exp_avg_sq, const float* grad, int64_t n,
+                                double lr, double beta1, double beta2, double eps, double weight_decay,
+                                int32_t decoupled, int64_t step, void* stream) {
+    if (step < 1 || n < 0) return fail(TTAMM_E_INVALID, "adamw_dense: bad arguments");
+    DenseAdamArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.count = 1;
+    a.t[0] = DenseTensor{param, exp_avg, exp_avg_sq, grad, n};
+    a.ad = make_adam_consts(lr, beta1, beta2, eps, weight_decay, decoupled, step);
+    return launch_dense_adam(a, (hipStream_t)stream);
+}

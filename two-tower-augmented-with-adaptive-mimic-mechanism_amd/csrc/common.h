@@ -1,0 +1,85 @@
+// Shared device/host helpers for libttamm (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/ttamm.h"
+
+namespace ttamm {
+
+// ---- error plumbing ---------------------------------------------------------------
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+
+#define TTAMM_HIP(expr)                                                                    \
+    do {                                                                                   \
+        hipError_t _e = (expr);                                                            \
+        if (_e != hipSuccess)                                                              \
+            return ::ttamm::fail(TTAMM_E_HIP, std::string(#expr " failed: ") +             \
+                                                  hipGetErrorString(_e));                  \
+    } while (0)
+
+#define TTAMM_LAUNCH_CHECK()                                                               \
+    do {                                                                                   \
+        hipError_t _e = hipGetLastError();                                                 \
+        if (_e != hipSuccess)                                                              \
+            return ::ttamm::fail(TTAMM_E_HIP, std::string("kernel launch failed: ") +      \
+                                                  hipGetErrorString(_e) + " at " + __FILE__); \
+    } while (0)
+
+#define TTAMM_REQUIRE(cond, msg)                                                           \
+    do {                                                                                   \
+        if (!(cond)) return ::ttamm::fail(TTAMM_E_INVALID, (msg));                         \
+    } while (0)
+
+static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+static inline size_t align_up(size_t a, size_t b) { return (a + b - 1) / b * b; }
+
+// ---- workspace bump allocator (host side) -----------------------------------------------
+struct Arena {
+    char* base;
+    size_t cap;
+    size_t off;
+    bool measuring;  // when true only sizes are accumulated
+    template <typename T>
+    T* take(size_t count) {
+        off = align_up(off, 256);
+        T* p = measuring ? nullptr : reinterpret_cast<T*>(base + off);
+        off += count * sizeof(T);
+        return p;
+    }
+    bool ok() const { return measuring || off <= cap; }
+};
+
+// ---- device helpers -------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Philox4x32-10 counter-based RNG (Salmon et al., SC'11).
+struct u32x4 {
+    uint32_t x, y, z, w;
+};
+__device__ __forceinline__ u32x4 philox4x32(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+        const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+        c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+// RNG stream domains, kept in the high bits of counter word w.
+enum : uint32_t {
+    RNG_NEGATIVES = 1u << 28,
+    RNG_DROPOUT = 2u << 28,
+};
+
+}  // namespace ttamm

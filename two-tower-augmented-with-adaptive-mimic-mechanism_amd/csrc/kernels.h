@@ -1,0 +1,241 @@
+// Internal launcher interface between the kernels (*.hip) and the step executor.
+#pragma once
+
+#include "common.h"
+
+namespace ttamm {
+
+// ------------------------------------------------------------------------------------
+// GEMM family (gemm.hip).  fp32 in, fp32 accumulate on v_mfma_f32_32x32x2_f32.
+// ------------------------------------------------------------------------------------
+enum Epilogue : int {
+    EPI_STORE = 0,          // C = acc (+bias)
+    EPI_HIDDEN = 1,         // C = dropout(relu(acc + bias))             (encoders.py:132-138)
+    EPI_GATE_HIDDEN = 2,    // C = relu(acc + bias)                        (encoders.py:158-159)
+    EPI_GATE_OUT = 3,       // g = sigmoid(acc + bias); t = g*e + (1-g)*f; mimic augment
+    EPI_DGRAD_RELU = 4,     // C = acc * (aux0 > 0)                        (ReLU backward)
+    EPI_DGRAD_GATE_EF = 5,  // C[:, :D] = acc + dT*g ; C[:, D:] = acc + dT*(1-g)
+    EPI_DGRAD_HIDDEN = 6,   // C = (aux0 > 0) ? acc * inv_keep : 0          (dropout+ReLU bwd)
+};
+
+struct GemmProblem {
+    // A [M, K] row-major; row r is A + (a_idx ? a_idx[r] : r) * lda
+    const float* A;
+    const int64_t* a_idx;
+    int64_t lda;
+    // B: b_kn == 0 -> B stored [N, K] (nn.Linear weight, y = x W^T)
+    //    b_kn == 1 -> B stored [K, N] (dgrad: dX = dY W)
+    const float* B;
+    int64_t ldb;
+    int b_kn;
+    int M, N, K;
+    int epi;
+    float* C;
+    int64_t ldc;
+    const float* bias;
+    // epilogue operands (meaning depends on epi)
+    const float* aux0;  // EPI_GATE_OUT: ef [M, 2D]; DGRAD_RELU / DGRAD_HIDDEN: activation
+    const float* aux1;  // EPI_DGRAD_GATE_EF: dT [M, D]
+    const float* aux2;  // EPI_DGRAD_GATE_EF: g  [M, D]
+    int64_t ld_aux0, ld_aux1;
+    float* out1;        // EPI_GATE_OUT: g
+    float* out2;        // EPI_GATE_OUT: t
+    float* out3;        // EPI_GATE_OUT: a (mimic rows), may be null
+    const float* table; // EPI_GATE_OUT: mimic table (may be null)
+    const int64_t* idx; // EPI_GATE_OUT: rows into table
+    int64_t ld_out;     // EPI_GATE_OUT: ld of g/t/a
+    // dropout (EPI_HIDDEN / EPI_DGRAD_HIDDEN)
+    float keep_prob;    // 1 - p
+    float inv_keep;     // 1 / (1 - p)   (torch: noise.div_(1 - p))
+    const uint8_t* keep_mask;  // optional injected [M, N]
+    uint32_t rng_k0, rng_k1, rng_c2, rng_c3;
+    int tile_begin;     // filled by the launcher
+    int tiles_n;
+};
+
+constexpr int kMaxGemmProblems = 2;
+struct GemmBatch {
+    GemmProblem p[kMaxGemmProblems];
+    int count;
+    int total_tiles;
+};
+
+int launch_gemm(GemmBatch& batch, hipStream_t s);
+
+// Weight-gradient GEMM (split-K over rows) + fixed-order reduce.
+//   dW[m, n] = sum_r dY[r, m] * X[r, n] ;  db[m] = sum_r dY[r, m]
+struct WgradProblem {
+    const float* dY;
+    int64_t ld_dy;
+    const float* X;
+    const int64_t* x_idx;  // gather rows of X (features) or null
+    int64_t ld_x;
+    int R, M, N;           // rows, out features, in features
+    float* grad_w;         // [M, N]
+    float* grad_b;         // [M] (may be null)
+    float* slab;           // workspace [splits, M, N+1]
+    int splits;            // chunks of rows
+    int rows_per_split;
+    int tile_begin;
+    int tiles_m, tiles_n;
+};
+constexpr int kMaxWgradProblems = 16;
+struct WgradBatch {
+    WgradProblem p[kMaxWgradProblems];
+    int count;
+    int total_blocks;
+};
+int wgrad_rows_per_split(int R);
+size_t wgrad_slab_floats(int R, int M, int N);
+int launch_wgrad(WgradBatch& batch, hipStream_t s);
+
+// ------------------------------------------------------------------------------------
+// Row kernels (rows.hip)
+// ------------------------------------------------------------------------------------
+int launch_gather_rows(const float* table, int dim, const int64_t* idx, int64_t n, float* out,
+                       int64_t out_ld, hipStream_t s);
+// t = e (+ f); a = table[idx]; aug = t + a   (non-gated fusion)
+int launch_combine(const float* e, int64_t ld_e, const float* f, int64_t ld_f, const float* table,
+                   const int64_t* idx, int64_t n, int dim, float* t, float* a, float* aug,
+                   hipStream_t s);
+int launch_mse(const float* x, const float* y, int64_t n, float* out, hipStream_t s);
+// dq = (dT*e - dT*f) * (1-g) * g   (gate backward through the sigmoid)
+int launch_gate_dq(const float* dT, const float* ef, const float* g, int64_t n, int dim, float* dq,
+                   hipStream_t s);
+
+struct ScoreArgs {
+    int64_t B;
+    int N;
+    int D;
+    const float* user_aug;  // [B, D]
+    const float* item_aug;  // [B(1+N), D]
+    const float* t_user;    // [B, D]
+    const float* t_item;    // [B(1+N), D]
+    const float* a_user;    // [B, D] or null
+    const float* a_item;    // [B(1+N), D] or null
+    float lambda_u, lambda_i;
+    int mimic;
+    float* dT_user;   // [B, D]
+    float* dT_item;   // [B(1+N), D]
+    float* dA_user;   // [B, D]  (mimic)
+    float* dA_pos;    // [B, D]  (mimic)
+    float* partials;  // [blocks, 3]
+    int blocks;
+};
+int score_blocks(int64_t B);
+int launch_score_loss(const ScoreArgs& a, hipStream_t s);
+int launch_loss_finalize(const float* partials, int blocks, int64_t B, int N, int D, float lambda_u,
+                         float lambda_i, int mimic, float* loss_out, double* loss_accum,
+                         hipStream_t s);
+
+// ------------------------------------------------------------------------------------
+// Coalesce + optimizers (optim.hip)
+// ------------------------------------------------------------------------------------
+struct CoalesceWs {
+    int32_t* keys_in;
+    int32_t* vals_in;
+    int32_t* keys_out;
+    int32_t* vals_out;
+    int32_t* flags;     // [n]
+    int32_t* uid;       // [n]   inclusive scan
+    int32_t* seg_start; // [n+1]
+    int32_t* n_unique;  // [1]
+    void* temp;
+    size_t temp_bytes;
+};
+size_t coalesce_temp_bytes(int64_t n);
+// sort rows by index; unique rows + segment starts
+int launch_coalesce(const int64_t* idx, int64_t n, int64_t table_rows, CoalesceWs& ws, hipStream_t s);
+
+// Optimizer constants, derived on the host in double precision the way torch does and
+// rounded to fp32 once (adam.py:419-547 single-tensor path; _functional.py:24-84).
+struct AdamConsts {
+    float decay;     // 1 - lr*wd                (AdamW decoupled decay)
+    float w1;        // 1 - beta1                (lerp weight)
+    float b2;        // beta2
+    float w2;        // 1 - beta2                (addcmul value)
+    float eps;
+    float neg_step;  // -lr / bias_correction1
+    float bc2_sqrt;  // sqrt(bias_correction2)
+    float wd;        // weight_decay (Adam L2 form)
+    int decoupled;
+};
+struct SparseConsts {
+    float w1;        // 1 - beta1
+    float w2;        // 1 - beta2
+    float eps;
+    float neg_step;  // -lr * sqrt(bias_correction2) / bias_correction1
+};
+
+struct RowUpdateArgs {
+    int64_t n;              // rows in the tower batch (upper bound of unique count)
+    int dim;
+    const int32_t* n_unique;
+    const int32_t* seg_start;
+    const int32_t* keys;    // sorted keys
+    const int32_t* rows;    // sorted tower row ids
+    // ID table gradient source: dE[row] (ld)
+    const float* dE;
+    int64_t ld_dE;
+    ttamm_table id;
+    // mimic table gradient source: row < split_row ? dA_lo[row] : dA_hi[row]
+    const float* dA_lo;
+    const float* dA_hi;
+    int64_t split_row;
+    ttamm_table mimic;
+    // dense-optimized tables stage their touched rows in side buffers [n, 3, dim] (p, m, v)
+    float* side_id;
+    float* side_mimic;
+    SparseConsts sp;
+    AdamConsts ad;
+};
+int launch_row_update(const RowUpdateArgs& a, hipStream_t s);
+
+struct SweepSeg {
+    float* p;
+    float* m;
+    float* v;
+    int64_t n;  // elements
+};
+constexpr int kMaxSweepSegs = 4;
+struct SweepArgs {
+    SweepSeg seg[kMaxSweepSegs];
+    int count;
+    AdamConsts ad;
+};
+// AdamW with g = 0 over whole tables (adam.py:419-547 for rows the batch did not touch)
+int launch_dense_sweep(const SweepArgs& a, hipStream_t s);
+// write back side-buffer rows: table[key[u]] = side[u]
+int launch_side_scatter(const int32_t* n_unique, const int32_t* keys, const int32_t* seg_start,
+                        const float* side, int64_t n, int dim, ttamm_table t, hipStream_t s);
+
+struct DenseTensor {
+    float* p;
+    float* m;
+    float* v;
+    const float* g;
+    int64_t n;
+};
+constexpr int kMaxDenseTensors = 24;
+struct DenseAdamArgs {
+    DenseTensor t[kMaxDenseTensors];
+    int count;
+    AdamConsts ad;
+};
+int launch_dense_adam(const DenseAdamArgs& a, hipStream_t s);
+
+int launch_sparse_adam_rows(float* w, float* m, float* v, int dim, const int64_t* rows,
+                            const float* grad, int64_t n, SparseConsts sp, hipStream_t s);
+
+AdamConsts make_adam_consts(double lr, double beta1, double beta2, double eps, double wd,
+                            int decoupled, int64_t step);
+SparseConsts make_sparse_consts(double lr, double beta1, double beta2, double eps, int64_t step);
+
+// ------------------------------------------------------------------------------------
+// Sampler (sampler.hip)
+// ------------------------------------------------------------------------------------
+int launch_sample_negatives(const int64_t* users, int64_t batch, int num_neg, int64_t num_items,
+                            const int64_t* pos_offsets, const int64_t* pos_values, uint64_t seed,
+                            uint64_t counter, int64_t* out, uint32_t* status, hipStream_t s);
+
+}  // namespace ttamm

@@ -1,0 +1,330 @@
+// Optimizer side of the training step: gradient coalescing for the row tables and the
+// fused SparseAdam / AdamW updates.
+//
+// Row tables receive per-row gradient contributions from the batch (duplicates allowed).
+// They are coalesced by a stable radix sort of the int32 row keys, so duplicate rows are
+// summed in batch order — the order torch's CPU index_add / coalesce use
+// (training.py:822 backward; _functional.py:44 grad.coalesce()).
+//
+// Tables in the dense group (the adaptive-mimic tables, adaptive_mimic.py:35-36, put in the
+// AdamW group by training.py:306-307) are updated over EVERY row every step.  That sweep is
+// split into (1) an AdamW update of the touched rows with their gradient into a side buffer,
+// (2) a pure streaming AdamW(g = 0) pass over the whole table — the dominant HBM kernel of
+// the step, 24 bytes per element — and (3) a scatter of the side rows over the swept table.
+// The result equals one dense AdamW step over the full dense gradient.
+#include <hipcub/hipcub.hpp>
+
+#include "kernels.h"
+
+#pragma clang fp contract(off)
+
+namespace ttamm {
+
+namespace {
+
+// torch single-tensor Adam/AdamW (adam.py:419-547):
+//   p *= 1 - lr*wd ; m.lerp_(g, 1-b1) ; v = v*b2 + (1-b2)*g*g ;
+//   p += -step * m / (sqrt(v)/sqrt(bc2) + eps)
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, const AdamConsts& c) {
+    if (c.decoupled) {
+        p = p * c.decay;
+    } else if (c.wd != 0.f) {
+        g = g + p * c.wd;
+    }
+    m = fmaf(c.w1, g - m, m);  // ATen lerp (|w| < 0.5): self + w * (end - self), vectorised as fmadd
+    v = v * c.b2;
+    v = v + c.w2 * g * g;
+    const float denom = sqrtf(v) / c.bc2_sqrt + c.eps;
+    p = p + c.neg_step * (m / denom);
+}
+
+// torch SparseAdam on one coalesced element (_functional.py:61-84).
+__device__ __forceinline__ void sparse_adam_elem(float& p, float& m, float& v, float g, const SparseConsts& c) {
+    const float om = m, ov = v;
+    float um = (g - om) * c.w1;
+    float uv = (g * g - ov) * c.w2;
+    m = om + um;
+    v = ov + uv;
+    const float numer = um + om;
+    const float denom = sqrtf(uv + ov) + c.eps;
+    p = p + c.neg_step * (numer / denom);
+}
+
+__global__ void keys_init_kernel(const int64_t* __restrict__ idx, int64_t n, int32_t* __restrict__ keys,
+                                 int32_t* __restrict__ vals) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        keys[i] = (int32_t)idx[i];
+        vals[i] = (int32_t)i;
+    }
+}
+
+__global__ void seg_flags_kernel(const int32_t* __restrict__ keys, int64_t n, int32_t* __restrict__ flags) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
+}
+
+__global__ void seg_start_kernel(const int32_t* __restrict__ flags, const int32_t* __restrict__ uid, int64_t n,
+                                 int32_t* __restrict__ seg_start, int32_t* __restrict__ n_unique) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        if (flags[i]) seg_start[uid[i] - 1] = (int32_t)i;
+        if (i == n - 1) {
+            n_unique[0] = uid[i];
+            seg_start[uid[i]] = (int32_t)n;
+        }
+    }
+}
+
+// One wave per unique row: sum its contributions (fixed order), then update the ID table
+// (SparseAdam in place, or AdamW into a side buffer) and the mimic table (AdamW -> side).
+constexpr int kRowWaves = 4;
+__global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArgs A) {
+    const int lane = threadIdx.x & 63;
+    const int64_t u = (int64_t)blockIdx.x * kRowWaves + (threadIdx.x >> 6);
+    if (u >= A.n || u >= (int64_t)A.n_unique[0]) return;
+    const int k0 = A.seg_start[u], k1 = A.seg_start[u + 1];
+    const int64_t key = A.keys[k0];
+    const int D = A.dim;
+    for (int d = lane; d < D; d += 64) {
+        float ge = 0.f, ga = 0.f;
+        for (int k = k0; k < k1; ++k) {
+            const int64_t r = A.rows[k];
+            ge += A.dE[r * A.ld_dE + d];
+            if (A.mimic.weight) ga += (r < A.split_row ? A.dA_lo : A.dA_hi)[r * D + d];
+        }
+        {
+            const int64_t o = key * D + d;
+            float p = A.id.weight[o], m = A.id.exp_avg[o], v = A.id.exp_avg_sq[o];
+            if (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM) {
+                sparse_adam_elem(p, m, v, ge, A.sp);
+                A.id.weight[o] = p;
+                A.id.exp_avg[o] = m;
+                A.id.exp_avg_sq[o] = v;
+            } else {
+                adam_elem(p, m, v, ge, A.ad);
+                float* sd = A.side_id + u * 3 * D;
+                sd[d] = p;
+                sd[D + d] = m;
+                sd[2 * D + d] = v;
+            }
+        }
+        if (A.mimic.weight) {
+            const int64_t o = key * D + d;
+            float p = A.mimic.weight[o], m = A.mimic.exp_avg[o], v = A.mimic.exp_avg_sq[o];
+            adam_elem(p, m, v, ga, A.ad);
+            float* sd = A.side_mimic + u * 3 * D;
+            sd[d] = p;
+            sd[D + d] = m;
+            sd[2 * D + d] = v;
+        }
+    }
+}
+
+// Streaming AdamW(g = 0) over whole tables: 12 B read + 12 B written per element.
+__global__ __launch_bounds__(256) void dense_sweep_kernel(SweepArgs A) {
+    for (int s = 0; s < A.count; ++s) {
+        const SweepSeg& S = A.seg[s];
+        const int64_t n4 = S.n >> 2;
+        float4* P = reinterpret_cast<float4*>(S.p);
+        float4* Mm = reinterpret_cast<float4*>(S.m);
+        float4* V = reinterpret_cast<float4*>(S.v);
+        const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+            float4 p = P[i], m = Mm[i], v = V[i];
+            adam_elem(p.x, m.x, v.x, 0.f, A.ad);
+            adam_elem(p.y, m.y, v.y, 0.f, A.ad);
+            adam_elem(p.z, m.z, v.z, 0.f, A.ad);
+            adam_elem(p.w, m.w, v.w, 0.f, A.ad);
+            P[i] = p;
+            Mm[i] = m;
+            V[i] = v;
+        }
+        // scalar tail
+        for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < S.n; i += stride) {
+            float p = S.p[i], m = S.m[i], v = S.v[i];
+            adam_elem(p, m, v, 0.f, A.ad);
+            S.p[i] = p;
+            S.m[i] = m;
+            S.v[i] = v;
+        }
+    }
+}
+
+__global__ void side_scatter_kernel(const int32_t* __restrict__ n_unique, const int32_t* __restrict__ keys,
+                                    const int32_t* __restrict__ seg_start, const float* __restrict__ side, int64_t n,
+                                    int dim, ttamm_table t) {
+    const int64_t total = n * dim;
+    const int64_t nu = n_unique[0];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t u = i / dim;
+        if (u >= nu) return;
+        const int d = (int)(i - u * dim);
+        const int64_t key = keys[seg_start[u]];
+        const float* sd = side + u * 3 * dim;
+        const int64_t o = key * dim + d;
+        t.weight[o] = sd[d];
+        t.exp_avg[o] = sd[dim + d];
+        t.exp_avg_sq[o] = sd[2 * dim + d];
+    }
+}
+
+__global__ void dense_adam_kernel(DenseAdamArgs A, int64_t total) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        int64_t off = i;
+        int t = 0;
+        while (t < A.count - 1 && off >= A.t[t].n) {
+            off -= A.t[t].n;
+            ++t;
+        }
+        const DenseTensor& T = A.t[t];
+        float p = T.p[off], m = T.m[off], v = T.v[off];
+        adam_elem(p, m, v, T.g[off], A.ad);
+        T.p[off] = p;
+        T.m[off] = m;
+        T.v[off] = v;
+    }
+}
+
+__global__ void sparse_adam_rows_kernel(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
+                                        int dim, const int64_t* __restrict__ rows, const float* __restrict__ grad,
+                                        int64_t n, SparseConsts c) {
+    const int64_t total = n * dim;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t u = i / dim;
+        const int d = (int)(i - u * dim);
+        const int64_t o = rows[u] * dim + d;
+        float p = w[o], mm = m[o], vv = v[o];
+        sparse_adam_elem(p, mm, vv, grad[i], c);
+        w[o] = p;
+        m[o] = mm;
+        v[o] = vv;
+    }
+}
+
+inline unsigned grid_for(int64_t work, int threads = 256, int64_t cap = 65536) {
+    int64_t g = ceil_div(work, threads);
+    if (g > cap) g = cap;
+    if (g < 1) g = 1;
+    return (unsigned)g;
+}
+
+inline int end_bit_for(int64_t rows) {
+    int b = 1;
+    while (b < 31 && (int64_t(1) << b) < rows) ++b;
+    return b;
+}
+
+}  // namespace
+
+AdamConsts make_adam_consts(double lr, double beta1, double beta2, double eps, double wd, int decoupled,
+                            int64_t step) {
+    AdamConsts c;
+    const double bc1 = 1.0 - std::pow(beta1, (double)step);
+    const double bc2 = 1.0 - std::pow(beta2, (double)step);
+    c.decay = (float)(1.0 - lr * wd);
+    c.w1 = (float)(1.0 - beta1);
+    c.b2 = (float)beta2;
+    c.w2 = (float)(1.0 - beta2);
+    c.eps = (float)eps;
+    c.neg_step = (float)(-(lr / bc1));
+    c.bc2_sqrt = (float)std::pow(bc2, 0.5);
+    c.wd = (float)wd;
+    c.decoupled = decoupled;
+    return c;
+}
+
+SparseConsts make_sparse_consts(double lr, double beta1, double beta2, double eps, int64_t step) {
+    SparseConsts c;
+    const double bc1 = 1.0 - std::pow(beta1, (double)step);
+    const double bc2 = 1.0 - std::pow(beta2, (double)step);
+    c.w1 = (float)(1.0 - beta1);
+    c.w2 = (float)(1.0 - beta2);
+    c.eps = (float)eps;
+    c.neg_step = (float)(-(lr * std::sqrt(bc2) / bc1));
+    return c;
+}
+
+size_t coalesce_temp_bytes(int64_t n) {
+    size_t sort_bytes = 0, scan_bytes = 0;
+    const int nn = (int)(n > 0 ? n : 1);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr,
+                                       (int32_t*)nullptr, nn, 0, 31, (hipStream_t)0);
+    (void)hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, (int32_t*)nullptr, (int32_t*)nullptr, nn, (hipStream_t)0);
+    return (sort_bytes > scan_bytes ? sort_bytes : scan_bytes) + 256;
+}
+
+int launch_coalesce(const int64_t* idx, int64_t n, int64_t table_rows, CoalesceWs& ws, hipStream_t s) {
+    TTAMM_REQUIRE(table_rows < (int64_t(1) << 31), "coalesce: table too large for int32 keys");
+    if (n <= 0) {
+        TTAMM_HIP(hipMemsetAsync(ws.n_unique, 0, sizeof(int32_t), s));
+        return TTAMM_OK;
+    }
+    hipLaunchKernelGGL(keys_init_kernel, dim3(grid_for(n, 256, 1 << 30)), dim3(256), 0, s, idx, n, ws.keys_in,
+                       ws.vals_in);
+    TTAMM_LAUNCH_CHECK();
+    size_t bytes = ws.temp_bytes;
+    TTAMM_HIP(hipcub::DeviceRadixSort::SortPairs(ws.temp, bytes, ws.keys_in, ws.keys_out, ws.vals_in, ws.vals_out,
+                                                 (int)n, 0, end_bit_for(table_rows), s));
+    hipLaunchKernelGGL(seg_flags_kernel, dim3(grid_for(n, 256, 1 << 30)), dim3(256), 0, s, ws.keys_out, n, ws.flags);
+    TTAMM_LAUNCH_CHECK();
+    bytes = ws.temp_bytes;
+    TTAMM_HIP(hipcub::DeviceScan::InclusiveSum(ws.temp, bytes, ws.flags, ws.uid, (int)n, s));
+    hipLaunchKernelGGL(seg_start_kernel, dim3(grid_for(n, 256, 1 << 30)), dim3(256), 0, s, ws.flags, ws.uid, n,
+                       ws.seg_start, ws.n_unique);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_row_update(const RowUpdateArgs& a, hipStream_t s) {
+    if (a.n <= 0) return TTAMM_OK;
+    hipLaunchKernelGGL(row_update_kernel, dim3((unsigned)ceil_div(a.n, kRowWaves)), dim3(64 * kRowWaves), 0, s, a);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_dense_sweep(const SweepArgs& a, hipStream_t s) {
+    int64_t total4 = 0;
+    for (int i = 0; i < a.count; ++i) {
+        TTAMM_REQUIRE(((uintptr_t)a.seg[i].p | (uintptr_t)a.seg[i].m | (uintptr_t)a.seg[i].v) % 16 == 0,
+                      "dense sweep: tables must be 16-byte aligned");
+        total4 += a.seg[i].n >> 2;
+    }
+    if (a.count == 0) return TTAMM_OK;
+    // 2048 blocks x 256 threads: 8 blocks per CU, grid-stride over the tables
+    hipLaunchKernelGGL(dense_sweep_kernel, dim3(grid_for(total4, 256, 2048)), dim3(256), 0, s, a);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_side_scatter(const int32_t* n_unique, const int32_t* keys, const int32_t* seg_start, const float* side,
+                        int64_t n, int dim, ttamm_table t, hipStream_t s) {
+    if (n <= 0) return TTAMM_OK;
+    hipLaunchKernelGGL(side_scatter_kernel, dim3(grid_for(n * dim)), dim3(256), 0, s, n_unique, keys, seg_start, side,
+                       n, dim, t);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_dense_adam(const DenseAdamArgs& a, hipStream_t s) {
+    int64_t total = 0;
+    for (int i = 0; i < a.count; ++i) total += a.t[i].n;
+    if (total == 0) return TTAMM_OK;
+    hipLaunchKernelGGL(dense_adam_kernel, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s, a, total);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_sparse_adam_rows(float* w, float* m, float* v, int dim, const int64_t* rows, const float* grad, int64_t n,
+                            SparseConsts c, hipStream_t s) {
+    if (n <= 0) return TTAMM_OK;
+    hipLaunchKernelGGL(sparse_adam_rows_kernel, dim3(grid_for(n * dim)), dim3(256), 0, s, w, m, v, dim, rows, grad,
+                       n, c);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+}  // namespace ttamm

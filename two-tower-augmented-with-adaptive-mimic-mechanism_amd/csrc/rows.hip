@@ -1,0 +1,297 @@
+// Row-wise kernels of the training step: embedding row gather, non-gated fusion,
+// the gate's sigmoid backward, and the fused score + BCE + mimic-MSE forward/backward.
+#include "kernels.h"
+
+namespace ttamm {
+
+namespace {
+
+// out[r, :] = table[idx[r], :]   (nn.Embedding forward, encoders.py:222-223).
+// One float4 per thread, flat over n * dim/4; bit-exact copy.
+__global__ void gather_rows_vec4(const float* __restrict__ table, int d4, const int64_t* __restrict__ idx,
+                                 int64_t n, float* __restrict__ out, int64_t out_ld) {
+    const int64_t total = n * d4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / d4;
+        const int c = (int)(i - r * d4);
+        const float4 v = reinterpret_cast<const float4*>(table + idx[r] * (int64_t)d4 * 4)[c];
+        reinterpret_cast<float4*>(out + r * out_ld)[c] = v;
+    }
+}
+
+__global__ void gather_rows_scalar(const float* __restrict__ table, int dim, const int64_t* __restrict__ idx,
+                                   int64_t n, float* __restrict__ out, int64_t out_ld) {
+    const int64_t total = n * dim;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / dim;
+        const int c = (int)(i - r * dim);
+        out[r * out_ld + c] = table[idx[r] * (int64_t)dim + c];
+    }
+}
+
+// t = e (+ f) ; a = table[idx] ; aug = t + a      (encoders.py:225-240, adaptive_mimic.py:88-95)
+__global__ void combine_kernel(const float* __restrict__ e, int64_t ld_e, const float* __restrict__ f,
+                               int64_t ld_f, const float* __restrict__ table, const int64_t* __restrict__ idx,
+                               int64_t n, int dim, float* __restrict__ t, float* __restrict__ a,
+                               float* __restrict__ aug) {
+    const int64_t total = n * dim;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / dim;
+        const int c = (int)(i - r * dim);
+        float tv = e[r * ld_e + c];
+        if (f) tv = tv + f[r * ld_f + c];
+        if (t) t[i] = tv;
+        float av = tv;
+        if (table) {
+            const float am = table[idx[r] * (int64_t)dim + c];
+            if (a) a[i] = am;
+            av = tv + am;
+        }
+        aug[i] = av;
+    }
+}
+
+// dq = (dT*e - dT*f) * (1 - g) * g
+// autograd of gate*e + (1-gate)*f then SigmoidBackward (grad*(1-y)*y), encoders.py:164-168.
+__global__ void gate_dq_kernel(const float* __restrict__ dT, const float* __restrict__ ef,
+                               const float* __restrict__ g, int64_t n, int dim, float* __restrict__ dq) {
+    const int64_t total = n * dim;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / dim;
+        const int c = (int)(i - r * dim);
+        const float d = dT[i];
+        const float ev = ef[r * 2 * dim + c], fv = ef[r * 2 * dim + dim + c];
+        const float gv = g[i];
+        const float dg = d * ev - d * fv;
+        dq[i] = dg * (1.0f - gv) * gv;
+    }
+}
+
+// BCEWithLogits term, ATen form: (1-y)*x + m + log(exp(-m) + exp(-x-m)), m = max(-x, 0)
+__device__ __forceinline__ float bce_logit(float x, float y) {
+    const float m = fmaxf(-x, 0.f);
+    return (1.0f - y) * x + m + logf(expf(-m) + expf(-x - m));
+}
+
+// One wave per interaction b (training.py:770-803, Appendix A of SURVEY.md):
+//   s+ = <u_b, p_b>, s-_j = <u_b, n_bj>; ds = (sigmoid(s) - y) / (B(1+N))
+//   dT_user = ds+ p + sum_j ds-_j n_j ; dT_pos = ds+ u ; dT_neg_j = ds-_j u
+//   mimic: dA_user = dT_user + lu * 2/(B D) * (a_u - t_p) ; dA_pos = dT_pos + li * 2/(B D) * (a_p - t_u)
+constexpr int kScoreWaves = 4;
+constexpr int kMaxDChunks = 8;  // D <= 512
+constexpr int kMaxNeg = 64;
+
+__global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs A) {
+    __shared__ float red[kScoreWaves][3];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t b = (int64_t)blockIdx.x * kScoreWaves + w;
+    const int D = A.D, N = A.N;
+    const int64_t B = A.B;
+    const float inv_numel = 1.0f / (float)(B * (1 + N));
+    float bce = 0.f, mse_u = 0.f, mse_i = 0.f;
+    if (b < B) {
+        const int nch = (D + 63) / 64;
+        float u[kMaxDChunks], p[kMaxDChunks], du[kMaxDChunks];
+        float dot = 0.f;
+#pragma unroll
+        for (int c = 0; c < kMaxDChunks; ++c) {
+            u[c] = p[c] = du[c] = 0.f;
+            const int d = c * 64 + lane;
+            if (c < nch && d < D) {
+                u[c] = A.user_aug[b * D + d];
+                p[c] = A.item_aug[b * D + d];
+                dot += u[c] * p[c];
+            }
+        }
+        const float sp = wave_sum(dot);
+        const float dsp = (1.0f / (1.0f + expf(-sp)) - 1.0f) * inv_numel;
+        bce += bce_logit(sp, 1.0f);
+        // positive item row: dT_pos = ds+ * u ; user: ds+ * p
+#pragma unroll
+        for (int c = 0; c < kMaxDChunks; ++c) {
+            const int d = c * 64 + lane;
+            if (c < nch && d < D) {
+                A.dT_item[b * D + d] = dsp * u[c];
+                du[c] = dsp * p[c];
+            }
+        }
+        for (int j = 0; j < N; ++j) {
+            const int64_t nr = B + b * N + j;
+            float nv[kMaxDChunks];
+            float dn = 0.f;
+#pragma unroll
+            for (int c = 0; c < kMaxDChunks; ++c) {
+                nv[c] = 0.f;
+                const int d = c * 64 + lane;
+                if (c < nch && d < D) {
+                    nv[c] = A.item_aug[nr * D + d];
+                    dn += u[c] * nv[c];
+                }
+            }
+            const float sn = wave_sum(dn);
+            const float dsn = (1.0f / (1.0f + expf(-sn)) - 0.0f) * inv_numel;
+            bce += bce_logit(sn, 0.0f);
+#pragma unroll
+            for (int c = 0; c < kMaxDChunks; ++c) {
+                const int d = c * 64 + lane;
+                if (c < nch && d < D) {
+                    A.dT_item[nr * D + d] = dsn * u[c];
+                    du[c] += dsn * nv[c];
+                }
+            }
+        }
+        const float norm = 2.0f / (float)(B * D);
+#pragma unroll
+        for (int c = 0; c < kMaxDChunks; ++c) {
+            const int d = c * 64 + lane;
+            if (c < nch && d < D) {
+                A.dT_user[b * D + d] = du[c];
+                if (A.mimic) {
+                    const float au = A.a_user[b * D + d], tp = A.t_item[b * D + d];
+                    const float ap = A.a_item[b * D + d], tu = A.t_user[b * D + d];
+                    const float xu = au - tp, xi = ap - tu;
+                    mse_u += xu * xu;
+                    mse_i += xi * xi;
+                    A.dA_user[b * D + d] = du[c] + norm * xu * A.lambda_u;
+                    A.dA_pos[b * D + d] = dsp * u[c] + norm * xi * A.lambda_i;
+                }
+            }
+        }
+        mse_u = wave_sum(mse_u);
+        mse_i = wave_sum(mse_i);
+    }
+    if (lane == 0) {
+        red[w][0] = bce;
+        red[w][1] = mse_u;
+        red[w][2] = mse_i;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        float s = 0.f;
+        for (int i = 0; i < kScoreWaves; ++i) s += red[i][threadIdx.x];
+        A.partials[blockIdx.x * 3 + threadIdx.x] = s;
+    }
+}
+
+// Deterministic final reduction of the per-block partials; total loss as in training.py:798-803.
+__global__ void loss_finalize_kernel(const float* __restrict__ partials, int blocks, int64_t B, int N, int D,
+                                     float lu, float li, int mimic, float* __restrict__ loss_out,
+                                     double* __restrict__ loss_accum) {
+    __shared__ float red[3][256];
+    float s[3] = {0.f, 0.f, 0.f};
+    for (int i = threadIdx.x; i < blocks; i += blockDim.x)
+        for (int k = 0; k < 3; ++k) s[k] += partials[i * 3 + k];
+    for (int k = 0; k < 3; ++k) red[k][threadIdx.x] = s[k];
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if (threadIdx.x < o)
+            for (int k = 0; k < 3; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const float bce = red[0][0] / (float)(B * (1 + N));
+        const float mu = red[1][0] / (float)(B * D);
+        const float mi = red[2][0] / (float)(B * D);
+        float total = bce;
+        if (mimic && lu > 0.f) total = total + lu * mu;
+        if (mimic && li > 0.f) total = total + li * mi;
+        loss_out[0] = total;
+        loss_out[1] = bce;
+        loss_out[2] = mimic ? mu : 0.f;
+        loss_out[3] = mimic ? mi : 0.f;
+        if (loss_accum) {
+            loss_accum[0] += (double)total * (double)B;
+            loss_accum[1] += (double)B;
+        }
+    }
+}
+
+// mean((x - y)^2), one block, fixed reduction order (F.mse_loss, reduction='mean').
+__global__ void mse_kernel(const float* __restrict__ x, const float* __restrict__ y, int64_t n, float* __restrict__ out) {
+    __shared__ float red[1024];
+    float s = 0.f;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const float d = x[i] - y[i];
+        s += d * d;
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[0] = red[0] / (float)n;
+}
+
+inline unsigned grid_for(int64_t work, int threads = 256) {
+    int64_t g = ceil_div(work, threads);
+    if (g > 65536) g = 65536;
+    if (g < 1) g = 1;
+    return (unsigned)g;
+}
+
+}  // namespace
+
+int launch_gather_rows(const float* table, int dim, const int64_t* idx, int64_t n, float* out, int64_t out_ld,
+                       hipStream_t s) {
+    if (n <= 0) return TTAMM_OK;
+    const bool vec = (dim % 4 == 0) && (out_ld % 4 == 0) && ((uintptr_t)table % 16 == 0) &&
+                     ((uintptr_t)out % 16 == 0);
+    if (vec) {
+        hipLaunchKernelGGL(gather_rows_vec4, dim3(grid_for(n * (dim / 4))), dim3(256), 0, s, table, dim / 4, idx, n,
+                           out, out_ld);
+    } else {
+        hipLaunchKernelGGL(gather_rows_scalar, dim3(grid_for(n * dim)), dim3(256), 0, s, table, dim, idx, n, out,
+                           out_ld);
+    }
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_combine(const float* e, int64_t ld_e, const float* f, int64_t ld_f, const float* table,
+                   const int64_t* idx, int64_t n, int dim, float* t, float* a, float* aug, hipStream_t s) {
+    if (n <= 0) return TTAMM_OK;
+    hipLaunchKernelGGL(combine_kernel, dim3(grid_for(n * dim)), dim3(256), 0, s, e, ld_e, f, ld_f, table, idx, n,
+                       dim, t, a, aug);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_mse(const float* x, const float* y, int64_t n, float* out, hipStream_t s) {
+    TTAMM_REQUIRE(n > 0, "mse_loss: empty input");
+    hipLaunchKernelGGL(mse_kernel, dim3(1), dim3(1024), 0, s, x, y, n, out);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_gate_dq(const float* dT, const float* ef, const float* g, int64_t n, int dim, float* dq, hipStream_t s) {
+    if (n <= 0) return TTAMM_OK;
+    hipLaunchKernelGGL(gate_dq_kernel, dim3(grid_for(n * dim)), dim3(256), 0, s, dT, ef, g, n, dim, dq);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_score_loss(const ScoreArgs& a, hipStream_t s) {
+    TTAMM_REQUIRE(a.D <= 64 * kMaxDChunks, "score: embedding dim too large (max 512)");
+    TTAMM_REQUIRE(a.N >= 1 && a.N <= kMaxNeg, "score: negatives_per_positive out of range");
+    if (a.B <= 0) return TTAMM_OK;
+    hipLaunchKernelGGL(score_loss_kernel, dim3(a.blocks), dim3(64 * kScoreWaves), 0, s, a);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int score_blocks(int64_t B) { return (int)ceil_div(B, kScoreWaves); }
+
+int launch_loss_finalize(const float* partials, int blocks, int64_t B, int N, int D, float lu, float li, int mimic,
+                         float* loss_out, double* loss_accum, hipStream_t s) {
+    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, partials, blocks, B, N, D, lu, li, mimic,
+                       loss_out, loss_accum);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+}  // namespace ttamm

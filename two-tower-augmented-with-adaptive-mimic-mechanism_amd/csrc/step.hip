@@ -1,0 +1,701 @@
+// Native executor of one training step (the body of `_train_one_epoch`,
+// training.py:726-831), issued as a fixed sequence of gfx950 kernels on one HIP stream.
+//
+//   sample negatives                      samplers.py:11-85                (a11)
+//   tower forward (user & item grouped)   encoders.py:221-255              (a1, a3, a4)
+//     hidden Linear+ReLU+Dropout GEMMs    gathered feature rows, MFMA fp32
+//     final Linear -> f ; ID gather -> e  into one [rows, 2D] "ef" buffer
+//     gate GEMM 1 (ReLU), gate GEMM 2 (sigmoid, mix, mimic augment)      adaptive_mimic.py:88-95 (a2)
+//   score + BCE + mimic MSE fwd/bwd       training.py:770-803              (a5-a7)
+//   tower backward (dgrad chain grouped, then all weight grads in one launch)
+//   coalesce row grads, SparseAdam (ID tables), AdamW touched rows        (a9, a5)
+//   AdamW(g=0) stream over the full mimic tables, side-row scatter         (a5, a10)
+//   AdamW on the MLP / gate weights                                        (a10)
+#include <cstring>
+#include <vector>
+
+#include "kernels.h"
+
+namespace ttamm {
+
+namespace {
+
+struct TowerWs {
+    int64_t R = 0;
+    const int64_t* idx = nullptr;   // ID / mimic table rows
+    const int64_t* fidx = nullptr;  // feature rows (null: row r)
+    int64_t* idx_own = nullptr;     // item tower: [pos; neg]
+    float* hid[TTAMM_MAX_LINEAR] = {};
+    float* dhid[TTAMM_MAX_LINEAR] = {};
+    float* ef = nullptr;    // gated: [R, 2D] = [e | f]
+    float* e = nullptr;     // non-gated: [R, D]
+    float* f = nullptr;     // sum fusion: [R, D]
+    float* z = nullptr;     // gate hidden [R, Hg]
+    float* dz = nullptr;
+    float* g = nullptr;
+    float* t = nullptr;
+    float* a = nullptr;
+    float* aug = nullptr;
+    float* dT = nullptr;
+    float* dq = nullptr;
+    float* dEF = nullptr;  // [R, 2D]
+    float* dA = nullptr;   // [B, D]
+    float* gw[TTAMM_MAX_LINEAR] = {};
+    float* gb[TTAMM_MAX_LINEAR] = {};
+    float* ggw[2] = {};
+    float* ggb[2] = {};
+    float* slab[TTAMM_MAX_LINEAR + 2] = {};
+    CoalesceWs co{};
+    float* side_id = nullptr;
+    float* side_mimic = nullptr;
+};
+
+struct StepWs {
+    TowerWs user, item;
+    float* partials = nullptr;
+    int score_blocks = 0;
+};
+
+int tower_in_dim(const ttamm_tower& T, int l) { return l == 0 ? T.feat_dim : T.linear[l - 1].out_features; }
+
+// Validate one tower against the reference's own constraints.
+int validate_tower(const ttamm_tower& T, const char* name, int D, bool training) {
+    std::string n(name);
+    TTAMM_REQUIRE(T.id.weight, n + ": embedding table missing");
+    if (training) TTAMM_REQUIRE(T.id.exp_avg && T.id.exp_avg_sq, n + ": embedding optimizer state missing");
+    TTAMM_REQUIRE(T.id.dim == D, n + ": embedding dim mismatch");
+    TTAMM_REQUIRE(T.id.rows > 0, n + ": empty embedding table");
+    TTAMM_REQUIRE(T.n_linear >= 0 && T.n_linear <= TTAMM_MAX_LINEAR, n + ": too many feature-encoder layers");
+    TTAMM_REQUIRE(T.fusion >= TTAMM_FUSION_IDENTITY && T.fusion <= TTAMM_FUSION_GATED, n + ": unsupported fusion");
+    if (T.fusion != TTAMM_FUSION_IDENTITY) {
+        TTAMM_REQUIRE(T.features != nullptr && T.feat_dim > 0, n + ": fusion needs feature rows");
+        TTAMM_REQUIRE(T.feat_ld >= T.feat_dim, n + ": feature row stride too small");
+        for (int l = 0; l < T.n_linear; ++l) {
+            const ttamm_linear& L = T.linear[l];
+            TTAMM_REQUIRE(L.weight && L.bias, n + ": linear parameters missing");
+            if (training)
+                TTAMM_REQUIRE(L.weight_exp_avg && L.weight_exp_avg_sq && L.bias_exp_avg && L.bias_exp_avg_sq,
+                              n + ": linear optimizer state missing");
+            TTAMM_REQUIRE(L.in_features == tower_in_dim(T, l), n + ": feature-encoder layer shapes do not chain");
+        }
+        const int fo = T.n_linear ? T.linear[T.n_linear - 1].out_features : T.feat_dim;
+        TTAMM_REQUIRE(fo == D,
+                      n + ": Feature encoder output dimension must equal embedding dimension for 'sum' or 'gated' fusion.");
+        TTAMM_REQUIRE(T.dropout >= 0.f && T.dropout < 1.f, n + ": dropout must be in [0, 1)");
+    }
+    if (T.fusion == TTAMM_FUSION_GATED) {
+        const ttamm_linear &G1 = T.gate[0], &G2 = T.gate[1];
+        TTAMM_REQUIRE(G1.weight && G1.bias && G2.weight && G2.bias, n + ": gate parameters missing");
+        if (training)
+            TTAMM_REQUIRE(G1.weight_exp_avg && G1.weight_exp_avg_sq && G1.bias_exp_avg && G1.bias_exp_avg_sq &&
+                              G2.weight_exp_avg && G2.weight_exp_avg_sq && G2.bias_exp_avg && G2.bias_exp_avg_sq,
+                          n + ": gate optimizer state missing");
+        TTAMM_REQUIRE(G1.in_features == 2 * D && G2.out_features == D && G2.in_features == G1.out_features,
+                      n + ": gate shapes do not match the embedding dimension");
+    }
+    return TTAMM_OK;
+}
+
+int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
+    const int64_t B = A.b.batch;
+    const int N = A.b.num_neg;
+    const int D = A.user.id.dim;
+    const bool mimic = A.mimic_enabled != 0;
+    auto tower = [&](const ttamm_tower& T, TowerWs& w, int64_t R, bool own_idx) {
+        w.R = R;
+        if (own_idx) w.idx_own = ar.take<int64_t>(R);
+        for (int l = 0; l + 1 < T.n_linear; ++l) {
+            w.hid[l] = ar.take<float>((size_t)R * T.linear[l].out_features);
+            w.dhid[l] = ar.take<float>((size_t)R * T.linear[l].out_features);
+        }
+        const int Hg = T.fusion == TTAMM_FUSION_GATED ? T.gate[0].out_features : 0;
+        if (T.fusion == TTAMM_FUSION_GATED) {
+            w.ef = ar.take<float>((size_t)R * 2 * D);
+            w.dEF = ar.take<float>((size_t)R * 2 * D);
+            w.z = ar.take<float>((size_t)R * Hg);
+            w.dz = ar.take<float>((size_t)R * Hg);
+            w.g = ar.take<float>((size_t)R * D);
+            w.dq = ar.take<float>((size_t)R * D);
+        } else {
+            w.e = ar.take<float>((size_t)R * D);
+            if (T.fusion == TTAMM_FUSION_SUM) w.f = ar.take<float>((size_t)R * D);
+        }
+        w.t = ar.take<float>((size_t)R * D);
+        w.a = mimic ? ar.take<float>((size_t)R * D) : nullptr;
+        w.aug = ar.take<float>((size_t)R * D);
+        w.dT = ar.take<float>((size_t)R * D);
+        w.dA = mimic ? ar.take<float>((size_t)B * D) : nullptr;
+        if (T.fusion != TTAMM_FUSION_IDENTITY) {
+            for (int l = 0; l < T.n_linear; ++l) {
+                const ttamm_linear& L = T.linear[l];
+                w.gw[l] = ar.take<float>((size_t)L.out_features * L.in_features);
+                w.gb[l] = ar.take<float>((size_t)L.out_features);
+                w.slab[l] = ar.take<float>(wgrad_slab_floats((int)R, L.out_features, L.in_features));
+            }
+        }
+        if (T.fusion == TTAMM_FUSION_GATED) {
+            for (int q = 0; q < 2; ++q) {
+                const ttamm_linear& L = T.gate[q];
+                w.ggw[q] = ar.take<float>((size_t)L.out_features * L.in_features);
+                w.ggb[q] = ar.take<float>((size_t)L.out_features);
+                w.slab[TTAMM_MAX_LINEAR + q] = ar.take<float>(wgrad_slab_floats((int)R, L.out_features, L.in_features));
+            }
+        }
+        w.co.keys_in = ar.take<int32_t>(R);
+        w.co.vals_in = ar.take<int32_t>(R);
+        w.co.keys_out = ar.take<int32_t>(R);
+        w.co.vals_out = ar.take<int32_t>(R);
+        w.co.flags = ar.take<int32_t>(R);
+        w.co.uid = ar.take<int32_t>(R);
+        w.co.seg_start = ar.take<int32_t>(R + 1);
+        w.co.n_unique = ar.take<int32_t>(1);
+        w.co.temp_bytes = coalesce_temp_bytes(R);
+        w.co.temp = ar.take<char>(w.co.temp_bytes);
+        if (T.id.optimizer == TTAMM_OPT_DENSE) w.side_id = ar.take<float>((size_t)R * 3 * D);
+        if (mimic) w.side_mimic = ar.take<float>((size_t)R * 3 * D);
+    };
+    tower(A.user, ws.user, B, false);
+    tower(A.item, ws.item, B * (1 + N), true);
+    ws.score_blocks = score_blocks(B);
+    ws.partials = ar.take<float>((size_t)ws.score_blocks * 3);
+    return TTAMM_OK;
+}
+
+GemmProblem gp_base() {
+    GemmProblem p;
+    std::memset(&p, 0, sizeof(p));
+    p.keep_prob = 1.f;
+    p.inv_keep = 1.f;
+    return p;
+}
+
+struct Batcher {
+    GemmBatch b;
+    Batcher() { std::memset(&b, 0, sizeof(b)); }
+    void add(const GemmProblem& p) { b.p[b.count++] = p; }
+    int run(hipStream_t s) {
+        if (b.count == 0) return TTAMM_OK;
+        int rc = launch_gemm(b, s);
+        std::memset(&b, 0, sizeof(b));
+        return rc;
+    }
+};
+
+// Dropout RNG words: key = seed; counter words 2,3 = step counter / (domain | tower | layer)
+void set_dropout(GemmProblem& p, const ttamm_tower& T, const ttamm_batch& bt, int tower_id, int layer,
+                 const uint8_t* mask) {
+    const float pdrop = T.dropout;
+    p.keep_prob = 1.0f - pdrop;
+    // torch computes noise/(1-p) in fp32: 1.f / (1.f - p)
+    p.inv_keep = pdrop > 0.f ? 1.0f / (1.0f - pdrop) : 1.0f;
+    p.keep_mask = mask;
+    p.rng_k0 = (uint32_t)bt.seed;
+    p.rng_k1 = (uint32_t)(bt.seed >> 32);
+    p.rng_c2 = (uint32_t)bt.counter;
+    p.rng_c3 = RNG_DROPOUT | ((uint32_t)tower_id << 24) | ((uint32_t)layer << 20) |
+               ((uint32_t)(bt.counter >> 32) & 0xFFFFFu);
+}
+
+// ---- forward -------------------------------------------------------------------------------
+int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt, int D, bool mimic, hipStream_t s,
+                  int ntowers) {
+    int rc;
+    // ID rows -> e (ef[:, :D] when gated)
+    for (int k = 0; k < ntowers; ++k) {
+        const ttamm_tower& t = *T[k];
+        TowerWs& w = *W[k];
+        float* dst = t.fusion == TTAMM_FUSION_GATED ? w.ef : w.e;
+        const int64_t ld = t.fusion == TTAMM_FUSION_GATED ? 2 * D : D;
+        if ((rc = launch_gather_rows(t.id.weight, D, w.idx, w.R, dst, ld, s))) return rc;
+    }
+    // feature encoder layers
+    int maxL = 0;
+    for (int k = 0; k < ntowers; ++k)
+        if (T[k]->fusion != TTAMM_FUSION_IDENTITY) maxL = T[k]->n_linear > maxL ? T[k]->n_linear : maxL;
+    for (int l = 0; l < maxL; ++l) {
+        Batcher bb;
+        for (int k = 0; k < ntowers; ++k) {
+            const ttamm_tower& t = *T[k];
+            TowerWs& w = *W[k];
+            if (t.fusion == TTAMM_FUSION_IDENTITY || l >= t.n_linear) continue;
+            const ttamm_linear& L = t.linear[l];
+            GemmProblem p = gp_base();
+            if (l == 0) {
+                p.A = t.features;
+                p.a_idx = w.fidx;
+                p.lda = t.feat_ld;
+            } else {
+                p.A = w.hid[l - 1];
+                p.lda = t.linear[l - 1].out_features;
+            }
+            p.B = L.weight;
+            p.ldb = L.in_features;
+            p.b_kn = 0;
+            p.M = (int)w.R;
+            p.N = L.out_features;
+            p.K = L.in_features;
+            p.bias = L.bias;
+            if (l + 1 < t.n_linear) {
+                p.epi = EPI_HIDDEN;
+                p.C = w.hid[l];
+                p.ldc = L.out_features;
+                set_dropout(p, t, bt, k, l, k == 0 ? bt.user_keep_mask[l] : bt.item_keep_mask[l]);
+            } else {
+                p.epi = EPI_STORE;
+                if (t.fusion == TTAMM_FUSION_GATED) {
+                    p.C = w.ef + D;
+                    p.ldc = 2 * D;
+                } else {
+                    p.C = w.f;
+                    p.ldc = D;
+                }
+            }
+            bb.add(p);
+        }
+        if ((rc = bb.run(s))) return rc;
+    }
+    // feature encoder "identity" (no Linear): f = feature rows
+    for (int k = 0; k < ntowers; ++k) {
+        const ttamm_tower& t = *T[k];
+        if (t.fusion != TTAMM_FUSION_IDENTITY && t.n_linear == 0)
+            return fail(TTAMM_E_INVALID, "identity feature encoder is not supported by the fused step");
+    }
+    // fusion
+    Batcher g1, g2;
+    for (int k = 0; k < ntowers; ++k) {
+        const ttamm_tower& t = *T[k];
+        TowerWs& w = *W[k];
+        const float* table = mimic ? t.mimic.weight : nullptr;
+        if (t.fusion == TTAMM_FUSION_GATED) {
+            const int Hg = t.gate[0].out_features;
+            GemmProblem p = gp_base();
+            p.A = w.ef;
+            p.lda = 2 * D;
+            p.B = t.gate[0].weight;
+            p.ldb = 2 * D;
+            p.M = (int)w.R;
+            p.N = Hg;
+            p.K = 2 * D;
+            p.bias = t.gate[0].bias;
+            p.epi = EPI_GATE_HIDDEN;
+            p.C = w.z;
+            p.ldc = Hg;
+            g1.add(p);
+            GemmProblem q = gp_base();
+            q.A = w.z;
+            q.lda = Hg;
+            q.B = t.gate[1].weight;
+            q.ldb = Hg;
+            q.M = (int)w.R;
+            q.N = D;
+            q.K = Hg;
+            q.bias = t.gate[1].bias;
+            q.epi = EPI_GATE_OUT;
+            q.C = w.aug;
+            q.ldc = D;
+            q.aux0 = w.ef;
+            q.ld_aux0 = 2 * D;
+            q.out1 = w.g;
+            q.out2 = w.t;
+            q.out3 = w.a;
+            q.table = table;
+            q.idx = w.idx;
+            q.ld_out = D;
+            g2.add(q);
+        } else {
+            if ((rc = launch_combine(w.e, D, t.fusion == TTAMM_FUSION_SUM ? w.f : nullptr, D, table, w.idx, w.R, D, w.t,
+                                     w.a, w.aug, s)))
+                return rc;
+        }
+    }
+    if ((rc = g1.run(s))) return rc;
+    if ((rc = g2.run(s))) return rc;
+    return TTAMM_OK;
+}
+
+// ---- backward ------------------------------------------------------------------------------
+int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s, int ntowers) {
+    int rc;
+    // gate: dq, dz, dEF
+    Batcher b1, b2;
+    for (int k = 0; k < ntowers; ++k) {
+        const ttamm_tower& t = *T[k];
+        TowerWs& w = *W[k];
+        if (t.fusion != TTAMM_FUSION_GATED) continue;
+        const int Hg = t.gate[0].out_features;
+        if ((rc = launch_gate_dq(w.dT, w.ef, w.g, w.R, D, w.dq, s))) return rc;
+        GemmProblem p = gp_base();  // dz = (dq . G2) * (z > 0)
+        p.A = w.dq;
+        p.lda = D;
+        p.B = t.gate[1].weight;  // [D, Hg] = [K, N]
+        p.ldb = Hg;
+        p.b_kn = 1;
+        p.M = (int)w.R;
+        p.N = Hg;
+        p.K = D;
+        p.epi = EPI_DGRAD_RELU;
+        p.C = w.dz;
+        p.ldc = Hg;
+        p.aux0 = w.z;
+        p.ld_aux0 = Hg;
+        b1.add(p);
+        GemmProblem q = gp_base();  // [de | df] = dz . G1 + gate-mix terms
+        q.A = w.dz;
+        q.lda = Hg;
+        q.B = t.gate[0].weight;  // [Hg, 2D] = [K, N]
+        q.ldb = 2 * D;
+        q.b_kn = 1;
+        q.M = (int)w.R;
+        q.N = 2 * D;
+        q.K = Hg;
+        q.epi = EPI_DGRAD_GATE_EF;
+        q.C = w.dEF;
+        q.ldc = 2 * D;
+        q.aux1 = w.dT;
+        q.aux2 = w.g;
+        q.ld_aux1 = D;
+        b2.add(q);
+    }
+    if ((rc = b1.run(s))) return rc;
+    if ((rc = b2.run(s))) return rc;
+    // MLP dgrad chain (layers L-1 .. 1)
+    int maxL = 0;
+    for (int k = 0; k < ntowers; ++k)
+        if (T[k]->fusion != TTAMM_FUSION_IDENTITY) maxL = T[k]->n_linear > maxL ? T[k]->n_linear : maxL;
+    for (int step = 0; step + 1 < maxL; ++step) {
+        Batcher bb;
+        for (int k = 0; k < ntowers; ++k) {
+            const ttamm_tower& t = *T[k];
+            TowerWs& w = *W[k];
+            if (t.fusion == TTAMM_FUSION_IDENTITY) continue;
+            const int l = t.n_linear - 1 - step;  // layer whose input grad we compute
+            if (l < 1) continue;
+            const ttamm_linear& L = t.linear[l];
+            GemmProblem p = gp_base();
+            if (l == t.n_linear - 1) {
+                p.A = t.fusion == TTAMM_FUSION_GATED ? w.dEF + D : w.dT;
+                p.lda = t.fusion == TTAMM_FUSION_GATED ? 2 * D : D;
+            } else {
+                p.A = w.dhid[l];
+                p.lda = L.out_features;
+            }
+            p.B = L.weight;  // [out, in] = [K, N]
+            p.ldb = L.in_features;
+            p.b_kn = 1;
+            p.M = (int)w.R;
+            p.N = L.in_features;
+            p.K = L.out_features;
+            p.epi = EPI_DGRAD_HIDDEN;
+            p.C = w.dhid[l - 1];
+            p.ldc = L.in_features;
+            p.aux0 = w.hid[l - 1];
+            p.ld_aux0 = L.in_features;
+            const float pdrop = t.dropout;
+            p.inv_keep = pdrop > 0.f ? 1.0f / (1.0f - pdrop) : 1.0f;
+            bb.add(p);
+        }
+        if ((rc = bb.run(s))) return rc;
+    }
+    // all weight gradients in one grouped launch
+    WgradBatch wb;
+    std::memset(&wb, 0, sizeof(wb));
+    for (int k = 0; k < ntowers; ++k) {
+        const ttamm_tower& t = *T[k];
+        TowerWs& w = *W[k];
+        if (t.fusion == TTAMM_FUSION_IDENTITY) continue;
+        if (t.fusion == TTAMM_FUSION_GATED) {
+            const int Hg = t.gate[0].out_features;
+            WgradProblem g2{};
+            g2.dY = w.dq;
+            g2.ld_dy = D;
+            g2.X = w.z;
+            g2.ld_x = Hg;
+            g2.R = (int)w.R;
+            g2.M = D;
+            g2.N = Hg;
+            g2.grad_w = w.ggw[1];
+            g2.grad_b = w.ggb[1];
+            g2.slab = w.slab[TTAMM_MAX_LINEAR + 1];
+            wb.p[wb.count++] = g2;
+            WgradProblem g1{};
+            g1.dY = w.dz;
+            g1.ld_dy = Hg;
+            g1.X = w.ef;
+            g1.ld_x = 2 * D;
+            g1.R = (int)w.R;
+            g1.M = Hg;
+            g1.N = 2 * D;
+            g1.grad_w = w.ggw[0];
+            g1.grad_b = w.ggb[0];
+            g1.slab = w.slab[TTAMM_MAX_LINEAR];
+            wb.p[wb.count++] = g1;
+        }
+        for (int l = t.n_linear - 1; l >= 0; --l) {
+            const ttamm_linear& L = t.linear[l];
+            WgradProblem p{};
+            if (l == t.n_linear - 1) {
+                p.dY = t.fusion == TTAMM_FUSION_GATED ? w.dEF + D : w.dT;
+                p.ld_dy = t.fusion == TTAMM_FUSION_GATED ? 2 * D : D;
+            } else {
+                p.dY = w.dhid[l];
+                p.ld_dy = L.out_features;
+            }
+            if (l == 0) {
+                p.X = t.features;
+                p.x_idx = w.fidx;
+                p.ld_x = t.feat_ld;
+            } else {
+                p.X = w.hid[l - 1];
+                p.ld_x = t.linear[l - 1].out_features;
+            }
+            p.R = (int)w.R;
+            p.M = L.out_features;
+            p.N = L.in_features;
+            p.grad_w = w.gw[l];
+            p.grad_b = w.gb[l];
+            p.slab = w.slab[l];
+            wb.p[wb.count++] = p;
+        }
+    }
+    if ((rc = launch_wgrad(wb, s))) return rc;
+    return TTAMM_OK;
+}
+
+int tower_optimizer_rows(const ttamm_tower& t, TowerWs& w, int D, int64_t B, bool mimic, const SparseConsts& sp,
+                         const AdamConsts& ad, bool is_item, hipStream_t s) {
+    int rc;
+    if ((rc = launch_coalesce(w.idx, w.R, t.id.rows, w.co, s))) return rc;
+    RowUpdateArgs ru;
+    std::memset(&ru, 0, sizeof(ru));
+    ru.n = w.R;
+    ru.dim = D;
+    ru.n_unique = w.co.n_unique;
+    ru.seg_start = w.co.seg_start;
+    ru.keys = w.co.keys_out;
+    ru.rows = w.co.vals_out;
+    if (t.fusion == TTAMM_FUSION_GATED) {
+        ru.dE = w.dEF;
+        ru.ld_dE = 2 * D;
+    } else {
+        ru.dE = w.dT;
+        ru.ld_dE = D;
+    }
+    ru.id = t.id;
+    if (mimic) {
+        ru.mimic = t.mimic;
+        ru.dA_lo = w.dA;
+        ru.dA_hi = w.dT;
+        ru.split_row = is_item ? B : w.R;
+    }
+    ru.side_id = w.side_id;
+    ru.side_mimic = w.side_mimic;
+    ru.sp = sp;
+    ru.ad = ad;
+    return launch_row_update(ru, s);
+}
+
+int run_step(const ttamm_step_args& A, hipStream_t s) {
+    const int D = A.user.id.dim;
+    int rc;
+    if ((rc = validate_tower(A.user, "user_encoder", D, true))) return rc;
+    if ((rc = validate_tower(A.item, "item_encoder", D, true))) return rc;
+    TTAMM_REQUIRE(A.b.batch > 0, "empty batch");
+    TTAMM_REQUIRE(A.b.num_neg > 0, "num_negatives must be greater than zero.");
+    TTAMM_REQUIRE(A.item.id.rows > 1, "num_items must be greater than one.");
+    const bool mimic = A.mimic_enabled != 0;
+    if (mimic) {
+        TTAMM_REQUIRE(A.user.mimic.weight && A.item.mimic.weight, "mimic tables missing");
+        TTAMM_REQUIRE(A.user.mimic.dim == D && A.item.mimic.dim == D &&
+                          A.user.mimic.rows == A.user.id.rows && A.item.mimic.rows == A.item.id.rows,
+                      "Adaptive mimic requires user and item embedding dimensions to match.");
+    }
+    TTAMM_REQUIRE(A.hp.dense_step >= 1 && A.hp.sparse_step >= 1, "optimizer step counts must be >= 1");
+
+    Arena ar{static_cast<char*>(A.workspace), A.workspace_bytes, 0, false};
+    StepWs ws;
+    plan(ar, A, ws);
+    TTAMM_REQUIRE(ar.ok(), "workspace too small for this step");
+
+    const int64_t B = A.b.batch;
+    const int N = A.b.num_neg;
+    // ---- indices ------------------------------------------------------------------------
+    ws.user.idx = ws.user.fidx = A.b.users;
+    ws.item.idx = ws.item.fidx = ws.item.idx_own;
+    TTAMM_HIP(hipMemcpyAsync(ws.item.idx_own, A.b.pos_items, B * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+    int64_t* neg = ws.item.idx_own + B;
+    if (A.b.sample_negatives) {
+        if ((rc = launch_sample_negatives(A.b.users, B, N, A.item.id.rows, A.b.pos_offsets, A.b.pos_values, A.b.seed,
+                                          A.b.counter, neg, A.status, s)))
+            return rc;
+        if (A.b.neg_items)
+            TTAMM_HIP(hipMemcpyAsync(A.b.neg_items, neg, B * N * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+    } else {
+        TTAMM_REQUIRE(A.b.neg_items != nullptr, "negatives must be given when sample_negatives == 0");
+        TTAMM_HIP(hipMemcpyAsync(neg, A.b.neg_items, B * N * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+    }
+
+    const ttamm_tower* T[2] = {&A.user, &A.item};
+    TowerWs* W[2] = {&ws.user, &ws.item};
+    // ---- forward ------------------------------------------------------------------------
+    if ((rc = tower_forward(T, W, A.b, D, mimic, s, 2))) return rc;
+    // ---- score + loss (fwd + bwd seeds) -----------------------------------------------
+    ScoreArgs sa;
+    std::memset(&sa, 0, sizeof(sa));
+    sa.B = B;
+    sa.N = N;
+    sa.D = D;
+    sa.user_aug = ws.user.aug;
+    sa.item_aug = ws.item.aug;
+    sa.t_user = ws.user.t;
+    sa.t_item = ws.item.t;
+    sa.a_user = ws.user.a;
+    sa.a_item = ws.item.a;
+    sa.lambda_u = (float)A.hp.lambda_mimic_user;
+    sa.lambda_i = (float)A.hp.lambda_mimic_item;
+    sa.mimic = mimic ? 1 : 0;
+    sa.dT_user = ws.user.dT;
+    sa.dT_item = ws.item.dT;
+    sa.dA_user = ws.user.dA;
+    sa.dA_pos = ws.item.dA;
+    sa.partials = ws.partials;
+    sa.blocks = ws.score_blocks;
+    if ((rc = launch_score_loss(sa, s))) return rc;
+    if (A.loss_out) {
+        if ((rc = launch_loss_finalize(ws.partials, ws.score_blocks, B, N, D, sa.lambda_u, sa.lambda_i, sa.mimic,
+                                       A.loss_out, A.loss_accum, s)))
+            return rc;
+    }
+    // ---- backward -----------------------------------------------------------------------
+    if ((rc = tower_backward(T, W, D, s, 2))) return rc;
+    // ---- optimizers ---------------------------------------------------------------------
+    const ttamm_hparams& hp = A.hp;
+    const AdamConsts ad = make_adam_consts(hp.lr, hp.beta1, hp.beta2, hp.eps, hp.weight_decay,
+                                           hp.decoupled_weight_decay, hp.dense_step);
+    const SparseConsts sp = make_sparse_consts(hp.sparse_lr, hp.sparse_beta1, hp.sparse_beta2, hp.sparse_eps,
+                                               hp.sparse_step);
+    if ((rc = tower_optimizer_rows(A.user, ws.user, D, B, mimic, sp, ad, false, s))) return rc;
+    if ((rc = tower_optimizer_rows(A.item, ws.item, D, B, mimic, sp, ad, true, s))) return rc;
+    SweepArgs sw;
+    std::memset(&sw, 0, sizeof(sw));
+    sw.ad = ad;
+    auto add_seg = [&](const ttamm_table& tb) {
+        sw.seg[sw.count].p = tb.weight;
+        sw.seg[sw.count].m = tb.exp_avg;
+        sw.seg[sw.count].v = tb.exp_avg_sq;
+        sw.seg[sw.count].n = tb.rows * tb.dim;
+        sw.count++;
+    };
+    if (mimic) {
+        add_seg(A.user.mimic);
+        add_seg(A.item.mimic);
+    }
+    if (A.user.id.optimizer == TTAMM_OPT_DENSE) add_seg(A.user.id);
+    if (A.item.id.optimizer == TTAMM_OPT_DENSE) add_seg(A.item.id);
+    if (A.timing_events[0]) TTAMM_HIP(hipEventRecord((hipEvent_t)A.timing_events[0], s));
+    if ((rc = launch_dense_sweep(sw, s))) return rc;
+    if (A.timing_events[1]) TTAMM_HIP(hipEventRecord((hipEvent_t)A.timing_events[1], s));
+    for (int k = 0; k < 2; ++k) {
+        const ttamm_tower& t = *T[k];
+        TowerWs& w = *W[k];
+        if (mimic)
+            if ((rc = launch_side_scatter(w.co.n_unique, w.co.keys_out, w.co.seg_start, w.side_mimic, w.R, D, t.mimic,
+                                          s)))
+                return rc;
+        if (t.id.optimizer == TTAMM_OPT_DENSE)
+            if ((rc = launch_side_scatter(w.co.n_unique, w.co.keys_out, w.co.seg_start, w.side_id, w.R, D, t.id, s)))
+                return rc;
+    }
+    DenseAdamArgs da;
+    std::memset(&da, 0, sizeof(da));
+    da.ad = ad;
+    auto add_dense = [&](float* p, float* m, float* v, const float* g, int64_t n) {
+        da.t[da.count++] = DenseTensor{p, m, v, g, n};
+    };
+    for (int k = 0; k < 2; ++k) {
+        const ttamm_tower& t = *T[k];
+        TowerWs& w = *W[k];
+        if (t.fusion == TTAMM_FUSION_IDENTITY) continue;
+        for (int l = 0; l < t.n_linear; ++l) {
+            const ttamm_linear& L = t.linear[l];
+            add_dense(L.weight, L.weight_exp_avg, L.weight_exp_avg_sq, w.gw[l], (int64_t)L.out_features * L.in_features);
+            add_dense(L.bias, L.bias_exp_avg, L.bias_exp_avg_sq, w.gb[l], L.out_features);
+        }
+        if (t.fusion == TTAMM_FUSION_GATED) {
+            for (int q = 0; q < 2; ++q) {
+                const ttamm_linear& L = t.gate[q];
+                add_dense(L.weight, L.weight_exp_avg, L.weight_exp_avg_sq, w.ggw[q],
+                          (int64_t)L.out_features * L.in_features);
+                add_dense(L.bias, L.bias_exp_avg, L.bias_exp_avg_sq, w.ggb[q], L.out_features);
+            }
+        }
+    }
+    if ((rc = launch_dense_adam(da, s))) return rc;
+    return TTAMM_OK;
+}
+
+}  // namespace
+
+size_t train_step_workspace_size(const ttamm_step_args& A) {
+    Arena ar{nullptr, 0, 0, true};
+    StepWs ws;
+    plan(ar, A, ws);
+    return ar.off + 256;
+}
+
+int train_step(const ttamm_step_args& A, hipStream_t s) { return run_step(A, s); }
+
+// ---- eval-mode tower forward (TowerEncoder.forward + augment) -----------------------------
+size_t tower_forward_workspace_size(const ttamm_tower& T, int64_t n) {
+    Arena ar{nullptr, 0, 0, true};
+    const int D = T.id.dim;
+    for (int l = 0; l + 1 < T.n_linear; ++l) ar.take<float>((size_t)n * T.linear[l].out_features);
+    ar.take<float>((size_t)n * 2 * D);  // ef / e
+    ar.take<float>((size_t)n * D);      // f
+    if (T.fusion == TTAMM_FUSION_GATED) ar.take<float>((size_t)n * T.gate[0].out_features);
+    for (int q = 0; q < 3; ++q) ar.take<float>((size_t)n * D);  // g, t, a
+    return ar.off + 256;
+}
+
+int tower_forward_eval(const ttamm_tower& T, const int64_t* idx, const int64_t* fidx, int64_t n, int augment,
+                       float* out, void* wsp, size_t ws_bytes, hipStream_t s) {
+    const int D = T.id.dim;
+    int rc;
+    if ((rc = validate_tower(T, "tower", D, false))) return rc;
+    if (n <= 0) return TTAMM_OK;
+    Arena ar{static_cast<char*>(wsp), ws_bytes, 0, false};
+    TowerWs w;
+    w.R = n;
+    w.idx = idx;
+    w.fidx = fidx;
+    for (int l = 0; l + 1 < T.n_linear; ++l) w.hid[l] = ar.take<float>((size_t)n * T.linear[l].out_features);
+    float* efbuf = ar.take<float>((size_t)n * 2 * D);
+    float* fbuf = ar.take<float>((size_t)n * D);
+    float* zbuf = T.fusion == TTAMM_FUSION_GATED ? ar.take<float>((size_t)n * T.gate[0].out_features) : nullptr;
+    float* gbuf = ar.take<float>((size_t)n * D);
+    float* tbuf = ar.take<float>((size_t)n * D);
+    float* abuf = ar.take<float>((size_t)n * D);
+    TTAMM_REQUIRE(ar.ok(), "workspace too small for tower forward");
+    if (T.fusion == TTAMM_FUSION_GATED) {
+        w.ef = efbuf;
+        w.z = zbuf;
+        w.g = gbuf;
+    } else {
+        w.e = efbuf;
+        w.f = fbuf;
+    }
+    w.t = tbuf;
+    w.a = abuf;
+    w.aug = out;
+    // eval mode: no dropout
+    ttamm_tower te = T;
+    te.dropout = 0.f;
+    ttamm_batch bt;
+    std::memset(&bt, 0, sizeof(bt));
+    const ttamm_tower* TT[2] = {&te, nullptr};
+    TowerWs* WW[2] = {&w, nullptr};
+    const bool mimic = augment && T.mimic.weight;
+    if ((rc = tower_forward(TT, WW, bt, D, mimic, s, 1))) return rc;
+    return TTAMM_OK;
+}
+
+}  // namespace ttamm

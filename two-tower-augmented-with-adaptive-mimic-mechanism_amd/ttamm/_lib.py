@@ -1,0 +1,210 @@
+"""ctypes binding of libttamm.so (the C ABI declared in include/ttamm.h).
+
+This is the only place Python talks to the native library.  Every product code path on a
+ROCm device goes through here; there is no CPU fallback — a missing library raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+from typing import Optional
+
+import torch
+
+TTAMM_OK = 0
+TTAMM_E_INVALID = 1
+TTAMM_E_RUNTIME = 2
+TTAMM_E_HIP = 3
+
+MAX_LINEAR = 4
+FUSION_IDENTITY, FUSION_SUM, FUSION_GATED = 0, 1, 2
+OPT_SPARSE_ADAM, OPT_DENSE = 0, 1
+STATUS_SAMPLER_EXHAUSTED = 1
+
+_NATIVE_DIR = Path(__file__).resolve().parent / "_native"
+LIB_PATH = _NATIVE_DIR / "libttamm.so"
+
+c_f = ctypes.c_float
+c_d = ctypes.c_double
+c_i32 = ctypes.c_int32
+c_i64 = ctypes.c_int64
+c_u64 = ctypes.c_uint64
+c_vp = ctypes.c_void_p
+
+
+class Linear(ctypes.Structure):
+    _fields_ = [
+        ("weight", c_vp),
+        ("bias", c_vp),
+        ("weight_exp_avg", c_vp),
+        ("weight_exp_avg_sq", c_vp),
+        ("bias_exp_avg", c_vp),
+        ("bias_exp_avg_sq", c_vp),
+        ("in_features", c_i32),
+        ("out_features", c_i32),
+    ]
+
+
+class Table(ctypes.Structure):
+    _fields_ = [
+        ("weight", c_vp),
+        ("exp_avg", c_vp),
+        ("exp_avg_sq", c_vp),
+        ("rows", c_i64),
+        ("dim", c_i32),
+        ("optimizer", c_i32),
+    ]
+
+
+class Tower(ctypes.Structure):
+    _fields_ = [
+        ("id", Table),
+        ("mimic", Table),
+        ("features", c_vp),
+        ("feat_ld", c_i64),
+        ("feat_dim", c_i32),
+        ("fusion", c_i32),
+        ("n_linear", c_i32),
+        ("dropout", c_f),
+        ("linear", Linear * MAX_LINEAR),
+        ("gate", Linear * 2),
+    ]
+
+
+class HParams(ctypes.Structure):
+    _fields_ = [
+        ("lr", c_d),
+        ("beta1", c_d),
+        ("beta2", c_d),
+        ("eps", c_d),
+        ("weight_decay", c_d),
+        ("decoupled_weight_decay", c_i32),
+        ("sparse_lr", c_d),
+        ("sparse_beta1", c_d),
+        ("sparse_beta2", c_d),
+        ("sparse_eps", c_d),
+        ("dense_step", c_i64),
+        ("sparse_step", c_i64),
+        ("lambda_mimic_user", c_d),
+        ("lambda_mimic_item", c_d),
+    ]
+
+
+class Batch(ctypes.Structure):
+    _fields_ = [
+        ("users", c_vp),
+        ("pos_items", c_vp),
+        ("neg_items", c_vp),
+        ("batch", c_i64),
+        ("num_neg", c_i32),
+        ("sample_negatives", c_i32),
+        ("pos_offsets", c_vp),
+        ("pos_values", c_vp),
+        ("seed", c_u64),
+        ("counter", c_u64),
+        ("user_keep_mask", c_vp * MAX_LINEAR),
+        ("item_keep_mask", c_vp * MAX_LINEAR),
+    ]
+
+
+class StepArgs(ctypes.Structure):
+    _fields_ = [
+        ("user", Tower),
+        ("item", Tower),
+        ("mimic_enabled", c_i32),
+        ("hp", HParams),
+        ("b", Batch),
+        ("loss_out", c_vp),
+        ("loss_accum", c_vp),
+        ("status", c_vp),
+        ("workspace", c_vp),
+        ("workspace_bytes", ctypes.c_size_t),
+        ("timing_events", c_vp * 2),
+    ]
+
+
+# Symbol table: name -> (restype, argtypes).  tests/ check every one is exported and that this
+# table covers every function declared in include/ttamm.h.
+SIGNATURES = {
+    "ttamm_abi_version": (ctypes.c_int, []),
+    "ttamm_last_error": (ctypes.c_char_p, []),
+    "ttamm_train_step_workspace_size": (ctypes.c_size_t, [ctypes.POINTER(StepArgs)]),
+    "ttamm_train_step": (ctypes.c_int, [ctypes.POINTER(StepArgs), c_vp]),
+    "ttamm_gather_rows": (ctypes.c_int, [c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "ttamm_tower_forward_workspace_size": (ctypes.c_size_t, [ctypes.POINTER(Tower), c_i64]),
+    "ttamm_tower_forward": (
+        ctypes.c_int,
+        [ctypes.POINTER(Tower), c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, ctypes.c_size_t, c_vp],
+    ),
+    "ttamm_mimic_augment": (ctypes.c_int, [c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    "ttamm_mse_loss": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "ttamm_sample_negatives": (
+        ctypes.c_int,
+        [c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp],
+    ),
+    "ttamm_sparse_adam_rows": (
+        ctypes.c_int,
+        [c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_i64, c_d, c_d, c_d, c_d, c_i64, c_vp],
+    ),
+    "ttamm_adamw_dense": (
+        ctypes.c_int,
+        [c_vp, c_vp, c_vp, c_vp, c_i64, c_d, c_d, c_d, c_d, c_d, c_i32, c_i64, c_vp],
+    ),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def library_path() -> Path:
+    override = os.environ.get("TTAMM_LIBRARY")
+    return Path(override) if override else LIB_PATH
+
+
+def load() -> ctypes.CDLL:
+    """Load libttamm.so.  Raises RuntimeError if it has not been built (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = library_path()
+    if not path.exists():
+        raise RuntimeError(
+            f"libttamm.so not found at {path}; build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(make -C two-tower-augmented-with-adaptive-mimic-mechanism_amd/csrc)"
+        )
+    lib = ctypes.CDLL(str(path))
+    for name, (restype, argtypes) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = restype
+        fn.argtypes = argtypes
+    _lib = lib
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc == TTAMM_OK:
+        return
+    msg = load().ttamm_last_error().decode("utf-8", "replace")
+    if rc == TTAMM_E_INVALID:
+        raise ValueError(msg)
+    raise RuntimeError(msg)
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device: torch.device | None = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_rocm(t: torch.Tensor, what: str) -> None:
+    """The product path runs only on a ROCm device; CPU tensors are rejected (no fallback)."""
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"{what}: ttamm executes on an MI355X (ROCm) device; got a tensor on '{t.device}'. "
+            "Move the model and inputs to the GPU."
+        )

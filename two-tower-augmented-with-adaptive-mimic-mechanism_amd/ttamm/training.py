@@ -1,0 +1,388 @@
+"""Training step — drop-in for the hot loop of ``src/pipelines/training.py``.
+
+``train_one_epoch`` has the signature and return value of the reference's
+``_train_one_epoch`` (training.py:700-833).  Each batch is one call of the native executor
+``ttamm_train_step`` (libttamm), which runs the whole step on the MI355X:
+
+    negatives (samplers.py:11-85) -> both towers (encoders.py:221-255) -> mimic augment and
+    stop-grad MSE (adaptive_mimic.py:40-68) -> dot-product scores, BCE (training.py:770-803)
+    -> backward -> AdamW over the dense group incl. the FULL mimic tables and SparseAdam over
+    the ID tables (training.py:1311-1350).
+
+The caller's torch optimizers stay the owners of the optimizer state: their ``state`` holds
+the same ``exp_avg`` / ``exp_avg_sq`` / ``step`` entries torch would create, updated in place
+by the kernels, so ``optimizer.state_dict()`` and checkpoints (training.py:150-182) keep
+their format.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Any, Iterable, Mapping, Sequence
+
+import torch
+from torch import nn
+
+from . import _lib
+from .encoders import TowerEncoder, describe_tower, feature_layers
+from .samplers import PositivesCSR, draw_seed, positives_csr
+from .two_tower import TwoTowerModel
+
+
+class DotProductSimilarity(nn.Module):
+    """<u, v> over the last dim (training.py:53-59)."""
+
+    def forward(self, user_embedding: torch.Tensor, item_embedding: torch.Tensor) -> torch.Tensor:
+        return (user_embedding * item_embedding).sum(dim=-1)
+
+
+def _collect_parameter_groups(model: TwoTowerModel) -> tuple[list[nn.Parameter], list[nn.Parameter]]:
+    """(dense, sparse) parameter lists in the reference's order (training.py:276-309):
+    each tower's ID table first (sparse group if ``sparse=True``), then the tower's other
+    parameters, then every remaining model parameter (the mimic tables) — dense."""
+    dense: list[nn.Parameter] = []
+    sparse: list[nn.Parameter] = []
+    seen: set[int] = set()
+
+    def put(p: nn.Parameter, bucket: list[nn.Parameter]) -> None:
+        if id(p) not in seen:
+            seen.add(id(p))
+            bucket.append(p)
+
+    for tower in (model.user_encoder, model.item_encoder):
+        emb = getattr(tower, "embedding", None)
+        if isinstance(emb, nn.Embedding):
+            put(emb.weight, sparse if getattr(emb, "sparse", False) else dense)
+        for name, p in tower.named_parameters():
+            if name != "embedding.weight":
+                put(p, dense)
+    for p in model.parameters():
+        put(p, dense)
+    return dense, sparse
+
+
+# ---------------------------------------------------------------------------------------
+# optimizer state, torch-compatible
+# ---------------------------------------------------------------------------------------
+def _adam_state(opt: torch.optim.Optimizer, p: torch.Tensor) -> dict:
+    st = opt.state[p]
+    if len(st) == 0:  # torch/optim/adam.py _init_group
+        st["step"] = torch.tensor(0.0, dtype=torch.float32)
+        st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+    return st
+
+
+def _sparse_adam_state(opt: torch.optim.Optimizer, p: torch.Tensor) -> dict:
+    st = opt.state[p]
+    if len(st) == 0:  # torch/optim/sparse_adam.py step()
+        st["step"] = 0
+        st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+    return st
+
+
+def _single_group(opt: torch.optim.Optimizer) -> dict:
+    if len(opt.param_groups) != 1:
+        raise NotImplementedError("ttamm: one parameter group per optimizer (as training.py:1311-1350 builds)")
+    return opt.param_groups[0]
+
+
+def _pad_features(features: torch.Tensor | None) -> torch.Tensor | None:
+    """Feature rows with a 16-byte aligned row stride (zero-padded columns).  A view of an
+    already padded matrix (stride(0) % 4 == 0) is used as is."""
+    if features is None or features.numel() == 0:
+        return None
+    if features.dtype != torch.float32:
+        raise ValueError("ttamm: feature matrices must be float32")
+    _lib.require_rocm(features, "feature matrix")
+    if features.stride(-1) == 1 and features.stride(0) % 4 == 0 and features.data_ptr() % 16 == 0:
+        return features
+    rows, width = features.shape
+    padded = torch.zeros((rows, (width + 3) // 4 * 4), dtype=torch.float32, device=features.device)
+    padded[:, :width].copy_(features)
+    return padded[:, :width]
+
+
+class FusedTrainStep:
+    """Owns the native step descriptor and workspace for one (model, optimizers) pair."""
+
+    def __init__(
+        self,
+        model: TwoTowerModel,
+        optimizers: Sequence[torch.optim.Optimizer],
+        *,
+        negatives_per_positive: int,
+        positives: Mapping[int, set[int]] | PositivesCSR | None,
+        user_features: torch.Tensor | None,
+        item_features: torch.Tensor | None,
+        loss_weights: Mapping[str, Any] | None = None,
+        max_batch: int,
+        seed: int | None = None,
+    ) -> None:
+        if negatives_per_positive <= 0:
+            raise ValueError("num_negatives must be greater than zero.")
+        self.model = model
+        self.num_neg = int(negatives_per_positive)
+        ue, ie = model.user_encoder, model.item_encoder
+        if not isinstance(ue, TowerEncoder) or not isinstance(ie, TowerEncoder):
+            raise NotImplementedError("ttamm: towers must be ttamm.encoders.TowerEncoder")
+        self.device = ue.embedding.weight.device
+        _lib.require_rocm(ue.embedding.weight, "FusedTrainStep")
+        if ie.num_embeddings <= 1:
+            raise ValueError("num_items must be greater than one.")
+        mimic = getattr(model, "adaptive_mimic", None)
+        self.mimic = mimic
+        if mimic is not None and (ue.output_dim != ie.output_dim):
+            raise ValueError("Adaptive mimic requires user and item embedding dimensions to match.")
+
+        # ---- optimizers ---------------------------------------------------------------
+        dense_opt = sparse_opt = None
+        for opt in optimizers:
+            if isinstance(opt, torch.optim.SparseAdam):
+                sparse_opt = opt
+            elif isinstance(opt, (torch.optim.AdamW, torch.optim.Adam)):
+                dense_opt = opt
+            else:
+                raise NotImplementedError(f"ttamm: optimizer {type(opt).__name__} is not implemented (Adam/AdamW + SparseAdam)")
+        self.dense_opt, self.sparse_opt = dense_opt, sparse_opt
+        dense_ids = {id(p) for g in (dense_opt.param_groups if dense_opt else []) for p in g["params"]}
+        sparse_ids = {id(p) for g in (sparse_opt.param_groups if sparse_opt else []) for p in g["params"]}
+        if dense_opt is not None:
+            g = _single_group(dense_opt)
+            if g.get("amsgrad") or g.get("maximize"):
+                raise NotImplementedError("ttamm: amsgrad / maximize are not implemented")
+            self.decoupled = isinstance(dense_opt, torch.optim.AdamW) or bool(g.get("decoupled_weight_decay", False))
+        if sparse_opt is not None and _single_group(sparse_opt).get("maximize"):
+            raise NotImplementedError("ttamm: maximize is not implemented")
+
+        self.features = {"user": _pad_features(user_features), "item": _pad_features(item_features)}
+        state: dict[int, dict] = {}
+        handled: set[int] = set()
+        self._adam_steps: list[dict] = []
+        self._sparse_steps: list[dict] = []
+
+        def dense_param(p: torch.Tensor) -> None:
+            if id(p) not in dense_ids:
+                raise ValueError("ttamm: a trained parameter is missing from the dense optimizer")
+            st = _adam_state(dense_opt, p)
+            state[id(p)] = st
+            self._adam_steps.append(st)
+            handled.add(id(p))
+
+        self.towers = {}
+        for name, tower in (("user", ue), ("item", ie)):
+            emb = tower.embedding.weight
+            if id(emb) in sparse_ids:
+                st = _sparse_adam_state(sparse_opt, emb)
+                state[id(emb)] = st
+                self._sparse_steps.append(st)
+                handled.add(id(emb))
+                id_opt = _lib.OPT_SPARSE_ADAM
+            else:
+                dense_param(emb)
+                id_opt = _lib.OPT_DENSE
+            feats = self.features[name]
+            uses_features = tower.fusion != "identity" and feats is not None
+            if uses_features:
+                linears, _ = feature_layers(tower)
+                for layer in linears:
+                    dense_param(layer.weight)
+                    dense_param(layer.bias)
+                if tower.fusion == "gated":
+                    for i in (0, 2):
+                        dense_param(tower.adaptive_mimic.gate_network[i].weight)
+                        dense_param(tower.adaptive_mimic.gate_network[i].bias)
+            self.towers[name] = (tower, feats if uses_features else None, id_opt)
+        self.mimic_tables = {}
+        if mimic is not None:
+            for name, table in (("user", mimic.user_augmented.weight), ("item", mimic.item_augmented.weight)):
+                dense_param(table)
+                self.mimic_tables[name] = table
+        unhandled = [i for i in dense_ids | sparse_ids if i not in handled]
+        if unhandled:
+            raise NotImplementedError(
+                "ttamm: the optimizers hold parameters outside the fused step (e.g. concat projection)"
+            )
+        self.state = state
+
+        # ---- descriptor ---------------------------------------------------------------
+        args = _lib.StepArgs()
+        for name in ("user", "item"):
+            tower, feats, id_opt = self.towers[name]
+            desc = describe_tower(
+                tower if feats is not None else _IdentityView(tower),
+                features=feats,
+                mimic_table=self.mimic_tables.get(name),
+                state=state,
+                id_optimizer=id_opt,
+            )
+            setattr(args, name, desc)
+        args.mimic_enabled = 1 if mimic is not None else 0
+        lw = dict(loss_weights or {})
+        args.hp.lambda_mimic_user = float(lw.get("mimic_user", 0.0))
+        args.hp.lambda_mimic_item = float(lw.get("mimic_item", 0.0))
+        args.b.num_neg = self.num_neg
+        self.csr = None
+        if positives is not None:
+            self.csr = positives_csr(positives, device=self.device, num_users=ue.num_embeddings)
+            if self.csr.max_degree >= ie.num_embeddings:
+                raise RuntimeError("a user interacted with all items; cannot sample negatives.")
+            args.b.pos_offsets = self.csr.offsets.data_ptr()
+            args.b.pos_values = self.csr.values.data_ptr()
+        args.b.seed = draw_seed() if seed is None else int(seed)
+        self.loss_out = torch.zeros(4, dtype=torch.float32, device=self.device)
+        self.loss_accum = torch.zeros(2, dtype=torch.float64, device=self.device)
+        self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        args.loss_out = self.loss_out.data_ptr()
+        args.loss_accum = self.loss_accum.data_ptr()
+        args.status = self.status.data_ptr()
+        self.max_batch = int(max_batch)
+        args.b.batch = self.max_batch
+        self.lib = _lib.load()
+        self.ws_bytes = int(self.lib.ttamm_train_step_workspace_size(ctypes.byref(args)))
+        self.workspace = torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
+        args.workspace = self.workspace.data_ptr()
+        args.workspace_bytes = self.ws_bytes
+        self.neg_buffer = torch.empty(self.max_batch * self.num_neg, dtype=torch.long, device=self.device)
+        self.args = args
+        self.steps_done = 0
+        self.dense_step0 = int(self._adam_steps[0]["step"].item()) if self._adam_steps else 0
+        self.sparse_step0 = int(self._sparse_steps[0]["step"]) if self._sparse_steps else 0
+
+    # ------------------------------------------------------------------------------------
+    def _hparams(self) -> None:
+        hp = self.args.hp
+        if self.dense_opt is not None:
+            g = self.dense_opt.param_groups[0]
+            hp.lr = float(g["lr"])
+            hp.beta1, hp.beta2 = (float(b) for b in g["betas"])
+            hp.eps = float(g["eps"])
+            hp.weight_decay = float(g["weight_decay"])
+            hp.decoupled_weight_decay = 1 if self.decoupled else 0
+        if self.sparse_opt is not None:
+            g = self.sparse_opt.param_groups[0]
+            hp.sparse_lr = float(g["lr"])
+            hp.sparse_beta1, hp.sparse_beta2 = (float(b) for b in g["betas"])
+            hp.sparse_eps = float(g["eps"])
+        hp.dense_step = self.dense_step0 + self.steps_done + 1
+        hp.sparse_step = self.sparse_step0 + self.steps_done + 1
+
+    def step(
+        self,
+        users: torch.Tensor,
+        pos_items: torch.Tensor,
+        neg_items: torch.Tensor | None = None,
+        *,
+        keep_masks: Mapping[str, Sequence[torch.Tensor]] | None = None,
+        timing_events: tuple[Any, Any] | None = None,
+    ) -> None:
+        """Enqueue one training step on the current stream (no host synchronisation)."""
+        B = users.numel()
+        if B == 0:
+            return
+        if B > self.max_batch:
+            raise ValueError("ttamm: batch larger than the step was sized for")
+        if users.dtype != torch.long or pos_items.dtype != torch.long:
+            raise ValueError("Adaptive mimic indices must be torch.long tensors.")
+        _lib.require_rocm(users, "train step")
+        a = self.args
+        a.b.users = users.data_ptr()
+        a.b.pos_items = pos_items.data_ptr()
+        a.b.batch = B
+        if neg_items is not None:
+            if neg_items.numel() != B * self.num_neg or neg_items.dtype != torch.long:
+                raise ValueError("ttamm: negatives must be int64 [batch, negatives_per_positive]")
+            a.b.neg_items = neg_items.data_ptr()
+            a.b.sample_negatives = 0
+        else:
+            if self.csr is None:
+                raise ValueError("ttamm: positives are required to sample negatives")
+            a.b.neg_items = self.neg_buffer.data_ptr()
+            a.b.sample_negatives = 1
+        a.b.counter = self.steps_done
+        for side, field in (("user", a.b.user_keep_mask), ("item", a.b.item_keep_mask)):
+            masks = (keep_masks or {}).get(side) or []
+            for i in range(_lib.MAX_LINEAR):
+                field[i] = masks[i].data_ptr() if i < len(masks) and masks[i] is not None else None
+        a.timing_events[0] = timing_events[0] if timing_events else None
+        a.timing_events[1] = timing_events[1] if timing_events else None
+        self._hparams()
+        _lib.check(self.lib.ttamm_train_step(ctypes.byref(a), _lib.stream_handle(self.device)))
+        self.steps_done += 1
+
+    def finish(self) -> float:
+        """Synchronise, surface device-side errors, write the optimizer step counters back,
+        and return the epoch's mean loss weighted by positives (training.py:829-833)."""
+        torch.cuda.current_stream(self.device).synchronize()
+        if int(self.status.item()) & _lib.STATUS_SAMPLER_EXHAUSTED:
+            raise RuntimeError("Exceeded resampling attempts while drawing negatives.")
+        for st in self._adam_steps:
+            st["step"].fill_(float(self.dense_step0 + self.steps_done))
+        for st in self._sparse_steps:
+            st["step"] = self.sparse_step0 + self.steps_done
+        total, count = self.loss_accum.tolist()
+        return total / max(count, 1.0)
+
+    def last_losses(self) -> dict[str, float]:
+        v = self.loss_out.tolist()
+        return {"total": v[0], "bce": v[1], "mimic_user": v[2], "mimic_item": v[3]}
+
+
+class _IdentityView(nn.Module):
+    """A tower seen without its feature path (features absent: encoders.py:228-231)."""
+
+    def __init__(self, tower: TowerEncoder) -> None:
+        super().__init__()
+        object.__setattr__(self, "_t", tower)
+        self.fusion = "identity"
+        self.feature_encoder = None
+        self.embedding = tower.embedding
+
+
+def train_one_epoch(
+    model: TwoTowerModel,
+    dataloader: Iterable,
+    *,
+    optimizers: list[torch.optim.Optimizer],
+    criterion: nn.BCEWithLogitsLoss,
+    negatives_per_positive: int,
+    num_items: int,
+    user_positive_items: Mapping[int, set[int]],
+    user_features: torch.Tensor | None,
+    item_features: torch.Tensor | None,
+    device: torch.device,
+    gradient_clip_norm: float | None = None,
+    loss_weights: Mapping[str, Any] | None = None,
+    item_category_tensor: torch.Tensor | None = None,
+    major_category_id: int | None = None,
+) -> float:
+    """Drop-in for ``_train_one_epoch`` (training.py:700-833) executed on the MI355X."""
+    model.train()
+    if not isinstance(criterion, nn.BCEWithLogitsLoss) or criterion.reduction != "mean" or \
+            criterion.weight is not None or criterion.pos_weight is not None:
+        raise NotImplementedError("ttamm: the step implements BCEWithLogitsLoss(reduction='mean')")
+    if gradient_clip_norm is not None and gradient_clip_norm > 0:
+        raise NotImplementedError("ttamm: gradient clipping is not implemented in the fused step")
+    lw = dict(loss_weights or {})
+    if float(lw.get("category_alignment", 0.0)) > 0 and item_category_tensor is not None and major_category_id is not None:
+        raise NotImplementedError("ttamm: the category-alignment loss (training.py:530-579) is not implemented yet")
+    if num_items != model.item_encoder.num_embeddings:
+        raise ValueError("num_items does not match the item embedding table")
+    device = torch.device(device)
+    batches = iter(dataloader)
+    engine = None
+    for users, pos in batches:
+        users = users.to(device, non_blocking=True).reshape(-1)
+        pos = pos.to(device, non_blocking=True).reshape(-1)
+        if engine is None:
+            size = getattr(dataloader, "batch_size", None) or users.numel()
+            engine = FusedTrainStep(
+                model, optimizers, negatives_per_positive=negatives_per_positive, positives=user_positive_items,
+                user_features=user_features, item_features=item_features, loss_weights=lw,
+                max_batch=max(int(size), users.numel()),
+            )
+        engine.step(users, pos)  # stream-ordered: the caching allocator recycles inputs safely
+    if engine is None:
+        return 0.0
+    return engine.finish()
