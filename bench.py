@@ -1,0 +1,313 @@
+#!/usr/bin/env python3
+"""Throughput benchmark of the fused two-tower training step on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1]
+
+Workload (BASELINE.json configs[1], "C2"): 2M items x 200K users, 96-dim towers, feature
+MLP 605 -> 192 -> 96 (ReLU, dropout 0.15), gated fusion, adaptive mimic on, batch 8192,
+5 sampled negatives per positive (the reference's semantics), AdamW
+(lr 1e-3, wd 0.01) over the dense group incl. the full mimic tables + SparseAdam over the
+ID tables.  Synthetic data of that shape, random-init weights; inputs resident in HBM.
+
+One step = one call of ttamm_train_step on one batch (sampling, forward, loss, backward,
+both optimizers).  `value` = interactions (positives) per second over all ranks.
+Multi-GPU: one process per GPU (torch.distributed.run), every rank runs its own batch.
+
+The JSON line also carries
+  roofline:     the dominant kernel (the AdamW(g=0) sweep over the mimic tables) timed with
+                HIP events on the step's stream; algorithmic bytes 24 * (U+I) * D per launch.
+  cpu_baseline: the CPU oracle (oracle/cpu_reference.py, the reference's step restated on
+                PyTorch-CPU incl. its per-row sampler loop) timed on this host, rank 0, N=1.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "two-tower-augmented-with-adaptive-mimic-mechanism_amd"))
+sys.path.insert(0, str(ROOT))
+
+import torch  # noqa: E402
+
+METRIC = "training interactions/sec at 1/2/4/8 MI355X; Recall@20 parity vs CPU ref"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+CONFIGS = {
+    "c2": dict(U=200_000, I=2_000_000, D=96, H=192, F=605, B=8192, N=5, dropout=0.15, pos_per_user=20),
+    # small sanity config (not a bench line)
+    "tiny": dict(U=2_000, I=20_000, D=96, H=192, F=605, B=1024, N=5, dropout=0.15, pos_per_user=20),
+}
+
+
+def tower_cfg(c: dict) -> dict:
+    return {
+        "type": "tower",
+        "id_embedding": {"params": {"embedding_dim": c["D"], "sparse": True}, "init": {"type": "normal", "std": 0.02}},
+        "feature_encoder": {"type": "mlp", "hidden_dims": [c["H"]], "activation": "relu", "output_dim": c["D"],
+                            "dropout": c["dropout"]},
+        "fusion": "gated",
+        "output_dim": c["D"],
+    }
+
+
+# ---------------------------------------------------------------------------------------
+# synthetic data (SURVEY.md §8 d), generated on the device
+# ---------------------------------------------------------------------------------------
+def make_item_features(I: int, F: int, device, gen: torch.Generator) -> torch.Tensor:
+    """[I, F] inside a [I, round_up(F, 4)] zero-padded buffer: 3 category weights {1, .5, .333}
+    in cols 0-299, one author one-hot in cols 300-599, 5 N(0,1) numeric/text z-scores."""
+    Fp = (F + 3) // 4 * 4
+    x = torch.zeros((I, Fp), dtype=torch.float32, device=device)
+    ncat = min(300, F - 5)
+    nauth = min(300, F - 5 - ncat)
+    rows = torch.arange(I, device=device)
+    for w in (1.0, 0.5, 1.0 / 3.0):
+        cols = torch.randint(0, ncat, (I,), device=device, generator=gen)
+        x[rows, cols] = torch.maximum(x[rows, cols], torch.tensor(w, device=device))
+    if nauth > 0:
+        x[rows, ncat + torch.randint(0, nauth, (I,), device=device, generator=gen)] = 1.0
+    x[:, ncat + nauth:F] = torch.randn((I, F - ncat - nauth), device=device, generator=gen)
+    return x[:, :F]
+
+
+def zipf_items(n: int, I: int, s: float, device, gen: torch.Generator, perm: torch.Tensor) -> torch.Tensor:
+    ranks = torch.arange(1, I + 1, device=device, dtype=torch.float64)
+    cdf = torch.cumsum(ranks.pow(-s), 0)
+    cdf /= cdf[-1].clone()
+    u = torch.rand(n, device=device, dtype=torch.float64, generator=gen)
+    r = torch.searchsorted(cdf, u).clamp_(max=I - 1)
+    return perm[r]
+
+
+class Workload:
+    def __init__(self, c: dict, device, seed: int):
+        import ttamm
+        from ttamm.samplers import PositivesCSR
+
+        self.c = c
+        gen = torch.Generator(device=device).manual_seed(seed)
+        torch.manual_seed(seed)
+        U, I, F = c["U"], c["I"], c["F"]
+        self.item_features = make_item_features(I, F, device, gen)
+        perm = torch.randperm(I, device=device, generator=gen)
+        per = c["pos_per_user"]
+        items = zipf_items(U * per, I, 1.05, device, gen, perm).view(U, per)
+        items, _ = torch.sort(items, dim=1)
+        offsets = torch.arange(0, U * per + 1, per, device=device, dtype=torch.long)
+        self.csr = PositivesCSR(offsets, items.reshape(-1).contiguous(), U, per)
+        # user features: mean of the user's positives (features.py:269-315)
+        Fp = self.item_features.stride(0)
+        uf = torch.zeros((U, Fp), dtype=torch.float32, device=device)
+        full = self.item_features.as_strided((I, Fp), (Fp, 1))
+        for lo in range(0, U, 16384):
+            hi = min(U, lo + 16384)
+            uf[lo:hi] = full[items[lo:hi].reshape(-1)].view(hi - lo, per, Fp).mean(dim=1)
+        self.user_features = uf[:, :F]
+        # interactions: every (user, positive) pair, shuffled once (DataLoader shuffle=True)
+        self.users_all = torch.arange(U, device=device).repeat_interleave(per)
+        self.items_all = items.reshape(-1)
+        order = torch.randperm(U * per, device=device, generator=gen)
+        self.users_all = self.users_all[order].contiguous()
+        self.items_all = self.items_all[order].contiguous()
+        # model + optimizers (training.py:1266-1350)
+        cfg = tower_cfg(c)
+        ue = ttamm.build_tower_encoder(cfg, num_embeddings=U, feature_dim=F, device=device)
+        ie = ttamm.build_tower_encoder(cfg, num_embeddings=I, feature_dim=F, device=device)
+        mm = ttamm.AdaptiveMimicMechanism(num_users=U, num_items=I, embedding_dim=c["D"]).to(device)
+        self.model = ttamm.TwoTowerModel(ue, ie, similarity=ttamm.DotProductSimilarity(), adaptive_mimic=mm)
+        dense, sparse = ttamm._collect_parameter_groups(self.model)
+        self.opts = [torch.optim.AdamW(dense, lr=1e-3, weight_decay=0.01), torch.optim.SparseAdam(sparse, lr=1e-3)]
+        self.engine = ttamm.FusedTrainStep(
+            self.model, self.opts, negatives_per_positive=c["N"], positives=self.csr,
+            user_features=self.user_features, item_features=self.item_features,
+            loss_weights={"mimic_user": 0.15, "mimic_item": 0.15}, max_batch=c["B"], seed=seed,
+        )
+        self.cursor = 0
+
+    def batch(self):
+        B = self.c["B"]
+        n = self.users_all.numel()
+        if self.cursor + B > n:
+            self.cursor = 0
+        sl = slice(self.cursor, self.cursor + B)
+        self.cursor += B
+        return self.users_all[sl], self.items_all[sl]
+
+
+# ---------------------------------------------------------------------------------------
+# CPU baseline: the oracle's restatement of the reference step on this host
+# ---------------------------------------------------------------------------------------
+def cpu_baseline(c: dict, steps: int, warmup: int, seed: int) -> dict:
+    from oracle import cpu_reference as ref
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    gen = torch.Generator().manual_seed(seed)
+    torch.manual_seed(seed)
+    U, I, F, B, N = c["U"], c["I"], c["F"], c["B"], c["N"]
+    item_features = make_item_features(I, F, "cpu", gen).contiguous()
+    per = c["pos_per_user"]
+    perm = torch.randperm(I, generator=gen)
+    items = zipf_items(U * per, I, 1.05, "cpu", gen, perm).view(U, per)
+    user_features = item_features[items[:, 0]]  # cheap stand-in of the same shape (values do not change the work)
+    tcfg = tower_cfg(c)
+    tcfg = {**tcfg, "adaptive_mimic": {}}
+    model = ref.build_model(tcfg, num_users=U, num_items=I, user_feature_dim=F, item_feature_dim=F, mimic=True)
+    opts = ref.build_optimizers(model, lr=1e-3, weight_decay=0.01)
+    # positives as the reference holds them: dict[user] -> set(items) (preprocessing.py:151-154)
+    need_users = torch.randint(0, U, ((steps + warmup) * B,), generator=gen)
+    positives = {int(u): set(items[int(u)].tolist()) for u in need_users.unique().tolist()}
+    batches = []
+    for k in range(steps + warmup):
+        us = need_users[k * B:(k + 1) * B]
+        ps = items[us, torch.randint(0, per, (B,), generator=gen)]
+        batches.append((us, ps))
+    lw = {"mimic_user": 0.15, "mimic_item": 0.15}
+    ref.train_one_epoch(model, batches[:warmup], opts, negatives_per_positive=N, num_items=I, positives=positives,
+                        user_features=user_features, item_features=item_features, loss_weights=lw)
+    _, seen, secs = ref.train_one_epoch(model, batches[warmup:], opts, negatives_per_positive=N, num_items=I,
+                                        positives=positives, user_features=user_features,
+                                        item_features=item_features, loss_weights=lw)
+    return {
+        "value": round(seen / secs, 1),
+        "unit": "interactions/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{steps} timed steps (+{warmup} warm-up) of the C2-shaped step, batch {B}, on "
+                  f"{threads} host threads: oracle/cpu_reference.py (reference per-row sampler, AdamW over the "
+                  f"full {U}x{c['D']} + {I}x{c['D']} mimic tables, SparseAdam)",
+    }
+
+
+def load_traffic(config: str) -> float | None:
+    """HBM bytes per sweep launch from the committed rocprofv3 PMC pass (profiles/)."""
+    path = ROOT / "profiles" / "pmc_traffic.json"
+    try:
+        data = json.loads(path.read_text())
+        return data.get(config, {}).get("dense_sweep_kernel_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--cpu-steps", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist_mod
+
+        dist = dist_mod
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    c = CONFIGS[args.config]
+
+    from ttamm import _lib
+
+    w = Workload(c, device, args.seed + rank)
+    eng = w.engine
+    for _ in range(args.warmup):
+        u, p = w.batch()
+        eng.step(u, p)
+    torch.cuda.synchronize()
+
+    # per-step HIP events around the dominant kernel, on the step's stream
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for a, b in evs:  # materialise the hipEvent_t handles
+        a.record()
+        b.record()
+    torch.cuda.synchronize()
+    batches = [w.batch() for _ in range(args.steps)]
+
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        u, p = batches[k]
+        eng.step(u, p, timing_events=(evs[k][0].cuda_event, evs[k][1].cuda_event))
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss = eng.finish()
+    sweep_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+
+    B, U, I, D = c["B"], c["U"], c["I"], c["D"]
+    interactions = args.steps * B * world
+    value = interactions / elapsed
+    sweep_bytes = 24 * (U + I) * D
+    achieved = sweep_bytes / (sweep_ms * 1e-3) / 1e9
+    traffic = load_traffic(args.config)
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "interactions/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic: C2 shapes, Zipf(1.05) positives (20/user), features shaped like features.py, "
+                "random-init weights",
+        "config": {
+            "workload": f"{args.config.upper()}: {I} items x {U} users, D={D}, MLP {c['F']}->{c['H']}->{D} "
+                        f"(ReLU, dropout {c['dropout']}), gated fusion, adaptive mimic, B={B}, "
+                        f"N={c['N']} sampled negatives, AdamW + SparseAdam",
+            "global_batch": B * world,
+            "negatives_per_positive": c["N"],
+            "parallelism": f"dp{world}" if world > 1 else "single",
+        },
+        "final_loss": round(loss, 6),
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "dense_sweep_kernel (AdamW g=0 over user+item mimic tables)",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": sweep_bytes,
+            "avg_launch_ms": round(sweep_ms, 4),
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(c, args.cpu_steps, 1, args.seed)
+        except Exception as exc:  # reported, not fatal to the GPU measurement
+            out["cpu_baseline"] = {"error": repr(exc)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

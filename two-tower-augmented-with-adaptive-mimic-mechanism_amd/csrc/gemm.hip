@@ -1,19 +1,30 @@
-// fp32 MFMA GEMMs for the tower MLP and fusion gate (gfx950).
+// fp32 MFMA GEMMs of the tower MLP and fusion gate (gfx950).
 //
-// Forward / data-gradient kernel:  C[M,N] = epilogue( A[M,K] . op(B) )
-//   - A rows may be gathered by an int64 index (feature rows by user/item id,
-//     training.py:741-747,775) so the gathered [rows, F] matrix is never materialised.
-//   - B is either an nn.Linear weight [N,K] (forward, y = x W^T) or [K,N] (dgrad, dX = dY W).
-//   - Epilogues fuse bias, ReLU, Dropout, Sigmoid gate mixing and the adaptive-mimic
-//     augmentation (encoders.py:126-168, adaptive_mimic.py:88-95).
-// Weight-gradient kernel:  dW[m,n] = sum_r dY[r,m] X[r,n], split over row chunks, with the
-//   bias gradient riding along as an implicit all-ones column n == N; partial slabs are
-//   summed in a fixed order (deterministic).
+//   C[M,N] = epilogue( sum_k A(m,k) * B(k,n) )
 //
-// Matrix core: v_mfma_f32_32x32x2_f32 (exact fp32, one fma per product).  Each lane of a
-// wave supplies one A and one B value per instruction; lane half h = lane>>5 owns k-slot h.
-// Within a 16-deep k-tile, lane half h walks k = 8h .. 8h+7, so its A/B fragments for four
-// consecutive MFMAs are one contiguous float4 in LDS (ds_read_b128).
+// Operands are staged HBM -> registers -> LDS (double buffered, one barrier per k-tile) in the
+// orientation they have in memory:
+//   MN-major  ([m][k] rows, k contiguous: an activation row or an nn.Linear weight row) —
+//             LDS [mn][BK+4]; a lane reads its 4 next k values with one ds_read_b128.
+//   K-major   ([k][m] rows, m contiguous: dgrad's weight, and both operands of the weight
+//             gradient where k runs over batch rows) — LDS [BK][mn]; one ds_read_b32 per k.
+// The operand whose memory rows are indexed by m (forward A) or by k (weight-gradient A)
+// may be gathered through an int64 index, so gathered feature rows
+// (training.py:741-747,775) are never materialised.
+//
+// Matrix core: v_mfma_f32_32x32x2_f32 (exact fp32: one rounding per product, like an fma
+// chain).  Lane half h = lane>>5 owns k-slot h; inside a BK = 16 tile it walks k = 8h..8h+7.
+//
+// Epilogue: the accumulators go through LDS (in row slices) and 256 threads apply the fused
+// elementwise tail with float4 loads/stores: bias, ReLU, dropout (encoders.py:132-138),
+// ReLU', sigmoid gate mix + adaptive-mimic augment (encoders.py:164-168,
+// adaptive_mimic.py:88-95), gate-mix backward.
+//
+// Weight gradients: dW^T[n_in, m_out] = X^T . dY, split over row chunks, written to fp32
+// slabs and summed in a fixed order by wgrad_reduce_kernel; the bias gradient rides along as
+// an implicit all-ones column of X.
+#include <cstring>
+
 #include "kernels.h"
 
 namespace ttamm {
@@ -22,221 +33,261 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
-// Kernel-argument (constant address space) view of a struct.
+// Kernel-argument (constant address space) view of a struct: indexing the by-value problem
+// table with a block-uniform index then compiles to scalar loads instead of a scratch copy.
 #define KArg(T) __attribute__((address_space(4))) T
 
 constexpr int BK = 16;
-constexpr int SK = BK + 4;  // LDS row stride (floats): 80 B rows keep ds_read_b128 conflict-free
+constexpr int SK = BK + 4;  // MN-major LDS row stride (floats): keeps ds_read_b128 conflict-free
 constexpr int kThreads = 256;
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
-
-__device__ __forceinline__ bool aligned16(const void* p) {
-    return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+__device__ __forceinline__ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+__device__ __forceinline__ float f4get(const float4& v, int q) {
+    return q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
 }
 
-// Load 4 consecutive k elements of row `rp` starting at k (masked by K).
-__device__ __forceinline__ float4 load4_k(const float* rp, int k, int K, bool vec) {
-    if (rp == nullptr) return make_float4(0.f, 0.f, 0.f, 0.f);
-    if (vec && k + 3 < K) return *reinterpret_cast<const float4*>(rp + k);
-    float4 v;
-    v.x = (k + 0 < K) ? rp[k + 0] : 0.f;
-    v.y = (k + 1 < K) ? rp[k + 1] : 0.f;
-    v.z = (k + 2 < K) ? rp[k + 2] : 0.f;
-    v.w = (k + 3 < K) ? rp[k + 3] : 0.f;
-    return v;
+// Operand fetch in two halves so the prefetch of a k-tile is never waited on early:
+//   raw4:  one unconditional float4 load at a clamped in-bounds column (c <= ld - 4);
+//   mask4: applied only when the tile is written to LDS (after the MFMAs of the current
+//          tile): zeroes out-of-range elements, inserts the implicit all-ones column
+//          (bias gradient) and drops the whole fetch when `ok` is false.
+__device__ __forceinline__ int clamp_col(int c, int ld) { return max(0, min(c, ld - 4)); }
+__device__ __forceinline__ float4 raw4(const float* rp, int c, int ld) {
+    return *reinterpret_cast<const float4*>(rp + clamp_col(c, ld));
 }
-
-template <int BM, int BN, int WAVES_M, int WAVES_N>
-struct GemmCfg {
-    static constexpr int TM = BM / WAVES_M;
-    static constexpr int TN = BN / WAVES_N;
-    static constexpr int I = TM / 32;
-    static constexpr int J = TN / 32;
-    static constexpr int A_LOADS = (BM * 4 + kThreads - 1) / kThreads;
-    static constexpr int B_LOADS = (BN * 4 + kThreads - 1) / kThreads;
-    static_assert(WAVES_M * WAVES_N == 4, "4 waves per block");
-    static_assert(TM % 32 == 0 && TN % 32 == 0, "wave tile must be a multiple of 32");
-};
+__device__ __forceinline__ float4 mask4(float4 v, int c, int lim, int ld, int ones, bool ok) {
+    const bool same = clamp_col(c, ld) == c;
+    float t[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int ce = c + e;
+        t[e] = (ok && same && ce < lim) ? t[e] : ((ok && ce == ones) ? 1.0f : 0.f);
+    }
+    return make_float4(t[0], t[1], t[2], t[3]);
+}
 
 __device__ __forceinline__ uint32_t keep_threshold(float keep_prob) {
-    double t = (double)keep_prob * 4294967296.0;
+    const double t = (double)keep_prob * 4294967296.0;
     return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
 }
 
-// Epilogue for one MFMA accumulator set.  acc[i][j] register r of lane (li, h) holds
-// C[row = i*32 + (r&3) + 8*(r>>2) + 4h][col = j*32 + li] of the wave tile.
-template <int E, int I, int J, int TM, int TN, int WAVES_N>
-__device__ __forceinline__ void epilogue(const KArg(GemmProblem) & P, f32x16 (&acc)[I][J], int m0, int n0, int wm,
-                                         int wn, int li, int h) {
-    const int M = P.M, N = P.N;
-    const bool use_rng = (E == EPI_HIDDEN) && P.keep_mask == nullptr && P.keep_prob < 1.0f;
-    const uint32_t thresh = keep_threshold(P.keep_prob);
+template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KMAJ_, bool B_KMAJ_>
+struct Cfg {
+    static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_;
+    static constexpr bool A_KMAJ = A_KMAJ_, B_KMAJ = B_KMAJ_;
+    static constexpr int TM = BM / WAVES_M, TN = BN / WAVES_N;
+    static constexpr int I = TM / 32, J = TN / 32;
+    static constexpr int A_F4 = BM * BK / 4, B_F4 = BN * BK / 4;
+    static constexpr int A_LOADS = (A_F4 + kThreads - 1) / kThreads;
+    static constexpr int B_LOADS = (B_F4 + kThreads - 1) / kThreads;
+    static constexpr int A_STAGE = A_KMAJ ? BK * BM : BM * SK;  // floats per buffer
+    static constexpr int B_STAGE = B_KMAJ ? BK * BN : BN * SK;
+    static constexpr int STAGE = 2 * (A_STAGE + B_STAGE);
+    static constexpr int CLD = BN + 4;                           // epilogue tile row stride
+    static constexpr int EPI_PHASES = WAVES_M >= 2 ? 2 : 1;     // row slices of the epilogue
+    static constexpr int EPI_ROWS = BM / EPI_PHASES;
+    static constexpr int EPI = EPI_ROWS * CLD;
+    static constexpr int KIDX = A_KMAJ ? 2 * 512 : 0;              // int64 gather rows (floats)
+    static constexpr int LDS = (STAGE + KIDX) > EPI ? (STAGE + KIDX) : EPI;
+    static_assert(WAVES_M * WAVES_N == 4, "4 waves per block");
+    static_assert(TM % 32 == 0 && TN % 32 == 0, "wave tile must be a multiple of 32");
+    static_assert(WAVES_M % EPI_PHASES == 0, "epilogue slices must hold whole wave rows");
+};
+
+// ---- the fused elementwise tail on 4 consecutive columns of one row ----------------------
+template <int E>
+__device__ __forceinline__ void epilogue4(const KArg(GemmProblem) & P, float4 v, int split, int row, int col) {
+    const int N = P.N;
+    float x[4] = {v.x, v.y, v.z, v.w};
+    if (E == EPI_STORE || E == EPI_HIDDEN || E == EPI_GATE_HIDDEN || E == EPI_GATE_OUT) {
+        if (P.bias) {
 #pragma unroll
-    for (int i = 0; i < I; ++i) {
+            for (int e = 0; e < 4; ++e)
+                if (col + e < N) x[e] += P.bias[col + e];
+        }
+    }
+    if (E == EPI_HIDDEN) {
+        u32x4 rnd = {0u, 0u, 0u, 0u};
+        if (P.keep_mask == nullptr && P.keep_prob < 1.0f)
+            rnd = philox4x32(u32x4{(uint32_t)row, (uint32_t)col, P.rng_c2, P.rng_c3}, P.rng_k0, P.rng_k1);
+        const uint32_t thresh = keep_threshold(P.keep_prob);
 #pragma unroll
-        for (int j = 0; j < J; ++j) {
-            const int col = n0 + wn * TN + j * 32 + li;
-            const bool col_ok = col < N;
-            float bias = 0.f;
-            if (E == EPI_STORE || E == EPI_HIDDEN || E == EPI_GATE_HIDDEN || E == EPI_GATE_OUT)
-                if (P.bias && col_ok) bias = P.bias[col];
+        for (int e = 0; e < 4; ++e) {
+            float hv = x[e] > 0.f ? x[e] : 0.f;
+            if (P.keep_prob < 1.0f && col + e < N) {
+                bool keep;
+                if (P.keep_mask) keep = P.keep_mask[(int64_t)row * N + col + e] != 0;
+                else keep = (e == 0 ? rnd.x : e == 1 ? rnd.y : e == 2 ? rnd.z : rnd.w) < thresh;
+                hv = hv * (keep ? P.inv_keep : 0.f);
+            }
+            x[e] = hv;
+        }
+    } else if (E == EPI_GATE_HIDDEN) {
 #pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                const int rbase = m0 + wm * TM + i * 32 + 8 * g4 + 4 * h;
-                u32x4 rnd = {0u, 0u, 0u, 0u};
-                if (use_rng)
-                    rnd = philox4x32(u32x4{(uint32_t)rbase, (uint32_t)col, P.rng_c2, P.rng_c3}, P.rng_k0, P.rng_k1);
+        for (int e = 0; e < 4; ++e) x[e] = x[e] > 0.f ? x[e] : 0.f;
+    } else if (E == EPI_GATE_OUT) {
+        const float* efr = P.aux0 + (int64_t)row * P.ld_aux0;
+        const int64_t oo = (int64_t)row * P.ld_out + col;
+        const float* arow = P.table ? P.table + P.idx[row] * (int64_t)N : nullptr;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int row = rbase + e;
-                    float v = acc[i][j][4 * g4 + e];
-                    if (row < M && col_ok) {
-                        const int64_t off = (int64_t)row * P.ldc + col;
-                        if (E == EPI_STORE) {
-                            P.C[off] = v + bias;
-                        } else if (E == EPI_HIDDEN) {
-                            v = v + bias;
-                            v = v > 0.f ? v : 0.f;
-                            if (P.keep_prob < 1.0f) {
-                                bool keep;
-                                if (P.keep_mask) {
-                                    keep = P.keep_mask[(int64_t)row * N + col] != 0;
-                                } else {
-                                    const uint32_t w = e == 0 ? rnd.x : e == 1 ? rnd.y : e == 2 ? rnd.z : rnd.w;
-                                    keep = w < thresh;
-                                }
-                                v = v * (keep ? P.inv_keep : 0.f);
-                            }
-                            P.C[off] = v;
-                        } else if (E == EPI_GATE_HIDDEN) {
-                            v = v + bias;
-                            P.C[off] = v > 0.f ? v : 0.f;
-                        } else if (E == EPI_GATE_OUT) {
-                            v = v + bias;
-                            const float g = sigmoidf_(v);
-                            const float* efr = P.aux0 + (int64_t)row * P.ld_aux0;
-                            const float ev = efr[col], fv = efr[N + col];
-                            const float t = g * ev + (1.0f - g) * fv;
-                            const int64_t oo = (int64_t)row * P.ld_out + col;
-                            P.out1[oo] = g;
-                            P.out2[oo] = t;
-                            float aug = t;
-                            if (P.table) {
-                                const float a = P.table[P.idx[row] * (int64_t)N + col];
-                                P.out3[oo] = a;
-                                aug = t + a;
-                            }
-                            P.C[off] = aug;
-                        } else if (E == EPI_DGRAD_RELU) {
-                            const float z = P.aux0[(int64_t)row * P.ld_aux0 + col];
-                            P.C[off] = z > 0.f ? v : 0.f;
-                        } else if (E == EPI_DGRAD_GATE_EF) {
-                            const int D = N >> 1;
-                            const int c = col < D ? col : col - D;
-                            const float dt = P.aux1[(int64_t)row * P.ld_aux1 + c];
-                            const float g = P.aux2[(int64_t)row * P.ld_aux1 + c];
-                            P.C[off] = col < D ? v + dt * g : v + dt * (1.0f - g);
-                        } else if (E == EPI_DGRAD_HIDDEN) {
-                            const float hv = P.aux0[(int64_t)row * P.ld_aux0 + col];
-                            P.C[off] = hv > 0.f ? v * P.inv_keep : 0.f;
-                        }
-                    }
-                }
+        for (int e = 0; e < 4; ++e) {
+            if (col + e >= N) continue;
+            const float g = sigmoidf_(x[e]);
+            const float t = g * efr[col + e] + (1.0f - g) * efr[N + col + e];
+            P.out1[oo + e] = g;
+            P.out2[oo + e] = t;
+            if (arow) {
+                const float a = arow[col + e];
+                P.out3[oo + e] = a;
+                x[e] = t + a;
+            } else {
+                x[e] = t;
             }
         }
+    } else if (E == EPI_DGRAD_RELU) {
+        const float* z = P.aux0 + (int64_t)row * P.ld_aux0 + col;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (col + e < N) x[e] = z[e] > 0.f ? x[e] : 0.f;
+    } else if (E == EPI_DGRAD_GATE_EF) {
+        const int D = N >> 1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int c = col + e;
+            if (c >= N) continue;
+            const int cc = c < D ? c : c - D;
+            const float dt = P.aux1[(int64_t)row * P.ld_aux1 + cc];
+            const float g = P.aux2[(int64_t)row * P.ld_aux1 + cc];
+            x[e] = c < D ? x[e] + dt * g : x[e] + dt * (1.0f - g);
+        }
+    } else if (E == EPI_DGRAD_HIDDEN) {
+        const float* hp = P.aux0 + (int64_t)row * P.ld_aux0 + col;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (col + e < N) x[e] = hp[e] > 0.f ? x[e] * P.inv_keep : 0.f;
+    }
+    float* C = P.C + (int64_t)split * P.slab_stride + (int64_t)row * P.ldc + col;
+    if (col + 3 < N && (P.ldc % 4 == 0) && aligned16(C)) {
+        *reinterpret_cast<float4*>(C) = make_float4(x[0], x[1], x[2], x[3]);
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (col + e < N) C[e] = x[e];
     }
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N>
+template <class CF, int E>
 __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
-    using Cfg = GemmCfg<BM, BN, WAVES_M, WAVES_N>;
-    constexpr int I = Cfg::I, J = Cfg::J, TM = Cfg::TM, TN = Cfg::TN;
+    constexpr int BM = CF::BM, BN = CF::BN, TM = CF::TM, TN = CF::TN, I = CF::I, J = CF::J;
+    constexpr bool AK = CF::A_KMAJ, BKM = CF::B_KMAJ;
+    __shared__ __attribute__((aligned(16))) float lds[CF::LDS];
 
-    __shared__ __attribute__((aligned(16))) float As[2][BM][SK];
-    __shared__ __attribute__((aligned(16))) float Bs[2][BN][SK];
-
-    // ---- locate problem / tile --------------------------------------------------------
-    // The problem table is read straight from the kernarg segment with a wave-uniform index
-    // (scalar loads); indexing the by-value argument would copy it to scratch.
+    // ---- problem / tile --------------------------------------------------------------------
     const KArg(GemmBatch)* kb = (const KArg(GemmBatch)*)(__builtin_amdgcn_kernarg_segment_ptr());
     int tile = blockIdx.x;
     int pi = 0;
-    if (kb->count > 1 && tile >= kb->p[1].tile_begin) pi = 1;
+#pragma unroll 1
+    for (int q = 1; q < kb->count; ++q)
+        if (tile >= kb->p[q].tile_begin) pi = q;
     const KArg(GemmProblem)& P = kb->p[pi];
     tile -= P.tile_begin;
+    const int tiles_mn = P.tiles_m * P.tiles_n;
+    const int split = tile / tiles_mn;
+    tile -= split * tiles_mn;
     const int tm = tile / P.tiles_n, tn = tile - tm * P.tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
-    const int M = P.M, N = P.N, K = P.K;
+    const int M = P.M, N = P.N;
+    const int k_begin = split * P.k_split;
+    const int k_end = min(P.K, k_begin + P.k_split);
 
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / CF::WAVES_N, wn = wave % CF::WAVES_N;
     const int li = lane & 31, h = lane >> 5;
+    float* As = lds;
+    float* Bs = lds + 2 * CF::A_STAGE;
 
-    const bool a_vec = (P.lda % 4 == 0) && aligned16(P.A);
-    const bool b_vec = (P.ldb % 4 == 0) && aligned16(P.B);
-
-    // ---- per-thread A row pointers (gather resolved once) -----------------------------
-    const float* a_rp[Cfg::A_LOADS];
-    int a_row[Cfg::A_LOADS], a_c4[Cfg::A_LOADS];
+    // ---- global -> register staging ---------------------------------------------------------
+    // MN-major A: thread -> (m row, 4 k), row pointers resolved once (gather on m).
+    // K-major A:  thread -> (k row, 4 m), gather indices of the whole k range staged in LDS.
+    const float* a_rp[CF::A_LOADS];
+    bool a_ok[CF::A_LOADS];
+    int a_r[CF::A_LOADS], a_c[CF::A_LOADS];
 #pragma unroll
-    for (int it = 0; it < Cfg::A_LOADS; ++it) {
+    for (int it = 0; it < CF::A_LOADS; ++it) {
         const int lin = tid + it * kThreads;
-        a_row[it] = lin >> 2;
-        a_c4[it] = lin & 3;
-        const int gr = m0 + a_row[it];
-        a_rp[it] = nullptr;
-        if (lin < BM * 4 && gr < M) {
-            const int64_t src = P.a_idx ? P.a_idx[gr] : (int64_t)gr;
-            a_rp[it] = P.A + src * P.lda;
+        if (!AK) {
+            a_r[it] = lin >> 2;
+            a_c[it] = (lin & 3) * 4;
+            const int gm = m0 + a_r[it];
+            a_ok[it] = lin < CF::A_F4 && gm < M;
+            const int gmc = min(gm, M - 1);
+            a_rp[it] = P.A + (P.a_idx ? P.a_idx[gmc] : (int64_t)gmc) * P.lda;
+        } else {
+            a_r[it] = lin / (BM / 4);
+            a_c[it] = (lin % (BM / 4)) * 4;
+            a_ok[it] = lin < CF::A_F4;
+            a_rp[it] = P.A;
         }
     }
-
-    float4 ra[Cfg::A_LOADS];
-    float4 rb[Cfg::B_LOADS];
+    int64_t* kidx = reinterpret_cast<int64_t*>(lds + CF::STAGE);  // K-major gather rows
+    if (AK) {
+        for (int k = tid; k < k_end - k_begin; k += kThreads)
+            kidx[k] = P.a_idx ? P.a_idx[k_begin + k] : (int64_t)(k_begin + k);
+        __syncthreads();
+    }
+    float4 ra[CF::A_LOADS], rb[CF::B_LOADS];
 
     auto load_tile = [&](int k0) {
 #pragma unroll
-        for (int it = 0; it < Cfg::A_LOADS; ++it) ra[it] = load4_k(a_rp[it], k0 + a_c4[it] * 4, K, a_vec);
-#pragma unroll
-        for (int it = 0; it < Cfg::B_LOADS; ++it) {
-            const int lin = tid + it * kThreads;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (lin < BN * 4) {
-                if (!P.b_kn) {
-                    const int n = n0 + (lin >> 2), k = k0 + (lin & 3) * 4;
-                    if (n < N) v = load4_k(P.B + (int64_t)n * P.ldb, k, K, b_vec);
-                } else {
-                    constexpr int NV = BN / 4;
-                    const int kr = lin / NV, nv = lin - kr * NV;
-                    const int k = k0 + kr, n = n0 + nv * 4;
-                    if (k < K) v = load4_k(P.B + (int64_t)k * P.ldb, n, N, b_vec);
-                }
+        for (int it = 0; it < CF::A_LOADS; ++it) {
+            if (!AK) {
+                ra[it] = raw4(a_rp[it], k0 + a_c[it], P.lda);
+            } else {
+                const int k = min(k0 + a_r[it], k_end - 1);
+                ra[it] = raw4(P.A + kidx[k - k_begin] * P.lda, m0 + a_c[it], P.lda);
             }
-            rb[it] = v;
+        }
+#pragma unroll
+        for (int it = 0; it < CF::B_LOADS; ++it) {
+            const int lin = tid + it * kThreads;
+            if (!BKM) {
+                const int n = min(n0 + (lin >> 2), N - 1);
+                rb[it] = raw4(P.B + (int64_t)n * P.ldb, k0 + (lin & 3) * 4, P.ldb);
+            } else {
+                const int k = min(k0 + lin / (BN / 4), k_end - 1);
+                rb[it] = raw4(P.B + (int64_t)k * P.ldb, n0 + (lin % (BN / 4)) * 4, P.ldb);
+            }
         }
     };
-    auto store_tile = [&](int buf) {
+    auto store_tile = [&](int buf, int k0) {
+        float* as = As + buf * CF::A_STAGE;
+        float* bs = Bs + buf * CF::B_STAGE;
 #pragma unroll
-        for (int it = 0; it < Cfg::A_LOADS; ++it) {
+        for (int it = 0; it < CF::A_LOADS; ++it) {
             const int lin = tid + it * kThreads;
-            if (lin < BM * 4) *reinterpret_cast<float4*>(&As[buf][a_row[it]][a_c4[it] * 4]) = ra[it];
+            if (lin >= CF::A_F4) continue;
+            if (!AK) {
+                const float4 v = mask4(ra[it], k0 + a_c[it], k_end, P.lda, -1, a_ok[it]);
+                *reinterpret_cast<float4*>(as + a_r[it] * SK + a_c[it]) = v;
+            } else {
+                const float4 v =
+                    mask4(ra[it], m0 + a_c[it], P.a_cols, P.lda, P.a_ones_col, k0 + a_r[it] < k_end);
+                *reinterpret_cast<float4*>(as + a_r[it] * BM + a_c[it]) = v;
+            }
         }
 #pragma unroll
-        for (int it = 0; it < Cfg::B_LOADS; ++it) {
+        for (int it = 0; it < CF::B_LOADS; ++it) {
             const int lin = tid + it * kThreads;
-            if (lin < BN * 4) {
-                if (!P.b_kn) {
-                    *reinterpret_cast<float4*>(&Bs[buf][lin >> 2][(lin & 3) * 4]) = rb[it];
-                } else {
-                    constexpr int NV = BN / 4;
-                    const int kr = lin / NV, nv = lin - kr * NV;
-                    Bs[buf][nv * 4 + 0][kr] = rb[it].x;
-                    Bs[buf][nv * 4 + 1][kr] = rb[it].y;
-                    Bs[buf][nv * 4 + 2][kr] = rb[it].z;
-                    Bs[buf][nv * 4 + 3][kr] = rb[it].w;
-                }
+            if (lin >= CF::B_F4) continue;
+            if (!BKM) {
+                const int n = n0 + (lin >> 2), c = k0 + (lin & 3) * 4;
+                *reinterpret_cast<float4*>(bs + (lin >> 2) * SK + (lin & 3) * 4) =
+                    mask4(rb[it], c, k_end, P.ldb, -1, n < N);
+            } else {
+                const int kr = lin / (BN / 4), nc = (lin % (BN / 4)) * 4;
+                *reinterpret_cast<float4*>(bs + kr * BN + nc) =
+                    mask4(rb[it], n0 + nc, N, P.ldb, -1, k0 + kr < k_end);
             }
         }
     };
@@ -249,149 +300,81 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    const int nk = (K + BK - 1) / BK;
-    load_tile(0);
-    store_tile(0);
+    const int nk = k_end > k_begin ? (k_end - k_begin + BK - 1) / BK : 0;
+    if (nk > 0) {
+        load_tile(k_begin);
+        store_tile(0, k_begin);
+    }
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = kt & 1;
-        if (kt + 1 < nk) load_tile((kt + 1) * BK);
+        if (kt + 1 < nk) load_tile(k_begin + (kt + 1) * BK);
+        const float* as = As + buf * CF::A_STAGE;
+        const float* bs = Bs + buf * CF::B_STAGE;
 #pragma unroll
         for (int s4 = 0; s4 < 2; ++s4) {
             float4 af[I], bf[J];
 #pragma unroll
-            for (int i = 0; i < I; ++i)
-                af[i] = *reinterpret_cast<const float4*>(&As[buf][wm * TM + i * 32 + li][8 * h + 4 * s4]);
+            for (int i = 0; i < I; ++i) {
+                const int m = wm * TM + i * 32 + li;
+                if (!AK) {
+                    af[i] = *reinterpret_cast<const float4*>(as + m * SK + 8 * h + 4 * s4);
+                } else {
+                    const float* c = as + (8 * h + 4 * s4) * BM + m;
+                    af[i] = make_float4(c[0], c[BM], c[2 * BM], c[3 * BM]);
+                }
+            }
 #pragma unroll
-            for (int j = 0; j < J; ++j)
-                bf[j] = *reinterpret_cast<const float4*>(&Bs[buf][wn * TN + j * 32 + li][8 * h + 4 * s4]);
+            for (int j = 0; j < J; ++j) {
+                const int n = wn * TN + j * 32 + li;
+                if (!BKM) {
+                    bf[j] = *reinterpret_cast<const float4*>(bs + n * SK + 8 * h + 4 * s4);
+                } else {
+                    const float* c = bs + (8 * h + 4 * s4) * BN + n;
+                    bf[j] = make_float4(c[0], c[BN], c[2 * BN], c[3 * BN]);
+                }
+            }
 #pragma unroll
             for (int q = 0; q < 4; ++q)
 #pragma unroll
                 for (int i = 0; i < I; ++i)
 #pragma unroll
-                    for (int j = 0; j < J; ++j) {
-                        const float a = q == 0 ? af[i].x : q == 1 ? af[i].y : q == 2 ? af[i].z : af[i].w;
-                        const float b = q == 0 ? bf[j].x : q == 1 ? bf[j].y : q == 2 ? bf[j].z : bf[j].w;
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < J; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(af[i], q), f4get(bf[j], q), acc[i][j],
+                                                                         0, 0, 0);
+        }
+        if (kt + 1 < nk) store_tile(buf ^ 1, k_begin + (kt + 1) * BK);
+        __syncthreads();
+    }
+
+    // ---- epilogue through LDS, in row slices ----------------------------------------------------
+    float* Cs = lds;
+    for (int ph = 0; ph < CF::EPI_PHASES; ++ph) {
+        const int row_lo = ph * CF::EPI_ROWS;
+        if (wm * TM >= row_lo && wm * TM < row_lo + CF::EPI_ROWS) {
+#pragma unroll
+            for (int i = 0; i < I; ++i)
+#pragma unroll
+                for (int j = 0; j < J; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int rr = wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h - row_lo;
+                        Cs[rr * CF::CLD + wn * TN + j * 32 + li] = acc[i][j][r];
                     }
         }
-        if (kt + 1 < nk) store_tile(buf ^ 1);
         __syncthreads();
-    }
-
-    // ---- epilogue (dispatched once; each variant fully unrolled so acc stays in registers)
-    switch (P.epi) {
-        case EPI_STORE: epilogue<EPI_STORE, I, J, TM, TN, WAVES_N>(P, acc, m0, n0, wm, wn, li, h); break;
-        case EPI_HIDDEN: epilogue<EPI_HIDDEN, I, J, TM, TN, WAVES_N>(P, acc, m0, n0, wm, wn, li, h); break;
-        case EPI_GATE_HIDDEN: epilogue<EPI_GATE_HIDDEN, I, J, TM, TN, WAVES_N>(P, acc, m0, n0, wm, wn, li, h); break;
-        case EPI_GATE_OUT: epilogue<EPI_GATE_OUT, I, J, TM, TN, WAVES_N>(P, acc, m0, n0, wm, wn, li, h); break;
-        case EPI_DGRAD_RELU: epilogue<EPI_DGRAD_RELU, I, J, TM, TN, WAVES_N>(P, acc, m0, n0, wm, wn, li, h); break;
-        case EPI_DGRAD_GATE_EF:
-            epilogue<EPI_DGRAD_GATE_EF, I, J, TM, TN, WAVES_N>(P, acc, m0, n0, wm, wn, li, h);
-            break;
-        case EPI_DGRAD_HIDDEN: epilogue<EPI_DGRAD_HIDDEN, I, J, TM, TN, WAVES_N>(P, acc, m0, n0, wm, wn, li, h); break;
-        default: break;
+        constexpr int C4 = BN / 4;
+        for (int idx = tid; idx < CF::EPI_ROWS * C4; idx += kThreads) {
+            const int rr = idx / C4, c4 = idx - rr * C4;
+            const int row = m0 + row_lo + rr, col = n0 + c4 * 4;
+            if (row < M && col < N)
+                epilogue4<E>(P, *reinterpret_cast<const float4*>(Cs + rr * CF::CLD + c4 * 4), split, row, col);
+        }
+        __syncthreads();
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// Weight gradient: per block a 64x64 tile of dW (+ bias column) over one chunk of rows.
-// ---------------------------------------------------------------------------------------
-constexpr int WBM = 64, WBN = 64, WBK = 16;
-
-__global__ __launch_bounds__(kThreads) void wgrad_kernel(WgradBatch batch) {
-    __shared__ __attribute__((aligned(16))) float Ys[2][WBK][WBM];
-    __shared__ __attribute__((aligned(16))) float Xs[2][WBK][WBN];
-
-    const KArg(WgradBatch)* kb = (const KArg(WgradBatch)*)(__builtin_amdgcn_kernarg_segment_ptr());
-    int blk = blockIdx.x;
-    int pi = 0;
-#pragma unroll 1
-    for (int q = 1; q < kb->count; ++q)
-        if (blk >= kb->p[q].tile_begin) pi = q;
-    const KArg(WgradProblem)& P = kb->p[pi];
-    blk -= P.tile_begin;
-    const int tiles = P.tiles_m * P.tiles_n;
-    const int split = blk / tiles;
-    const int t2 = blk - split * tiles;
-    const int tm = t2 / P.tiles_n, tn = t2 - tm * P.tiles_n;
-    const int m0 = tm * WBM, n0 = tn * WBN;
-    const int r0 = split * P.rows_per_split;
-    const int r1 = min(P.R, r0 + P.rows_per_split);
-    const int M = P.M, NN = P.N + 1;  // implicit ones column at n == N
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
-    const int li = lane & 31, h = lane >> 5;
-
-    const bool y_vec = (P.ld_dy % 4 == 0) && aligned16(P.dY);
-    const bool x_vec = (P.ld_x % 4 == 0) && aligned16(P.X);
-
-    // thread -> (row in k-tile, float4 column)
-    const int lr = tid >> 4, lc = (tid & 15) * 4;
-    float4 ry, rx;
-
-    auto load_tile = [&](int rr) {
-        const int r = rr + lr;
-        ry = make_float4(0.f, 0.f, 0.f, 0.f);
-        rx = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (r < r1) {
-            const float* yp = P.dY + (int64_t)r * P.ld_dy;
-            ry = load4_k(yp, m0 + lc, M, y_vec);
-            const int64_t src = P.x_idx ? P.x_idx[r] : (int64_t)r;
-            const float* xp = P.X + src * P.ld_x;
-            const int n = n0 + lc;
-            if (x_vec && n + 3 < P.N) {
-                rx = *reinterpret_cast<const float4*>(xp + n);
-            } else {
-                float t[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int ne = n + e;
-                    t[e] = ne < P.N ? xp[ne] : (ne == P.N ? 1.0f : 0.f);
-                }
-                rx = make_float4(t[0], t[1], t[2], t[3]);
-            }
-        }
-    };
-    auto store_tile = [&](int buf) {
-        *reinterpret_cast<float4*>(&Ys[buf][lr][lc]) = ry;
-        *reinterpret_cast<float4*>(&Xs[buf][lr][lc]) = rx;
-    };
-
-    f32x16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-
-    const int nk = (r1 - r0 + WBK - 1) / WBK;
-    if (nk > 0) {
-        load_tile(r0);
-        store_tile(0);
-    }
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        const int buf = kt & 1;
-        if (kt + 1 < nk) load_tile(r0 + (kt + 1) * WBK);
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            const float a = Ys[buf][8 * h + s][wm * 32 + li];
-            const float b = Xs[buf][8 * h + s][wn * 32 + li];
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
-        }
-        if (kt + 1 < nk) store_tile(buf ^ 1);
-        __syncthreads();
-    }
-
-    float* slab = P.slab + (int64_t)split * M * NN;
-    const int col = n0 + wn * 32 + li;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (row < M && col < NN) slab[(int64_t)row * NN + col] = acc[r];
-    }
-}
-
+// grad_w[m_out][n_in] = sum_s slab[s][n_in][m_out] ; grad_b[m_out] = sum_s slab[s][N_in][m_out]
 __global__ void wgrad_reduce_kernel(WgradBatch batch, int64_t total) {
     const KArg(WgradBatch)* kb = (const KArg(WgradBatch)*)(__builtin_amdgcn_kernarg_segment_ptr());
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -404,45 +387,69 @@ __global__ void wgrad_reduce_kernel(WgradBatch batch, int64_t total) {
         off -= sz;
     }
     const KArg(WgradProblem)& P = kb->p[pi];
-    const int NN = P.N + 1;
-    const int64_t plane = (int64_t)P.M * NN;
+    const int Mo = P.M;
+    const int64_t plane = (int64_t)(P.N + 1) * Mo;
+    const int n = (int)(off / Mo), m = (int)(off - (int64_t)n * Mo);
     float s = 0.f;
     for (int sp = 0; sp < P.splits; ++sp) s += P.slab[sp * plane + off];
-    const int m = (int)(off / NN), n = (int)(off - (int64_t)m * NN);
-    if (n < P.N) {
-        P.grad_w[(int64_t)m * P.N + n] = s;
-    } else if (P.grad_b) {
-        P.grad_b[m] = s;
-    }
+    if (n < P.N) P.grad_w[(int64_t)m * P.N + n] = s;
+    else if (P.grad_b) P.grad_b[m] = s;
 }
 
-template <int BM, int BN, int WM, int WN>
-int launch_cfg(GemmBatch& b, hipStream_t s) {
+template <class CF, int E>
+int launch_one(GemmBatch& b, hipStream_t s) {
     int tiles = 0;
     for (int i = 0; i < b.count; ++i) {
         GemmProblem& p = b.p[i];
-        p.tiles_n = (int)ceil_div(p.N, BN);
+        p.tiles_m = (int)ceil_div(p.M, CF::BM);
+        p.tiles_n = (int)ceil_div(p.N, CF::BN);
+        if (p.k_split <= 0) p.k_split = p.K;
         p.tile_begin = tiles;
-        tiles += (int)ceil_div(p.M, BM) * p.tiles_n;
+        tiles += p.tiles_m * p.tiles_n * (int)ceil_div(p.K, p.k_split);
     }
     b.total_tiles = tiles;
     if (tiles == 0) return TTAMM_OK;
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN>), dim3(tiles), dim3(kThreads), 0, s, b);
+    hipLaunchKernelGGL((gemm_kernel<CF, E>), dim3(tiles), dim3(kThreads), 0, s, b);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
+}
+
+template <class CF>
+int dispatch_epi(GemmBatch& b, hipStream_t s) {
+    switch (b.p[0].epi) {
+        case EPI_STORE: return launch_one<CF, EPI_STORE>(b, s);
+        case EPI_HIDDEN: return launch_one<CF, EPI_HIDDEN>(b, s);
+        case EPI_GATE_HIDDEN: return launch_one<CF, EPI_GATE_HIDDEN>(b, s);
+        case EPI_GATE_OUT: return launch_one<CF, EPI_GATE_OUT>(b, s);
+        case EPI_DGRAD_RELU: return launch_one<CF, EPI_DGRAD_RELU>(b, s);
+        case EPI_DGRAD_GATE_EF: return launch_one<CF, EPI_DGRAD_GATE_EF>(b, s);
+        case EPI_DGRAD_HIDDEN: return launch_one<CF, EPI_DGRAD_HIDDEN>(b, s);
+        default: return fail(TTAMM_E_INVALID, "gemm: unknown epilogue");
+    }
 }
 
 }  // namespace
 
 int launch_gemm(GemmBatch& b, hipStream_t s) {
+    if (b.count == 0) return TTAMM_OK;
     int maxN = 0;
+    const int bkn = b.p[0].b_kn;
     for (int i = 0; i < b.count; ++i) {
-        const GemmProblem& p = b.p[i];
+        GemmProblem& p = b.p[i];
         TTAMM_REQUIRE(p.M >= 0 && p.N > 0 && p.K > 0, "gemm: bad shape");
+        TTAMM_REQUIRE(p.epi == b.p[0].epi && p.b_kn == bkn && !p.a_kmaj, "gemm: grouped problems must share a variant");
+        TTAMM_REQUIRE(p.lda % 4 == 0 && p.ldb % 4 == 0 && ((uintptr_t)p.A | (uintptr_t)p.B) % 16 == 0,
+                      "gemm: operands must be 16-byte aligned with leading dims % 4 == 0");
+        p.k_split = p.K;
+        p.slab_stride = 0;
         maxN = p.N > maxN ? p.N : maxN;
     }
-    if (maxN > 96) return launch_cfg<128, 192, 2, 2>(b, s);
-    return launch_cfg<128, 96, 4, 1>(b, s);
+    if (maxN > 96) {
+        if (bkn) return dispatch_epi<Cfg<128, 192, 2, 2, false, true>>(b, s);
+        return dispatch_epi<Cfg<128, 192, 2, 2, false, false>>(b, s);
+    }
+    if (bkn) return dispatch_epi<Cfg<128, 96, 4, 1, false, true>>(b, s);
+    return dispatch_epi<Cfg<128, 96, 4, 1, false, false>>(b, s);
 }
 
 int wgrad_rows_per_split(int R) {
@@ -456,25 +463,67 @@ size_t wgrad_slab_floats(int R, int M, int N) {
     return (size_t)splits * M * (N + 1);
 }
 
-int launch_wgrad(WgradBatch& b, hipStream_t s) {
-    int blocks = 0;
+// Weight gradients as C = X^T dY (M = n_in + 1 incl. the ones column, N = m_out, K = rows),
+// both operands K-major; one launch per tile configuration, then one fixed-order reduce.
+int launch_wgrad(WgradBatch& wb, hipStream_t s) {
+    GemmBatch wide, narrow;  // m_out > 96 / <= 96
+    std::memset(&wide, 0, sizeof(wide));
+    std::memset(&narrow, 0, sizeof(narrow));
+    auto flush = [&](GemmBatch& g, bool is_wide) -> int {
+        if (g.count == 0) return TTAMM_OK;
+        const int rc = is_wide ? launch_one<Cfg<128, 192, 2, 2, true, true>, EPI_STORE>(g, s)
+                               : launch_one<Cfg<128, 96, 4, 1, true, true>, EPI_STORE>(g, s);
+        std::memset(&g, 0, sizeof(g));
+        return rc;
+    };
     int64_t total = 0;
-    for (int i = 0; i < b.count; ++i) {
-        WgradProblem& p = b.p[i];
-        p.rows_per_split = wgrad_rows_per_split(p.R);
-        p.splits = p.R > 0 ? (int)ceil_div(p.R, p.rows_per_split) : 1;
-        p.tiles_m = (int)ceil_div(p.M, WBM);
-        p.tiles_n = (int)ceil_div(p.N + 1, WBN);
-        p.tile_begin = blocks;
-        blocks += p.splits * p.tiles_m * p.tiles_n;
-        total += (int64_t)p.M * (p.N + 1);
+    for (int i = 0; i < wb.count; ++i) {
+        WgradProblem& w = wb.p[i];
+        w.rows_per_split = wgrad_rows_per_split(w.R);
+        w.splits = w.R > 0 ? (int)ceil_div(w.R, w.rows_per_split) : 1;
+        total += (int64_t)w.M * (w.N + 1);
+        if (w.R <= 0) {  // no rows: the slab (one split) is zero
+            TTAMM_HIP(hipMemsetAsync(w.slab, 0, sizeof(float) * w.M * (w.N + 1), s));
+            continue;
+        }
+        TTAMM_REQUIRE(w.ld_x % 4 == 0 && w.ld_dy % 4 == 0 && ((uintptr_t)w.X | (uintptr_t)w.dY) % 16 == 0,
+                      "wgrad: operands must be 16-byte aligned with leading dims % 4 == 0");
+        GemmProblem p;
+        std::memset(&p, 0, sizeof(p));
+        p.A = w.X;
+        p.a_idx = w.x_idx;
+        p.lda = w.ld_x;
+        p.a_kmaj = 1;
+        p.a_cols = w.N;
+        p.a_ones_col = w.N;
+        p.B = w.dY;
+        p.ldb = w.ld_dy;
+        p.b_kn = 1;
+        p.M = w.N + 1;
+        p.N = w.M;
+        p.K = w.R;
+        p.k_split = w.rows_per_split;
+        p.epi = EPI_STORE;
+        p.C = w.slab;
+        p.ldc = w.M;
+        p.slab_stride = (int64_t)(w.N + 1) * w.M;
+        p.keep_prob = 1.f;
+        p.inv_keep = 1.f;
+        const bool is_wide = w.M > 96;
+        GemmBatch& g = is_wide ? wide : narrow;
+        if (g.count == kMaxGemmProblems) {
+            const int rc = flush(g, is_wide);
+            if (rc) return rc;
+        }
+        g.p[g.count++] = p;
     }
-    b.total_blocks = blocks;
-    if (blocks == 0) return TTAMM_OK;
-    hipLaunchKernelGGL(wgrad_kernel, dim3(blocks), dim3(kThreads), 0, s, b);
-    TTAMM_LAUNCH_CHECK();
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, s, b, total);
-    TTAMM_LAUNCH_CHECK();
+    int rc;
+    if ((rc = flush(wide, true))) return rc;
+    if ((rc = flush(narrow, false))) return rc;
+    if (total > 0) {
+        hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, s, wb, total);
+        TTAMM_LAUNCH_CHECK();
+    }
     return TTAMM_OK;
 }
 

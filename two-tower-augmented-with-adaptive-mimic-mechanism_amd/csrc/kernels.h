@@ -49,11 +49,18 @@ struct GemmProblem {
     float inv_keep;     // 1 / (1 - p)   (torch: noise.div_(1 - p))
     const uint8_t* keep_mask;  // optional injected [M, N]
     uint32_t rng_k0, rng_k1, rng_c2, rng_c3;
+    // K-major A (weight gradient: A = X^T, rows of X indexed by k, gathered by a_idx)
+    int a_kmaj;
+    int a_cols;          // valid columns of X (m < a_cols)
+    int a_ones_col;      // column of implicit ones (bias gradient), -1 = none
+    // split-K over rows: each split writes its own slab at C + split * slab_stride
+    int k_split;
+    int64_t slab_stride;
     int tile_begin;     // filled by the launcher
-    int tiles_n;
+    int tiles_m, tiles_n;
 };
 
-constexpr int kMaxGemmProblems = 2;
+constexpr int kMaxGemmProblems = 8;
 struct GemmBatch {
     GemmProblem p[kMaxGemmProblems];
     int count;
@@ -98,6 +105,8 @@ int launch_gather_rows(const float* table, int dim, const int64_t* idx, int64_t 
 int launch_combine(const float* e, int64_t ld_e, const float* f, int64_t ld_f, const float* table,
                    const int64_t* idx, int64_t n, int dim, float* t, float* a, float* aug,
                    hipStream_t s);
+int launch_pad_rows(const float* src, int64_t rows, int cols, int64_t ld_src, float* dst, int ld_dst,
+                    hipStream_t s);
 int launch_mse(const float* x, const float* y, int64_t n, float* out, hipStream_t s);
 // dq = (dT*e - dT*f) * (1-g) * g   (gate backward through the sigmoid)
 int launch_gate_dq(const float* dT, const float* ef, const float* g, int64_t n, int dim, float* dq,
@@ -183,6 +192,9 @@ struct RowUpdateArgs {
     const float* dA_hi;
     int64_t split_row;
     ttamm_table mimic;
+    // per-position partial sums of the segmented reduction [n, dim]
+    float* piece_e;
+    float* piece_a;
     // dense-optimized tables stage their touched rows in side buffers [n, 3, dim] (p, m, v)
     float* side_id;
     float* side_mimic;

@@ -76,22 +76,80 @@ __global__ void seg_start_kernel(const int32_t* __restrict__ flags, const int32_
     }
 }
 
-// One wave per unique row: sum its contributions (fixed order), then update the ID table
-// (SparseAdam in place, or AdamW into a side buffer) and the mimic table (AdamW -> side).
+// Segmented sum of the row-gradient contributions, in two fixed-order levels so a hot row
+// (a popular item with hundreds of duplicates in the batch) does not serialise one wave:
+//   piece_sum: one wave per chunk of kPiece sorted positions sums each run of equal keys
+//              inside its chunk ("piece") and stores it at the run's first position;
+//   row_update: one wave per unique row adds its pieces in position order, then applies
+//              the optimizer.  Both orders are fixed, so results are deterministic.
+constexpr int kPiece = 32;
 constexpr int kRowWaves = 4;
+
+__device__ __forceinline__ const float* dA_row(const RowUpdateArgs& A, int64_t r) {
+    return (r < A.split_row ? A.dA_lo : A.dA_hi) + r * A.dim;
+}
+
+__global__ __launch_bounds__(64 * kRowWaves) void piece_sum_kernel(RowUpdateArgs A) {
+    __shared__ int64_t srows[kRowWaves][kPiece];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t chunk = (int64_t)blockIdx.x * kRowWaves + w;
+    const int64_t k0 = chunk * kPiece;
+    if (k0 >= A.n) return;
+    const int cnt = (int)min((int64_t)kPiece, A.n - k0);
+    // positions of the chunk: lane p holds row / key / "last of a run" for position k0 + p
+    int64_t my_row = 0;
+    int my_key = 0, my_last = 1;
+    if (lane < cnt) {
+        my_row = A.rows[k0 + lane];
+        my_key = A.keys[k0 + lane];
+    }
+    const int next_key = __shfl_down(my_key, 1, 64);
+    if (lane + 1 < cnt) my_last = next_key != my_key;
+    const uint64_t last_mask = __ballot(lane < cnt && my_last);
+    if (lane < kPiece) srows[w][lane] = my_row;  // read back uniformly inside the d loop
+    __builtin_amdgcn_wave_barrier();
+    const int D = A.dim;
+    const bool mimic = A.mimic.weight != nullptr;
+    for (int d = lane; d < D; d += 64) {
+        float ve[kPiece], va[kPiece];
+#pragma unroll
+        for (int p = 0; p < kPiece; ++p) {  // issue every load of the chunk before adding
+            const int64_t r = srows[w][p];
+            ve[p] = p < cnt ? A.dE[r * A.ld_dE + d] : 0.f;
+            va[p] = (mimic && p < cnt) ? dA_row(A, r)[d] : 0.f;
+        }
+        float ge = 0.f, ga = 0.f;
+        int start = 0;
+#pragma unroll
+        for (int p = 0; p < kPiece; ++p) {
+            if (p < cnt) {
+                ge += ve[p];
+                ga += va[p];
+                if ((last_mask >> p) & 1ull) {
+                    A.piece_e[(k0 + start) * D + d] = ge;
+                    if (mimic) A.piece_a[(k0 + start) * D + d] = ga;
+                    ge = ga = 0.f;
+                    start = p + 1;
+                }
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArgs A) {
     const int lane = threadIdx.x & 63;
     const int64_t u = (int64_t)blockIdx.x * kRowWaves + (threadIdx.x >> 6);
     if (u >= A.n || u >= (int64_t)A.n_unique[0]) return;
-    const int k0 = A.seg_start[u], k1 = A.seg_start[u + 1];
+    const int64_t k0 = A.seg_start[u], k1 = A.seg_start[u + 1];
     const int64_t key = A.keys[k0];
     const int D = A.dim;
+    const bool mimic = A.mimic.weight != nullptr;
     for (int d = lane; d < D; d += 64) {
-        float ge = 0.f, ga = 0.f;
-        for (int k = k0; k < k1; ++k) {
-            const int64_t r = A.rows[k];
-            ge += A.dE[r * A.ld_dE + d];
-            if (A.mimic.weight) ga += (r < A.split_row ? A.dA_lo : A.dA_hi)[r * D + d];
+        float ge = A.piece_e[k0 * D + d];
+        float ga = mimic ? A.piece_a[k0 * D + d] : 0.f;
+        for (int64_t k = (k0 / kPiece + 1) * kPiece; k < k1; k += kPiece) {
+            ge += A.piece_e[k * D + d];
+            if (mimic) ga += A.piece_a[k * D + d];
         }
         {
             const int64_t o = key * D + d;
@@ -109,7 +167,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArg
                 sd[2 * D + d] = v;
             }
         }
-        if (A.mimic.weight) {
+        if (mimic) {
             const int64_t o = key * D + d;
             float p = A.mimic.weight[o], m = A.mimic.exp_avg[o], v = A.mimic.exp_avg_sq[o];
             adam_elem(p, m, v, ga, A.ad);
@@ -281,6 +339,9 @@ int launch_coalesce(const int64_t* idx, int64_t n, int64_t table_rows, CoalesceW
 
 int launch_row_update(const RowUpdateArgs& a, hipStream_t s) {
     if (a.n <= 0) return TTAMM_OK;
+    hipLaunchKernelGGL(piece_sum_kernel, dim3((unsigned)ceil_div(ceil_div(a.n, kPiece), kRowWaves)),
+                       dim3(64 * kRowWaves), 0, s, a);
+    TTAMM_LAUNCH_CHECK();
     hipLaunchKernelGGL(row_update_kernel, dim3((unsigned)ceil_div(a.n, kRowWaves)), dim3(64 * kRowWaves), 0, s, a);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;

@@ -54,6 +54,19 @@ __global__ void combine_kernel(const float* __restrict__ e, int64_t ld_e, const 
     }
 }
 
+// dst[r, c] = c < cols ? src[r, c] : 0   (16-byte aligned copy of an nn.Linear weight whose
+// in_features is not a multiple of 4, e.g. the 605-wide first feature layer)
+__global__ void pad_rows_kernel(const float* __restrict__ src, int64_t rows, int cols, int64_t ld_src,
+                                float* __restrict__ dst, int ld_dst) {
+    const int64_t total = rows * ld_dst;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / ld_dst;
+        const int c = (int)(i - r * ld_dst);
+        dst[i] = c < cols ? src[r * ld_src + c] : 0.f;
+    }
+}
+
 // dq = (dT*e - dT*f) * (1 - g) * g
 // autograd of gate*e + (1-gate)*f then SigmoidBackward (grad*(1-y)*y), encoders.py:164-168.
 __global__ void gate_dq_kernel(const float* __restrict__ dT, const float* __restrict__ ef,
@@ -264,6 +277,15 @@ int launch_combine(const float* e, int64_t ld_e, const float* f, int64_t ld_f, c
 int launch_mse(const float* x, const float* y, int64_t n, float* out, hipStream_t s) {
     TTAMM_REQUIRE(n > 0, "mse_loss: empty input");
     hipLaunchKernelGGL(mse_kernel, dim3(1), dim3(1024), 0, s, x, y, n, out);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_pad_rows(const float* src, int64_t rows, int cols, int64_t ld_src, float* dst, int ld_dst,
+                    hipStream_t s) {
+    if (rows <= 0) return TTAMM_OK;
+    hipLaunchKernelGGL(pad_rows_kernel, dim3(grid_for(rows * ld_dst)), dim3(256), 0, s, src, rows, cols, ld_src, dst,
+                       ld_dst);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

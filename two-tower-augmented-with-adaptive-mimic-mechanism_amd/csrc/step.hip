@@ -48,6 +48,9 @@ struct TowerWs {
     CoalesceWs co{};
     float* side_id = nullptr;
     float* side_mimic = nullptr;
+    float* piece_e = nullptr;
+    float* piece_a = nullptr;
+    float* wpad = nullptr;  // first feature layer weight, in_features padded to a multiple of 4
 };
 
 struct StepWs {
@@ -57,6 +60,10 @@ struct StepWs {
 };
 
 int tower_in_dim(const ttamm_tower& T, int l) { return l == 0 ? T.feat_dim : T.linear[l - 1].out_features; }
+inline int round4(int x) { return (x + 3) / 4 * 4; }
+bool needs_wpad(const ttamm_tower& T) {
+    return T.fusion != TTAMM_FUSION_IDENTITY && T.n_linear > 0 && T.linear[0].in_features % 4 != 0;
+}
 
 // Validate one tower against the reference's own constraints.
 int validate_tower(const ttamm_tower& T, const char* name, int D, bool training) {
@@ -64,12 +71,15 @@ int validate_tower(const ttamm_tower& T, const char* name, int D, bool training)
     TTAMM_REQUIRE(T.id.weight, n + ": embedding table missing");
     if (training) TTAMM_REQUIRE(T.id.exp_avg && T.id.exp_avg_sq, n + ": embedding optimizer state missing");
     TTAMM_REQUIRE(T.id.dim == D, n + ": embedding dim mismatch");
+    TTAMM_REQUIRE(D % 4 == 0, n + ": ttamm requires embedding_dim % 4 == 0");
     TTAMM_REQUIRE(T.id.rows > 0, n + ": empty embedding table");
     TTAMM_REQUIRE(T.n_linear >= 0 && T.n_linear <= TTAMM_MAX_LINEAR, n + ": too many feature-encoder layers");
     TTAMM_REQUIRE(T.fusion >= TTAMM_FUSION_IDENTITY && T.fusion <= TTAMM_FUSION_GATED, n + ": unsupported fusion");
     if (T.fusion != TTAMM_FUSION_IDENTITY) {
         TTAMM_REQUIRE(T.features != nullptr && T.feat_dim > 0, n + ": fusion needs feature rows");
         TTAMM_REQUIRE(T.feat_ld >= T.feat_dim, n + ": feature row stride too small");
+        TTAMM_REQUIRE(T.feat_ld % 4 == 0 && (uintptr_t)T.features % 16 == 0,
+                      n + ": feature rows must be 16-byte aligned (row stride % 4 == 0)");
         for (int l = 0; l < T.n_linear; ++l) {
             const ttamm_linear& L = T.linear[l];
             TTAMM_REQUIRE(L.weight && L.bias, n + ": linear parameters missing");
@@ -77,6 +87,7 @@ int validate_tower(const ttamm_tower& T, const char* name, int D, bool training)
                 TTAMM_REQUIRE(L.weight_exp_avg && L.weight_exp_avg_sq && L.bias_exp_avg && L.bias_exp_avg_sq,
                               n + ": linear optimizer state missing");
             TTAMM_REQUIRE(L.in_features == tower_in_dim(T, l), n + ": feature-encoder layer shapes do not chain");
+            TTAMM_REQUIRE(L.out_features % 4 == 0, n + ": ttamm requires feature-encoder widths % 4 == 0");
         }
         const int fo = T.n_linear ? T.linear[T.n_linear - 1].out_features : T.feat_dim;
         TTAMM_REQUIRE(fo == D,
@@ -92,6 +103,7 @@ int validate_tower(const ttamm_tower& T, const char* name, int D, bool training)
                           n + ": gate optimizer state missing");
         TTAMM_REQUIRE(G1.in_features == 2 * D && G2.out_features == D && G2.in_features == G1.out_features,
                       n + ": gate shapes do not match the embedding dimension");
+        TTAMM_REQUIRE(G1.out_features % 4 == 0, n + ": ttamm requires the gate hidden width % 4 == 0");
     }
     return TTAMM_OK;
 }
@@ -151,6 +163,9 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         w.co.n_unique = ar.take<int32_t>(1);
         w.co.temp_bytes = coalesce_temp_bytes(R);
         w.co.temp = ar.take<char>(w.co.temp_bytes);
+        if (needs_wpad(T)) w.wpad = ar.take<float>((size_t)T.linear[0].out_features * round4(T.linear[0].in_features));
+        w.piece_e = ar.take<float>((size_t)R * D);
+        if (mimic) w.piece_a = ar.take<float>((size_t)R * D);
         if (T.id.optimizer == TTAMM_OPT_DENSE) w.side_id = ar.take<float>((size_t)R * 3 * D);
         if (mimic) w.side_mimic = ar.take<float>((size_t)R * 3 * D);
     };
@@ -166,6 +181,7 @@ GemmProblem gp_base() {
     std::memset(&p, 0, sizeof(p));
     p.keep_prob = 1.f;
     p.inv_keep = 1.f;
+    p.a_ones_col = -1;
     return p;
 }
 
@@ -230,6 +246,13 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
             }
             p.B = L.weight;
             p.ldb = L.in_features;
+            if (l == 0 && w.wpad) {
+                if ((rc = launch_pad_rows(L.weight, L.out_features, L.in_features, L.in_features, w.wpad,
+                                          round4(L.in_features), s)))
+                    return rc;
+                p.B = w.wpad;
+                p.ldb = round4(L.in_features);
+            }
             p.b_kn = 0;
             p.M = (int)w.R;
             p.N = L.out_features;
@@ -489,6 +512,8 @@ int tower_optimizer_rows(const ttamm_tower& t, TowerWs& w, int D, int64_t B, boo
     }
     ru.side_id = w.side_id;
     ru.side_mimic = w.side_mimic;
+    ru.piece_e = w.piece_e;
+    ru.piece_a = w.piece_a;
     ru.sp = sp;
     ru.ad = ad;
     return launch_row_update(ru, s);
@@ -653,6 +678,7 @@ size_t tower_forward_workspace_size(const ttamm_tower& T, int64_t n) {
     ar.take<float>((size_t)n * D);      // f
     if (T.fusion == TTAMM_FUSION_GATED) ar.take<float>((size_t)n * T.gate[0].out_features);
     for (int q = 0; q < 3; ++q) ar.take<float>((size_t)n * D);  // g, t, a
+    if (needs_wpad(T)) ar.take<float>((size_t)T.linear[0].out_features * round4(T.linear[0].in_features));
     return ar.off + 256;
 }
 
@@ -674,6 +700,7 @@ int tower_forward_eval(const ttamm_tower& T, const int64_t* idx, const int64_t* 
     float* gbuf = ar.take<float>((size_t)n * D);
     float* tbuf = ar.take<float>((size_t)n * D);
     float* abuf = ar.take<float>((size_t)n * D);
+    if (needs_wpad(T)) w.wpad = ar.take<float>((size_t)T.linear[0].out_features * round4(T.linear[0].in_features));
     TTAMM_REQUIRE(ar.ok(), "workspace too small for tower forward");
     if (T.fusion == TTAMM_FUSION_GATED) {
         w.ef = efbuf;

@@ -395,8 +395,13 @@ def tower_forward(
     feats = None
     if use_features:
         feats = features.reshape(-1, features.shape[-1])
-        if feats.stride(-1) != 1:
-            feats = feats.contiguous()
+        if feats.dtype != torch.float32:
+            raise ValueError("ttamm: features must be float32")
+        if feats.stride(-1) != 1 or feats.stride(0) % 4 or feats.data_ptr() % 16:
+            width = feats.shape[1]
+            padded = torch.zeros((feats.shape[0], (width + 3) // 4 * 4), dtype=torch.float32, device=feats.device)
+            padded[:, :width].copy_(feats)
+            feats = padded[:, :width]
         if feats.shape[0] != n:
             raise ValueError("ttamm: features must have one row per index")
     desc = describe_tower(tower, features=feats, mimic_table=mimic_table)
