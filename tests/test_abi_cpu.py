@@ -1,0 +1,114 @@
+"""The C ABI boundary without a GPU: libttamm.so loads, exports every entry point that
+include/ttamm.h declares, the ctypes mirror covers them all, and the ctypes struct layouts
+equal what a C compiler (gcc) produces for the header."""
+
+import ctypes
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "ttamm.h"
+
+
+def header_functions() -> list[str]:
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(ttamm_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_parses_as_c_and_cxx(tmp_path):
+    src = tmp_path / "h.c"
+    src.write_text(f'#include "{HEADER}"\nint main(void) {{ return TTAMM_ABI_VERSION == 1 ? 0 : 1; }}\n')
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", str(src), "-o", str(tmp_path / "h")], check=True)
+    subprocess.run([str(tmp_path / "h")], check=True)
+    cxx = tmp_path / "h.cpp"
+    cxx.write_text(src.read_text())
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", str(cxx), "-o", str(tmp_path / "hx")], check=True)
+
+
+def test_library_exports_every_declared_function():
+    from ttamm import _lib
+
+    lib = _lib.load()
+    declared = header_functions()
+    assert declared, "no functions parsed from the header"
+    assert sorted(_lib.SIGNATURES) == declared
+    out = subprocess.run(["nm", "-D", "--defined-only", str(_lib.library_path())], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (ttamm_\w+)", out))
+    assert set(declared) <= exported, sorted(set(declared) - exported)
+    for name in declared:
+        assert hasattr(lib, name)
+    assert lib.ttamm_abi_version() == 1
+    assert lib.ttamm_last_error() is not None
+
+
+STRUCTS = {
+    "ttamm_linear": "Linear",
+    "ttamm_table": "Table",
+    "ttamm_tower": "Tower",
+    "ttamm_hparams": "HParams",
+    "ttamm_batch": "Batch",
+    "ttamm_step_args": "StepArgs",
+}
+
+
+def test_ctypes_layout_matches_c(tmp_path):
+    from ttamm import _lib
+
+    lines = [f'#include "{HEADER}"', "#include <stdio.h>", "#include <stddef.h>", "int main(void) {"]
+    for cname, pyname in STRUCTS.items():
+        cls = getattr(_lib, pyname)
+        lines.append(f'printf("{pyname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in cls._fields_:
+            lines.append(f'printf("{pyname}.{fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", str(src), "-o", str(exe)], check=True)
+    got = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                              check=True).stdout.splitlines())
+    for cname, pyname in STRUCTS.items():
+        cls = getattr(_lib, pyname)
+        assert int(got[f"{pyname} size"]) == ctypes.sizeof(cls), pyname
+        for fname, _ in cls._fields_:
+            assert int(got[f"{pyname}.{fname}"]) == getattr(cls, fname).offset, f"{pyname}.{fname}"
+
+
+def test_errors_map_to_reference_exceptions():
+    """Invalid arguments come back as TTAMM_E_INVALID -> ValueError, with no device work."""
+    from ttamm import _lib
+
+    lib = _lib.load()
+    with pytest.raises(ValueError):
+        _lib.check(lib.ttamm_gather_rows(None, 10, 0, None, 5, None, 0, None))
+    with pytest.raises(ValueError):
+        _lib.check(lib.ttamm_sample_negatives(None, 4, 0, 10, None, None, 0, 0, None, None, None))
+    with pytest.raises(ValueError, match="num_items must be greater than one"):
+        _lib.check(lib.ttamm_sample_negatives(None, 4, 2, 1, None, None, 0, 0, None, None, None))
+    with pytest.raises(ValueError):
+        _lib.check(lib.ttamm_adamw_dense(None, None, None, None, 4, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1, 0, None))
+    with pytest.raises(ValueError):
+        _lib.check(lib.ttamm_train_step(None, None))
+
+
+def test_train_step_validation_rejects_bad_descriptors():
+    """The executor validates the reference's shape constraints before touching the GPU."""
+    from ttamm import _lib
+
+    lib = _lib.load()
+    args = _lib.StepArgs()
+    with pytest.raises(ValueError, match="embedding table"):
+        _lib.check(lib.ttamm_train_step(ctypes.byref(args), None))
+    fake = 4096  # never dereferenced: validation fails first
+    for tower in (args.user, args.item):
+        tower.id.weight = tower.id.exp_avg = tower.id.exp_avg_sq = fake
+        tower.id.rows = 10
+        tower.id.dim = 6
+    with pytest.raises(ValueError, match="% 4"):
+        _lib.check(lib.ttamm_train_step(ctypes.byref(args), None))
+    assert lib.ttamm_train_step_workspace_size(ctypes.byref(args)) > 0

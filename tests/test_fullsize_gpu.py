@@ -1,0 +1,84 @@
+"""Size-independent properties of the fused step at BASELINE C2 shapes (2M items x 200K
+users, D=96, F=605, H=192, B=8192, N=5), where the CPU oracle is too slow to compare
+element by element:
+  * determinism — two runs from the same state and seed agree bit for bit (no atomics on
+    the data path; fixed-order reductions);
+  * untouched rows of the dense-group mimic tables follow torch's AdamW with g = 0 exactly;
+  * sampled negatives are in range and never a user's positive;
+  * the loss goes down."""
+
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+@pytest.fixture(scope="module")
+def c2():
+    import bench
+
+    return bench.CONFIGS["c2"]
+
+
+def _checksum(model) -> list[float]:
+    return [float(p.detach().double().sum().item()) for p in model.parameters()]
+
+
+def test_c2_deterministic_and_adamw_untouched_rows(c2):
+    import bench
+
+    w1 = bench.Workload(c2, torch.device("cuda"), seed=99)
+    table0 = w1.model.adaptive_mimic.item_augmented.weight.detach().clone()
+    batches = [w1.batch() for _ in range(2)]
+    w1.engine.step(*batches[0])
+    torch.cuda.synchronize()
+    touched = torch.cat([batches[0][1], w1.engine.neg_buffer]).unique()
+    mask = torch.ones(c2["I"], dtype=torch.bool, device="cuda")
+    mask[touched] = False
+    rows = mask.nonzero().squeeze(1)[:4096]
+    # torch AdamW, g = 0, step 1, from zero moments: p*(1-lr*wd) - lr/bc1 * m/(sqrt(v)/sqrt(bc2)+eps) with m=v=0
+    p = table0[rows].cpu()
+    opt_p = torch.nn.Parameter(p.clone())
+    opt = torch.optim.AdamW([opt_p], lr=1e-3, weight_decay=0.01)
+    opt_p.grad = torch.zeros_like(p)
+    opt.step()
+    got = w1.model.adaptive_mimic.item_augmented.weight[rows].detach().cpu()
+    assert torch.equal(got, opt_p.detach())
+    w1.engine.step(*batches[1])
+    w1.engine.finish()
+    sums1 = _checksum(w1.model)
+    del w1
+    torch.cuda.empty_cache()
+    w2 = bench.Workload(c2, torch.device("cuda"), seed=99)
+    for b in [w2.batch() for _ in range(2)]:
+        w2.engine.step(*b)
+    w2.engine.finish()
+    assert _checksum(w2.model) == sums1
+
+
+def test_c2_negatives_and_loss(c2):
+    import bench
+
+    w = bench.Workload(c2, torch.device("cuda"), seed=5)
+    losses = []
+    for k in range(30):
+        users, pos = w.batch()
+        w.engine.step(users, pos)
+        if k % 10 == 0:
+            torch.cuda.synchronize()
+            neg = w.engine.neg_buffer.view(-1, c2["N"])
+            assert int(neg.min()) >= 0 and int(neg.max()) < c2["I"]
+            lo = w.csr.offsets[users]
+            vals = w.csr.values.view(c2["U"], -1)[users]  # 20 positives per user (fixed-degree CSR)
+            assert not (neg.unsqueeze(2) == vals.unsqueeze(1)).any()
+            assert lo.numel() == users.numel()
+        losses.append(w.engine.last_losses()["total"])
+    w.engine.finish()
+    assert all(torch.isfinite(torch.tensor(losses)))
+    assert sum(losses[-5:]) / 5 < sum(losses[:5]) / 5

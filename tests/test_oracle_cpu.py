@@ -1,0 +1,88 @@
+"""The CPU oracle against (1) the reference's own known-answer / property tests, restated,
+and (2) the committed golden fixtures (regression guard for the oracle itself)."""
+
+import pytest
+import torch
+
+from golden_io import NAMES, load
+from helpers import named_optimizer_state, rel_err, run_oracle
+from oracle import cpu_reference as ref
+
+
+# ---- reference tests restated on the oracle (tests/test_metrics.py, test_training_utils.py,
+#      test_samplers.py, test_adaptive_mimic.py, test_encoders.py) ---------------------------
+def test_ranking_metrics_known_answer():
+    """tests/test_metrics.py:4-19."""
+    m = ref.ranking_metrics({0: [3, 2, 1], 1: [4, 5, 6]}, {0: {1, 2}, 1: {4}}, [1, 2, 3])
+    assert m.recall[1] == 0.5
+    assert m.precision[1] == 0.5
+    assert m.hit_rate[1] == 0.5
+    assert m.recall[3] > m.recall[1]
+    assert abs(m.mrr - 0.75) < 1e-6
+
+
+def test_metric_lookup_known_answer():
+    """tests/test_training_utils.py:44-52: recall@2 == 1.0 for {0: [1, 2, 3]} vs {0: {2}}."""
+    m = ref.ranking_metrics({0: [1, 2, 3]}, {0: {2}}, [1, 2, 3])
+    assert m.recall[2] == pytest.approx(1.0)
+    assert 5 not in m.precision
+
+
+def test_sampler_excludes_positives():
+    """tests/test_samplers.py:6-19."""
+    torch.manual_seed(0)
+    positives = {0: {1, 2}, 1: {0}}
+    neg = ref.sample_negative_items(torch.tensor([0, 1]), num_items=5, positives=positives, num_negatives=2)
+    assert neg.shape == (2, 2)
+    assert all(i not in positives[0] for i in neg[0].tolist())
+    assert all(i not in positives[1] for i in neg[1].tolist())
+
+
+def test_sampler_errors():
+    with pytest.raises(ValueError):
+        ref.sample_negative_items(torch.tensor([0]), num_items=5, positives={}, num_negatives=0)
+    with pytest.raises(ValueError):
+        ref.sample_negative_items(torch.tensor([0]), num_items=1, positives={}, num_negatives=1)
+    with pytest.raises(RuntimeError):
+        ref.sample_negative_items(torch.tensor([0]), num_items=3, positives={0: {0, 1, 2}}, num_negatives=1)
+
+
+def test_mimic_shapes_and_losses():
+    """tests/test_adaptive_mimic.py:6-33."""
+    mech = ref.OracleMimic(4, 6, 8, init_std=0.01)
+    u = torch.tensor([0, 1])
+    i = torch.tensor([2, 3])
+    ue, ie = torch.zeros((2, 8)), torch.ones((2, 8))
+    au, a_u = ref.gather_aug(mech.user_augmented, u, ue)
+    ai, a_i = ref.gather_aug(mech.item_augmented, i, ie)
+    assert au.shape == ue.shape and ai.shape == ie.shape
+    assert torch.nn.functional.mse_loss(a_u, ie).item() >= 0
+    with pytest.raises(ValueError):
+        ref.gather_aug(mech.item_augmented, i.int(), ie)
+    with pytest.raises(ValueError):
+        ref.OracleMimic(0, 6, 8)
+
+
+def test_gated_tower_shape():
+    """tests/test_encoders.py:6-26."""
+    cfg = {"type": "tower", "id_embedding": {"params": {"embedding_dim": 8}},
+           "feature_encoder": {"type": "linear", "output_dim": 8}, "fusion": "gated",
+           "adaptive_mimic": {"hidden_dim": 16}}
+    tower = ref.build_tower(cfg, num_embeddings=5, feature_dim=4)
+    out = ref.tower_forward(tower, torch.tensor([0, 1, 2]), torch.randn(3, 4), training=False)
+    assert out.shape == (3, 8)
+
+
+# ---- golden fixtures -------------------------------------------------------------------------
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_reproduces_golden(name):
+    prob, arr = load(name)
+    gm, go, gres = run_oracle(prob, lr=0.0, betas=(0.0, 0.999), steps=1)
+    want = torch.from_numpy(arr["grads/loss"])
+    got = torch.tensor([gres[0].total, gres[0].bce, gres[0].mimic_user, gres[0].mimic_item], dtype=torch.float64)
+    assert torch.allclose(got, want, rtol=1e-6, atol=1e-7)
+    for pname, st in named_optimizer_state(gm, go).items():
+        assert rel_err(st["exp_avg"], torch.from_numpy(arr[f"grads/{pname}"])) <= 1e-6, pname
+    sm, so, sres = run_oracle(prob, steps=3)
+    for k, v in sm.state_dict().items():
+        assert torch.allclose(v, torch.from_numpy(arr[f"steps3/param/{k}"]), rtol=1e-6, atol=1e-8), k

@@ -24,8 +24,13 @@
 // slabs and summed in a fixed order by wgrad_reduce_kernel; the bias gradient rides along as
 // an implicit all-ones column of X.
 #include <cstring>
+#include <type_traits>
 
 #include "kernels.h"
+
+#ifndef TTAMM_GEMM_ABLATE
+#define TTAMM_GEMM_ABLATE 0
+#endif
 
 namespace ttamm {
 
@@ -96,29 +101,30 @@ struct Cfg {
 };
 
 // ---- the fused elementwise tail on 4 consecutive columns of one row ----------------------
+// N % 4 == 0 (every layer width is a multiple of 4), so a column group is always whole and
+// every operand access is one float4.  `bias4` is the group's bias (zero if none).
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
 template <int E>
-__device__ __forceinline__ void epilogue4(const KArg(GemmProblem) & P, float4 v, int split, int row, int col) {
+__device__ __forceinline__ void epilogue4(const KArg(GemmProblem) & P, float4 v, float4 bias4, int split, int row,
+                                          int col) {
     const int N = P.N;
-    float x[4] = {v.x, v.y, v.z, v.w};
-    if (E == EPI_STORE || E == EPI_HIDDEN || E == EPI_GATE_HIDDEN || E == EPI_GATE_OUT) {
-        if (P.bias) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (col + e < N) x[e] += P.bias[col + e];
-        }
-    }
+    float x[4] = {v.x + bias4.x, v.y + bias4.y, v.z + bias4.z, v.w + bias4.w};
     if (E == EPI_HIDDEN) {
         u32x4 rnd = {0u, 0u, 0u, 0u};
-        if (P.keep_mask == nullptr && P.keep_prob < 1.0f)
+        const bool drop = P.keep_prob < 1.0f;
+        if (drop && P.keep_mask == nullptr)
             rnd = philox4x32(u32x4{(uint32_t)row, (uint32_t)col, P.rng_c2, P.rng_c3}, P.rng_k0, P.rng_k1);
+        uint32_t km = 0xFFFFFFFFu;
+        if (drop && P.keep_mask) km = *reinterpret_cast<const uint32_t*>(P.keep_mask + (int64_t)row * N + col);
         const uint32_t thresh = keep_threshold(P.keep_prob);
+        const uint32_t w[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             float hv = x[e] > 0.f ? x[e] : 0.f;
-            if (P.keep_prob < 1.0f && col + e < N) {
-                bool keep;
-                if (P.keep_mask) keep = P.keep_mask[(int64_t)row * N + col + e] != 0;
-                else keep = (e == 0 ? rnd.x : e == 1 ? rnd.y : e == 2 ? rnd.z : rnd.w) < thresh;
+            if (drop) {
+                const bool keep = P.keep_mask ? ((km >> (8 * e)) & 0xFFu) != 0 : w[e] < thresh;
                 hv = hv * (keep ? P.inv_keep : 0.f);
             }
             x[e] = hv;
@@ -128,53 +134,46 @@ __device__ __forceinline__ void epilogue4(const KArg(GemmProblem) & P, float4 v,
         for (int e = 0; e < 4; ++e) x[e] = x[e] > 0.f ? x[e] : 0.f;
     } else if (E == EPI_GATE_OUT) {
         const float* efr = P.aux0 + (int64_t)row * P.ld_aux0;
-        const int64_t oo = (int64_t)row * P.ld_out + col;
-        const float* arow = P.table ? P.table + P.idx[row] * (int64_t)N : nullptr;
+        const float4 ev = ld4(efr + col), fv = ld4(efr + N + col);
+        const float e4[4] = {ev.x, ev.y, ev.z, ev.w}, f4[4] = {fv.x, fv.y, fv.z, fv.w};
+        float g[4], t[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            if (col + e >= N) continue;
-            const float g = sigmoidf_(x[e]);
-            const float t = g * efr[col + e] + (1.0f - g) * efr[N + col + e];
-            P.out1[oo + e] = g;
-            P.out2[oo + e] = t;
-            if (arow) {
-                const float a = arow[col + e];
-                P.out3[oo + e] = a;
-                x[e] = t + a;
-            } else {
-                x[e] = t;
-            }
+            g[e] = sigmoidf_(x[e]);
+            t[e] = g[e] * e4[e] + (1.0f - g[e]) * f4[e];
+        }
+        const int64_t oo = (int64_t)row * P.ld_out + col;
+        st4(P.out1 + oo, make_float4(g[0], g[1], g[2], g[3]));
+        st4(P.out2 + oo, make_float4(t[0], t[1], t[2], t[3]));
+        if (P.table) {
+            const float4 a = ld4(P.table + P.idx[row] * (int64_t)N + col);
+            st4(P.out3 + oo, a);
+            x[0] = t[0] + a.x, x[1] = t[1] + a.y, x[2] = t[2] + a.z, x[3] = t[3] + a.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[e] = t[e];
         }
     } else if (E == EPI_DGRAD_RELU) {
-        const float* z = P.aux0 + (int64_t)row * P.ld_aux0 + col;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-            if (col + e < N) x[e] = z[e] > 0.f ? x[e] : 0.f;
+        const float4 z = ld4(P.aux0 + (int64_t)row * P.ld_aux0 + col);
+        x[0] = z.x > 0.f ? x[0] : 0.f, x[1] = z.y > 0.f ? x[1] : 0.f;
+        x[2] = z.z > 0.f ? x[2] : 0.f, x[3] = z.w > 0.f ? x[3] : 0.f;
     } else if (E == EPI_DGRAD_GATE_EF) {
         const int D = N >> 1;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int c = col + e;
-            if (c >= N) continue;
-            const int cc = c < D ? c : c - D;
-            const float dt = P.aux1[(int64_t)row * P.ld_aux1 + cc];
-            const float g = P.aux2[(int64_t)row * P.ld_aux1 + cc];
-            x[e] = c < D ? x[e] + dt * g : x[e] + dt * (1.0f - g);
+        const int cc = col < D ? col : col - D;  // a group never straddles D (D % 4 == 0)
+        const float4 dt = ld4(P.aux1 + (int64_t)row * P.ld_aux1 + cc);
+        const float4 g = ld4(P.aux2 + (int64_t)row * P.ld_aux1 + cc);
+        if (col < D) {
+            x[0] += dt.x * g.x, x[1] += dt.y * g.y, x[2] += dt.z * g.z, x[3] += dt.w * g.w;
+        } else {
+            x[0] += dt.x * (1.0f - g.x), x[1] += dt.y * (1.0f - g.y);
+            x[2] += dt.z * (1.0f - g.z), x[3] += dt.w * (1.0f - g.w);
         }
     } else if (E == EPI_DGRAD_HIDDEN) {
-        const float* hp = P.aux0 + (int64_t)row * P.ld_aux0 + col;
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-            if (col + e < N) x[e] = hp[e] > 0.f ? x[e] * P.inv_keep : 0.f;
+        const float4 hv = ld4(P.aux0 + (int64_t)row * P.ld_aux0 + col);
+        x[0] = hv.x > 0.f ? x[0] * P.inv_keep : 0.f, x[1] = hv.y > 0.f ? x[1] * P.inv_keep : 0.f;
+        x[2] = hv.z > 0.f ? x[2] * P.inv_keep : 0.f, x[3] = hv.w > 0.f ? x[3] * P.inv_keep : 0.f;
     }
-    float* C = P.C + (int64_t)split * P.slab_stride + (int64_t)row * P.ldc + col;
-    if (col + 3 < N && (P.ldc % 4 == 0) && aligned16(C)) {
-        *reinterpret_cast<float4*>(C) = make_float4(x[0], x[1], x[2], x[3]);
-    } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-            if (col + e < N) C[e] = x[e];
-    }
+    st4(P.C + (int64_t)split * P.slab_stride + (int64_t)row * P.ldc + col, make_float4(x[0], x[1], x[2], x[3]));
 }
 
 template <class CF, int E>
@@ -238,59 +237,18 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
     }
     float4 ra[CF::A_LOADS], rb[CF::B_LOADS];
 
-    auto load_tile = [&](int k0) {
+    // Interior blocks with whole k-tiles take the FAST variant of the main loop: pointers
+    // resolved once, plain float4 loads, no masking.  Edge blocks take the masked variant.
+    // The choice is block-uniform and made once, outside the loop.
+    const bool fast = ((k_end - k_begin) % BK == 0) && (n0 + BN <= N) &&
+                      (AK ? (m0 + BM <= P.a_cols) : (m0 + BM <= M));
+    const float* b_rp[CF::B_LOADS];
 #pragma unroll
-        for (int it = 0; it < CF::A_LOADS; ++it) {
-            if (!AK) {
-                ra[it] = raw4(a_rp[it], k0 + a_c[it], P.lda);
-            } else {
-                const int k = min(k0 + a_r[it], k_end - 1);
-                ra[it] = raw4(P.A + kidx[k - k_begin] * P.lda, m0 + a_c[it], P.lda);
-            }
-        }
-#pragma unroll
-        for (int it = 0; it < CF::B_LOADS; ++it) {
-            const int lin = tid + it * kThreads;
-            if (!BKM) {
-                const int n = min(n0 + (lin >> 2), N - 1);
-                rb[it] = raw4(P.B + (int64_t)n * P.ldb, k0 + (lin & 3) * 4, P.ldb);
-            } else {
-                const int k = min(k0 + lin / (BN / 4), k_end - 1);
-                rb[it] = raw4(P.B + (int64_t)k * P.ldb, n0 + (lin % (BN / 4)) * 4, P.ldb);
-            }
-        }
-    };
-    auto store_tile = [&](int buf, int k0) {
-        float* as = As + buf * CF::A_STAGE;
-        float* bs = Bs + buf * CF::B_STAGE;
-#pragma unroll
-        for (int it = 0; it < CF::A_LOADS; ++it) {
-            const int lin = tid + it * kThreads;
-            if (lin >= CF::A_F4) continue;
-            if (!AK) {
-                const float4 v = mask4(ra[it], k0 + a_c[it], k_end, P.lda, -1, a_ok[it]);
-                *reinterpret_cast<float4*>(as + a_r[it] * SK + a_c[it]) = v;
-            } else {
-                const float4 v =
-                    mask4(ra[it], m0 + a_c[it], P.a_cols, P.lda, P.a_ones_col, k0 + a_r[it] < k_end);
-                *reinterpret_cast<float4*>(as + a_r[it] * BM + a_c[it]) = v;
-            }
-        }
-#pragma unroll
-        for (int it = 0; it < CF::B_LOADS; ++it) {
-            const int lin = tid + it * kThreads;
-            if (lin >= CF::B_F4) continue;
-            if (!BKM) {
-                const int n = n0 + (lin >> 2), c = k0 + (lin & 3) * 4;
-                *reinterpret_cast<float4*>(bs + (lin >> 2) * SK + (lin & 3) * 4) =
-                    mask4(rb[it], c, k_end, P.ldb, -1, n < N);
-            } else {
-                const int kr = lin / (BN / 4), nc = (lin % (BN / 4)) * 4;
-                *reinterpret_cast<float4*>(bs + kr * BN + nc) =
-                    mask4(rb[it], n0 + nc, N, P.ldb, -1, k0 + kr < k_end);
-            }
-        }
-    };
+    for (int it = 0; it < CF::B_LOADS; ++it) {
+        const int lin = tid + it * kThreads;
+        if (!BKM) b_rp[it] = P.B + (int64_t)min(n0 + (lin >> 2), N - 1) * P.ldb + (lin & 3) * 4;
+        else b_rp[it] = P.B + (int64_t)(lin / (BN / 4)) * P.ldb + n0 + (lin % (BN / 4)) * 4;
+    }
 
     f32x16 acc[I][J];
 #pragma unroll
@@ -300,52 +258,126 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    const int nk = k_end > k_begin ? (k_end - k_begin + BK - 1) / BK : 0;
-    if (nk > 0) {
-        load_tile(k_begin);
-        store_tile(0, k_begin);
-    }
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        const int buf = kt & 1;
-        if (kt + 1 < nk) load_tile(k_begin + (kt + 1) * BK);
-        const float* as = As + buf * CF::A_STAGE;
-        const float* bs = Bs + buf * CF::B_STAGE;
+    auto mainloop = [&](auto fast_tag) {
+        constexpr bool FAST = decltype(fast_tag)::value;
+        auto load_tile = [&](int k0) {
 #pragma unroll
-        for (int s4 = 0; s4 < 2; ++s4) {
-            float4 af[I], bf[J];
-#pragma unroll
-            for (int i = 0; i < I; ++i) {
-                const int m = wm * TM + i * 32 + li;
+            for (int it = 0; it < CF::A_LOADS; ++it) {
                 if (!AK) {
-                    af[i] = *reinterpret_cast<const float4*>(as + m * SK + 8 * h + 4 * s4);
+                    ra[it] = FAST ? *reinterpret_cast<const float4*>(a_rp[it] + k0 + a_c[it])
+                                  : raw4(a_rp[it], k0 + a_c[it], P.lda);
                 } else {
-                    const float* c = as + (8 * h + 4 * s4) * BM + m;
-                    af[i] = make_float4(c[0], c[BM], c[2 * BM], c[3 * BM]);
+                    const int k = FAST ? k0 + a_r[it] : min(k0 + a_r[it], k_end - 1);
+                    const float* rp = P.A + kidx[k - k_begin] * P.lda;
+                    ra[it] = FAST ? *reinterpret_cast<const float4*>(rp + m0 + a_c[it]) : raw4(rp, m0 + a_c[it], P.lda);
                 }
             }
 #pragma unroll
-            for (int j = 0; j < J; ++j) {
-                const int n = wn * TN + j * 32 + li;
+            for (int it = 0; it < CF::B_LOADS; ++it) {
+                const int lin = tid + it * kThreads;
                 if (!BKM) {
-                    bf[j] = *reinterpret_cast<const float4*>(bs + n * SK + 8 * h + 4 * s4);
+                    rb[it] = FAST ? *reinterpret_cast<const float4*>(b_rp[it] + k0)
+                                  : raw4(b_rp[it] - (lin & 3) * 4, k0 + (lin & 3) * 4, P.ldb);
+                } else if (FAST) {
+                    rb[it] = *reinterpret_cast<const float4*>(b_rp[it] + (int64_t)k0 * P.ldb);
                 } else {
-                    const float* c = bs + (8 * h + 4 * s4) * BN + n;
-                    bf[j] = make_float4(c[0], c[BN], c[2 * BN], c[3 * BN]);
+                    const int k = min(k0 + lin / (BN / 4), k_end - 1);
+                    rb[it] = raw4(P.B + (int64_t)k * P.ldb, n0 + (lin % (BN / 4)) * 4, P.ldb);
+                }
+            }
+        };
+        auto store_tile = [&](int buf, int k0) {
+            float* as = As + buf * CF::A_STAGE;
+            float* bs = Bs + buf * CF::B_STAGE;
+#pragma unroll
+            for (int it = 0; it < CF::A_LOADS; ++it) {
+                const int lin = tid + it * kThreads;
+                if (lin >= CF::A_F4) continue;
+                if (!AK) {
+                    const float4 v = FAST ? ra[it] : mask4(ra[it], k0 + a_c[it], k_end, P.lda, -1, a_ok[it]);
+                    *reinterpret_cast<float4*>(as + a_r[it] * SK + a_c[it]) = v;
+                } else {
+                    const float4 v = FAST ? ra[it]
+                                          : mask4(ra[it], m0 + a_c[it], P.a_cols, P.lda, P.a_ones_col,
+                                                  k0 + a_r[it] < k_end);
+                    *reinterpret_cast<float4*>(as + a_r[it] * BM + a_c[it]) = v;
                 }
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int i = 0; i < I; ++i)
-#pragma unroll
-                    for (int j = 0; j < J; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(af[i], q), f4get(bf[j], q), acc[i][j],
-                                                                         0, 0, 0);
+            for (int it = 0; it < CF::B_LOADS; ++it) {
+                const int lin = tid + it * kThreads;
+                if (lin >= CF::B_F4) continue;
+                if (!BKM) {
+                    const int n = n0 + (lin >> 2), c = k0 + (lin & 3) * 4;
+                    *reinterpret_cast<float4*>(bs + (lin >> 2) * SK + (lin & 3) * 4) =
+                        FAST ? rb[it] : mask4(rb[it], c, k_end, P.ldb, -1, n < N);
+                } else {
+                    const int kr = lin / (BN / 4), nc = (lin % (BN / 4)) * 4;
+                    *reinterpret_cast<float4*>(bs + kr * BN + nc) =
+                        FAST ? rb[it] : mask4(rb[it], n0 + nc, N, P.ldb, -1, k0 + kr < k_end);
+                }
+            }
+        };
+
+        const int nk = k_end > k_begin ? (k_end - k_begin + BK - 1) / BK : 0;
+        if (nk > 0) {
+            load_tile(k_begin);
+            store_tile(0, k_begin);
         }
-        if (kt + 1 < nk) store_tile(buf ^ 1, k_begin + (kt + 1) * BK);
         __syncthreads();
-    }
+        for (int kt = 0; kt < nk; ++kt) {
+            const int buf = kt & 1;
+#if TTAMM_GEMM_ABLATE == 1  // developer ablation: no k-loop traffic (measures the MFMA/LDS loop)
+            if (false) load_tile(k_begin + (kt + 1) * BK);
+#else
+            if (kt + 1 < nk) load_tile(k_begin + (kt + 1) * BK);
+#endif
+            const float* as = As + buf * CF::A_STAGE;
+            const float* bs = Bs + buf * CF::B_STAGE;
+#pragma unroll
+            for (int s4 = 0; s4 < 2; ++s4) {
+                float4 af[I], bf[J];
+#pragma unroll
+                for (int i = 0; i < I; ++i) {
+                    const int m = wm * TM + i * 32 + li;
+                    if (!AK) {
+                        af[i] = *reinterpret_cast<const float4*>(as + m * SK + 8 * h + 4 * s4);
+                    } else {
+                        const float* c = as + (8 * h + 4 * s4) * BM + m;
+                        af[i] = make_float4(c[0], c[BM], c[2 * BM], c[3 * BM]);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                    const int n = wn * TN + j * 32 + li;
+                    if (!BKM) {
+                        bf[j] = *reinterpret_cast<const float4*>(bs + n * SK + 8 * h + 4 * s4);
+                    } else {
+                        const float* c = bs + (8 * h + 4 * s4) * BN + n;
+                        bf[j] = make_float4(c[0], c[BN], c[2 * BN], c[3 * BN]);
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int i = 0; i < I; ++i)
+#pragma unroll
+                        for (int j = 0; j < J; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(af[i], q), f4get(bf[j], q),
+                                                                             acc[i][j], 0, 0, 0);
+            }
+#if TTAMM_GEMM_ABLATE == 1
+            if (false) store_tile(buf ^ 1, k_begin + (kt + 1) * BK);
+#else
+            if (kt + 1 < nk) store_tile(buf ^ 1, k_begin + (kt + 1) * BK);
+#endif
+#if TTAMM_GEMM_ABLATE != 2
+            __syncthreads();
+#endif
+        }
+    };
+    if (fast) mainloop(std::true_type{});
+    else mainloop(std::false_type{});
 
     // ---- epilogue through LDS, in row slices ----------------------------------------------------
     float* Cs = lds;
@@ -363,12 +395,20 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
                     }
         }
         __syncthreads();
+        // each thread owns one 4-column group (bias loaded once) and walks rows
         constexpr int C4 = BN / 4;
-        for (int idx = tid; idx < CF::EPI_ROWS * C4; idx += kThreads) {
-            const int rr = idx / C4, c4 = idx - rr * C4;
-            const int row = m0 + row_lo + rr, col = n0 + c4 * 4;
-            if (row < M && col < N)
-                epilogue4<E>(P, *reinterpret_cast<const float4*>(Cs + rr * CF::CLD + c4 * 4), split, row, col);
+        constexpr int RSTEP = kThreads / C4;
+        const int c4 = tid % C4, r0 = tid / C4;
+        const int col = n0 + c4 * 4;
+        if (r0 < RSTEP && col < N) {
+            const bool has_bias = (E == EPI_STORE || E == EPI_HIDDEN || E == EPI_GATE_HIDDEN || E == EPI_GATE_OUT) &&
+                                  P.bias != nullptr;
+            const float4 bias4 = has_bias ? ld4(P.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+            for (int rr = r0; rr < CF::EPI_ROWS; rr += RSTEP) {
+                const int row = m0 + row_lo + rr;
+                if (row < M) epilogue4<E>(P, ld4(Cs + rr * CF::CLD + c4 * 4), bias4, split, row, col);
+            }
         }
         __syncthreads();
     }
@@ -440,6 +480,7 @@ int launch_gemm(GemmBatch& b, hipStream_t s) {
         TTAMM_REQUIRE(p.epi == b.p[0].epi && p.b_kn == bkn && !p.a_kmaj, "gemm: grouped problems must share a variant");
         TTAMM_REQUIRE(p.lda % 4 == 0 && p.ldb % 4 == 0 && ((uintptr_t)p.A | (uintptr_t)p.B) % 16 == 0,
                       "gemm: operands must be 16-byte aligned with leading dims % 4 == 0");
+        TTAMM_REQUIRE(p.N % 4 == 0 && p.ldc % 4 == 0 && (uintptr_t)p.C % 16 == 0, "gemm: output must be float4-aligned");
         p.k_split = p.K;
         p.slab_stride = 0;
         maxN = p.N > maxN ? p.N : maxN;

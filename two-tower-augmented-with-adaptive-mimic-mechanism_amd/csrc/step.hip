@@ -257,6 +257,9 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
             p.M = (int)w.R;
             p.N = L.out_features;
             p.K = L.in_features;
+            // the feature rows and the padded weight are zero beyond F: run K to the padded
+            // width so every k-tile is whole (fast GEMM path)
+            if (l == 0 && w.wpad && t.feat_ld >= round4(L.in_features)) p.K = round4(L.in_features);
             p.bias = L.bias;
             if (l + 1 < t.n_linear) {
                 p.epi = EPI_HIDDEN;

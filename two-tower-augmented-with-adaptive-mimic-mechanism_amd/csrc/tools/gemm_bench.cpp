@@ -1,0 +1,128 @@
+// Developer micro-benchmark of the step's GEMM shapes (C2: R = 57344 tower rows).
+// Build: make -C csrc tools ; run on the GPU box: ./build/gemm_bench
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "../kernels.h"
+
+using namespace ttamm;
+
+#define CK(x)                                                                      \
+    do {                                                                           \
+        hipError_t e = (x);                                                        \
+        if (e != hipSuccess) {                                                     \
+            printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); \
+            return 1;                                                              \
+        }                                                                          \
+    } while (0)
+
+static float* dev_rand(size_t n, std::mt19937& g, float scale = 1.f) {
+    std::vector<float> h(n);
+    std::normal_distribution<float> d(0.f, scale);
+    for (auto& x : h) x = d(g);
+    float* p;
+    if (hipMalloc(&p, n * 4) != hipSuccess) return nullptr;
+    if (hipMemcpy(p, h.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    return p;
+}
+
+int main() {
+    std::mt19937 g(1);
+    const int R = 57344, F = 608, H = 192, D = 96;
+    float* X = dev_rand((size_t)2000000 * F, g, 0.3f);
+    float* W1 = dev_rand((size_t)H * F, g, 0.05f);
+    float* b1 = dev_rand(H, g, 0.01f);
+    float* Hb = dev_rand((size_t)R * H, g);
+    float* dY = dev_rand((size_t)R * H, g);
+    float* W2 = dev_rand((size_t)D * H, g, 0.05f);
+    float* dF = dev_rand((size_t)R * D, g);
+    float *C, *slab, *gw, *gb;
+    CK(hipMalloc(&C, (size_t)R * H * 4));
+    CK(hipMalloc(&slab, (size_t)(R / 512 + 1) * (F + 1) * H * 4));
+    CK(hipMalloc(&gw, (size_t)H * F * 4));
+    CK(hipMalloc(&gb, (size_t)H * 4));
+    std::vector<int64_t> hidx(R);
+    std::uniform_int_distribution<int64_t> ui(0, 1999999);
+    for (auto& v : hidx) v = ui(g);
+    int64_t* idx;
+    CK(hipMalloc(&idx, R * 8));
+    CK(hipMemcpy(idx, hidx.data(), R * 8, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+
+    auto base = [] {
+        GemmProblem p;
+        std::memset(&p, 0, sizeof(p));
+        p.keep_prob = 1.f;
+        p.inv_keep = 1.f;
+        p.a_ones_col = -1;
+        return p;
+    };
+    auto time_it = [&](const char* name, double flop, auto fn) -> int {
+        for (int i = 0; i < 3; ++i) fn();
+        CK(hipEventRecord(e0, 0));
+        const int iters = 20;
+        for (int i = 0; i < iters; ++i) fn();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        const double us = ms * 1e3 / iters;
+        printf("%-34s %9.1f us  %7.1f TF/s  (%s)\n", name, us, flop / (us * 1e-6) / 1e12, ttamm_last_error());
+        return 0;
+    };
+    // layer-1 forward: [R, F](gathered) x W1^T -> [R, H], bias+ReLU+dropout
+    time_it("fwd L1 R x 608 -> 192 (gather)", 2.0 * R * F * H, [&] {
+        GemmBatch b;
+        std::memset(&b, 0, sizeof(b));
+        GemmProblem p = base();
+        p.A = X, p.a_idx = idx, p.lda = F, p.B = W1, p.ldb = F, p.M = R, p.N = H, p.K = F;
+        p.epi = EPI_HIDDEN, p.C = C, p.ldc = H, p.bias = b1, p.keep_prob = 0.85f, p.inv_keep = 1.f / 0.85f;
+        b.p[0] = p, b.count = 1;
+        launch_gemm(b, 0);
+    });
+    time_it("fwd L2 R x 192 -> 96", 2.0 * R * H * D, [&] {
+        GemmBatch b;
+        std::memset(&b, 0, sizeof(b));
+        GemmProblem p = base();
+        p.A = Hb, p.lda = H, p.B = W2, p.ldb = H, p.M = R, p.N = D, p.K = H;
+        p.epi = EPI_STORE, p.C = C, p.ldc = D, p.bias = b1;
+        b.p[0] = p, b.count = 1;
+        launch_gemm(b, 0);
+    });
+    time_it("dgrad R x 96 -> 192 (W KN)", 2.0 * R * H * D, [&] {
+        GemmBatch b;
+        std::memset(&b, 0, sizeof(b));
+        GemmProblem p = base();
+        p.A = dF, p.lda = D, p.B = W2, p.ldb = H, p.b_kn = 1, p.M = R, p.N = H, p.K = D;
+        p.epi = EPI_DGRAD_HIDDEN, p.C = C, p.ldc = H, p.aux0 = Hb, p.ld_aux0 = H;
+        b.p[0] = p, b.count = 1;
+        launch_gemm(b, 0);
+    });
+    time_it("wgrad W1 192 x 608 over R (gather)", 2.0 * R * (F + 1) * H, [&] {
+        WgradBatch wb;
+        std::memset(&wb, 0, sizeof(wb));
+        WgradProblem w{};
+        w.dY = dY, w.ld_dy = H, w.X = X, w.x_idx = idx, w.ld_x = F, w.R = R, w.M = H, w.N = F - 3;
+        w.grad_w = gw, w.grad_b = gb, w.slab = slab;
+        wb.p[0] = w, wb.count = 1;
+        launch_wgrad(wb, 0);
+    });
+    time_it("wgrad W2 96 x 192 over R", 2.0 * R * (H + 1) * D, [&] {
+        WgradBatch wb;
+        std::memset(&wb, 0, sizeof(wb));
+        WgradProblem w{};
+        w.dY = dF, w.ld_dy = D, w.X = Hb, w.ld_x = H, w.R = R, w.M = D, w.N = H;
+        w.grad_w = gw, w.grad_b = gb, w.slab = slab;
+        wb.p[0] = w, wb.count = 1;
+        launch_wgrad(wb, 0);
+    });
+    CK(hipDeviceSynchronize());
+    printf("done\n");
+    return 0;
+}
