@@ -11,7 +11,11 @@ ID tables.  Synthetic data of that shape, random-init weights; inputs resident i
 
 One step = one call of ttamm_train_step on one batch (sampling, forward, loss, backward,
 both optimizers).  `value` = interactions (positives) per second over all ranks.
-Multi-GPU: one process per GPU (torch.distributed.run), every rank runs its own batch.
+Multi-GPU (weak scaling): one process per GPU (torch.distributed.run, RCCL).  Rank r owns
+users and items with id % N == r — C2-sized shards, so the global model is N x C2 — and runs
+the row-sharded step of ttamm/sharded.py on a C2 batch of its own users: item requests and
+(t | a) / (dT | dA) rows go through all-to-alls, the MLP / gate gradients through one
+all-reduce.
 
 The JSON line also carries
   roofline:     the dominant kernel (the AdamW(g=0) sweep over the mimic tables) timed with
@@ -87,18 +91,23 @@ def zipf_items(n: int, I: int, s: float, device, gen: torch.Generator, perm: tor
 
 
 class Workload:
-    def __init__(self, c: dict, device, seed: int):
+    """C2 data + model on one GPU, or rank `rank`'s C2-sized shard of an N x C2 model."""
+
+    def __init__(self, c: dict, device, seed: int, world: int = 1, rank: int = 0, step_seed: int | None = None):
         import ttamm
         from ttamm.samplers import PositivesCSR
 
         self.c = c
+        self.world = world
         gen = torch.Generator(device=device).manual_seed(seed)
         torch.manual_seed(seed)
-        U, I, F = c["U"], c["I"], c["F"]
+        U, I, F = c["U"], c["I"], c["F"]  # this rank's rows
+        Ig = I * world  # global item count
         self.item_features = make_item_features(I, F, device, gen)
-        perm = torch.randperm(I, device=device, generator=gen)
+        # popularity ranks over the global catalogue: same permutation on every rank
+        perm = torch.randperm(Ig, device=device, generator=torch.Generator(device=device).manual_seed(7))
         per = c["pos_per_user"]
-        items = zipf_items(U * per, I, 1.05, device, gen, perm).view(U, per)
+        items = zipf_items(U * per, Ig, 1.05, device, gen, perm).view(U, per)
         items, _ = torch.sort(items, dim=1)
         offsets = torch.arange(0, U * per + 1, per, device=device, dtype=torch.long)
         self.csr = PositivesCSR(offsets, items.reshape(-1).contiguous(), U, per)
@@ -108,7 +117,10 @@ class Workload:
         full = self.item_features.as_strided((I, Fp), (Fp, 1))
         for lo in range(0, U, 16384):
             hi = min(U, lo + 16384)
-            uf[lo:hi] = full[items[lo:hi].reshape(-1)].view(hi - lo, per, Fp).mean(dim=1)
+            # sharded: the positives' feature rows live on their owners; a local row of the
+            # same shape stands in (the values do not change the work)
+            rows = torch.div(items[lo:hi].reshape(-1), world, rounding_mode="floor")
+            uf[lo:hi] = full[rows].view(hi - lo, per, Fp).mean(dim=1)
         self.user_features = uf[:, :F]
         # interactions: every (user, positive) pair, shuffled once (DataLoader shuffle=True)
         self.users_all = torch.arange(U, device=device).repeat_interleave(per)
@@ -124,11 +136,17 @@ class Workload:
         self.model = ttamm.TwoTowerModel(ue, ie, similarity=ttamm.DotProductSimilarity(), adaptive_mimic=mm)
         dense, sparse = ttamm._collect_parameter_groups(self.model)
         self.opts = [torch.optim.AdamW(dense, lr=1e-3, weight_decay=0.01), torch.optim.SparseAdam(sparse, lr=1e-3)]
-        self.engine = ttamm.FusedTrainStep(
-            self.model, self.opts, negatives_per_positive=c["N"], positives=self.csr,
-            user_features=self.user_features, item_features=self.item_features,
-            loss_weights={"mimic_user": 0.15, "mimic_item": 0.15}, max_batch=c["B"], seed=seed,
-        )
+        kw = dict(negatives_per_positive=c["N"], positives=self.csr, user_features=self.user_features,
+                  item_features=self.item_features, loss_weights={"mimic_user": 0.15, "mimic_item": 0.15},
+                  max_batch=c["B"])
+        if world == 1:
+            self.engine = ttamm.FusedTrainStep(self.model, self.opts, seed=seed, **kw)
+        else:
+            from ttamm.sharded import ShardedTrainStep, TorchComm
+
+            # step_seed: the same on every rank (the Philox streams are keyed by global position)
+            self.engine = ShardedTrainStep(self.model, self.opts, world_size=world, rank=rank, num_items=Ig,
+                                           comm=TorchComm(), seed=step_seed, **kw)
         self.cursor = 0
 
     def batch(self):
@@ -223,7 +241,7 @@ def main() -> None:
 
     from ttamm import _lib
 
-    w = Workload(c, device, args.seed + rank)
+    w = Workload(c, device, args.seed + rank, world=world, rank=rank, step_seed=args.seed)
     eng = w.engine
     for _ in range(args.warmup):
         u, p = w.batch()
@@ -259,7 +277,9 @@ def main() -> None:
     B, U, I, D = c["B"], c["U"], c["I"], c["D"]
     interactions = args.steps * B * world
     value = interactions / elapsed
-    sweep_bytes = 24 * (U + I) * D
+    # one process: one sweep over both mimic tables; sharded: the events bracket the owner's
+    # item-table sweep (ITEM_BWD phase)
+    sweep_bytes = 24 * (U + I) * D if world == 1 else 24 * I * D
     achieved = sweep_bytes / (sweep_ms * 1e-3) / 1e9
     traffic = load_traffic(args.config)
     out = {
@@ -277,17 +297,19 @@ def main() -> None:
         "data": "synthetic: C2 shapes, Zipf(1.05) positives (20/user), features shaped like features.py, "
                 "random-init weights",
         "config": {
-            "workload": f"{args.config.upper()}: {I} items x {U} users, D={D}, MLP {c['F']}->{c['H']}->{D} "
-                        f"(ReLU, dropout {c['dropout']}), gated fusion, adaptive mimic, B={B}, "
-                        f"N={c['N']} sampled negatives, AdamW + SparseAdam",
+            "workload": f"{args.config.upper()}: {I * world} items x {U * world} users, D={D}, "
+                        f"MLP {c['F']}->{c['H']}->{D} (ReLU, dropout {c['dropout']}), gated fusion, adaptive mimic, "
+                        f"B={B} per GPU, N={c['N']} sampled negatives, AdamW + SparseAdam",
             "global_batch": B * world,
             "negatives_per_positive": c["N"],
-            "parallelism": f"dp{world}" if world > 1 else "single",
+            "parallelism": f"row-sharded tables x{world} (all-to-all) + replicated MLP (all-reduce)"
+                           if world > 1 else "single",
         },
         "final_loss": round(loss, 6),
         "roofline": {
             "bound": "hbm",
-            "kernel": "dense_sweep_kernel (AdamW g=0 over user+item mimic tables)",
+            "kernel": "dense_sweep_kernel (AdamW g=0 over user+item mimic tables)" if world == 1
+                  else "dense_sweep_kernel (AdamW g=0 over the rank's item mimic table shard)",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 1
+#define TTAMM_ABI_VERSION 2
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -49,6 +49,28 @@ extern "C" {
 /* Which optimizer owns a row table (training.py:276-309, :1311-1350). */
 #define TTAMM_OPT_SPARSE_ADAM 0 /* nn.Embedding(sparse=True) -> torch.optim.SparseAdam      */
 #define TTAMM_OPT_DENSE 1       /* every other parameter       -> AdamW / Adam (dense group) */
+
+/* Phases of one training step (ttamm_step_args.phase).  0 = the whole step in one process.
+ * A row-sharded multi-GPU step (item rows owned by rank i % W) runs them with
+ * exchanges in between; several bits may be set in one call and run in this order:
+ *   SAMPLE   requester: draw negatives for its users into b.neg_items
+ *            [all-to-all: requested item ids (+ their global request positions) -> owners]
+ *   ITEM_FWD owner: item tower over the requested local rows           -> item_fwd_out (t | a)
+ *            [all-to-all: (t | a) rows back to the requesters]  (overlaps USER_FWD)
+ *   USER_FWD requester: user tower forward
+ *   USER     requester: scores + losses, user-tower backward, user-table updates;
+ *            (dT | dA) of its item requests                            -> item_bwd_out
+ *            [all-to-all: (dT | dA) rows -> owners]
+ *   ITEM_BWD owner: item-tower backward, item-table updates
+ *            [all-reduce (sum): the replicated-weight gradient arena dense_grads]
+ *   DENSE    AdamW/Adam on the replicated feature-encoder and gate weights */
+#define TTAMM_PHASE_ALL 0
+#define TTAMM_PHASE_SAMPLE 1
+#define TTAMM_PHASE_ITEM_FWD 2
+#define TTAMM_PHASE_USER_FWD 4
+#define TTAMM_PHASE_USER 8
+#define TTAMM_PHASE_ITEM_BWD 16
+#define TTAMM_PHASE_DENSE 32
 
 /* Device-side status word bits (written by kernels, read by the host at epoch end). */
 #define TTAMM_STATUS_SAMPLER_EXHAUSTED 1u /* samplers.py:78-81 */
@@ -141,6 +163,27 @@ typedef struct ttamm_step_args {
     size_t workspace_bytes;
     void* timing_events[2]; /* optional hipEvent_t pair recorded around the dense
                                mimic-table AdamW sweep (bench roofline); NULL = off   */
+    /* ---- row-sharded multi-GPU step (phase != TTAMM_PHASE_ALL) ----------------------
+     * The same workspace must be passed to every phase of a step.                        */
+    int32_t phase;                /* TTAMM_PHASE_* bits                                      */
+    int64_t row_base;             /* global position of this rank's first interaction: keys
+                                     the negative-sampling and dropout streams so W ranks
+                                     draw exactly what one process would over the global
+                                     batch                                                   */
+    int64_t global_batch;         /* interactions over all ranks; losses are normalised by it
+                                     and loss_out holds this rank's share (0 = batch)        */
+    int64_t num_items_global;     /* sampler range (0 = item.id.rows)                        */
+    const int64_t* item_rows;     /* owner: local item rows requested this step              */
+    const int64_t* item_row_keys; /* owner: global request position of each requested row   */
+    int64_t n_item_rows;
+    int64_t item_rows_capacity;   /* workspace bound for n_item_rows                         */
+    float* item_fwd_out;          /* owner:     [n_item_rows, 2*dim] (t | a)                 */
+    const float* item_fwd_in;     /* requester: [batch*(1+num_neg), 2*dim] (t | a), rows
+                                     ordered [positives; negatives (b-major)]               */
+    float* item_bwd_out;          /* requester: [batch*(1+num_neg), 2*dim] (dT | dA)         */
+    const float* item_bwd_in;     /* owner:     [n_item_rows, 2*dim] (dT | dA)               */
+    float* dense_grads;           /* replicated-weight gradient arena
+                                     (ttamm_dense_grad_floats floats)                        */
 } ttamm_step_args;
 
 /* ---------------------------------------------------------------------------------- */
@@ -155,6 +198,10 @@ const char* ttamm_last_error(void);
  * AdamW (dense group incl. the full mimic tables) and SparseAdam (ID tables). */
 size_t ttamm_train_step_workspace_size(const ttamm_step_args* args);
 int ttamm_train_step(const ttamm_step_args* args, void* stream);
+
+/* Size (floats) of the replicated-weight gradient arena of a sharded step: both towers'
+ * feature-encoder and gate weight+bias gradients, contiguous (the all-reduce buffer). */
+int64_t ttamm_dense_grad_floats(const ttamm_step_args* args);
 
 /* nn.Embedding forward / AdaptiveMimicMechanism._gather_and_reshape
  * (encoders.py:222-223, adaptive_mimic.py:97-105): out[r, :] = table[idx[r], :]. */

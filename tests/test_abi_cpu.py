@@ -21,7 +21,7 @@ def header_functions() -> list[str]:
 
 def test_header_parses_as_c_and_cxx(tmp_path):
     src = tmp_path / "h.c"
-    src.write_text(f'#include "{HEADER}"\nint main(void) {{ return TTAMM_ABI_VERSION == 1 ? 0 : 1; }}\n')
+    src.write_text(f'#include "{HEADER}"\nint main(void) {{ return TTAMM_ABI_VERSION == 2 ? 0 : 1; }}\n')
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", str(src), "-o", str(tmp_path / "h")], check=True)
     subprocess.run([str(tmp_path / "h")], check=True)
     cxx = tmp_path / "h.cpp"
@@ -42,7 +42,7 @@ def test_library_exports_every_declared_function():
     assert set(declared) <= exported, sorted(set(declared) - exported)
     for name in declared:
         assert hasattr(lib, name)
-    assert lib.ttamm_abi_version() == 1
+    assert lib.ttamm_abi_version() == _lib.ABI_VERSION
     assert lib.ttamm_last_error() is not None
 
 

@@ -1,0 +1,137 @@
+"""The sharded step's exchange layer on CPU: row ownership, request routing and the three
+all-to-alls + all-reduce of ttamm/sharded.py, served by torch.distributed (gloo, world_size 2,
+two processes) and by the in-process loopback — both must route every row to the right place
+in the right order, including a rank that receives no requests."""
+
+from __future__ import annotations
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from ttamm.sharded import AllReduce, AllToAll, RowOwnership, TorchComm, Wait, route_requests, run_loopback
+
+
+def test_row_ownership():
+    for W in (1, 2, 3, 8):
+        total = 0
+        for r in range(W):
+            own = RowOwnership(W, r)
+            n = own.local_count(29)
+            total += n
+            ids = own.global_ids(torch.arange(n))
+            assert torch.equal(own.owner(ids), torch.full_like(ids, r))
+            assert torch.equal(own.local(ids), torch.arange(n))
+            full = torch.arange(29 * 2).view(29, 2)
+            assert torch.equal(own.shard(full)[:, 0] // 2, ids)
+        assert total == 29
+    with pytest.raises(ValueError):
+        RowOwnership(2, 2)
+
+
+def _requests(W: int, rank: int, case: str):
+    g = torch.Generator().manual_seed(100 + rank)
+    B, N = 5, 3
+    R = B * (1 + N)
+    if case == "skewed":  # every item owned by rank 0: the other ranks receive nothing
+        items = torch.randint(0, 40, (R,), generator=g) * W
+    else:
+        items = torch.randint(0, 97, (R,), generator=g)
+    Bg = W * B
+    keys = torch.cat([torch.arange(B) + rank * B, torch.arange(B * N) + Bg + rank * B * N])
+    return items, keys
+
+
+def _exchange_program(W: int, rank: int, case: str):
+    own = RowOwnership(W, rank)
+    items, keys = _requests(W, rank, case)
+    route = yield from route_requests(own, items, keys)
+    assert torch.equal(own.owner(own.global_ids(route.rows)), torch.full_like(route.rows, rank))
+    # owner: payload rows (global id, request key, 7) for what it was asked
+    payload = torch.stack([own.global_ids(route.rows).double(), route.keys.double(),
+                           torch.full((route.rows.numel(),), 7.0, dtype=torch.float64)], dim=1)
+    h = yield AllToAll(payload, route.recv_counts, route.send_counts, async_op=True)
+    back = yield Wait(h)
+    fwd = torch.empty_like(back)
+    fwd.index_copy_(0, route.order, back)
+    # requester: gradient rows keyed by its request positions
+    grads = torch.stack([keys.double() * 3.0, items.double()], dim=1)
+    to_owner = yield AllToAll(grads.index_select(0, route.order), route.send_counts, route.recv_counts)
+    acc = torch.tensor([float(rank + 1), 2.0 ** -rank])
+    yield AllReduce(acc)
+    return {"items": items, "keys": keys, "fwd": fwd, "route_rows": route.rows, "route_keys": route.keys,
+            "to_owner": to_owner, "acc": acc, "recv": route.recv_counts}
+
+
+def _check(W: int, outs: list[dict], case: str):
+    for rank, o in enumerate(outs):
+        # rows come back to the requester in request order
+        assert torch.equal(o["fwd"][:, 0], o["items"].double())
+        assert torch.equal(o["fwd"][:, 1], o["keys"].double())
+        # each owner got, for every row it computed, the gradient of that very request
+        assert torch.equal(o["to_owner"][:, 0], o["route_keys"].double() * 3.0)
+        own = RowOwnership(W, rank)
+        assert torch.equal(o["to_owner"][:, 1], own.global_ids(o["route_rows"]).double())
+        assert torch.equal(o["acc"], torch.tensor([sum(range(1, W + 1)), sum(2.0 ** -r for r in range(W))],
+                                                  dtype=o["acc"].dtype))
+        if case == "skewed" and rank > 0:
+            assert o["route_rows"].numel() == 0
+    total = sum(o["route_rows"].numel() for o in outs)
+    assert total == sum(o["items"].numel() for o in outs)
+
+
+@pytest.mark.parametrize("W", [1, 2, 3])
+@pytest.mark.parametrize("case", ["uniform", "skewed"])
+def test_exchange_loopback(W, case):
+    outs = run_loopback([_exchange_program(W, r, case) for r in range(W)])
+    _check(W, outs, case)
+
+
+def _worker(rank: int, world: int, port: int, case: str, q) -> None:
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = TorchComm().run(_exchange_program(world, rank, case))
+        q.put((rank, {k: (v.tolist() if torch.is_tensor(v) else v) for k, v in out.items()},
+               {k: str(v.dtype) for k, v in out.items() if torch.is_tensor(v)}))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("case", ["uniform", "skewed"])
+def test_exchange_gloo_world2(case):
+    W = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, W, port, case, q)) for r in range(W)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(W):
+        rank, out, dtypes = q.get(timeout=120)
+        got[rank] = {k: (torch.tensor(v, dtype=getattr(torch, dtypes[k].split(".")[1])) if k in dtypes else v)
+                     for k, v in out.items()}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    outs = [got[r] for r in range(W)]
+    for o in outs:  # empty tensors lose their trailing shape in the round trip through lists
+        for k in ("fwd", "to_owner"):
+            o[k] = o[k].reshape(-1, 3 if k == "fwd" else 2)
+    _check(W, outs, case)
+    # identical to the loopback schedule
+    ref = run_loopback([_exchange_program(W, r, case) for r in range(W)])
+    for a, b in zip(outs, ref):
+        assert torch.equal(a["fwd"], b["fwd"]) and torch.equal(a["to_owner"], b["to_owner"])

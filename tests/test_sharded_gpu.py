@@ -1,0 +1,143 @@
+"""The row-sharded multi-GPU step (ttamm/sharded.py) against the one-process step over the
+global batch, on one GPU: W virtual ranks run in lock step in this process (run_loopback
+serves their all-to-alls / all-reduces), each with its shard of the tables and a replica of
+the MLP / gate weights.
+
+A W-rank step is the reference step over the concatenated (rank-major) global batch, so:
+  * sampled negatives are bit-identical (Philox streams keyed by global slot);
+  * dropout masks are identical (keyed by global request position) — checked implicitly;
+  * losses and every gradient agree to 1e-5 norm-wise relative (only fp32 summation order
+    differs: per-rank partial sums, then the all-reduce);
+  * after three real optimizer steps parameters agree within 5e-5 absolute (golden-test
+    tolerance: Adam normalises each update to ~lr)."""
+
+from __future__ import annotations
+
+import pytest
+import torch
+
+import ttamm
+from helpers import LOSS_WEIGHTS, Shape, make_problem, named_optimizer_state, rel_err
+from ttamm.sharded import RowOwnership, ShardedTrainStep, run_loopback
+
+pytestmark = pytest.mark.gpu
+
+TABLES = ("user_encoder.embedding.weight", "item_encoder.embedding.weight",
+          "adaptive_mimic.user_augmented.weight", "adaptive_mimic.item_augmented.weight")
+SEED = 4242
+
+
+def _model(shape: Shape, U: int, I: int, state: dict):
+    cfg = shape.tower_cfg()
+    ue = ttamm.build_tower_encoder(cfg, num_embeddings=U, feature_dim=shape.F, device="cuda")
+    ie = ttamm.build_tower_encoder(cfg, num_embeddings=I, feature_dim=shape.F, device="cuda")
+    mm = ttamm.AdaptiveMimicMechanism(num_users=U, num_items=I, embedding_dim=shape.D).cuda() if shape.mimic else None
+    m = ttamm.TwoTowerModel(ue, ie, similarity=ttamm.DotProductSimilarity(), adaptive_mimic=mm)
+    m.load_state_dict({k: v.cuda() for k, v in state.items()}, strict=True)
+    return m
+
+
+def _opts(model, lr, betas):
+    dense, sparse = ttamm._collect_parameter_groups(model)
+    opts = [torch.optim.AdamW(dense, lr=1e-3, weight_decay=0.01, betas=betas),
+            torch.optim.SparseAdam(sparse, lr=1e-3, betas=betas)]
+    for o in opts:
+        for g in o.param_groups:
+            g["lr"] = lr
+    return opts
+
+
+def _setup(shape: Shape, W: int, *, lr: float, betas, steps: int):
+    prob = make_problem(shape, seed=77)
+    state = prob.model.state_dict()
+    gen = torch.Generator().manual_seed(5)
+    # rank r's interactions use only users it owns (u % W == r); global batch is rank-major
+    batches = []
+    for _ in range(steps):
+        per_rank = []
+        for r in range(W):
+            owned = torch.arange(r, shape.U, W)
+            users = owned[torch.randint(0, owned.numel(), (shape.B,), generator=gen)]
+            pos = torch.tensor([sorted(prob.positives[int(u)])[0] for u in users], dtype=torch.long)
+            per_rank.append((users, pos))
+        batches.append(per_rank)
+    # one process over the global batch
+    gm = _model(shape, shape.U, shape.I, state)
+    gopts = _opts(gm, lr, betas)
+    geng = ttamm.FusedTrainStep(gm, gopts, negatives_per_positive=shape.N, positives=prob.positives,
+                                user_features=prob.user_features.cuda(), item_features=prob.item_features.cuda(),
+                                loss_weights=LOSS_WEIGHTS, max_batch=W * shape.B, seed=SEED)
+    # W ranks
+    ranks = []
+    for r in range(W):
+        own = RowOwnership(W, r)
+        st = {k: (own.shard(v) if k in TABLES else v.clone()) for k, v in state.items()}
+        m = _model(shape, own.local_count(shape.U), own.local_count(shape.I), st)
+        opts = _opts(m, lr, betas)
+        local_pos = {u // W: prob.positives[u] for u in range(r, shape.U, W)}
+        eng = ShardedTrainStep(m, opts, world_size=W, rank=r, num_items=shape.I, negatives_per_positive=shape.N,
+                               positives=local_pos, user_features=own.shard(prob.user_features).cuda(),
+                               item_features=own.shard(prob.item_features).cuda(), loss_weights=LOSS_WEIGHTS,
+                               max_batch=shape.B, seed=SEED)
+        ranks.append((own, m, opts, eng))
+    return prob, batches, (gm, gopts, geng), ranks
+
+
+def _run(batches, g, ranks, W):
+    gm, gopts, geng = g
+    glosses, rlosses, negs = [], [], []
+    for per_rank in batches:
+        users = torch.cat([u for u, _ in per_rank]).cuda()
+        pos = torch.cat([p for _, p in per_rank]).cuda()
+        geng.step(users, pos)
+        glosses.append(geng.last_losses())
+        progs = [eng.program((u // W).cuda(), p.cuda()) for (own, m, o, eng), (u, p) in zip(ranks, per_rank)]
+        run_loopback(progs)
+        rlosses.append([eng.last_losses() for (_, _, _, eng) in ranks])
+        negs.append((geng.neg_buffer.clone(), [eng.neg_buffer.clone() for (_, _, _, eng) in ranks]))
+    gavg = geng.finish()
+    ravg = run_loopback([eng.finish_program() for (_, _, _, eng) in ranks])
+    return glosses, rlosses, negs, gavg, ravg
+
+
+@pytest.mark.parametrize("W,shape", [
+    (2, Shape()),
+    (3, Shape(hidden_dims=(16, 12))),
+    (2, Shape(dropout=0.0, gate_hidden=20)),
+])
+def test_sharded_gradients_match_global_step(W, shape):
+    prob, batches, g, ranks = _setup(shape, W, lr=0.0, betas=(0.0, 0.999), steps=1)
+    glosses, rlosses, negs, gavg, ravg = _run(batches, g, ranks, W)
+    B, N = shape.B, shape.N
+    gneg, rneg = negs[0]
+    for r in range(W):
+        assert torch.equal(rneg[r][: B * N], gneg[r * B * N:(r + 1) * B * N]), f"rank {r} negatives differ"
+    for key in ("total", "bce", "mimic_user", "mimic_item"):
+        for r in range(W):
+            assert abs(rlosses[0][r][key] - glosses[0][key]) <= 1e-5 * max(abs(glosses[0][key]), 1e-12), key
+    for r in range(W):
+        assert abs(ravg[r] - gavg) <= 1e-5 * abs(gavg)
+    gm, gopts, _ = g
+    gstate = named_optimizer_state(gm, gopts)
+    for own, m, opts, _ in ranks:
+        rstate = named_optimizer_state(m, opts)
+        for name, st in rstate.items():
+            want = gstate[name]["exp_avg"]
+            if name in TABLES:
+                want = want[own.rank:: W]
+            assert rel_err(st["exp_avg"], want) <= 1e-5, (own.rank, name)
+
+
+def test_sharded_three_steps_match_global_step():
+    W, shape = 2, Shape()
+    prob, batches, g, ranks = _setup(shape, W, lr=1e-3, betas=(0.9, 0.999), steps=3)
+    glosses, rlosses, _, _, _ = _run(batches, g, ranks, W)
+    for s in range(3):
+        assert abs(rlosses[s][0]["total"] - glosses[s]["total"]) <= 1e-5 * abs(glosses[s]["total"])
+    gm = g[0]
+    gsd = gm.state_dict()
+    for own, m, _, _ in ranks:
+        for k, v in m.state_dict().items():
+            want = gsd[k][own.rank:: W] if k in TABLES else gsd[k]
+            d = (v - want).abs().max().item()
+            assert d <= 5e-5, f"rank {own.rank} {k}: {d:.2e}"

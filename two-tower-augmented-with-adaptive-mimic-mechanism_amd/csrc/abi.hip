@@ -17,6 +17,7 @@ int fail(int code, const std::string& msg) {
 
 size_t train_step_workspace_size(const ttamm_step_args& A);
 int train_step(const ttamm_step_args& A, hipStream_t s);
+int64_t dense_grad_floats(const ttamm_step_args& A);
 size_t tower_forward_workspace_size(const ttamm_tower& T, int64_t n);
 int tower_forward_eval(const ttamm_tower& T, const int64_t* idx, const int64_t* fidx, int64_t n, int augment,
                        float* out, void* ws, size_t ws_bytes, hipStream_t s);
@@ -34,6 +35,11 @@ TTAMM_API const char* ttamm_last_error(void) { return g_last_error.c_str(); }
 TTAMM_API size_t ttamm_train_step_workspace_size(const ttamm_step_args* args) {
     if (!args) return 0;
     return train_step_workspace_size(*args);
+}
+
+TTAMM_API int64_t ttamm_dense_grad_floats(const ttamm_step_args* args) {
+    if (!args) return 0;
+    return dense_grad_floats(*args);
 }
 
 TTAMM_API int ttamm_train_step(const ttamm_step_args* args, void* stream) {
@@ -62,7 +68,7 @@ TTAMM_API int ttamm_tower_forward(const ttamm_tower* tower, const int64_t* idx, 
 TTAMM_API int ttamm_mimic_augment(const float* table, int64_t table_rows, int32_t dim, const int64_t* idx, int64_t n,
                                   const float* base, float* out, float* aug_out, void* stream) {
     if (n < 0 || dim <= 0 || table_rows <= 0) return fail(TTAMM_E_INVALID, "mimic_augment: bad shape");
-    return launch_combine(base, dim, nullptr, 0, table, idx, n, dim, nullptr, aug_out, out, (hipStream_t)stream);
+    return launch_combine(base, dim, nullptr, 0, table, idx, n, dim, nullptr, aug_out, dim, out, (hipStream_t)stream);
 }
 
 TTAMM_API int ttamm_mse_loss(const float* input, const float* target, int64_t n, float* out, void* stream) {
@@ -72,7 +78,7 @@ TTAMM_API int ttamm_mse_loss(const float* input, const float* target, int64_t n,
 TTAMM_API int ttamm_sample_negatives(const int64_t* users, int64_t batch, int32_t num_neg, int64_t num_items,
                                      const int64_t* pos_offsets, const int64_t* pos_values, uint64_t seed,
                                      uint64_t counter, int64_t* out, uint32_t* status, void* stream) {
-    return launch_sample_negatives(users, batch, num_neg, num_items, pos_offsets, pos_values, seed, counter, out,
+    return launch_sample_negatives(users, batch, num_neg, num_items, pos_offsets, pos_values, seed, counter, 0, out,
                                    status, (hipStream_t)stream);
 }
 

@@ -114,8 +114,11 @@ __device__ __forceinline__ void epilogue4(const KArg(GemmProblem) & P, float4 v,
     if (E == EPI_HIDDEN) {
         u32x4 rnd = {0u, 0u, 0u, 0u};
         const bool drop = P.keep_prob < 1.0f;
-        if (drop && P.keep_mask == nullptr)
-            rnd = philox4x32(u32x4{(uint32_t)row, (uint32_t)col, P.rng_c2, P.rng_c3}, P.rng_k0, P.rng_k1);
+        if (drop && P.keep_mask == nullptr) {
+            const int64_t key = P.row_key ? P.row_key[row]
+                                          : (row < P.key_split ? P.key_base0 + row : P.key_base1 + (row - P.key_split));
+            rnd = philox4x32(u32x4{(uint32_t)key, (uint32_t)col, P.rng_c2, P.rng_c3}, P.rng_k0, P.rng_k1);
+        }
         uint32_t km = 0xFFFFFFFFu;
         if (drop && P.keep_mask) km = *reinterpret_cast<const uint32_t*>(P.keep_mask + (int64_t)row * N + col);
         const uint32_t thresh = keep_threshold(P.keep_prob);
@@ -142,8 +145,8 @@ __device__ __forceinline__ void epilogue4(const KArg(GemmProblem) & P, float4 v,
             g[e] = sigmoidf_(x[e]);
             t[e] = g[e] * e4[e] + (1.0f - g[e]) * f4[e];
         }
-        const int64_t oo = (int64_t)row * P.ld_out + col;
-        st4(P.out1 + oo, make_float4(g[0], g[1], g[2], g[3]));
+        const int64_t oo = (int64_t)row * P.ld_out2 + col;
+        st4(P.out1 + (int64_t)row * P.ld_out + col, make_float4(g[0], g[1], g[2], g[3]));
         st4(P.out2 + oo, make_float4(t[0], t[1], t[2], t[3]));
         if (P.table) {
             const float4 a = ld4(P.table + P.idx[row] * (int64_t)N + col);
@@ -161,7 +164,7 @@ __device__ __forceinline__ void epilogue4(const KArg(GemmProblem) & P, float4 v,
         const int D = N >> 1;
         const int cc = col < D ? col : col - D;  // a group never straddles D (D % 4 == 0)
         const float4 dt = ld4(P.aux1 + (int64_t)row * P.ld_aux1 + cc);
-        const float4 g = ld4(P.aux2 + (int64_t)row * P.ld_aux1 + cc);
+        const float4 g = ld4(P.aux2 + (int64_t)row * P.ld_aux2 + cc);
         if (col < D) {
             x[0] += dt.x * g.x, x[1] += dt.y * g.y, x[2] += dt.z * g.z, x[3] += dt.w * g.w;
         } else {
@@ -173,6 +176,7 @@ __device__ __forceinline__ void epilogue4(const KArg(GemmProblem) & P, float4 v,
         x[0] = hv.x > 0.f ? x[0] * P.inv_keep : 0.f, x[1] = hv.y > 0.f ? x[1] * P.inv_keep : 0.f;
         x[2] = hv.z > 0.f ? x[2] * P.inv_keep : 0.f, x[3] = hv.w > 0.f ? x[3] * P.inv_keep : 0.f;
     }
+    if (E == EPI_GATE_OUT && P.C == nullptr) return;  // sharded item owner: aug is formed by the requester
     st4(P.C + (int64_t)split * P.slab_stride + (int64_t)row * P.ldc + col, make_float4(x[0], x[1], x[2], x[3]));
 }
 

@@ -37,18 +37,24 @@ struct GemmProblem {
     const float* aux0;  // EPI_GATE_OUT: ef [M, 2D]; DGRAD_RELU / DGRAD_HIDDEN: activation
     const float* aux1;  // EPI_DGRAD_GATE_EF: dT [M, D]
     const float* aux2;  // EPI_DGRAD_GATE_EF: g  [M, D]
-    int64_t ld_aux0, ld_aux1;
+    int64_t ld_aux0, ld_aux1, ld_aux2;
     float* out1;        // EPI_GATE_OUT: g
     float* out2;        // EPI_GATE_OUT: t
     float* out3;        // EPI_GATE_OUT: a (mimic rows), may be null
     const float* table; // EPI_GATE_OUT: mimic table (may be null)
     const int64_t* idx; // EPI_GATE_OUT: rows into table
-    int64_t ld_out;     // EPI_GATE_OUT: ld of g/t/a
+    int64_t ld_out;     // EPI_GATE_OUT: ld of g
+    int64_t ld_out2;    // EPI_GATE_OUT: ld of t / a  (C = aug may be null)
     // dropout (EPI_HIDDEN / EPI_DGRAD_HIDDEN)
     float keep_prob;    // 1 - p
     float inv_keep;     // 1 / (1 - p)   (torch: noise.div_(1 - p))
     const uint8_t* keep_mask;  // optional injected [M, N]
     uint32_t rng_k0, rng_k1, rng_c2, rng_c3;
+    // dropout stream key of output row r (its global interaction position, so a sharded
+    // step draws the same masks as one process over the whole global batch):
+    //   row_key ? row_key[r] : (r < key_split ? key_base0 + r : key_base1 + (r - key_split))
+    const int64_t* row_key;
+    int64_t key_base0, key_base1, key_split;
     // K-major A (weight gradient: A = X^T, rows of X indexed by k, gathered by a_idx)
     int a_kmaj;
     int a_cols;          // valid columns of X (m < a_cols)
@@ -102,38 +108,43 @@ int launch_wgrad(WgradBatch& batch, hipStream_t s);
 int launch_gather_rows(const float* table, int dim, const int64_t* idx, int64_t n, float* out,
                        int64_t out_ld, hipStream_t s);
 // t = e (+ f); a = table[idx]; aug = t + a   (non-gated fusion)
+// t = e (+ f); a = table[idx]; aug = t (+ a).  t / a rows at stride ld_ta; aug may be null.
 int launch_combine(const float* e, int64_t ld_e, const float* f, int64_t ld_f, const float* table,
-                   const int64_t* idx, int64_t n, int dim, float* t, float* a, float* aug,
+                   const int64_t* idx, int64_t n, int dim, float* t, float* a, int64_t ld_ta, float* aug,
                    hipStream_t s);
 int launch_pad_rows(const float* src, int64_t rows, int cols, int64_t ld_src, float* dst, int ld_dst,
                     hipStream_t s);
 int launch_mse(const float* x, const float* y, int64_t n, float* out, hipStream_t s);
 // dq = (dT*e - dT*f) * (1-g) * g   (gate backward through the sigmoid)
-int launch_gate_dq(const float* dT, const float* ef, const float* g, int64_t n, int dim, float* dq,
-                   hipStream_t s);
+int launch_gate_dq(const float* dT, int64_t ld_dT, const float* ef, const float* g, int64_t n, int dim,
+                   float* dq, hipStream_t s);
 
 struct ScoreArgs {
     int64_t B;
+    int64_t Bg;             // global batch (loss normalisation), == B in a 1-process step
     int N;
     int D;
     const float* user_aug;  // [B, D]
-    const float* item_aug;  // [B(1+N), D]
+    const float* item_aug;  // [B(1+N), ld_item] or null: t_item (+ a_item) computed in place
     const float* t_user;    // [B, D]
-    const float* t_item;    // [B(1+N), D]
+    const float* t_item;    // [B(1+N), ld_item]
     const float* a_user;    // [B, D] or null
-    const float* a_item;    // [B(1+N), D] or null
+    const float* a_item;    // [B(1+N), ld_item] or null
+    int64_t ld_item;
     float lambda_u, lambda_i;
     int mimic;
     float* dT_user;   // [B, D]
-    float* dT_item;   // [B(1+N), D]
+    float* dT_item;   // [B(1+N), ld_dti]
     float* dA_user;   // [B, D]  (mimic)
-    float* dA_pos;    // [B, D]  (mimic)
+    float* dA_item;   // (mimic) [B, ld_dti] positives only, or all B(1+N) rows when dA_all
+    int dA_all;
+    int64_t ld_dti;
     float* partials;  // [blocks, 3]
     int blocks;
 };
 int score_blocks(int64_t B);
 int launch_score_loss(const ScoreArgs& a, hipStream_t s);
-int launch_loss_finalize(const float* partials, int blocks, int64_t B, int N, int D, float lambda_u,
+int launch_loss_finalize(const float* partials, int blocks, int64_t B, int64_t Bg, int N, int D, float lambda_u,
                          float lambda_i, int mimic, float* loss_out, double* loss_accum,
                          hipStream_t s);
 
@@ -190,6 +201,7 @@ struct RowUpdateArgs {
     // mimic table gradient source: row < split_row ? dA_lo[row] : dA_hi[row]
     const float* dA_lo;
     const float* dA_hi;
+    int64_t ld_dA;
     int64_t split_row;
     ttamm_table mimic;
     // per-position partial sums of the segmented reduction [n, dim]
@@ -246,8 +258,9 @@ SparseConsts make_sparse_consts(double lr, double beta1, double beta2, double ep
 // ------------------------------------------------------------------------------------
 // Sampler (sampler.hip)
 // ------------------------------------------------------------------------------------
+// slot_base: global index of this batch's first slot (row_base * num_neg) — the Philox stream key
 int launch_sample_negatives(const int64_t* users, int64_t batch, int num_neg, int64_t num_items,
                             const int64_t* pos_offsets, const int64_t* pos_values, uint64_t seed,
-                            uint64_t counter, int64_t* out, uint32_t* status, hipStream_t s);
+                            uint64_t counter, int64_t slot_base, int64_t* out, uint32_t* status, hipStream_t s);
 
 }  // namespace ttamm

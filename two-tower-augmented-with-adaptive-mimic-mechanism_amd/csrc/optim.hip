@@ -86,7 +86,7 @@ constexpr int kPiece = 32;
 constexpr int kRowWaves = 4;
 
 __device__ __forceinline__ const float* dA_row(const RowUpdateArgs& A, int64_t r) {
-    return (r < A.split_row ? A.dA_lo : A.dA_hi) + r * A.dim;
+    return (r < A.split_row ? A.dA_lo : A.dA_hi) + r * A.ld_dA;
 }
 
 __global__ __launch_bounds__(64 * kRowWaves) void piece_sum_kernel(RowUpdateArgs A) {

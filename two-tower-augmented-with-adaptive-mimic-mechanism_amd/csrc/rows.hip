@@ -34,7 +34,7 @@ __global__ void gather_rows_scalar(const float* __restrict__ table, int dim, con
 // t = e (+ f) ; a = table[idx] ; aug = t + a      (encoders.py:225-240, adaptive_mimic.py:88-95)
 __global__ void combine_kernel(const float* __restrict__ e, int64_t ld_e, const float* __restrict__ f,
                                int64_t ld_f, const float* __restrict__ table, const int64_t* __restrict__ idx,
-                               int64_t n, int dim, float* __restrict__ t, float* __restrict__ a,
+                               int64_t n, int dim, float* __restrict__ t, float* __restrict__ a, int64_t ld_ta,
                                float* __restrict__ aug) {
     const int64_t total = n * dim;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
@@ -43,14 +43,14 @@ __global__ void combine_kernel(const float* __restrict__ e, int64_t ld_e, const 
         const int c = (int)(i - r * dim);
         float tv = e[r * ld_e + c];
         if (f) tv = tv + f[r * ld_f + c];
-        if (t) t[i] = tv;
+        if (t) t[r * ld_ta + c] = tv;
         float av = tv;
         if (table) {
             const float am = table[idx[r] * (int64_t)dim + c];
-            if (a) a[i] = am;
+            if (a) a[r * ld_ta + c] = am;
             av = tv + am;
         }
-        aug[i] = av;
+        if (aug) aug[i] = av;
     }
 }
 
@@ -69,14 +69,14 @@ __global__ void pad_rows_kernel(const float* __restrict__ src, int64_t rows, int
 
 // dq = (dT*e - dT*f) * (1 - g) * g
 // autograd of gate*e + (1-gate)*f then SigmoidBackward (grad*(1-y)*y), encoders.py:164-168.
-__global__ void gate_dq_kernel(const float* __restrict__ dT, const float* __restrict__ ef,
+__global__ void gate_dq_kernel(const float* __restrict__ dT, int64_t ld_dT, const float* __restrict__ ef,
                                const float* __restrict__ g, int64_t n, int dim, float* __restrict__ dq) {
     const int64_t total = n * dim;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = i / dim;
         const int c = (int)(i - r * dim);
-        const float d = dT[i];
+        const float d = dT[r * ld_dT + c];
         const float ev = ef[r * 2 * dim + c], fv = ef[r * 2 * dim + dim + c];
         const float gv = g[i];
         const float dg = d * ev - d * fv;
@@ -91,12 +91,20 @@ __device__ __forceinline__ float bce_logit(float x, float y) {
 }
 
 // One wave per interaction b (training.py:770-803, Appendix A of SURVEY.md):
-//   s+ = <u_b, p_b>, s-_j = <u_b, n_bj>; ds = (sigmoid(s) - y) / (B(1+N))
+//   s+ = <u_b, p_b>, s-_j = <u_b, n_bj>; ds = (sigmoid(s) - y) / (Bg(1+N))
 //   dT_user = ds+ p + sum_j ds-_j n_j ; dT_pos = ds+ u ; dT_neg_j = ds-_j u
-//   mimic: dA_user = dT_user + lu * 2/(B D) * (a_u - t_p) ; dA_pos = dT_pos + li * 2/(B D) * (a_p - t_u)
+//   mimic: dA_user = dT_user + lu * 2/(Bg D) * (a_u - t_p) ; dA_pos = dT_pos + li * 2/(Bg D) * (a_p - t_u)
+//          (dA_all: negative rows' dA = dT_neg, the requester ships (dT | dA) for every row)
+// Bg is the global batch: in a sharded step each rank's terms are its share of the global mean.
 constexpr int kScoreWaves = 4;
 constexpr int kMaxDChunks = 8;  // D <= 512
 constexpr int kMaxNeg = 64;
+
+__device__ __forceinline__ float item_aug_at(const ScoreArgs& A, int64_t r, int d) {
+    if (A.item_aug) return A.item_aug[r * A.ld_item + d];
+    const float t = A.t_item[r * A.ld_item + d];
+    return A.a_item ? t + A.a_item[r * A.ld_item + d] : t;
+}
 
 __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs A) {
     __shared__ float red[kScoreWaves][3];
@@ -104,7 +112,8 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
     const int64_t b = (int64_t)blockIdx.x * kScoreWaves + w;
     const int D = A.D, N = A.N;
     const int64_t B = A.B;
-    const float inv_numel = 1.0f / (float)(B * (1 + N));
+    const int64_t ldi = A.ld_dti;
+    const float inv_numel = 1.0f / (float)(A.Bg * (1 + N));
     float bce = 0.f, mse_u = 0.f, mse_i = 0.f;
     if (b < B) {
         const int nch = (D + 63) / 64;
@@ -116,7 +125,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
             const int d = c * 64 + lane;
             if (c < nch && d < D) {
                 u[c] = A.user_aug[b * D + d];
-                p[c] = A.item_aug[b * D + d];
+                p[c] = item_aug_at(A, b, d);
                 dot += u[c] * p[c];
             }
         }
@@ -128,7 +137,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
         for (int c = 0; c < kMaxDChunks; ++c) {
             const int d = c * 64 + lane;
             if (c < nch && d < D) {
-                A.dT_item[b * D + d] = dsp * u[c];
+                A.dT_item[b * ldi + d] = dsp * u[c];
                 du[c] = dsp * p[c];
             }
         }
@@ -141,7 +150,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
                 nv[c] = 0.f;
                 const int d = c * 64 + lane;
                 if (c < nch && d < D) {
-                    nv[c] = A.item_aug[nr * D + d];
+                    nv[c] = item_aug_at(A, nr, d);
                     dn += u[c] * nv[c];
                 }
             }
@@ -152,25 +161,27 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
             for (int c = 0; c < kMaxDChunks; ++c) {
                 const int d = c * 64 + lane;
                 if (c < nch && d < D) {
-                    A.dT_item[nr * D + d] = dsn * u[c];
+                    const float g = dsn * u[c];
+                    A.dT_item[nr * ldi + d] = g;
+                    if (A.mimic && A.dA_all) A.dA_item[nr * ldi + d] = g;
                     du[c] += dsn * nv[c];
                 }
             }
         }
-        const float norm = 2.0f / (float)(B * D);
+        const float norm = 2.0f / (float)(A.Bg * D);
 #pragma unroll
         for (int c = 0; c < kMaxDChunks; ++c) {
             const int d = c * 64 + lane;
             if (c < nch && d < D) {
                 A.dT_user[b * D + d] = du[c];
                 if (A.mimic) {
-                    const float au = A.a_user[b * D + d], tp = A.t_item[b * D + d];
-                    const float ap = A.a_item[b * D + d], tu = A.t_user[b * D + d];
+                    const float au = A.a_user[b * D + d], tp = A.t_item[b * A.ld_item + d];
+                    const float ap = A.a_item[b * A.ld_item + d], tu = A.t_user[b * D + d];
                     const float xu = au - tp, xi = ap - tu;
                     mse_u += xu * xu;
                     mse_i += xi * xi;
                     A.dA_user[b * D + d] = du[c] + norm * xu * A.lambda_u;
-                    A.dA_pos[b * D + d] = dsp * u[c] + norm * xi * A.lambda_i;
+                    A.dA_item[b * ldi + d] = dsp * u[c] + norm * xi * A.lambda_i;
                 }
             }
         }
@@ -191,7 +202,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
 }
 
 // Deterministic final reduction of the per-block partials; total loss as in training.py:798-803.
-__global__ void loss_finalize_kernel(const float* __restrict__ partials, int blocks, int64_t B, int N, int D,
+__global__ void loss_finalize_kernel(const float* __restrict__ partials, int blocks, int64_t B, int64_t Bg, int N, int D,
                                      float lu, float li, int mimic, float* __restrict__ loss_out,
                                      double* __restrict__ loss_accum) {
     __shared__ float red[3][256];
@@ -206,9 +217,10 @@ __global__ void loss_finalize_kernel(const float* __restrict__ partials, int blo
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        const float bce = red[0][0] / (float)(B * (1 + N));
-        const float mu = red[1][0] / (float)(B * D);
-        const float mi = red[2][0] / (float)(B * D);
+        // sharded step: this rank's share of the global means (the host sums loss_out over ranks)
+        const float bce = red[0][0] / (float)(Bg * (1 + N));
+        const float mu = red[1][0] / (float)(Bg * D);
+        const float mi = red[2][0] / (float)(Bg * D);
         float total = bce;
         if (mimic && lu > 0.f) total = total + lu * mu;
         if (mimic && li > 0.f) total = total + li * mi;
@@ -217,7 +229,7 @@ __global__ void loss_finalize_kernel(const float* __restrict__ partials, int blo
         loss_out[2] = mimic ? mu : 0.f;
         loss_out[3] = mimic ? mi : 0.f;
         if (loss_accum) {
-            loss_accum[0] += (double)total * (double)B;
+            loss_accum[0] += (double)total * (double)Bg;
             loss_accum[1] += (double)B;
         }
     }
@@ -266,10 +278,11 @@ int launch_gather_rows(const float* table, int dim, const int64_t* idx, int64_t 
 }
 
 int launch_combine(const float* e, int64_t ld_e, const float* f, int64_t ld_f, const float* table,
-                   const int64_t* idx, int64_t n, int dim, float* t, float* a, float* aug, hipStream_t s) {
+                   const int64_t* idx, int64_t n, int dim, float* t, float* a, int64_t ld_ta, float* aug,
+                   hipStream_t s) {
     if (n <= 0) return TTAMM_OK;
     hipLaunchKernelGGL(combine_kernel, dim3(grid_for(n * dim)), dim3(256), 0, s, e, ld_e, f, ld_f, table, idx, n,
-                       dim, t, a, aug);
+                       dim, t, a, ld_ta, aug);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }
@@ -290,9 +303,10 @@ int launch_pad_rows(const float* src, int64_t rows, int cols, int64_t ld_src, fl
     return TTAMM_OK;
 }
 
-int launch_gate_dq(const float* dT, const float* ef, const float* g, int64_t n, int dim, float* dq, hipStream_t s) {
+int launch_gate_dq(const float* dT, int64_t ld_dT, const float* ef, const float* g, int64_t n, int dim, float* dq,
+                   hipStream_t s) {
     if (n <= 0) return TTAMM_OK;
-    hipLaunchKernelGGL(gate_dq_kernel, dim3(grid_for(n * dim)), dim3(256), 0, s, dT, ef, g, n, dim, dq);
+    hipLaunchKernelGGL(gate_dq_kernel, dim3(grid_for(n * dim)), dim3(256), 0, s, dT, ld_dT, ef, g, n, dim, dq);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }
@@ -308,9 +322,9 @@ int launch_score_loss(const ScoreArgs& a, hipStream_t s) {
 
 int score_blocks(int64_t B) { return (int)ceil_div(B, kScoreWaves); }
 
-int launch_loss_finalize(const float* partials, int blocks, int64_t B, int N, int D, float lu, float li, int mimic,
-                         float* loss_out, double* loss_accum, hipStream_t s) {
-    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, partials, blocks, B, N, D, lu, li, mimic,
+int launch_loss_finalize(const float* partials, int blocks, int64_t B, int64_t Bg, int N, int D, float lu, float li,
+                         int mimic, float* loss_out, double* loss_accum, hipStream_t s) {
+    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, partials, blocks, B, Bg, N, D, lu, li, mimic,
                        loss_out, loss_accum);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;

@@ -30,7 +30,8 @@ __device__ __forceinline__ bool is_positive(const int64_t* __restrict__ vals, in
 __global__ void sample_negatives_kernel(const int64_t* __restrict__ users, int64_t batch, int num_neg,
                                         uint64_t num_items, const int64_t* __restrict__ pos_offsets,
                                         const int64_t* __restrict__ pos_values, uint32_t k0, uint32_t k1,
-                                        uint64_t counter, int64_t* __restrict__ out, uint32_t* __restrict__ status) {
+                                        uint64_t counter, int64_t slot_base, int64_t* __restrict__ out,
+                                        uint32_t* __restrict__ status) {
     const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (slot >= batch * num_neg) return;
     const int64_t b = slot / num_neg;
@@ -42,9 +43,10 @@ __global__ void sample_negatives_kernel(const int64_t* __restrict__ users, int64
     }
     int64_t cand = 0;
     bool ok = false;
+    const int64_t key = slot_base + slot;  // global slot: a sharded batch draws what one process would
     for (int attempt = 0; attempt < kMaxDraws && !ok; ++attempt) {
         const u32x4 r = philox4x32(
-            u32x4{(uint32_t)slot, (uint32_t)(slot >> 32), (uint32_t)counter,
+            u32x4{(uint32_t)key, (uint32_t)(key >> 32), (uint32_t)counter,
                   RNG_NEGATIVES | ((uint32_t)attempt << 20) | ((uint32_t)(counter >> 32) & 0xFFFFFu)},
             k0, k1);
         const uint64_t r64 = ((uint64_t)r.x << 32) | r.y;
@@ -59,14 +61,14 @@ __global__ void sample_negatives_kernel(const int64_t* __restrict__ users, int64
 
 int launch_sample_negatives(const int64_t* users, int64_t batch, int num_neg, int64_t num_items,
                             const int64_t* pos_offsets, const int64_t* pos_values, uint64_t seed, uint64_t counter,
-                            int64_t* out, uint32_t* status, hipStream_t s) {
+                            int64_t slot_base, int64_t* out, uint32_t* status, hipStream_t s) {
     TTAMM_REQUIRE(num_neg > 0, "num_negatives must be greater than zero.");
     TTAMM_REQUIRE(num_items > 1, "num_items must be greater than one.");
     const int64_t slots = batch * num_neg;
     if (slots <= 0) return TTAMM_OK;
     hipLaunchKernelGGL(sample_negatives_kernel, dim3((unsigned)ceil_div(slots, 256)), dim3(256), 0, s, users, batch,
                        num_neg, (uint64_t)num_items, pos_offsets, pos_values, (uint32_t)seed, (uint32_t)(seed >> 32),
-                       counter, out, status);
+                       counter, slot_base, out, status);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

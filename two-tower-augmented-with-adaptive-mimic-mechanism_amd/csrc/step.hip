@@ -11,6 +11,10 @@
 //   coalesce row grads, SparseAdam (ID tables), AdamW touched rows        (a9, a5)
 //   AdamW(g=0) stream over the full mimic tables, side-row scatter         (a5, a10)
 //   AdamW on the MLP / gate weights                                        (a10)
+//
+// A row-sharded multi-GPU step runs the same pieces as phases (ttamm.h TTAMM_PHASE_*): the
+// item tower of a rank runs over the item rows it owns, for whoever requested them; the
+// host moves (t | a) and (dT | dA) rows between phases and all-reduces the gradient arena.
 #include <cstring>
 #include <vector>
 
@@ -20,11 +24,17 @@ namespace ttamm {
 
 namespace {
 
+enum Role { ROLE_USER = 0, ROLE_ITEM = 1 };
+
 struct TowerWs {
+    int role = ROLE_USER;
     int64_t R = 0;
     const int64_t* idx = nullptr;   // ID / mimic table rows
     const int64_t* fidx = nullptr;  // feature rows (null: row r)
-    int64_t* idx_own = nullptr;     // item tower: [pos; neg]
+    int64_t* idx_own = nullptr;     // 1-process item tower: [pos; neg]
+    // dropout stream key of row r (see GemmProblem::row_key)
+    const int64_t* row_key = nullptr;
+    int64_t key_base0 = 0, key_base1 = 0, key_split = 0;
     float* hid[TTAMM_MAX_LINEAR] = {};
     float* dhid[TTAMM_MAX_LINEAR] = {};
     float* ef = nullptr;    // gated: [R, 2D] = [e | f]
@@ -33,13 +43,19 @@ struct TowerWs {
     float* z = nullptr;     // gate hidden [R, Hg]
     float* dz = nullptr;
     float* g = nullptr;
-    float* t = nullptr;
+    float* t = nullptr;     // [R, t_ld] (a alongside at the same stride)
     float* a = nullptr;
-    float* aug = nullptr;
-    float* dT = nullptr;
+    int64_t t_ld = 0;
+    float* aug = nullptr;   // [R, D] or null (sharded item owner)
+    const float* dT = nullptr;  // [R, dT_ld]
+    float* dT_own = nullptr;
+    int64_t dT_ld = 0;
+    const float* dA = nullptr;  // mimic-table grad rows (user: all rows; item: positives or all)
+    float* dA_own = nullptr;
+    int64_t dA_ld = 0;
+    int64_t dA_split = 0;       // rows < dA_split read dA, the rest read dT
     float* dq = nullptr;
     float* dEF = nullptr;  // [R, 2D]
-    float* dA = nullptr;   // [B, D]
     float* gw[TTAMM_MAX_LINEAR] = {};
     float* gb[TTAMM_MAX_LINEAR] = {};
     float* ggw[2] = {};
@@ -108,12 +124,49 @@ int validate_tower(const ttamm_tower& T, const char* name, int D, bool training)
     return TTAMM_OK;
 }
 
+bool sharded(const ttamm_step_args& A) { return A.phase != TTAMM_PHASE_ALL; }
+int64_t global_batch(const ttamm_step_args& A) { return A.global_batch > 0 ? A.global_batch : A.b.batch; }
+
+// The replicated-weight gradient arena: per tower (user, item) the feature-encoder layers'
+// weight, bias, then the gate's, each piece padded to 64 floats (256 B).
+inline size_t pad64(size_t n) { return (n + 63) / 64 * 64; }
+size_t tower_grad_floats(const ttamm_tower& T) {
+    size_t n = 0;
+    if (T.fusion == TTAMM_FUSION_IDENTITY) return 0;
+    for (int l = 0; l < T.n_linear; ++l)
+        n += pad64((size_t)T.linear[l].out_features * T.linear[l].in_features) + pad64(T.linear[l].out_features);
+    if (T.fusion == TTAMM_FUSION_GATED)
+        for (int q = 0; q < 2; ++q)
+            n += pad64((size_t)T.gate[q].out_features * T.gate[q].in_features) + pad64(T.gate[q].out_features);
+    return n;
+}
+void carve_grads(const ttamm_tower& T, TowerWs& w, float*& cur) {
+    if (T.fusion == TTAMM_FUSION_IDENTITY) return;
+    for (int l = 0; l < T.n_linear; ++l) {
+        w.gw[l] = cur;
+        cur += pad64((size_t)T.linear[l].out_features * T.linear[l].in_features);
+        w.gb[l] = cur;
+        cur += pad64(T.linear[l].out_features);
+    }
+    if (T.fusion == TTAMM_FUSION_GATED)
+        for (int q = 0; q < 2; ++q) {
+            w.ggw[q] = cur;
+            cur += pad64((size_t)T.gate[q].out_features * T.gate[q].in_features);
+            w.ggb[q] = cur;
+            cur += pad64(T.gate[q].out_features);
+        }
+}
+
+// Workspace layout.  Deterministic in the arguments, so every phase call of a sharded step
+// finds the previous phases' activations where it left them.
 int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
     const int64_t B = A.b.batch;
     const int N = A.b.num_neg;
     const int D = A.user.id.dim;
     const bool mimic = A.mimic_enabled != 0;
-    auto tower = [&](const ttamm_tower& T, TowerWs& w, int64_t R, bool own_idx) {
+    const bool shard = sharded(A);
+    // ext_io: the item tower's t / a / dT / dA live in the caller's exchange buffers
+    auto tower = [&](const ttamm_tower& T, TowerWs& w, int64_t R, bool own_idx, bool ext_io, int64_t dA_rows) {
         w.R = R;
         if (own_idx) w.idx_own = ar.take<int64_t>(R);
         for (int l = 0; l + 1 < T.n_linear; ++l) {
@@ -132,24 +185,28 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
             w.e = ar.take<float>((size_t)R * D);
             if (T.fusion == TTAMM_FUSION_SUM) w.f = ar.take<float>((size_t)R * D);
         }
-        w.t = ar.take<float>((size_t)R * D);
-        w.a = mimic ? ar.take<float>((size_t)R * D) : nullptr;
-        w.aug = ar.take<float>((size_t)R * D);
-        w.dT = ar.take<float>((size_t)R * D);
-        w.dA = mimic ? ar.take<float>((size_t)B * D) : nullptr;
+        if (!ext_io) {
+            w.t = ar.take<float>((size_t)R * D);
+            w.a = mimic ? ar.take<float>((size_t)R * D) : nullptr;
+            w.t_ld = D;
+            w.aug = ar.take<float>((size_t)R * D);
+            w.dT_own = ar.take<float>((size_t)R * D);
+            w.dT = w.dT_own;
+            w.dT_ld = D;
+            w.dA_own = mimic ? ar.take<float>((size_t)dA_rows * D) : nullptr;
+            w.dA = w.dA_own;
+            w.dA_ld = D;
+            w.dA_split = dA_rows;
+        }
         if (T.fusion != TTAMM_FUSION_IDENTITY) {
             for (int l = 0; l < T.n_linear; ++l) {
                 const ttamm_linear& L = T.linear[l];
-                w.gw[l] = ar.take<float>((size_t)L.out_features * L.in_features);
-                w.gb[l] = ar.take<float>((size_t)L.out_features);
                 w.slab[l] = ar.take<float>(wgrad_slab_floats((int)R, L.out_features, L.in_features));
             }
         }
         if (T.fusion == TTAMM_FUSION_GATED) {
             for (int q = 0; q < 2; ++q) {
                 const ttamm_linear& L = T.gate[q];
-                w.ggw[q] = ar.take<float>((size_t)L.out_features * L.in_features);
-                w.ggb[q] = ar.take<float>((size_t)L.out_features);
                 w.slab[TTAMM_MAX_LINEAR + q] = ar.take<float>(wgrad_slab_floats((int)R, L.out_features, L.in_features));
             }
         }
@@ -169,10 +226,19 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         if (T.id.optimizer == TTAMM_OPT_DENSE) w.side_id = ar.take<float>((size_t)R * 3 * D);
         if (mimic) w.side_mimic = ar.take<float>((size_t)R * 3 * D);
     };
-    tower(A.user, ws.user, B, false);
-    tower(A.item, ws.item, B * (1 + N), true);
+    ws.user.role = ROLE_USER;
+    ws.item.role = ROLE_ITEM;
+    tower(A.user, ws.user, B, false, false, B);
+    if (shard)
+        tower(A.item, ws.item, A.item_rows_capacity, false, true, 0);
+    else
+        tower(A.item, ws.item, B * (1 + N), true, false, B);
     ws.score_blocks = score_blocks(B);
     ws.partials = ar.take<float>((size_t)ws.score_blocks * 3);
+    // gradient arena: the caller's all-reduce buffer when sharded, else workspace
+    float* arena = shard ? A.dense_grads : ar.take<float>(tower_grad_floats(A.user) + tower_grad_floats(A.item));
+    carve_grads(A.user, ws.user, arena);
+    carve_grads(A.item, ws.item, arena);
     return TTAMM_OK;
 }
 
@@ -210,6 +276,13 @@ void set_dropout(GemmProblem& p, const ttamm_tower& T, const ttamm_batch& bt, in
     p.rng_c2 = (uint32_t)bt.counter;
     p.rng_c3 = RNG_DROPOUT | ((uint32_t)tower_id << 24) | ((uint32_t)layer << 20) |
                ((uint32_t)(bt.counter >> 32) & 0xFFFFFu);
+}
+
+void set_keys(GemmProblem& p, const TowerWs& w) {
+    p.row_key = w.row_key;
+    p.key_base0 = w.key_base0;
+    p.key_base1 = w.key_base1;
+    p.key_split = w.key_split;
 }
 
 // ---- forward -------------------------------------------------------------------------------
@@ -265,7 +338,8 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
                 p.epi = EPI_HIDDEN;
                 p.C = w.hid[l];
                 p.ldc = L.out_features;
-                set_dropout(p, t, bt, k, l, k == 0 ? bt.user_keep_mask[l] : bt.item_keep_mask[l]);
+                set_dropout(p, t, bt, w.role, l, w.role == ROLE_USER ? bt.user_keep_mask[l] : bt.item_keep_mask[l]);
+                set_keys(p, w);
             } else {
                 p.epi = EPI_STORE;
                 if (t.fusion == TTAMM_FUSION_GATED) {
@@ -327,10 +401,11 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
             q.table = table;
             q.idx = w.idx;
             q.ld_out = D;
+            q.ld_out2 = w.t_ld;
             g2.add(q);
         } else {
             if ((rc = launch_combine(w.e, D, t.fusion == TTAMM_FUSION_SUM ? w.f : nullptr, D, table, w.idx, w.R, D, w.t,
-                                     w.a, w.aug, s)))
+                                     w.a, w.t_ld, w.aug, s)))
                 return rc;
         }
     }
@@ -349,7 +424,7 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
         TowerWs& w = *W[k];
         if (t.fusion != TTAMM_FUSION_GATED) continue;
         const int Hg = t.gate[0].out_features;
-        if ((rc = launch_gate_dq(w.dT, w.ef, w.g, w.R, D, w.dq, s))) return rc;
+        if ((rc = launch_gate_dq(w.dT, w.dT_ld, w.ef, w.g, w.R, D, w.dq, s))) return rc;
         GemmProblem p = gp_base();  // dz = (dq . G2) * (z > 0)
         p.A = w.dq;
         p.lda = D;
@@ -378,8 +453,9 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
         q.C = w.dEF;
         q.ldc = 2 * D;
         q.aux1 = w.dT;
+        q.ld_aux1 = w.dT_ld;
         q.aux2 = w.g;
-        q.ld_aux1 = D;
+        q.ld_aux2 = D;
         b2.add(q);
     }
     if ((rc = b1.run(s))) return rc;
@@ -400,7 +476,7 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
             GemmProblem p = gp_base();
             if (l == t.n_linear - 1) {
                 p.A = t.fusion == TTAMM_FUSION_GATED ? w.dEF + D : w.dT;
-                p.lda = t.fusion == TTAMM_FUSION_GATED ? 2 * D : D;
+                p.lda = t.fusion == TTAMM_FUSION_GATED ? 2 * D : w.dT_ld;
             } else {
                 p.A = w.dhid[l];
                 p.lda = L.out_features;
@@ -461,7 +537,7 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
             WgradProblem p{};
             if (l == t.n_linear - 1) {
                 p.dY = t.fusion == TTAMM_FUSION_GATED ? w.dEF + D : w.dT;
-                p.ld_dy = t.fusion == TTAMM_FUSION_GATED ? 2 * D : D;
+                p.ld_dy = t.fusion == TTAMM_FUSION_GATED ? 2 * D : w.dT_ld;
             } else {
                 p.dY = w.dhid[l];
                 p.ld_dy = L.out_features;
@@ -487,8 +563,8 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
     return TTAMM_OK;
 }
 
-int tower_optimizer_rows(const ttamm_tower& t, TowerWs& w, int D, int64_t B, bool mimic, const SparseConsts& sp,
-                         const AdamConsts& ad, bool is_item, hipStream_t s) {
+int tower_optimizer_rows(const ttamm_tower& t, TowerWs& w, int D, bool mimic, const SparseConsts& sp,
+                         const AdamConsts& ad, hipStream_t s) {
     int rc;
     if ((rc = launch_coalesce(w.idx, w.R, t.id.rows, w.co, s))) return rc;
     RowUpdateArgs ru;
@@ -504,14 +580,15 @@ int tower_optimizer_rows(const ttamm_tower& t, TowerWs& w, int D, int64_t B, boo
         ru.ld_dE = 2 * D;
     } else {
         ru.dE = w.dT;
-        ru.ld_dE = D;
+        ru.ld_dE = w.dT_ld;
     }
     ru.id = t.id;
     if (mimic) {
         ru.mimic = t.mimic;
         ru.dA_lo = w.dA;
         ru.dA_hi = w.dT;
-        ru.split_row = is_item ? B : w.R;
+        ru.ld_dA = w.dA_ld;
+        ru.split_row = w.dA_split;
     }
     ru.side_id = w.side_id;
     ru.side_mimic = w.side_mimic;
@@ -521,108 +598,32 @@ int tower_optimizer_rows(const ttamm_tower& t, TowerWs& w, int D, int64_t B, boo
     ru.ad = ad;
     return launch_row_update(ru, s);
 }
+void add_seg(SweepArgs& sw, const ttamm_table& tb) {
+    sw.seg[sw.count].p = tb.weight;
+    sw.seg[sw.count].m = tb.exp_avg;
+    sw.seg[sw.count].v = tb.exp_avg_sq;
+    sw.seg[sw.count].n = tb.rows * tb.dim;
+    sw.count++;
+}
 
-int run_step(const ttamm_step_args& A, hipStream_t s) {
-    const int D = A.user.id.dim;
+// Touched-row updates of the tables of `n` towers, then the AdamW(g=0) sweep over their
+// dense-group tables and the scatter of the staged touched rows.
+int table_updates(const ttamm_tower* T[2], TowerWs* W[2], int n, int D, bool mimic, const SparseConsts& sp,
+                  const AdamConsts& ad, void* const events[2], hipStream_t s) {
     int rc;
-    if ((rc = validate_tower(A.user, "user_encoder", D, true))) return rc;
-    if ((rc = validate_tower(A.item, "item_encoder", D, true))) return rc;
-    TTAMM_REQUIRE(A.b.batch > 0, "empty batch");
-    TTAMM_REQUIRE(A.b.num_neg > 0, "num_negatives must be greater than zero.");
-    TTAMM_REQUIRE(A.item.id.rows > 1, "num_items must be greater than one.");
-    const bool mimic = A.mimic_enabled != 0;
-    if (mimic) {
-        TTAMM_REQUIRE(A.user.mimic.weight && A.item.mimic.weight, "mimic tables missing");
-        TTAMM_REQUIRE(A.user.mimic.dim == D && A.item.mimic.dim == D &&
-                          A.user.mimic.rows == A.user.id.rows && A.item.mimic.rows == A.item.id.rows,
-                      "Adaptive mimic requires user and item embedding dimensions to match.");
-    }
-    TTAMM_REQUIRE(A.hp.dense_step >= 1 && A.hp.sparse_step >= 1, "optimizer step counts must be >= 1");
-
-    Arena ar{static_cast<char*>(A.workspace), A.workspace_bytes, 0, false};
-    StepWs ws;
-    plan(ar, A, ws);
-    TTAMM_REQUIRE(ar.ok(), "workspace too small for this step");
-
-    const int64_t B = A.b.batch;
-    const int N = A.b.num_neg;
-    // ---- indices ------------------------------------------------------------------------
-    ws.user.idx = ws.user.fidx = A.b.users;
-    ws.item.idx = ws.item.fidx = ws.item.idx_own;
-    TTAMM_HIP(hipMemcpyAsync(ws.item.idx_own, A.b.pos_items, B * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
-    int64_t* neg = ws.item.idx_own + B;
-    if (A.b.sample_negatives) {
-        if ((rc = launch_sample_negatives(A.b.users, B, N, A.item.id.rows, A.b.pos_offsets, A.b.pos_values, A.b.seed,
-                                          A.b.counter, neg, A.status, s)))
-            return rc;
-        if (A.b.neg_items)
-            TTAMM_HIP(hipMemcpyAsync(A.b.neg_items, neg, B * N * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
-    } else {
-        TTAMM_REQUIRE(A.b.neg_items != nullptr, "negatives must be given when sample_negatives == 0");
-        TTAMM_HIP(hipMemcpyAsync(neg, A.b.neg_items, B * N * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
-    }
-
-    const ttamm_tower* T[2] = {&A.user, &A.item};
-    TowerWs* W[2] = {&ws.user, &ws.item};
-    // ---- forward ------------------------------------------------------------------------
-    if ((rc = tower_forward(T, W, A.b, D, mimic, s, 2))) return rc;
-    // ---- score + loss (fwd + bwd seeds) -----------------------------------------------
-    ScoreArgs sa;
-    std::memset(&sa, 0, sizeof(sa));
-    sa.B = B;
-    sa.N = N;
-    sa.D = D;
-    sa.user_aug = ws.user.aug;
-    sa.item_aug = ws.item.aug;
-    sa.t_user = ws.user.t;
-    sa.t_item = ws.item.t;
-    sa.a_user = ws.user.a;
-    sa.a_item = ws.item.a;
-    sa.lambda_u = (float)A.hp.lambda_mimic_user;
-    sa.lambda_i = (float)A.hp.lambda_mimic_item;
-    sa.mimic = mimic ? 1 : 0;
-    sa.dT_user = ws.user.dT;
-    sa.dT_item = ws.item.dT;
-    sa.dA_user = ws.user.dA;
-    sa.dA_pos = ws.item.dA;
-    sa.partials = ws.partials;
-    sa.blocks = ws.score_blocks;
-    if ((rc = launch_score_loss(sa, s))) return rc;
-    if (A.loss_out) {
-        if ((rc = launch_loss_finalize(ws.partials, ws.score_blocks, B, N, D, sa.lambda_u, sa.lambda_i, sa.mimic,
-                                       A.loss_out, A.loss_accum, s)))
-            return rc;
-    }
-    // ---- backward -----------------------------------------------------------------------
-    if ((rc = tower_backward(T, W, D, s, 2))) return rc;
-    // ---- optimizers ---------------------------------------------------------------------
-    const ttamm_hparams& hp = A.hp;
-    const AdamConsts ad = make_adam_consts(hp.lr, hp.beta1, hp.beta2, hp.eps, hp.weight_decay,
-                                           hp.decoupled_weight_decay, hp.dense_step);
-    const SparseConsts sp = make_sparse_consts(hp.sparse_lr, hp.sparse_beta1, hp.sparse_beta2, hp.sparse_eps,
-                                               hp.sparse_step);
-    if ((rc = tower_optimizer_rows(A.user, ws.user, D, B, mimic, sp, ad, false, s))) return rc;
-    if ((rc = tower_optimizer_rows(A.item, ws.item, D, B, mimic, sp, ad, true, s))) return rc;
+    for (int k = 0; k < n; ++k)
+        if ((rc = tower_optimizer_rows(*T[k], *W[k], D, mimic, sp, ad, s))) return rc;
     SweepArgs sw;
     std::memset(&sw, 0, sizeof(sw));
     sw.ad = ad;
-    auto add_seg = [&](const ttamm_table& tb) {
-        sw.seg[sw.count].p = tb.weight;
-        sw.seg[sw.count].m = tb.exp_avg;
-        sw.seg[sw.count].v = tb.exp_avg_sq;
-        sw.seg[sw.count].n = tb.rows * tb.dim;
-        sw.count++;
-    };
-    if (mimic) {
-        add_seg(A.user.mimic);
-        add_seg(A.item.mimic);
-    }
-    if (A.user.id.optimizer == TTAMM_OPT_DENSE) add_seg(A.user.id);
-    if (A.item.id.optimizer == TTAMM_OPT_DENSE) add_seg(A.item.id);
-    if (A.timing_events[0]) TTAMM_HIP(hipEventRecord((hipEvent_t)A.timing_events[0], s));
+    if (mimic)
+        for (int k = 0; k < n; ++k) add_seg(sw, T[k]->mimic);
+    for (int k = 0; k < n; ++k)
+        if (T[k]->id.optimizer == TTAMM_OPT_DENSE) add_seg(sw, T[k]->id);
+    if (events && events[0]) TTAMM_HIP(hipEventRecord((hipEvent_t)events[0], s));
     if ((rc = launch_dense_sweep(sw, s))) return rc;
-    if (A.timing_events[1]) TTAMM_HIP(hipEventRecord((hipEvent_t)A.timing_events[1], s));
-    for (int k = 0; k < 2; ++k) {
+    if (events && events[1]) TTAMM_HIP(hipEventRecord((hipEvent_t)events[1], s));
+    for (int k = 0; k < n; ++k) {
         const ttamm_tower& t = *T[k];
         TowerWs& w = *W[k];
         if (mimic)
@@ -633,6 +634,10 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
             if ((rc = launch_side_scatter(w.co.n_unique, w.co.keys_out, w.co.seg_start, w.side_id, w.R, D, t.id, s)))
                 return rc;
     }
+    return TTAMM_OK;
+}
+
+int dense_update(const ttamm_tower* T[2], TowerWs* W[2], const AdamConsts& ad, hipStream_t s) {
     DenseAdamArgs da;
     std::memset(&da, 0, sizeof(da));
     da.ad = ad;
@@ -657,7 +662,191 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
             }
         }
     }
-    if ((rc = launch_dense_adam(da, s))) return rc;
+    return launch_dense_adam(da, s);
+}
+
+int validate_step(const ttamm_step_args& A) {
+    const int D = A.user.id.dim;
+    int rc;
+    if ((rc = validate_tower(A.user, "user_encoder", D, true))) return rc;
+    if ((rc = validate_tower(A.item, "item_encoder", D, true))) return rc;
+    TTAMM_REQUIRE(A.b.batch > 0, "empty batch");
+    TTAMM_REQUIRE(A.b.num_neg > 0, "num_negatives must be greater than zero.");
+    const int64_t num_items = A.num_items_global > 0 ? A.num_items_global : A.item.id.rows;
+    TTAMM_REQUIRE(num_items > 1, "num_items must be greater than one.");
+    if (A.mimic_enabled) {
+        TTAMM_REQUIRE(A.user.mimic.weight && A.item.mimic.weight, "mimic tables missing");
+        TTAMM_REQUIRE(A.user.mimic.dim == D && A.item.mimic.dim == D &&
+                          A.user.mimic.rows == A.user.id.rows && A.item.mimic.rows == A.item.id.rows,
+                      "Adaptive mimic requires user and item embedding dimensions to match.");
+    }
+    TTAMM_REQUIRE(A.hp.dense_step >= 1 && A.hp.sparse_step >= 1, "optimizer step counts must be >= 1");
+    TTAMM_REQUIRE(A.row_base >= 0 && (A.global_batch == 0 || A.global_batch >= A.row_base + A.b.batch),
+                  "row_base / global_batch out of range");
+    if (!sharded(A)) return TTAMM_OK;
+    const int ph = A.phase;
+    TTAMM_REQUIRE((ph & ~63) == 0, "unknown phase bits");
+    TTAMM_REQUIRE(A.item_rows_capacity >= 0 && A.n_item_rows >= 0 && A.n_item_rows <= A.item_rows_capacity,
+                  "n_item_rows exceeds item_rows_capacity");
+    if (ph & TTAMM_PHASE_SAMPLE)
+        TTAMM_REQUIRE(!A.b.sample_negatives || A.b.neg_items, "sharded SAMPLE phase needs b.neg_items for the exchange");
+    if ((ph & (TTAMM_PHASE_ITEM_FWD | TTAMM_PHASE_ITEM_BWD)) && A.n_item_rows > 0)
+        TTAMM_REQUIRE(A.item_rows && A.item_row_keys, "item_rows / item_row_keys missing");
+    if (ph & TTAMM_PHASE_ITEM_FWD) TTAMM_REQUIRE(A.item_fwd_out || A.n_item_rows == 0, "item_fwd_out missing");
+    if (ph & TTAMM_PHASE_USER) TTAMM_REQUIRE(A.item_fwd_in && A.item_bwd_out, "item_fwd_in / item_bwd_out missing");
+    if (ph & TTAMM_PHASE_ITEM_BWD) TTAMM_REQUIRE(A.item_bwd_in || A.n_item_rows == 0, "item_bwd_in missing");
+    if (ph & (TTAMM_PHASE_USER | TTAMM_PHASE_ITEM_BWD | TTAMM_PHASE_DENSE))
+        TTAMM_REQUIRE(A.dense_grads != nullptr, "dense_grads missing");
+    return TTAMM_OK;
+}
+
+int run_step(const ttamm_step_args& A, hipStream_t s) {
+    int rc;
+    if ((rc = validate_step(A))) return rc;
+    const int D = A.user.id.dim;
+    const bool mimic = A.mimic_enabled != 0;
+    const bool shard = sharded(A);
+    const int ph = shard ? A.phase : 63;
+
+    Arena ar{static_cast<char*>(A.workspace), A.workspace_bytes, 0, false};
+    StepWs ws;
+    plan(ar, A, ws);
+    TTAMM_REQUIRE(ar.ok(), "workspace too small for this step");
+
+    const int64_t B = A.b.batch;
+    const int N = A.b.num_neg;
+    const int64_t Bg = global_batch(A);
+    const int64_t num_items = A.num_items_global > 0 ? A.num_items_global : A.item.id.rows;
+    // ---- row bindings -----------------------------------------------------------------------
+    TowerWs& U = ws.user;
+    TowerWs& I = ws.item;
+    U.idx = U.fidx = A.b.users;
+    U.key_split = B;
+    U.key_base0 = A.row_base;
+    int64_t* neg = nullptr;
+    if (shard) {
+        I.R = A.n_item_rows;
+        I.idx = I.fidx = A.item_rows;
+        I.row_key = A.item_row_keys;
+        I.t = A.item_fwd_out;
+        I.a = mimic && A.item_fwd_out ? A.item_fwd_out + D : nullptr;
+        I.t_ld = 2 * D;
+        I.aug = nullptr;
+        I.dT = A.item_bwd_in;
+        I.dT_ld = 2 * D;
+        I.dA = A.item_bwd_in ? A.item_bwd_in + D : nullptr;
+        I.dA_ld = 2 * D;
+        I.dA_split = I.R;  // every row's mimic gradient is shipped in (dT | dA)
+        TTAMM_REQUIRE(coalesce_temp_bytes(I.R) <= I.co.temp_bytes, "coalesce workspace too small for n_item_rows");
+        neg = A.b.neg_items;
+    } else {
+        I.idx = I.fidx = I.idx_own;
+        // item row r < B is interaction r's positive, else negative slot r - B
+        I.key_split = B;
+        I.key_base0 = A.row_base;
+        I.key_base1 = Bg + A.row_base * N;
+        neg = I.idx_own + B;
+    }
+    const ttamm_tower* T[2] = {&A.user, &A.item};
+    TowerWs* W[2] = {&U, &I};
+    const ttamm_hparams& hp = A.hp;
+    const AdamConsts ad = make_adam_consts(hp.lr, hp.beta1, hp.beta2, hp.eps, hp.weight_decay,
+                                           hp.decoupled_weight_decay, hp.dense_step);
+    const SparseConsts sp = make_sparse_consts(hp.sparse_lr, hp.sparse_beta1, hp.sparse_beta2, hp.sparse_eps,
+                                               hp.sparse_step);
+
+    // ---- negatives --------------------------------------------------------------------------
+    if (ph & TTAMM_PHASE_SAMPLE) {
+        if (!shard)
+            TTAMM_HIP(hipMemcpyAsync(I.idx_own, A.b.pos_items, B * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+        if (A.b.sample_negatives) {
+            if ((rc = launch_sample_negatives(A.b.users, B, N, num_items, A.b.pos_offsets, A.b.pos_values, A.b.seed,
+                                              A.b.counter, A.row_base * N, neg, A.status, s)))
+                return rc;
+            if (!shard && A.b.neg_items)
+                TTAMM_HIP(hipMemcpyAsync(A.b.neg_items, neg, B * N * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+        } else if (!shard) {
+            TTAMM_REQUIRE(A.b.neg_items != nullptr, "negatives must be given when sample_negatives == 0");
+            TTAMM_HIP(hipMemcpyAsync(neg, A.b.neg_items, B * N * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+        }
+    }
+    // ---- forward ----------------------------------------------------------------------------
+    if (!shard) {
+        if ((rc = tower_forward(T, W, A.b, D, mimic, s, 2))) return rc;
+    } else {
+        const ttamm_tower* Ti[2] = {&A.item, nullptr};
+        TowerWs* Wi[2] = {&I, nullptr};
+        if ((ph & TTAMM_PHASE_ITEM_FWD) && I.R > 0)
+            if ((rc = tower_forward(Ti, Wi, A.b, D, mimic, s, 1))) return rc;
+        if (ph & TTAMM_PHASE_USER_FWD)
+            if ((rc = tower_forward(T, W, A.b, D, mimic, s, 1))) return rc;
+    }
+    // ---- score + loss (fwd + bwd seeds), user-side backward ---------------------------------
+    if (ph & TTAMM_PHASE_USER) {
+        ScoreArgs sa;
+        std::memset(&sa, 0, sizeof(sa));
+        sa.B = B;
+        sa.Bg = Bg;
+        sa.N = N;
+        sa.D = D;
+        sa.user_aug = U.aug;
+        sa.t_user = U.t;
+        sa.a_user = U.a;
+        sa.lambda_u = (float)A.hp.lambda_mimic_user;
+        sa.lambda_i = (float)A.hp.lambda_mimic_item;
+        sa.mimic = mimic ? 1 : 0;
+        sa.dT_user = U.dT_own;
+        sa.dA_user = U.dA_own;
+        if (shard) {
+            sa.item_aug = nullptr;
+            sa.t_item = A.item_fwd_in;
+            sa.a_item = mimic ? A.item_fwd_in + D : nullptr;
+            sa.ld_item = 2 * D;
+            sa.dT_item = A.item_bwd_out;
+            sa.dA_item = mimic ? A.item_bwd_out + D : nullptr;
+            sa.dA_all = 1;
+            sa.ld_dti = 2 * D;
+        } else {
+            sa.item_aug = I.aug;
+            sa.t_item = I.t;
+            sa.a_item = I.a;
+            sa.ld_item = D;
+            sa.dT_item = I.dT_own;
+            sa.dA_item = I.dA_own;
+            sa.ld_dti = D;
+        }
+        sa.partials = ws.partials;
+        sa.blocks = ws.score_blocks;
+        if ((rc = launch_score_loss(sa, s))) return rc;
+        if (A.loss_out) {
+            if ((rc = launch_loss_finalize(ws.partials, ws.score_blocks, B, Bg, N, D, sa.lambda_u, sa.lambda_i, sa.mimic,
+                                           A.loss_out, A.loss_accum, s)))
+                return rc;
+        }
+        if (!shard) {
+            // ---- the whole backward + optimizers in one process --------------------------------
+            if ((rc = tower_backward(T, W, D, s, 2))) return rc;
+            if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, A.timing_events, s))) return rc;
+            return dense_update(T, W, ad, s);
+        }
+        if ((rc = tower_backward(T, W, D, s, 1))) return rc;
+        if ((rc = table_updates(T, W, 1, D, mimic, sp, ad, nullptr, s))) return rc;
+    }
+    // ---- item-side backward on the owner ------------------------------------------------------
+    if (ph & TTAMM_PHASE_ITEM_BWD) {
+        const ttamm_tower* Ti[2] = {&A.item, nullptr};
+        TowerWs* Wi[2] = {&I, nullptr};
+        if (I.R > 0) {
+            if ((rc = tower_backward(Ti, Wi, D, s, 1))) return rc;
+        } else {
+            // no requests: this rank's item-tower gradient share is zero
+            const size_t n = tower_grad_floats(A.item);
+            if (n) TTAMM_HIP(hipMemsetAsync(I.gw[0] ? I.gw[0] : I.ggw[0], 0, n * sizeof(float), s));
+        }
+        if ((rc = table_updates(Ti, Wi, 1, D, mimic, sp, ad, A.timing_events, s))) return rc;
+    }
+    if (ph & TTAMM_PHASE_DENSE)
+        if ((rc = dense_update(T, W, ad, s))) return rc;
     return TTAMM_OK;
 }
 
@@ -668,6 +857,10 @@ size_t train_step_workspace_size(const ttamm_step_args& A) {
     StepWs ws;
     plan(ar, A, ws);
     return ar.off + 256;
+}
+
+int64_t dense_grad_floats(const ttamm_step_args& A) {
+    return (int64_t)(tower_grad_floats(A.user) + tower_grad_floats(A.item));
 }
 
 int train_step(const ttamm_step_args& A, hipStream_t s) { return run_step(A, s); }
@@ -714,6 +907,7 @@ int tower_forward_eval(const ttamm_tower& T, const int64_t* idx, const int64_t* 
         w.f = fbuf;
     }
     w.t = tbuf;
+    w.t_ld = D;
     w.a = abuf;
     w.aug = out;
     // eval mode: no dropout

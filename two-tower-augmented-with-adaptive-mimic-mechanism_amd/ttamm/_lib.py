@@ -122,7 +122,33 @@ class StepArgs(ctypes.Structure):
         ("workspace", c_vp),
         ("workspace_bytes", ctypes.c_size_t),
         ("timing_events", c_vp * 2),
+        # row-sharded multi-GPU step (ttamm.h TTAMM_PHASE_*)
+        ("phase", c_i32),
+        ("row_base", c_i64),
+        ("global_batch", c_i64),
+        ("num_items_global", c_i64),
+        ("item_rows", c_vp),
+        ("item_row_keys", c_vp),
+        ("n_item_rows", c_i64),
+        ("item_rows_capacity", c_i64),
+        ("item_fwd_out", c_vp),
+        ("item_fwd_in", c_vp),
+        ("item_bwd_out", c_vp),
+        ("item_bwd_in", c_vp),
+        ("dense_grads", c_vp),
     ]
+
+
+ABI_VERSION = 2  # ttamm.h TTAMM_ABI_VERSION
+
+# ttamm.h TTAMM_PHASE_*
+PHASE_ALL = 0
+PHASE_SAMPLE = 1
+PHASE_ITEM_FWD = 2
+PHASE_USER_FWD = 4
+PHASE_USER = 8
+PHASE_ITEM_BWD = 16
+PHASE_DENSE = 32
 
 
 # Symbol table: name -> (restype, argtypes).  tests/ check every one is exported and that this
@@ -132,6 +158,7 @@ SIGNATURES = {
     "ttamm_last_error": (ctypes.c_char_p, []),
     "ttamm_train_step_workspace_size": (ctypes.c_size_t, [ctypes.POINTER(StepArgs)]),
     "ttamm_train_step": (ctypes.c_int, [ctypes.POINTER(StepArgs), c_vp]),
+    "ttamm_dense_grad_floats": (c_i64, [ctypes.POINTER(StepArgs)]),
     "ttamm_gather_rows": (ctypes.c_int, [c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "ttamm_tower_forward_workspace_size": (ctypes.c_size_t, [ctypes.POINTER(Tower), c_i64]),
     "ttamm_tower_forward": (

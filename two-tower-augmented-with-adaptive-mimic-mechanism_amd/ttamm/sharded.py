@@ -1,0 +1,330 @@
+"""Row-sharded multi-GPU training step (one process per GPU, RCCL over xGMI).
+
+The reference trains on one device (training.py:1243-1244); a W-rank step here is defined as
+the reference's step over the GLOBAL batch formed by concatenating the ranks' batches
+(rank-major).  Each rank owns
+
+  * users u with u % W == rank (local row u // W): ID + mimic rows, feature rows, positives;
+    a rank's batch holds only its own users, so the user side needs no exchange;
+  * items i with i % W == rank (local row i // W): ID + mimic rows and feature rows; the item
+    tower of an item runs on its owner for whoever requested it;
+  * a replica of the feature-encoder / gate weights (all-reduced gradients).
+
+Per step (ttamm.h TTAMM_PHASE_*):
+
+  SAMPLE    negatives for the rank's users, from the global item range
+  a2a       requested item ids + their global request positions -> owners
+  ITEM_FWD  owner: item tower over the requested rows            -> (t | a) rows
+  a2a       (t | a) rows -> requesters               (overlaps USER_FWD on the GPU)
+  USER_FWD  user tower
+  USER      scores, losses, user backward + user-table updates   -> (dT | dA) rows
+  a2a       (dT | dA) rows -> owners
+  ITEM_BWD  owner: item backward + item-table updates
+  allreduce replicated-weight gradients (+ this rank's loss share, same buffer)
+  DENSE     AdamW on the replicated weights
+
+Negative sampling and dropout draw from Philox streams keyed by global positions, so the W
+ranks draw exactly what one process would for the global batch; losses are normalised by the
+global batch.  Every rank sweeps AdamW(g=0) over its own table shards only.
+
+The step is written as an SPMD program that yields a request at each collective.
+``TorchComm`` serves the requests with torch.distributed (RCCL on ROCm, gloo on CPU);
+``run_loopback`` runs W programs in one process in lock step (the single-GPU parity test).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Any, Callable, Generator, Mapping, Sequence
+
+import torch
+
+from . import _lib
+from .training import FusedTrainStep
+
+
+# ---------------------------------------------------------------------------------------
+# ownership
+# ---------------------------------------------------------------------------------------
+@dataclass(frozen=True)
+class RowOwnership:
+    """Row i of a table lives on rank i % world_size at local row i // world_size."""
+
+    world_size: int
+    rank: int
+
+    def __post_init__(self) -> None:
+        if self.world_size < 1 or not 0 <= self.rank < self.world_size:
+            raise ValueError("ttamm: bad (world_size, rank)")
+
+    def local_count(self, rows: int) -> int:
+        return max(0, (rows - self.rank + self.world_size - 1) // self.world_size)
+
+    def owner(self, ids: torch.Tensor) -> torch.Tensor:
+        return torch.remainder(ids, self.world_size)
+
+    def local(self, ids: torch.Tensor) -> torch.Tensor:
+        return torch.div(ids, self.world_size, rounding_mode="floor")
+
+    def global_ids(self, local_rows: torch.Tensor) -> torch.Tensor:
+        return local_rows * self.world_size + self.rank
+
+    def shard(self, full: torch.Tensor) -> torch.Tensor:
+        """This rank's rows of a global table (a copy, contiguous)."""
+        return full[self.rank :: self.world_size].contiguous()
+
+
+# ---------------------------------------------------------------------------------------
+# collectives as requests
+# ---------------------------------------------------------------------------------------
+@dataclass
+class AllToAll:
+    """Rows of ``send`` grouped by destination (``send_splits`` rows each) -> rows grouped by
+    source (``recv_splits`` rows each)."""
+
+    send: torch.Tensor
+    send_splits: list[int]
+    recv_splits: list[int]
+    async_op: bool = False
+
+
+@dataclass
+class Wait:
+    handle: Any
+
+
+@dataclass
+class AllReduce:
+    """In-place sum over ranks."""
+
+    tensor: torch.Tensor
+
+
+Program = Generator[Any, Any, Any]
+
+
+class TorchComm:
+    """Serves a program's requests with torch.distributed (backend "nccl" is RCCL on ROCm)."""
+
+    def __init__(self, group: Any = None) -> None:
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.group = group
+
+    def __call__(self, req: Any) -> Any:
+        dist = self.dist
+        if isinstance(req, AllToAll):
+            out = req.send.new_empty((sum(req.recv_splits),) + tuple(req.send.shape[1:]))
+            work = dist.all_to_all_single(out, req.send.contiguous(), req.recv_splits, req.send_splits,
+                                          group=self.group, async_op=req.async_op)
+            return (work, out) if req.async_op else out
+        if isinstance(req, Wait):
+            work, out = req.handle
+            work.wait()
+            return out
+        if isinstance(req, AllReduce):
+            dist.all_reduce(req.tensor, group=self.group)
+            return req.tensor
+        raise TypeError(f"unknown collective request {req!r}")
+
+    def run(self, program: Program) -> Any:
+        res = None
+        try:
+            while True:
+                res = self(program.send(res))
+        except StopIteration as stop:
+            return stop.value
+
+
+def run_loopback(programs: Sequence[Program]) -> list[Any]:
+    """Run W SPMD programs in one process, serving their collectives jointly.  Rank order is
+    the reduction order of AllReduce (fixed, deterministic)."""
+    W = len(programs)
+    results: list[Any] = [None] * W
+    done: list[bool] = [False] * W
+    values: list[Any] = [None] * W
+    while not all(done):
+        reqs: list[Any] = [None] * W
+        for r, prog in enumerate(programs):
+            if done[r]:
+                continue
+            try:
+                reqs[r] = prog.send(results[r])
+            except StopIteration as stop:
+                done[r] = True
+                values[r] = stop.value
+        if all(done):
+            break
+        if any(done):
+            raise RuntimeError("loopback: ranks issued different collective sequences")
+        kind = type(reqs[0])
+        if any(type(q) is not kind for q in reqs):
+            raise RuntimeError("loopback: ranks issued different collectives")
+        if kind is AllToAll:
+            chunks = [list(torch.split(q.send, q.send_splits)) for q in reqs]
+            for d in range(W):
+                got = torch.cat([chunks[s][d] for s in range(W)])
+                if got.shape[0] != sum(reqs[d].recv_splits):
+                    raise RuntimeError("loopback: recv splits do not match the senders")
+                results[d] = ("done", got) if reqs[d].async_op else got
+        elif kind is Wait:
+            for r in range(W):
+                results[r] = reqs[r].handle[1]
+        elif kind is AllReduce:
+            total = reqs[0].tensor.clone()
+            for r in range(1, W):
+                total += reqs[r].tensor
+            for r in range(W):
+                reqs[r].tensor.copy_(total)
+                results[r] = reqs[r].tensor
+        else:
+            raise TypeError(f"unknown collective request {reqs[0]!r}")
+    return values
+
+
+# ---------------------------------------------------------------------------------------
+# request routing
+# ---------------------------------------------------------------------------------------
+@dataclass
+class Route:
+    order: torch.Tensor  # request positions grouped by owner rank (stable)
+    send_counts: list[int]  # requests to each owner
+    recv_counts: list[int]  # requests from each requester
+    rows: torch.Tensor  # owner side: local rows requested [n_recv]
+    keys: torch.Tensor  # owner side: global request positions [n_recv]
+
+
+def route_requests(own: RowOwnership, items: torch.Tensor, keys: torch.Tensor) -> Program:
+    """Program: send (local row, key) of every requested item to its owner.  Returns a Route."""
+    W = own.world_size
+    owner = own.owner(items)
+    order = torch.argsort(owner, stable=True)
+    counts = torch.bincount(owner, minlength=W)
+    recv = yield AllToAll(counts, [1] * W, [1] * W)
+    send_counts = counts.tolist()
+    recv_counts = recv.tolist()
+    packed = torch.stack([own.local(items)[order], keys[order]], dim=1)
+    got = yield AllToAll(packed, send_counts, recv_counts)
+    return Route(order, send_counts, recv_counts, got[:, 0].contiguous(), got[:, 1].contiguous())
+
+
+# ---------------------------------------------------------------------------------------
+# the sharded step
+# ---------------------------------------------------------------------------------------
+class ShardedTrainStep(FusedTrainStep):
+    """FusedTrainStep over a rank's shard.  ``model`` holds this rank's rows of the user / item
+    ID and mimic tables (``RowOwnership.shard``) and a replica of the feature-encoder and gate
+    weights; ``user_features`` / ``item_features`` are this rank's rows; ``positives`` is
+    keyed by LOCAL user row and holds GLOBAL item ids; ``num_items`` is the global item count.
+
+    Every rank must call ``step`` with the same batch size (the global batch is W x B, rank r's
+    interactions are global positions [r B, (r+1) B)); ``step`` and ``finish`` are collective.
+    """
+
+    def __init__(self, model, optimizers, *, world_size: int, rank: int, num_items: int,
+                 comm: Callable[[Program], Any] | None = None, **kw: Any) -> None:
+        self.own = RowOwnership(world_size, rank)
+        self.comm = comm
+        super().__init__(model, optimizers, num_items=num_items, **kw)
+
+    def _configure(self, args: _lib.StepArgs) -> None:
+        W = self.own.world_size
+        R = self.max_batch * (1 + self.num_neg)
+        # worst case: every requester sends all its rows to this owner
+        self.capacity = W * R
+        args.phase = _lib.PHASE_SAMPLE  # any non-zero phase: size the sharded workspace
+        args.item_rows_capacity = self.capacity
+        args.num_items_global = self.num_items
+        n_grad = int(self.lib.ttamm_dense_grad_floats(ctypes.byref(args)))
+        # gradient arena + this rank's loss share: one all-reduce carries both
+        self.arena = torch.zeros(n_grad + 4, dtype=torch.float32, device=self.device)
+        self.n_grad = n_grad
+        self.loss_out = self.arena[n_grad:]
+        args.loss_out = self.loss_out.data_ptr()
+        args.dense_grads = self.arena.data_ptr()
+        D = self.model.user_encoder.embedding.weight.shape[1]
+        self.D = D
+        self.fwd_out = torch.empty((self.capacity, 2 * D), dtype=torch.float32, device=self.device)
+        self.fwd_in = torch.empty((R, 2 * D), dtype=torch.float32, device=self.device)
+        self.bwd_out = torch.empty((R, 2 * D), dtype=torch.float32, device=self.device)
+
+    def _phase(self, bits: int) -> None:
+        self.args.phase = bits
+        _lib.check(self.lib.ttamm_train_step(ctypes.byref(self.args), _lib.stream_handle(self.device)))
+
+    def program(self, users: torch.Tensor, pos_items: torch.Tensor, neg_items: torch.Tensor | None = None, *,
+                keep_masks: Mapping[str, Sequence[torch.Tensor]] | None = None,
+                timing_events: tuple[Any, Any] | None = None) -> Program:
+        """One step as an SPMD program (yields collective requests).  ``timing_events`` (a
+        hipEvent_t pair) bracket the owner's item-table AdamW sweep."""
+        if not self._bind_batch(users, pos_items, neg_items, keep_masks):
+            raise ValueError("ttamm: empty batch in a sharded step (every rank must step)")
+        a = self.args
+        W, rank = self.own.world_size, self.own.rank
+        B, N, D = users.numel(), self.num_neg, self.D
+        Bg = W * B
+        a.row_base = rank * B
+        a.global_batch = Bg
+        a.timing_events[0] = a.timing_events[1] = None
+        self._hparams()
+        negs = neg_items.reshape(-1) if neg_items is not None else self.neg_buffer[: B * N]
+        self._phase(_lib.PHASE_SAMPLE)
+        # ---- route the item requests [positives; negatives] to their owners -----------------
+        req = torch.cat([pos_items.reshape(-1), negs])
+        dev = req.device
+        keys = torch.cat([torch.arange(B, device=dev) + rank * B,
+                          torch.arange(B * N, device=dev) + (Bg + rank * B * N)])
+        route = yield from route_requests(self.own, req, keys)
+        n = route.rows.numel()
+        if n > self.capacity:
+            raise RuntimeError("ttamm: item requests exceed the sharded step's capacity")
+        a.item_rows = route.rows.data_ptr()
+        a.item_row_keys = route.keys.data_ptr()
+        a.n_item_rows = n
+        a.item_fwd_out = self.fwd_out.data_ptr()
+        self._phase(_lib.PHASE_ITEM_FWD)
+        # ---- (t | a) back to the requesters, user tower meanwhile ----------------------------
+        h = yield AllToAll(self.fwd_out[:n], route.recv_counts, route.send_counts, async_op=True)
+        self._phase(_lib.PHASE_USER_FWD)
+        back = yield Wait(h)
+        R = B * (1 + N)
+        fwd_in = self.fwd_in[:R]
+        fwd_in.index_copy_(0, route.order, back)
+        a.item_fwd_in = fwd_in.data_ptr()
+        a.item_bwd_out = self.bwd_out.data_ptr()
+        self._phase(_lib.PHASE_USER)
+        # ---- (dT | dA) to the owners -----------------------------------------------------------
+        bwd_in = yield AllToAll(self.bwd_out[:R].index_select(0, route.order), route.send_counts,
+                                route.recv_counts)
+        a.item_bwd_in = bwd_in.data_ptr()
+        if timing_events:
+            a.timing_events[0], a.timing_events[1] = timing_events
+        self._phase(_lib.PHASE_ITEM_BWD)
+        a.timing_events[0] = a.timing_events[1] = None
+        yield AllReduce(self.arena)
+        self._phase(_lib.PHASE_DENSE)
+        self.steps_done += 1
+        # keep the step's device buffers alive until the stream has consumed them
+        self._live = (route, back, bwd_in, req, keys)
+
+    def step(self, users, pos_items, neg_items=None, *, keep_masks=None, timing_events=None) -> None:
+        if self.comm is None:
+            raise RuntimeError("ttamm: ShardedTrainStep.step needs comm= (e.g. TorchComm()); "
+                               "use program() with run_loopback for in-process ranks")
+        self.comm.run(self.program(users, pos_items, neg_items, keep_masks=keep_masks, timing_events=timing_events))
+
+    def finish_program(self) -> Program:
+        """Collective finish: global epoch loss (sum of the ranks' shares)."""
+        yield AllReduce(self.loss_accum)
+        return FusedTrainStep.finish(self)
+
+    def finish(self) -> float:
+        if self.comm is None:
+            raise RuntimeError("ttamm: ShardedTrainStep.finish needs comm=")
+        return self.comm.run(self.finish_program())
+
+    def last_losses(self) -> dict[str, float]:
+        """Global losses of the last step (the all-reduced shares)."""
+        return super().last_losses()

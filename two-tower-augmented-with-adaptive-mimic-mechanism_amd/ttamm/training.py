@@ -119,6 +119,7 @@ class FusedTrainStep:
         loss_weights: Mapping[str, Any] | None = None,
         max_batch: int,
         seed: int | None = None,
+        num_items: int | None = None,
     ) -> None:
         if negatives_per_positive <= 0:
             raise ValueError("num_negatives must be greater than zero.")
@@ -129,7 +130,9 @@ class FusedTrainStep:
             raise NotImplementedError("ttamm: towers must be ttamm.encoders.TowerEncoder")
         self.device = ue.embedding.weight.device
         _lib.require_rocm(ue.embedding.weight, "FusedTrainStep")
-        if ie.num_embeddings <= 1:
+        # the sampler's range: the item table, or the global item count of a sharded step
+        self.num_items = int(num_items) if num_items is not None else ie.num_embeddings
+        if self.num_items <= 1:
             raise ValueError("num_items must be greater than one.")
         mimic = getattr(model, "adaptive_mimic", None)
         self.mimic = mimic
@@ -226,7 +229,7 @@ class FusedTrainStep:
         self.csr = None
         if positives is not None:
             self.csr = positives_csr(positives, device=self.device, num_users=ue.num_embeddings)
-            if self.csr.max_degree >= ie.num_embeddings:
+            if self.csr.max_degree >= self.num_items:
                 raise RuntimeError("a user interacted with all items; cannot sample negatives.")
             args.b.pos_offsets = self.csr.offsets.data_ptr()
             args.b.pos_values = self.csr.values.data_ptr()
@@ -240,6 +243,7 @@ class FusedTrainStep:
         self.max_batch = int(max_batch)
         args.b.batch = self.max_batch
         self.lib = _lib.load()
+        self._configure(args)
         self.ws_bytes = int(self.lib.ttamm_train_step_workspace_size(ctypes.byref(args)))
         self.workspace = torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
         args.workspace = self.workspace.data_ptr()
@@ -251,6 +255,9 @@ class FusedTrainStep:
         self.sparse_step0 = int(self._sparse_steps[0]["step"]) if self._sparse_steps else 0
 
     # ------------------------------------------------------------------------------------
+    def _configure(self, args: _lib.StepArgs) -> None:
+        """Hook: descriptor fields that shape the workspace (set before it is sized)."""
+
     def _hparams(self) -> None:
         hp = self.args.hp
         if self.dense_opt is not None:
@@ -278,13 +285,25 @@ class FusedTrainStep:
         timing_events: tuple[Any, Any] | None = None,
     ) -> None:
         """Enqueue one training step on the current stream (no host synchronisation)."""
+        if not self._bind_batch(users, pos_items, neg_items, keep_masks):
+            return
+        a = self.args
+        a.timing_events[0] = timing_events[0] if timing_events else None
+        a.timing_events[1] = timing_events[1] if timing_events else None
+        self._hparams()
+        _lib.check(self.lib.ttamm_train_step(ctypes.byref(a), _lib.stream_handle(self.device)))
+        self.steps_done += 1
+
+    def _bind_batch(self, users, pos_items, neg_items, keep_masks) -> bool:
         B = users.numel()
         if B == 0:
-            return
+            return False
         if B > self.max_batch:
             raise ValueError("ttamm: batch larger than the step was sized for")
         if users.dtype != torch.long or pos_items.dtype != torch.long:
             raise ValueError("Adaptive mimic indices must be torch.long tensors.")
+        if pos_items.numel() != B:
+            raise ValueError("ttamm: one positive item per interaction")
         _lib.require_rocm(users, "train step")
         a = self.args
         a.b.users = users.data_ptr()
@@ -305,11 +324,7 @@ class FusedTrainStep:
             masks = (keep_masks or {}).get(side) or []
             for i in range(_lib.MAX_LINEAR):
                 field[i] = masks[i].data_ptr() if i < len(masks) and masks[i] is not None else None
-        a.timing_events[0] = timing_events[0] if timing_events else None
-        a.timing_events[1] = timing_events[1] if timing_events else None
-        self._hparams()
-        _lib.check(self.lib.ttamm_train_step(ctypes.byref(a), _lib.stream_handle(self.device)))
-        self.steps_done += 1
+        return True
 
     def finish(self) -> float:
         """Synchronise, surface device-side errors, write the optimizer step counters back,
