@@ -93,7 +93,8 @@ def zipf_items(n: int, I: int, s: float, device, gen: torch.Generator, perm: tor
 class Workload:
     """C2 data + model on one GPU, or rank `rank`'s C2-sized shard of an N x C2 model."""
 
-    def __init__(self, c: dict, device, seed: int, world: int = 1, rank: int = 0, step_seed: int | None = None):
+    def __init__(self, c: dict, device, seed: int, world: int = 1, rank: int = 0, step_seed: int | None = None,
+                 deferred: bool = True):
         import ttamm
         from ttamm.samplers import PositivesCSR
 
@@ -138,7 +139,7 @@ class Workload:
         self.opts = [torch.optim.AdamW(dense, lr=1e-3, weight_decay=0.01), torch.optim.SparseAdam(sparse, lr=1e-3)]
         kw = dict(negatives_per_positive=c["N"], positives=self.csr, user_features=self.user_features,
                   item_features=self.item_features, loss_weights={"mimic_user": 0.15, "mimic_item": 0.15},
-                  max_batch=c["B"])
+                  max_batch=c["B"], deferred_adamw=deferred)
         if world == 1:
             self.engine = ttamm.FusedTrainStep(self.model, self.opts, seed=seed, **kw)
         else:
@@ -223,6 +224,8 @@ def main() -> None:
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--cpu-steps", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager-adamw", action="store_true",
+                    help="sweep AdamW(g=0) over the whole mimic tables every step instead of the deferred exact replay")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -241,11 +244,13 @@ def main() -> None:
 
     from ttamm import _lib
 
-    w = Workload(c, device, args.seed + rank, world=world, rank=rank, step_seed=args.seed)
+    w = Workload(c, device, args.seed + rank, world=world, rank=rank, step_seed=args.seed,
+                 deferred=not args.eager_adamw)
     eng = w.engine
     for _ in range(args.warmup):
         u, p = w.batch()
         eng.step(u, p)
+    eng.flush()  # the timed region starts with every table row current
     torch.cuda.synchronize()
 
     # per-step HIP events around the dominant kernel, on the step's stream
@@ -263,6 +268,8 @@ def main() -> None:
     for k in range(args.steps):
         u, p = batches[k]
         eng.step(u, p, timing_events=(evs[k][0].cuda_event, evs[k][1].cuda_event))
+    # deferred AdamW: the g = 0 updates still owed to untouched rows are part of the K steps' work
+    eng.flush()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 2
+#define TTAMM_ABI_VERSION 3
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -99,6 +99,12 @@ typedef struct ttamm_table {
     int64_t rows;
     int32_t dim;
     int32_t optimizer; /* TTAMM_OPT_* */
+    /* Dense-group (AdamW) tables only.  NULL: every step sweeps AdamW(g = 0) over the whole
+     * table (training.py:1316-1323 semantics, executed eagerly).  Non-NULL: per-row dense
+     * step count the row is current to; the g = 0 updates a row missed are replayed exactly
+     * (same fp32 operations, same per-step constants from adam_history) before the row is
+     * read, on a rolling 1/replay_slices of the rows each step, and by ttamm_flush_tables. */
+    int32_t* last_step;
 } ttamm_table;
 
 /* One tower: TowerEncoder (encoders.py:171-255) + its half of AdaptiveMimicMechanism
@@ -184,6 +190,12 @@ typedef struct ttamm_step_args {
     const float* item_bwd_in;     /* owner:     [n_item_rows, 2*dim] (dT | dA)               */
     float* dense_grads;           /* replicated-weight gradient arena
                                      (ttamm_dense_grad_floats floats)                        */
+    /* ---- deferred exact AdamW(g = 0) on tables with last_step (see ttamm_table) ---------- */
+    void* adam_history;           /* device ring: history_capacity entries of
+                                     ttamm_adam_history_entry_bytes() each                  */
+    int32_t history_capacity;     /* > replay_slices                                         */
+    int32_t replay_slices;        /* every row is replayed at least once per replay_slices
+                                     steps (bounds the lag a read has to catch up)           */
 } ttamm_step_args;
 
 /* ---------------------------------------------------------------------------------- */
@@ -202,6 +214,12 @@ int ttamm_train_step(const ttamm_step_args* args, void* stream);
 /* Size (floats) of the replicated-weight gradient arena of a sharded step: both towers'
  * feature-encoder and gate weight+bias gradients, contiguous (the all-reduce buffer). */
 int64_t ttamm_dense_grad_floats(const ttamm_step_args* args);
+
+/* Deferred AdamW(g = 0): bytes of one adam_history entry, and the flush that brings every row
+ * of every dense-group table with last_step up to hp.dense_step (call before the tables or
+ * their optimizer state are read outside the step: evaluation, checkpoints, epoch end). */
+size_t ttamm_adam_history_entry_bytes(void);
+int ttamm_flush_tables(const ttamm_step_args* args, void* stream);
 
 /* nn.Embedding forward / AdaptiveMimicMechanism._gather_and_reshape
  * (encoders.py:222-223, adaptive_mimic.py:97-105): out[r, :] = table[idx[r], :]. */

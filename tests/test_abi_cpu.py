@@ -20,8 +20,10 @@ def header_functions() -> list[str]:
 
 
 def test_header_parses_as_c_and_cxx(tmp_path):
+    from ttamm import _lib
+
     src = tmp_path / "h.c"
-    src.write_text(f'#include "{HEADER}"\nint main(void) {{ return TTAMM_ABI_VERSION == 2 ? 0 : 1; }}\n')
+    src.write_text(f'#include "{HEADER}"\nint main(void) {{ return TTAMM_ABI_VERSION == {_lib.ABI_VERSION} ? 0 : 1; }}\n')
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", str(src), "-o", str(tmp_path / "h")], check=True)
     subprocess.run([str(tmp_path / "h")], check=True)
     cxx = tmp_path / "h.cpp"

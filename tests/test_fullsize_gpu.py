@@ -37,6 +37,7 @@ def test_c2_deterministic_and_adamw_untouched_rows(c2):
     table0 = w1.model.adaptive_mimic.item_augmented.weight.detach().clone()
     batches = [w1.batch() for _ in range(2)]
     w1.engine.step(*batches[0])
+    w1.engine.flush()  # deferred AdamW: bring the untouched rows current before reading them
     torch.cuda.synchronize()
     touched = torch.cat([batches[0][1], w1.engine.neg_buffer]).unique()
     mask = torch.ones(c2["I"], dtype=torch.bool, device="cuda")

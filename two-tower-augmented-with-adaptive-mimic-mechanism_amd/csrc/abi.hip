@@ -18,6 +18,7 @@ int fail(int code, const std::string& msg) {
 size_t train_step_workspace_size(const ttamm_step_args& A);
 int train_step(const ttamm_step_args& A, hipStream_t s);
 int64_t dense_grad_floats(const ttamm_step_args& A);
+int flush_tables(const ttamm_step_args& A, hipStream_t s);
 size_t tower_forward_workspace_size(const ttamm_tower& T, int64_t n);
 int tower_forward_eval(const ttamm_tower& T, const int64_t* idx, const int64_t* fidx, int64_t n, int augment,
                        float* out, void* ws, size_t ws_bytes, hipStream_t s);
@@ -40,6 +41,14 @@ TTAMM_API size_t ttamm_train_step_workspace_size(const ttamm_step_args* args) {
 TTAMM_API int64_t ttamm_dense_grad_floats(const ttamm_step_args* args) {
     if (!args) return 0;
     return dense_grad_floats(*args);
+}
+
+TTAMM_API size_t ttamm_adam_history_entry_bytes(void) { return sizeof(AdamConsts); }
+
+TTAMM_API int ttamm_flush_tables(const ttamm_step_args* args, void* stream) {
+    if (!args) return fail(TTAMM_E_INVALID, "null step args");
+    g_last_error.clear();
+    return flush_tables(*args, (hipStream_t)stream);
 }
 
 TTAMM_API int ttamm_train_step(const ttamm_step_args* args, void* stream) {

@@ -7,6 +7,11 @@
 
 #include "../../include/ttamm.h"
 
+// A kernel argument viewed in place in the kernarg segment (address space 4): indexing an
+// array member of a by-value kernel argument with a runtime index would otherwise copy the
+// whole argument to scratch.  Use with __builtin_amdgcn_kernarg_segment_ptr().
+#define KArg(T) __attribute__((address_space(4))) T
+
 namespace ttamm {
 
 // ---- error plumbing ---------------------------------------------------------------

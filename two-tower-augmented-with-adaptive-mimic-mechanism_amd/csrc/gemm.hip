@@ -40,7 +40,6 @@ namespace {
 
 // Kernel-argument (constant address space) view of a struct: indexing the by-value problem
 // table with a block-uniform index then compiles to scalar loads instead of a scratch copy.
-#define KArg(T) __attribute__((address_space(4))) T
 
 constexpr int BK = 16;
 constexpr int SK = BK + 4;  // MN-major LDS row stride (floats): keeps ds_read_b128 conflict-free

@@ -212,8 +212,40 @@ struct RowUpdateArgs {
     float* side_mimic;
     SparseConsts sp;
     AdamConsts ad;
+    int32_t dense_step;     // deferred mode (table.last_step): rows are updated in place and
+                            // stamped current to this step
 };
 int launch_row_update(const RowUpdateArgs& a, hipStream_t s);
+
+// ---- deferred exact AdamW(g = 0) (ttamm.h ttamm_table.last_step) ------------------------
+// history[t % cap] holds the fp32 constants of dense step t; a row current to step l that is
+// brought to step T replays adam_elem(g = 0) with history[l+1 .. T] — the same operations the
+// eager sweep would have applied, so the bits agree.
+constexpr int kMaxAdamHistory = 512;
+int launch_history_put(AdamConsts* hist, int cap, int64_t step, const AdamConsts& c, hipStream_t s);
+struct ReplaySeg {
+    float* p;
+    float* m;
+    float* v;
+    int32_t* last;
+    int dim;
+    // rows [row_lo, row_hi) ...
+    int64_t row_lo, row_hi;
+    // ... or the unique keys of a coalesced batch (keys != null): keys[seg_start[u]], u < n_unique
+    const int32_t* keys;
+    const int32_t* seg_start;
+    const int32_t* n_unique;
+};
+constexpr int kMaxReplaySegs = 4;
+struct ReplayArgs {
+    ReplaySeg seg[kMaxReplaySegs];
+    int count;
+    const AdamConsts* hist;
+    int cap;
+    int32_t target;   // replay every row up to this dense step
+    int stamp;        // write last = target afterwards (row ranges only)
+};
+int launch_replay(const ReplayArgs& a, hipStream_t s);
 
 struct SweepSeg {
     float* p;

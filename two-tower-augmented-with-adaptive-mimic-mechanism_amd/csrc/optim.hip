@@ -159,6 +159,11 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArg
                 A.id.weight[o] = p;
                 A.id.exp_avg[o] = m;
                 A.id.exp_avg_sq[o] = v;
+            } else if (A.id.last_step) {  // deferred mode: the row was caught up before the forward
+                adam_elem(p, m, v, ge, A.ad);
+                A.id.weight[o] = p;
+                A.id.exp_avg[o] = m;
+                A.id.exp_avg_sq[o] = v;
             } else {
                 adam_elem(p, m, v, ge, A.ad);
                 float* sd = A.side_id + u * 3 * D;
@@ -171,11 +176,21 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArg
             const int64_t o = key * D + d;
             float p = A.mimic.weight[o], m = A.mimic.exp_avg[o], v = A.mimic.exp_avg_sq[o];
             adam_elem(p, m, v, ga, A.ad);
-            float* sd = A.side_mimic + u * 3 * D;
-            sd[d] = p;
-            sd[D + d] = m;
-            sd[2 * D + d] = v;
+            if (A.mimic.last_step) {
+                A.mimic.weight[o] = p;
+                A.mimic.exp_avg[o] = m;
+                A.mimic.exp_avg_sq[o] = v;
+            } else {
+                float* sd = A.side_mimic + u * 3 * D;
+                sd[d] = p;
+                sd[D + d] = m;
+                sd[2 * D + d] = v;
+            }
         }
+    }
+    if (lane == 0) {
+        if (A.id.optimizer != TTAMM_OPT_SPARSE_ADAM && A.id.last_step) A.id.last_step[key] = A.dense_step;
+        if (mimic && A.mimic.last_step) A.mimic.last_step[key] = A.dense_step;
     }
 }
 
@@ -207,6 +222,55 @@ __global__ __launch_bounds__(256) void dense_sweep_kernel(SweepArgs A) {
             S.v[i] = v;
         }
     }
+}
+
+// ---- deferred exact AdamW(g = 0) ----------------------------------------------------------
+constexpr int kMaxHistory = kMaxAdamHistory;
+
+__global__ void history_put_kernel(AdamConsts* hist, int cap, int64_t step, AdamConsts c) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) hist[step % cap] = c;
+}
+
+// One thread per element; blockIdx.y = segment.  A row current to step l is brought to
+// A.target by replaying adam_elem(g = 0) with the constants of steps l+1 .. target.
+__global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
+    const KArg(ReplayArgs)* ka = (const KArg(ReplayArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
+    const KArg(ReplaySeg)& S = ka->seg[blockIdx.y];
+    __shared__ AdamConsts H[kMaxHistory];
+    const int cap = ka->cap;
+    for (int i = threadIdx.x; i < cap; i += blockDim.x) H[i] = ka->hist[i];
+    __syncthreads();
+    const int dim = S.dim;
+    const int32_t target = ka->target;
+    const bool by_key = S.keys != nullptr;
+    const int64_t nrows = by_key ? (int64_t)S.n_unique[0] : S.row_hi - S.row_lo;
+    const int64_t total = nrows * dim;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = e / dim;
+        const int d = (int)(e - r * dim);
+        const int64_t row = by_key ? (int64_t)S.keys[S.seg_start[r]] : S.row_lo + r;
+        const int32_t l = S.last[row];
+        if (l >= target) continue;
+        const int64_t o = row * dim + d;
+        float p = S.p[o], m = S.m[o], v = S.v[o];
+        int j = (int)((l + 1) % cap);
+        for (int32_t t = l + 1; t <= target; ++t) {
+            const AdamConsts c = H[j];
+            adam_elem(p, m, v, 0.f, c);
+            j = j + 1 == cap ? 0 : j + 1;
+        }
+        S.p[o] = p;
+        S.m[o] = m;
+        S.v[o] = v;
+    }
+}
+
+__global__ void stamp_kernel(ReplayArgs) {
+    const KArg(ReplayArgs)* ka = (const KArg(ReplayArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
+    const KArg(ReplaySeg)& S = ka->seg[blockIdx.y];
+    for (int64_t r = S.row_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < S.row_hi;
+         r += (int64_t)gridDim.x * blockDim.x)
+        S.last[r] = ka->target;
 }
 
 __global__ void side_scatter_kernel(const int32_t* __restrict__ n_unique, const int32_t* __restrict__ keys,
@@ -358,6 +422,36 @@ int launch_dense_sweep(const SweepArgs& a, hipStream_t s) {
     // 2048 blocks x 256 threads: 8 blocks per CU, grid-stride over the tables
     hipLaunchKernelGGL(dense_sweep_kernel, dim3(grid_for(total4, 256, 2048)), dim3(256), 0, s, a);
     TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_history_put(AdamConsts* hist, int cap, int64_t step, const AdamConsts& c, hipStream_t s) {
+    TTAMM_REQUIRE(hist && cap > 1 && cap <= kMaxHistory, "adam history: capacity must be in [2, 512]");
+    hipLaunchKernelGGL(history_put_kernel, dim3(1), dim3(64), 0, s, hist, cap, step, c);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_replay(const ReplayArgs& a, hipStream_t s) {
+    if (a.count == 0) return TTAMM_OK;
+    TTAMM_REQUIRE(a.count <= kMaxReplaySegs && a.hist && a.cap > 1 && a.cap <= kMaxHistory,
+                  "replay: bad arguments");
+    int64_t most = 0;
+    for (int i = 0; i < a.count; ++i) {
+        const ReplaySeg& g = a.seg[i];
+        TTAMM_REQUIRE(g.p && g.m && g.v && g.last, "replay: table without deferred state");
+        const int64_t n = g.row_hi - g.row_lo;  // keys: the coalesced batch size bounds n_unique
+        most = n * g.dim > most ? n * g.dim : most;
+    }
+    if (most == 0) return TTAMM_OK;
+    hipLaunchKernelGGL(replay_kernel, dim3(grid_for(most, 256, 8192), a.count), dim3(256), 0, s, a);
+    TTAMM_LAUNCH_CHECK();
+    if (a.stamp) {
+        int64_t rows = 0;
+        for (int i = 0; i < a.count; ++i) rows = a.seg[i].row_hi - a.seg[i].row_lo > rows ? a.seg[i].row_hi - a.seg[i].row_lo : rows;
+        hipLaunchKernelGGL(stamp_kernel, dim3(grid_for(rows, 256, 4096), a.count), dim3(256), 0, s, a);
+        TTAMM_LAUNCH_CHECK();
+    }
     return TTAMM_OK;
 }
 

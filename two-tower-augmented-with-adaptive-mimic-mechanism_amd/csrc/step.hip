@@ -563,10 +563,61 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
     return TTAMM_OK;
 }
 
-int tower_optimizer_rows(const ttamm_tower& t, TowerWs& w, int D, bool mimic, const SparseConsts& sp,
-                         const AdamConsts& ad, hipStream_t s) {
+// Deferred exact AdamW(g = 0) (ttamm.h ttamm_table.last_step).
+struct Deferred {
+    bool on = false;
+    AdamConsts* hist = nullptr;
+    int cap = 0;
+    int slices = 1;
+    int32_t step = 0;  // the dense step this call executes
+};
+
+// The tables of a tower that belong to the dense (AdamW) group.
+int dense_tables(const ttamm_tower& t, bool mimic, const ttamm_table* out[2]) {
+    int n = 0;
+    if (mimic) out[n++] = &t.mimic;
+    if (t.id.optimizer == TTAMM_OPT_DENSE) out[n++] = &t.id;
+    return n;
+}
+
+ReplaySeg replay_seg(const ttamm_table& tb) {
+    ReplaySeg g;
+    std::memset(&g, 0, sizeof(g));
+    g.p = tb.weight;
+    g.m = tb.exp_avg;
+    g.v = tb.exp_avg_sq;
+    g.last = tb.last_step;
+    g.dim = tb.dim;
+    return g;
+}
+
+// Before a tower reads its rows: coalesce the batch's rows (also needed by the row updates)
+// and, deferred, bring the dense-group rows it touches current to step - 1.
+int tower_prepare(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred& df, hipStream_t s) {
     int rc;
     if ((rc = launch_coalesce(w.idx, w.R, t.id.rows, w.co, s))) return rc;
+    if (!df.on || w.R == 0) return TTAMM_OK;
+    ReplayArgs ra;
+    std::memset(&ra, 0, sizeof(ra));
+    ra.hist = df.hist;
+    ra.cap = df.cap;
+    ra.target = df.step - 1;
+    const ttamm_table* tabs[2];
+    const int n = dense_tables(t, mimic, tabs);
+    for (int i = 0; i < n; ++i) {
+        ReplaySeg g = replay_seg(*tabs[i]);
+        g.row_lo = 0;
+        g.row_hi = w.R;  // bound of the unique count
+        g.keys = w.co.keys_out;
+        g.seg_start = w.co.seg_start;
+        g.n_unique = w.co.n_unique;
+        ra.seg[ra.count++] = g;
+    }
+    return launch_replay(ra, s);
+}
+
+int tower_optimizer_rows(const ttamm_tower& t, TowerWs& w, int D, bool mimic, const SparseConsts& sp,
+                         const AdamConsts& ad, const Deferred& df, hipStream_t s) {
     RowUpdateArgs ru;
     std::memset(&ru, 0, sizeof(ru));
     ru.n = w.R;
@@ -596,6 +647,7 @@ int tower_optimizer_rows(const ttamm_tower& t, TowerWs& w, int D, bool mimic, co
     ru.piece_a = w.piece_a;
     ru.sp = sp;
     ru.ad = ad;
+    ru.dense_step = df.step;
     return launch_row_update(ru, s);
 }
 void add_seg(SweepArgs& sw, const ttamm_table& tb) {
@@ -606,13 +658,38 @@ void add_seg(SweepArgs& sw, const ttamm_table& tb) {
     sw.count++;
 }
 
-// Touched-row updates of the tables of `n` towers, then the AdamW(g=0) sweep over their
-// dense-group tables and the scatter of the staged touched rows.
+// Touched-row updates of the tables of `n` towers, then the AdamW(g=0) step of the rows the
+// batch did not touch: eagerly, one sweep over the dense-group tables and a scatter of the
+// staged touched rows; deferred, the replay of this step's 1/slices of the rows to `step`.
 int table_updates(const ttamm_tower* T[2], TowerWs* W[2], int n, int D, bool mimic, const SparseConsts& sp,
-                  const AdamConsts& ad, void* const events[2], hipStream_t s) {
+                  const AdamConsts& ad, const Deferred& df, void* const events[2], hipStream_t s) {
     int rc;
     for (int k = 0; k < n; ++k)
-        if ((rc = tower_optimizer_rows(*T[k], *W[k], D, mimic, sp, ad, s))) return rc;
+        if ((rc = tower_optimizer_rows(*T[k], *W[k], D, mimic, sp, ad, df, s))) return rc;
+    if (df.on) {
+        ReplayArgs ra;
+        std::memset(&ra, 0, sizeof(ra));
+        ra.hist = df.hist;
+        ra.cap = df.cap;
+        ra.target = df.step;
+        ra.stamp = 1;
+        const int slice = df.step % df.slices;
+        for (int k = 0; k < n; ++k) {
+            const ttamm_table* tabs[2];
+            const int nt = dense_tables(*T[k], mimic, tabs);
+            for (int i = 0; i < nt; ++i) {
+                ReplaySeg g = replay_seg(*tabs[i]);
+                const int64_t per = (tabs[i]->rows + df.slices - 1) / df.slices;
+                g.row_lo = std::min<int64_t>(tabs[i]->rows, slice * per);
+                g.row_hi = std::min<int64_t>(tabs[i]->rows, g.row_lo + per);
+                ra.seg[ra.count++] = g;
+            }
+        }
+        if (events && events[0]) TTAMM_HIP(hipEventRecord((hipEvent_t)events[0], s));
+        if ((rc = launch_replay(ra, s))) return rc;
+        if (events && events[1]) TTAMM_HIP(hipEventRecord((hipEvent_t)events[1], s));
+        return TTAMM_OK;
+    }
     SweepArgs sw;
     std::memset(&sw, 0, sizeof(sw));
     sw.ad = ad;
@@ -663,6 +740,32 @@ int dense_update(const ttamm_tower* T[2], TowerWs* W[2], const AdamConsts& ad, h
         }
     }
     return launch_dense_adam(da, s);
+}
+
+// Deferred mode is all-or-nothing over the dense-group tables of both towers.
+int deferred_of(const ttamm_step_args& A, Deferred& df) {
+    const bool mimic = A.mimic_enabled != 0;
+    int with = 0, total = 0;
+    for (const ttamm_tower* t : {&A.user, &A.item}) {
+        const ttamm_table* tabs[2];
+        const int n = dense_tables(*t, mimic, tabs);
+        for (int i = 0; i < n; ++i) {
+            ++total;
+            with += tabs[i]->last_step != nullptr ? 1 : 0;
+        }
+    }
+    if (with == 0) return TTAMM_OK;
+    TTAMM_REQUIRE(with == total, "deferred AdamW: every dense-group table needs last_step");
+    TTAMM_REQUIRE(A.adam_history != nullptr && A.replay_slices >= 1 && A.history_capacity > A.replay_slices &&
+                      A.history_capacity <= kMaxAdamHistory,
+                  "deferred AdamW: needs adam_history and replay_slices < history_capacity <= 512");
+    TTAMM_REQUIRE(A.hp.dense_step < (double)INT32_MAX, "deferred AdamW: step count out of range");
+    df.on = true;
+    df.hist = static_cast<AdamConsts*>(A.adam_history);
+    df.cap = A.history_capacity;
+    df.slices = A.replay_slices;
+    df.step = (int32_t)A.hp.dense_step;
+    return TTAMM_OK;
 }
 
 int validate_step(const ttamm_step_args& A) {
@@ -754,6 +857,10 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
                                            hp.decoupled_weight_decay, hp.dense_step);
     const SparseConsts sp = make_sparse_consts(hp.sparse_lr, hp.sparse_beta1, hp.sparse_beta2, hp.sparse_eps,
                                                hp.sparse_step);
+    Deferred df;
+    if ((rc = deferred_of(A, df))) return rc;
+    if (df.on && (ph & (TTAMM_PHASE_ITEM_FWD | TTAMM_PHASE_USER_FWD)))
+        if ((rc = launch_history_put(df.hist, df.cap, df.step, ad, s))) return rc;
 
     // ---- negatives --------------------------------------------------------------------------
     if (ph & TTAMM_PHASE_SAMPLE) {
@@ -772,14 +879,21 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     }
     // ---- forward ----------------------------------------------------------------------------
     if (!shard) {
+        if ((rc = tower_prepare(A.user, U, mimic, df, s))) return rc;
+        if ((rc = tower_prepare(A.item, I, mimic, df, s))) return rc;
         if ((rc = tower_forward(T, W, A.b, D, mimic, s, 2))) return rc;
     } else {
         const ttamm_tower* Ti[2] = {&A.item, nullptr};
         TowerWs* Wi[2] = {&I, nullptr};
-        if ((ph & TTAMM_PHASE_ITEM_FWD) && I.R > 0)
-            if ((rc = tower_forward(Ti, Wi, A.b, D, mimic, s, 1))) return rc;
-        if (ph & TTAMM_PHASE_USER_FWD)
+        if (ph & TTAMM_PHASE_ITEM_FWD) {
+            if ((rc = tower_prepare(A.item, I, mimic, df, s))) return rc;
+            if (I.R > 0)
+                if ((rc = tower_forward(Ti, Wi, A.b, D, mimic, s, 1))) return rc;
+        }
+        if (ph & TTAMM_PHASE_USER_FWD) {
+            if ((rc = tower_prepare(A.user, U, mimic, df, s))) return rc;
             if ((rc = tower_forward(T, W, A.b, D, mimic, s, 1))) return rc;
+        }
     }
     // ---- score + loss (fwd + bwd seeds), user-side backward ---------------------------------
     if (ph & TTAMM_PHASE_USER) {
@@ -826,11 +940,11 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         if (!shard) {
             // ---- the whole backward + optimizers in one process --------------------------------
             if ((rc = tower_backward(T, W, D, s, 2))) return rc;
-            if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, A.timing_events, s))) return rc;
+            if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, s))) return rc;
             return dense_update(T, W, ad, s);
         }
         if ((rc = tower_backward(T, W, D, s, 1))) return rc;
-        if ((rc = table_updates(T, W, 1, D, mimic, sp, ad, nullptr, s))) return rc;
+        if ((rc = table_updates(T, W, 1, D, mimic, sp, ad, df, nullptr, s))) return rc;
     }
     // ---- item-side backward on the owner ------------------------------------------------------
     if (ph & TTAMM_PHASE_ITEM_BWD) {
@@ -843,7 +957,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
             const size_t n = tower_grad_floats(A.item);
             if (n) TTAMM_HIP(hipMemsetAsync(I.gw[0] ? I.gw[0] : I.ggw[0], 0, n * sizeof(float), s));
         }
-        if ((rc = table_updates(Ti, Wi, 1, D, mimic, sp, ad, A.timing_events, s))) return rc;
+        if ((rc = table_updates(Ti, Wi, 1, D, mimic, sp, ad, df, A.timing_events, s))) return rc;
     }
     if (ph & TTAMM_PHASE_DENSE)
         if ((rc = dense_update(T, W, ad, s))) return rc;
@@ -864,6 +978,30 @@ int64_t dense_grad_floats(const ttamm_step_args& A) {
 }
 
 int train_step(const ttamm_step_args& A, hipStream_t s) { return run_step(A, s); }
+
+int flush_tables(const ttamm_step_args& A, hipStream_t s) {
+    Deferred df;
+    int rc;
+    if ((rc = deferred_of(A, df))) return rc;
+    if (!df.on) return TTAMM_OK;
+    ReplayArgs ra;
+    std::memset(&ra, 0, sizeof(ra));
+    ra.hist = df.hist;
+    ra.cap = df.cap;
+    ra.target = df.step;
+    ra.stamp = 1;
+    for (const ttamm_tower* t : {&A.user, &A.item}) {
+        const ttamm_table* tabs[2];
+        const int n = dense_tables(*t, A.mimic_enabled != 0, tabs);
+        for (int i = 0; i < n; ++i) {
+            ReplaySeg g = replay_seg(*tabs[i]);
+            g.row_lo = 0;
+            g.row_hi = tabs[i]->rows;
+            ra.seg[ra.count++] = g;
+        }
+    }
+    return launch_replay(ra, s);
+}
 
 // ---- eval-mode tower forward (TowerEncoder.forward + augment) -----------------------------
 size_t tower_forward_workspace_size(const ttamm_tower& T, int64_t n) {

@@ -55,6 +55,7 @@ class Table(ctypes.Structure):
         ("rows", c_i64),
         ("dim", c_i32),
         ("optimizer", c_i32),
+        ("last_step", c_vp),
     ]
 
 
@@ -136,10 +137,14 @@ class StepArgs(ctypes.Structure):
         ("item_bwd_out", c_vp),
         ("item_bwd_in", c_vp),
         ("dense_grads", c_vp),
+        # deferred exact AdamW(g = 0) on tables with last_step
+        ("adam_history", c_vp),
+        ("history_capacity", c_i32),
+        ("replay_slices", c_i32),
     ]
 
 
-ABI_VERSION = 2  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 3  # ttamm.h TTAMM_ABI_VERSION
 
 # ttamm.h TTAMM_PHASE_*
 PHASE_ALL = 0
@@ -159,6 +164,8 @@ SIGNATURES = {
     "ttamm_train_step_workspace_size": (ctypes.c_size_t, [ctypes.POINTER(StepArgs)]),
     "ttamm_train_step": (ctypes.c_int, [ctypes.POINTER(StepArgs), c_vp]),
     "ttamm_dense_grad_floats": (c_i64, [ctypes.POINTER(StepArgs)]),
+    "ttamm_adam_history_entry_bytes": (ctypes.c_size_t, []),
+    "ttamm_flush_tables": (ctypes.c_int, [ctypes.POINTER(StepArgs), c_vp]),
     "ttamm_gather_rows": (ctypes.c_int, [c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "ttamm_tower_forward_workspace_size": (ctypes.c_size_t, [ctypes.POINTER(Tower), c_i64]),
     "ttamm_tower_forward": (

@@ -120,6 +120,8 @@ class FusedTrainStep:
         max_batch: int,
         seed: int | None = None,
         num_items: int | None = None,
+        deferred_adamw: bool = True,
+        replay_slices: int = 64,
     ) -> None:
         if negatives_per_positive <= 0:
             raise ValueError("num_negatives must be greater than zero.")
@@ -243,6 +245,32 @@ class FusedTrainStep:
         self.max_batch = int(max_batch)
         args.b.batch = self.max_batch
         self.lib = _lib.load()
+        self.dense_step0 = int(self._adam_steps[0]["step"].item()) if self._adam_steps else 0
+        self.sparse_step0 = int(self._sparse_steps[0]["step"]) if self._sparse_steps else 0
+        # deferred exact AdamW(g = 0) on the dense-group tables (ttamm.h ttamm_table.last_step):
+        # the rows are current to dense_step0 now
+        self._deferred: list[torch.Tensor] = []
+        if deferred_adamw and self.dense_opt is not None:
+            if not 1 <= replay_slices <= 255:
+                raise ValueError("ttamm: replay_slices must be in [1, 255]")
+            tables = []
+            for name in ("user", "item"):
+                desc = getattr(args, name)
+                if self.mimic is not None:
+                    tables.append(desc.mimic)
+                if desc.id.optimizer == _lib.OPT_DENSE:
+                    tables.append(desc.id)
+            for tb in tables:
+                last = torch.full((tb.rows,), self.dense_step0, dtype=torch.int32, device=self.device)
+                tb.last_step = last.data_ptr()
+                self._deferred.append(last)
+            if tables:
+                cap = replay_slices + 2
+                self.adam_history = torch.zeros(cap * int(self.lib.ttamm_adam_history_entry_bytes()),
+                                                dtype=torch.uint8, device=self.device)
+                args.adam_history = self.adam_history.data_ptr()
+                args.history_capacity = cap
+                args.replay_slices = replay_slices
         self._configure(args)
         self.ws_bytes = int(self.lib.ttamm_train_step_workspace_size(ctypes.byref(args)))
         self.workspace = torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
@@ -251,8 +279,6 @@ class FusedTrainStep:
         self.neg_buffer = torch.empty(self.max_batch * self.num_neg, dtype=torch.long, device=self.device)
         self.args = args
         self.steps_done = 0
-        self.dense_step0 = int(self._adam_steps[0]["step"].item()) if self._adam_steps else 0
-        self.sparse_step0 = int(self._sparse_steps[0]["step"]) if self._sparse_steps else 0
 
     # ------------------------------------------------------------------------------------
     def _configure(self, args: _lib.StepArgs) -> None:
@@ -326,9 +352,19 @@ class FusedTrainStep:
                 field[i] = masks[i].data_ptr() if i < len(masks) and masks[i] is not None else None
         return True
 
+    def flush(self) -> None:
+        """Bring every row of the deferred dense-group tables current (enqueued, no sync).
+        Needed before the tables or their AdamW state are read outside the step."""
+        if not self._deferred or self.steps_done == 0:
+            return
+        self.args.hp.dense_step = self.dense_step0 + self.steps_done
+        _lib.check(self.lib.ttamm_flush_tables(ctypes.byref(self.args), _lib.stream_handle(self.device)))
+
     def finish(self) -> float:
-        """Synchronise, surface device-side errors, write the optimizer step counters back,
-        and return the epoch's mean loss weighted by positives (training.py:829-833)."""
+        """Flush deferred table updates, synchronise, surface device-side errors, write the
+        optimizer step counters back, and return the epoch's mean loss weighted by positives
+        (training.py:829-833)."""
+        self.flush()
         torch.cuda.current_stream(self.device).synchronize()
         if int(self.status.item()) & _lib.STATUS_SAMPLER_EXHAUSTED:
             raise RuntimeError("Exceeded resampling attempts while drawing negatives.")
