@@ -42,6 +42,7 @@ import torch  # noqa: E402
 
 METRIC = "training interactions/sec at 1/2/4/8 MI355X; Recall@20 parity vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+MFMA_FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 matrix (v_mfma_f32_32x32x2_f32), dense
 
 CONFIGS = {
     "c2": dict(U=200_000, I=2_000_000, D=96, H=192, F=605, B=8192, N=5, dropout=0.15, pos_per_user=20),
@@ -205,12 +206,12 @@ def cpu_baseline(c: dict, steps: int, warmup: int, seed: int) -> dict:
     }
 
 
-def load_traffic(config: str) -> float | None:
-    """HBM bytes per sweep launch from the committed rocprofv3 PMC pass (profiles/)."""
+def load_traffic(config: str) -> dict | None:
+    """HBM bytes per launch of the roofline kernels, from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json)."""
     path = ROOT / "profiles" / "pmc_traffic.json"
     try:
-        data = json.loads(path.read_text())
-        return data.get(config, {}).get("dense_sweep_kernel_bytes_per_launch")
+        return json.loads(path.read_text()).get(config)
     except (OSError, ValueError):
         return None
 
@@ -253,13 +254,15 @@ def main() -> None:
     eng.flush()  # the timed region starts with every table row current
     torch.cuda.synchronize()
 
-    # per-step HIP events around the dominant kernel, on the step's stream
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    for a, b in evs:  # materialise the hipEvent_t handles
-        a.record()
-        b.record()
+    # per-step HIP event pairs on the step's stream (ttamm.h ttamm_step_args.timing_events):
+    # [0,1] dense-group table maintenance, [2,3] the grouped first feature-layer forward GEMM
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    for quad in evs:  # materialise the hipEvent_t handles
+        for e in quad:
+            e.record()
     torch.cuda.synchronize()
     batches = [w.batch() for _ in range(args.steps)]
+    rows0 = getattr(eng, "item_rows_seen", 0)
 
     if dist is not None:
         dist.barrier()
@@ -267,7 +270,7 @@ def main() -> None:
     t0 = time.perf_counter()
     for k in range(args.steps):
         u, p = batches[k]
-        eng.step(u, p, timing_events=(evs[k][0].cuda_event, evs[k][1].cuda_event))
+        eng.step(u, p, timing_events=[e.cuda_event for e in evs[k]])
     # deferred AdamW: the g = 0 updates still owed to untouched rows are part of the K steps' work
     eng.flush()
     torch.cuda.synchronize()
@@ -279,16 +282,35 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     loss = eng.finish()
-    sweep_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    maint_ms = sum(q[0].elapsed_time(q[1]) for q in evs) / args.steps
+    gemm_ms = sum(q[2].elapsed_time(q[3]) for q in evs) / args.steps
 
-    B, U, I, D = c["B"], c["U"], c["I"], c["D"]
+    B, U, I, D, F, H, N = c["B"], c["U"], c["I"], c["D"], c["F"], c["H"], c["N"]
     interactions = args.steps * B * world
     value = interactions / elapsed
-    # one process: one sweep over both mimic tables; sharded: the events bracket the owner's
-    # item-table sweep (ITEM_BWD phase)
-    sweep_bytes = 24 * (U + I) * D if world == 1 else 24 * I * D
-    achieved = sweep_bytes / (sweep_ms * 1e-3) / 1e9
+    # first feature layer, grouped launch: rows x F x H multiply-adds (algorithmic F, not the
+    # MFMA's zero-padded K).  One process: user rows B + item rows B(1+N); sharded: the
+    # owner's item rows only (the events bracket its ITEM_FWD launch).
+    if world == 1:
+        l1_rows = B + B * (1 + N)
+    else:
+        l1_rows = (getattr(eng, "item_rows_seen", 0) - rows0) / args.steps
+    l1_flops = 2.0 * l1_rows * F * H
+    tflops = l1_flops / (gemm_ms * 1e-3) / 1e12
     traffic = load_traffic(args.config)
+    deferred = not args.eager_adamw
+    if deferred:
+        maint = {"kernel": "replay_kernel (deferred exact AdamW g=0, this step's 1/64 slice of the mimic tables)",
+                 "bound": "valu", "avg_launch_ms": round(maint_ms, 4),
+                 "note": "per-step share only; catch-up of touched rows and the closing flush are further "
+                         "replay_kernel launches (see profiles/)"}
+    else:
+        sweep_bytes = 24 * (U + I) * D if world == 1 else 24 * I * D
+        gbs = sweep_bytes / (maint_ms * 1e-3) / 1e9
+        maint = {"kernel": "dense_sweep_kernel (eager AdamW g=0 over the mimic tables)", "bound": "hbm",
+                 "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                 "traffic": (traffic or {}).get("dense_sweep_kernel_bytes_per_launch"),
+                 "algorithmic_bytes_per_launch": sweep_bytes, "avg_launch_ms": round(maint_ms, 4)}
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -305,26 +327,28 @@ def main() -> None:
                 "random-init weights",
         "config": {
             "workload": f"{args.config.upper()}: {I * world} items x {U * world} users, D={D}, "
-                        f"MLP {c['F']}->{c['H']}->{D} (ReLU, dropout {c['dropout']}), gated fusion, adaptive mimic, "
-                        f"B={B} per GPU, N={c['N']} sampled negatives, AdamW + SparseAdam",
+                        f"MLP {F}->{H}->{D} (ReLU, dropout {c['dropout']}), gated fusion, adaptive mimic, "
+                        f"B={B} per GPU, N={N} sampled negatives, AdamW + SparseAdam",
             "global_batch": B * world,
-            "negatives_per_positive": c["N"],
+            "negatives_per_positive": N,
             "parallelism": f"row-sharded tables x{world} (all-to-all) + replicated MLP (all-reduce)"
                            if world > 1 else "single",
+            "adamw_tables": "deferred exact replay" if deferred else "eager sweep",
         },
         "final_loss": round(loss, 6),
         "roofline": {
-            "bound": "hbm",
-            "kernel": "dense_sweep_kernel (AdamW g=0 over user+item mimic tables)" if world == 1
-                  else "dense_sweep_kernel (AdamW g=0 over the rank's item mimic table shard)",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "algorithmic_bytes_per_launch": sweep_bytes,
-            "avg_launch_ms": round(sweep_ms, 4),
+            "bound": "mfma",
+            "kernel": "gemm_kernel first feature layer forward (Linear 605->192 + ReLU + dropout, user and item "
+                      "rows grouped), fp32 MFMA 32x32x2",
+            "achieved": round(tflops, 2),
+            "peak": MFMA_FP32_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(tflops / MFMA_FP32_PEAK_TFLOPS, 4),
+            "traffic": (traffic or {}).get("l1_forward_gemm_bytes_per_launch"),
+            "algorithmic_flops_per_launch": l1_flops,
+            "avg_launch_ms": round(gemm_ms, 4),
         },
+        "table_maintenance": maint,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -244,6 +244,7 @@ struct ReplayArgs {
     int cap;
     int32_t target;   // replay every row up to this dense step
     int stamp;        // write last = target afterwards (row ranges only)
+    int decoupled;    // AdamW (decoupled weight decay) vs Adam (L2): the optimizer's, every step
 };
 int launch_replay(const ReplayArgs& a, hipStream_t s);
 

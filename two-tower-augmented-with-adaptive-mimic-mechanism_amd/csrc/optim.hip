@@ -25,8 +25,9 @@ namespace {
 // torch single-tensor Adam/AdamW (adam.py:419-547):
 //   p *= 1 - lr*wd ; m.lerp_(g, 1-b1) ; v = v*b2 + (1-b2)*g*g ;
 //   p += -step * m / (sqrt(v)/sqrt(bc2) + eps)
-__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, const AdamConsts& c) {
-    if (c.decoupled) {
+template <bool DECOUPLED>
+__device__ __forceinline__ void adam_elem_t(float& p, float& m, float& v, float g, const AdamConsts& c) {
+    if (DECOUPLED) {
         p = p * c.decay;
     } else if (c.wd != 0.f) {
         g = g + p * c.wd;
@@ -36,6 +37,13 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
     v = v + c.w2 * g * g;
     const float denom = sqrtf(v) / c.bc2_sqrt + c.eps;
     p = p + c.neg_step * (m / denom);
+}
+
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, const AdamConsts& c) {
+    if (c.decoupled)
+        adam_elem_t<true>(p, m, v, g, c);
+    else
+        adam_elem_t<false>(p, m, v, g, c);
 }
 
 // torch SparseAdam on one coalesced element (_functional.py:61-84).
@@ -231,8 +239,11 @@ __global__ void history_put_kernel(AdamConsts* hist, int cap, int64_t step, Adam
     if (threadIdx.x == 0 && blockIdx.x == 0) hist[step % cap] = c;
 }
 
-// One thread per element; blockIdx.y = segment.  A row current to step l is brought to
-// A.target by replaying adam_elem(g = 0) with the constants of steps l+1 .. target.
+// One thread per 4 consecutive elements of a row (dim % 4 == 0: four independent dependency
+// chains per thread sharing each step's constants); blockIdx.y = segment.  A row current to
+// step l is brought to A.target by replaying adam_elem(g = 0) with the constants of steps
+// l+1 .. target — the operations the eager sweep applies, so the bits agree.
+template <bool DECOUPLED>
 __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
     const KArg(ReplayArgs)* ka = (const KArg(ReplayArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
     const KArg(ReplaySeg)& S = ka->seg[blockIdx.y];
@@ -240,28 +251,33 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
     const int cap = ka->cap;
     for (int i = threadIdx.x; i < cap; i += blockDim.x) H[i] = ka->hist[i];
     __syncthreads();
-    const int dim = S.dim;
+    const int dim = S.dim, dim4 = dim >> 2;
     const int32_t target = ka->target;
     const bool by_key = S.keys != nullptr;
     const int64_t nrows = by_key ? (int64_t)S.n_unique[0] : S.row_hi - S.row_lo;
-    const int64_t total = nrows * dim;
+    const int64_t total = nrows * dim4;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = e / dim;
-        const int d = (int)(e - r * dim);
+        const int64_t r = e / dim4;
+        const int q = (int)(e - r * dim4);
         const int64_t row = by_key ? (int64_t)S.keys[S.seg_start[r]] : S.row_lo + r;
         const int32_t l = S.last[row];
         if (l >= target) continue;
-        const int64_t o = row * dim + d;
-        float p = S.p[o], m = S.m[o], v = S.v[o];
+        const int64_t o = row * dim + 4 * q;
+        float4 p = *reinterpret_cast<const float4*>(S.p + o);
+        float4 m = *reinterpret_cast<const float4*>(S.m + o);
+        float4 v = *reinterpret_cast<const float4*>(S.v + o);
         int j = (int)((l + 1) % cap);
         for (int32_t t = l + 1; t <= target; ++t) {
             const AdamConsts c = H[j];
-            adam_elem(p, m, v, 0.f, c);
+            adam_elem_t<DECOUPLED>(p.x, m.x, v.x, 0.f, c);
+            adam_elem_t<DECOUPLED>(p.y, m.y, v.y, 0.f, c);
+            adam_elem_t<DECOUPLED>(p.z, m.z, v.z, 0.f, c);
+            adam_elem_t<DECOUPLED>(p.w, m.w, v.w, 0.f, c);
             j = j + 1 == cap ? 0 : j + 1;
         }
-        S.p[o] = p;
-        S.m[o] = m;
-        S.v[o] = v;
+        *reinterpret_cast<float4*>(S.p + o) = p;
+        *reinterpret_cast<float4*>(S.m + o) = m;
+        *reinterpret_cast<float4*>(S.v + o) = v;
     }
 }
 
@@ -440,11 +456,16 @@ int launch_replay(const ReplayArgs& a, hipStream_t s) {
     for (int i = 0; i < a.count; ++i) {
         const ReplaySeg& g = a.seg[i];
         TTAMM_REQUIRE(g.p && g.m && g.v && g.last, "replay: table without deferred state");
+        TTAMM_REQUIRE(g.dim % 4 == 0 && ((uintptr_t)g.p | (uintptr_t)g.m | (uintptr_t)g.v) % 16 == 0,
+                      "replay: tables must be 16-byte aligned with dim % 4 == 0");
         const int64_t n = g.row_hi - g.row_lo;  // keys: the coalesced batch size bounds n_unique
-        most = n * g.dim > most ? n * g.dim : most;
+        most = n * (g.dim / 4) > most ? n * (g.dim / 4) : most;
     }
     if (most == 0) return TTAMM_OK;
-    hipLaunchKernelGGL(replay_kernel, dim3(grid_for(most, 256, 8192), a.count), dim3(256), 0, s, a);
+    if (a.decoupled)
+        hipLaunchKernelGGL(replay_kernel<true>, dim3(grid_for(most, 256, 16384), a.count), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(replay_kernel<false>, dim3(grid_for(most, 256, 16384), a.count), dim3(256), 0, s, a);
     TTAMM_LAUNCH_CHECK();
     if (a.stamp) {
         int64_t rows = 0;

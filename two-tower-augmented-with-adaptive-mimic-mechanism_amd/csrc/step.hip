@@ -287,7 +287,7 @@ void set_keys(GemmProblem& p, const TowerWs& w) {
 
 // ---- forward -------------------------------------------------------------------------------
 int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt, int D, bool mimic, hipStream_t s,
-                  int ntowers) {
+                  int ntowers, void* const* l0_events = nullptr) {
     int rc;
     // ID rows -> e (ef[:, :D] when gated)
     for (int k = 0; k < ntowers; ++k) {
@@ -352,7 +352,10 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
             }
             bb.add(p);
         }
+        const bool timed = l == 0 && l0_events && l0_events[0] && l0_events[1];
+        if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)l0_events[0], s));
         if ((rc = bb.run(s))) return rc;
+        if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)l0_events[1], s));
     }
     // feature encoder "identity" (no Linear): f = feature rows
     for (int k = 0; k < ntowers; ++k) {
@@ -570,6 +573,7 @@ struct Deferred {
     int cap = 0;
     int slices = 1;
     int32_t step = 0;  // the dense step this call executes
+    int decoupled = 1;
 };
 
 // The tables of a tower that belong to the dense (AdamW) group.
@@ -601,6 +605,7 @@ int tower_prepare(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred& 
     std::memset(&ra, 0, sizeof(ra));
     ra.hist = df.hist;
     ra.cap = df.cap;
+    ra.decoupled = df.decoupled;
     ra.target = df.step - 1;
     const ttamm_table* tabs[2];
     const int n = dense_tables(t, mimic, tabs);
@@ -671,6 +676,7 @@ int table_updates(const ttamm_tower* T[2], TowerWs* W[2], int n, int D, bool mim
         std::memset(&ra, 0, sizeof(ra));
         ra.hist = df.hist;
         ra.cap = df.cap;
+        ra.decoupled = df.decoupled;
         ra.target = df.step;
         ra.stamp = 1;
         const int slice = df.step % df.slices;
@@ -765,6 +771,7 @@ int deferred_of(const ttamm_step_args& A, Deferred& df) {
     df.cap = A.history_capacity;
     df.slices = A.replay_slices;
     df.step = (int32_t)A.hp.dense_step;
+    df.decoupled = A.hp.decoupled_weight_decay ? 1 : 0;
     return TTAMM_OK;
 }
 
@@ -881,14 +888,14 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     if (!shard) {
         if ((rc = tower_prepare(A.user, U, mimic, df, s))) return rc;
         if ((rc = tower_prepare(A.item, I, mimic, df, s))) return rc;
-        if ((rc = tower_forward(T, W, A.b, D, mimic, s, 2))) return rc;
+        if ((rc = tower_forward(T, W, A.b, D, mimic, s, 2, A.timing_events + 2))) return rc;
     } else {
         const ttamm_tower* Ti[2] = {&A.item, nullptr};
         TowerWs* Wi[2] = {&I, nullptr};
         if (ph & TTAMM_PHASE_ITEM_FWD) {
             if ((rc = tower_prepare(A.item, I, mimic, df, s))) return rc;
             if (I.R > 0)
-                if ((rc = tower_forward(Ti, Wi, A.b, D, mimic, s, 1))) return rc;
+                if ((rc = tower_forward(Ti, Wi, A.b, D, mimic, s, 1, A.timing_events + 2))) return rc;
         }
         if (ph & TTAMM_PHASE_USER_FWD) {
             if ((rc = tower_prepare(A.user, U, mimic, df, s))) return rc;
@@ -988,6 +995,7 @@ int flush_tables(const ttamm_step_args& A, hipStream_t s) {
     std::memset(&ra, 0, sizeof(ra));
     ra.hist = df.hist;
     ra.cap = df.cap;
+    ra.decoupled = df.decoupled;
     ra.target = df.step;
     ra.stamp = 1;
     for (const ttamm_tower* t : {&A.user, &A.item}) {

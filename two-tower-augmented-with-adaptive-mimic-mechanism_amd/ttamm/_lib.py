@@ -122,7 +122,7 @@ class StepArgs(ctypes.Structure):
         ("status", c_vp),
         ("workspace", c_vp),
         ("workspace_bytes", ctypes.c_size_t),
-        ("timing_events", c_vp * 2),
+        ("timing_events", c_vp * 4),
         # row-sharded multi-GPU step (ttamm.h TTAMM_PHASE_*)
         ("phase", c_i32),
         ("row_base", c_i64),
@@ -144,7 +144,7 @@ class StepArgs(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 3  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 4  # ttamm.h TTAMM_ABI_VERSION
 
 # ttamm.h TTAMM_PHASE_*
 PHASE_ALL = 0

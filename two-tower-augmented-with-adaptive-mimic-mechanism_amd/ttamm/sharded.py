@@ -227,6 +227,7 @@ class ShardedTrainStep(FusedTrainStep):
                  comm: Callable[[Program], Any] | None = None, **kw: Any) -> None:
         self.own = RowOwnership(world_size, rank)
         self.comm = comm
+        self.item_rows_seen = 0  # item-tower rows this owner ran (bench roofline)
         super().__init__(model, optimizers, num_items=num_items, **kw)
 
     def _configure(self, args: _lib.StepArgs) -> None:
@@ -256,9 +257,10 @@ class ShardedTrainStep(FusedTrainStep):
 
     def program(self, users: torch.Tensor, pos_items: torch.Tensor, neg_items: torch.Tensor | None = None, *,
                 keep_masks: Mapping[str, Sequence[torch.Tensor]] | None = None,
-                timing_events: tuple[Any, Any] | None = None) -> Program:
-        """One step as an SPMD program (yields collective requests).  ``timing_events`` (a
-        hipEvent_t pair) bracket the owner's item-table AdamW sweep."""
+                timing_events: Sequence[Any] | None = None) -> Program:
+        """One step as an SPMD program (yields collective requests).  ``timing_events``
+        (hipEvent_t handles, pairs as in ttamm.h) bracket the owner's item-table maintenance
+        and its item-tower first-layer GEMM."""
         if not self._bind_batch(users, pos_items, neg_items, keep_masks):
             raise ValueError("ttamm: empty batch in a sharded step (every rank must step)")
         a = self.args
@@ -267,7 +269,9 @@ class ShardedTrainStep(FusedTrainStep):
         Bg = W * B
         a.row_base = rank * B
         a.global_batch = Bg
-        a.timing_events[0] = a.timing_events[1] = None
+        ev = list(timing_events or []) + [None] * 4
+        for i in range(4):
+            a.timing_events[i] = None
         self._hparams()
         negs = neg_items.reshape(-1) if neg_items is not None else self.neg_buffer[: B * N]
         self._phase(_lib.PHASE_SAMPLE)
@@ -278,13 +282,16 @@ class ShardedTrainStep(FusedTrainStep):
                           torch.arange(B * N, device=dev) + (Bg + rank * B * N)])
         route = yield from route_requests(self.own, req, keys)
         n = route.rows.numel()
+        self.item_rows_seen += n
         if n > self.capacity:
             raise RuntimeError("ttamm: item requests exceed the sharded step's capacity")
         a.item_rows = route.rows.data_ptr()
         a.item_row_keys = route.keys.data_ptr()
         a.n_item_rows = n
         a.item_fwd_out = self.fwd_out.data_ptr()
+        a.timing_events[2], a.timing_events[3] = ev[2], ev[3]
         self._phase(_lib.PHASE_ITEM_FWD)
+        a.timing_events[2] = a.timing_events[3] = None
         # ---- (t | a) back to the requesters, user tower meanwhile ----------------------------
         h = yield AllToAll(self.fwd_out[:n], route.recv_counts, route.send_counts, async_op=True)
         self._phase(_lib.PHASE_USER_FWD)
@@ -299,8 +306,7 @@ class ShardedTrainStep(FusedTrainStep):
         bwd_in = yield AllToAll(self.bwd_out[:R].index_select(0, route.order), route.send_counts,
                                 route.recv_counts)
         a.item_bwd_in = bwd_in.data_ptr()
-        if timing_events:
-            a.timing_events[0], a.timing_events[1] = timing_events
+        a.timing_events[0], a.timing_events[1] = ev[0], ev[1]
         self._phase(_lib.PHASE_ITEM_BWD)
         a.timing_events[0] = a.timing_events[1] = None
         yield AllReduce(self.arena)

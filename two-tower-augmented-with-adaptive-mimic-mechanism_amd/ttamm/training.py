@@ -308,14 +308,16 @@ class FusedTrainStep:
         neg_items: torch.Tensor | None = None,
         *,
         keep_masks: Mapping[str, Sequence[torch.Tensor]] | None = None,
-        timing_events: tuple[Any, Any] | None = None,
+        timing_events: Sequence[Any] | None = None,
     ) -> None:
-        """Enqueue one training step on the current stream (no host synchronisation)."""
+        """Enqueue one training step on the current stream (no host synchronisation).
+        ``timing_events``: hipEvent_t handles, pairs as in ttamm.h ttamm_step_args."""
         if not self._bind_batch(users, pos_items, neg_items, keep_masks):
             return
         a = self.args
-        a.timing_events[0] = timing_events[0] if timing_events else None
-        a.timing_events[1] = timing_events[1] if timing_events else None
+        ev = list(timing_events or [])
+        for i in range(4):
+            a.timing_events[i] = ev[i] if i < len(ev) else None
         self._hparams()
         _lib.check(self.lib.ttamm_train_step(ctypes.byref(a), _lib.stream_handle(self.device)))
         self.steps_done += 1
