@@ -225,6 +225,8 @@ def main() -> None:
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--cpu-steps", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo stages the exchanges through host memory (several ranks on one GPU, tests only)")
     ap.add_argument("--eager-adamw", action="store_true",
                     help="sweep AdamW(g=0) over the whole mimic tables every step instead of the deferred exact replay")
     args = ap.parse_args()
@@ -237,9 +239,13 @@ def main() -> None:
         import torch.distributed as dist_mod
 
         dist = dist_mod
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+    # more ranks than GPUs only with --dist-backend gloo (RCCL needs one GPU per rank)
+    device = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(device)
     c = CONFIGS[args.config]
 
@@ -278,7 +284,7 @@ def main() -> None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=device if args.dist_backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     loss = eng.finish()

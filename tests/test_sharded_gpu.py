@@ -141,3 +141,30 @@ def test_sharded_three_steps_match_global_step():
             want = gsd[k][own.rank:: W] if k in TABLES else gsd[k]
             d = (v - want).abs().max().item()
             assert d <= 5e-5, f"rank {own.rank} {k}: {d:.2e}"
+
+
+def test_bench_two_ranks_one_gpu_gloo():
+    """The real multi-process path (torch.distributed.run, TorchComm, ShardedTrainStep, bench
+    timing) with 2 ranks on one GPU; gloo stages the exchanges through the host because RCCL
+    needs one GPU per rank.  The 8-GPU RCCL run is the driver's."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(root / "bench.py"), "--gpus", "2",
+           "--config", "tiny", "--dist-backend", "gloo", "--no-cpu-baseline", "--steps", "3", "--warmup", "1"]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=root)
+    assert res.returncode == 0, res.stderr[-3000:]
+    line = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1
+    out = json.loads(line[0])
+    assert out["n_gpus"] == 2 and out["value"] > 0 and out["scaling"] == "weak"
+    assert "row-sharded" in out["config"]["parallelism"]
+    assert out["final_loss"] == out["final_loss"]  # finite, not NaN

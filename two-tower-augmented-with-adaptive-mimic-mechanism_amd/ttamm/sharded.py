@@ -105,27 +105,44 @@ Program = Generator[Any, Any, Any]
 
 
 class TorchComm:
-    """Serves a program's requests with torch.distributed (backend "nccl" is RCCL on ROCm)."""
+    """Serves a program's requests with torch.distributed (backend "nccl" is RCCL on ROCm).
+    With a gloo group, device tensors are staged through host memory (gloo moves CPU tensors
+    only) — for tests that put several ranks on one GPU, which RCCL does not allow."""
 
     def __init__(self, group: Any = None) -> None:
         import torch.distributed as dist
 
         self.dist = dist
         self.group = group
+        self.staged = dist.get_backend(group) == "gloo"
 
     def __call__(self, req: Any) -> Any:
         dist = self.dist
         if isinstance(req, AllToAll):
-            out = req.send.new_empty((sum(req.recv_splits),) + tuple(req.send.shape[1:]))
-            work = dist.all_to_all_single(out, req.send.contiguous(), req.recv_splits, req.send_splits,
+            send = req.send.contiguous()
+            dev = send.device
+            if self.staged:
+                send = send.cpu()
+            out = send.new_empty((sum(req.recv_splits),) + tuple(send.shape[1:]))
+            if self.staged:
+                dist.all_to_all_single(out, send, req.recv_splits, req.send_splits, group=self.group)
+                out = out.to(dev)
+                return (None, out) if req.async_op else out
+            work = dist.all_to_all_single(out, send, req.recv_splits, req.send_splits,
                                           group=self.group, async_op=req.async_op)
             return (work, out) if req.async_op else out
         if isinstance(req, Wait):
             work, out = req.handle
-            work.wait()
+            if work is not None:
+                work.wait()
             return out
         if isinstance(req, AllReduce):
-            dist.all_reduce(req.tensor, group=self.group)
+            if self.staged and req.tensor.device.type != "cpu":
+                host = req.tensor.cpu()
+                dist.all_reduce(host, group=self.group)
+                req.tensor.copy_(host)
+            else:
+                dist.all_reduce(req.tensor, group=self.group)
             return req.tensor
         raise TypeError(f"unknown collective request {req!r}")
 
