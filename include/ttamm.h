@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 4
+#define TTAMM_ABI_VERSION 5
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -216,6 +216,20 @@ int ttamm_train_step(const ttamm_step_args* args, void* stream);
 /* Size (floats) of the replicated-weight gradient arena of a sharded step: both towers'
  * feature-encoder and gate weight+bias gradients, contiguous (the all-reduce buffer). */
 int64_t ttamm_dense_grad_floats(const ttamm_step_args* args);
+
+/* ---- exact inner-product retrieval + top-k -------------------------------
+ * Replaces faiss.IndexFlatIP.search + the candidate filter of _evaluate_model
+ * (training.py:645-679 index build, :944-970 search and filter).  For each query q the k items
+ * i with the largest <queries[q], items[i]> (fp32) that are NOT in q's blocked set, best first;
+ * equal scores are ordered by item id.  Blocked sets: CSR blocked_offsets[n_queries + 1] over
+ * blocked_values sorted ascending per query (both NULL: nothing blocked).  Missing results
+ * (fewer than k unblocked items) are id -1 / score -inf.  dim % 8 == 0, dim <= 256, rows
+ * 16-byte aligned, 1 <= k <= 192. */
+size_t ttamm_retrieval_topk_workspace_size(int64_t n_queries, int64_t n_items, int32_t dim, int32_t k);
+int ttamm_retrieval_topk(const float* queries, int64_t n_queries, int64_t ldq, const float* items, int64_t n_items,
+                         int64_t ldi, int32_t dim, const int64_t* blocked_offsets, const int64_t* blocked_values,
+                         int32_t k, float* out_scores, int64_t* out_ids, void* workspace, size_t workspace_bytes,
+                         void* stream);
 
 /* Deferred AdamW(g = 0): bytes of one adam_history entry, and the flush that brings every row
  * of every dense-group table with last_step up to hp.dense_step (call before the tables or

@@ -392,3 +392,88 @@ def ranking_metrics(predictions: Mapping[int, Sequence[int]], truth: Mapping[int
         return float(np.mean(v)) if v else 0.0
 
     return RankingMetrics(**{name: {k: mean(acc[name][k]) for k in ks} for name in acc}, mrr=mean(mrr))
+
+
+# ---------------------------------------------------------------------------------------
+# evaluation: exact-IP retrieval (training.py:613-679 encode + IndexFlatIP; :917-1043
+# _evaluate_model, FAISS branch :944-970)
+# ---------------------------------------------------------------------------------------
+def encode_item_embeddings(model: OracleModel, *, num_items: int, item_features: torch.Tensor | None,
+                           batch_size: int = 8192) -> torch.Tensor:
+    """training.py:613-643 (eval mode, no grad; + augment_items when mimic is on)."""
+    model.eval()
+    out = []
+    with torch.no_grad():
+        for start in range(0, num_items, batch_size):
+            idx = torch.arange(start, min(start + batch_size, num_items), dtype=torch.long)
+            feats = item_features.index_select(0, idx) if item_features is not None else None
+            emb = tower_forward(model.item_encoder, idx, feats, training=False)
+            if model.adaptive_mimic is not None:
+                emb = gather_aug(model.adaptive_mimic.item_augmented, idx, emb)[0]
+            out.append(emb)
+    return torch.cat(out) if out else torch.empty((0, 0))
+
+
+def flat_ip_search(items: np.ndarray, queries: np.ndarray, k: int) -> tuple[np.ndarray, np.ndarray]:
+    """faiss.IndexFlatIP.search: (scores, ids) of the k largest inner products per query, ids -1
+    past the corpus size.  FAISS's tie order is unspecified; this restatement breaks ties by
+    the lower item id (the order ttamm's kernel implements)."""
+    scores = queries.astype(np.float32) @ items.astype(np.float32).T
+    nq, ni = scores.shape
+    ids = np.full((nq, k), -1, dtype=np.int64)
+    out = np.full((nq, k), -np.inf, dtype=np.float32)
+    for q in range(nq):
+        order = np.lexsort((np.arange(ni), -scores[q]))[:k]  # score desc, then id asc
+        ids[q, : order.size] = order
+        out[q, : order.size] = scores[q, order]
+    return out, ids
+
+
+def retrieve_with_faiss(items: np.ndarray, user_embedding: np.ndarray, blocked: set[int], ground_truth: set[int],
+                        *, max_k: int, faiss_search_k: int) -> list[int]:
+    """training.py:944-970 (_retrieve_with_faiss), dot-product index."""
+    search_limit = max(max_k + len(ground_truth), 1)
+    search_k = max(faiss_search_k, search_limit + len(blocked))
+    _, idx = flat_ip_search(items, user_embedding[None, :], search_k)
+    filtered: list[int] = []
+    seen: set[int] = set()
+    for item_id in idx[0].tolist():
+        if item_id in blocked or item_id in seen or item_id < 0:
+            continue
+        filtered.append(int(item_id))
+        seen.add(int(item_id))
+        if len(filtered) >= search_limit:
+            break
+    for item_id in ground_truth:
+        if item_id not in seen:
+            filtered.append(item_id)
+    return filtered[:max_k]
+
+
+def evaluate_model(model: OracleModel, *, train_positive_map: Mapping[int, set[int]],
+                   val_pairs: Sequence[tuple[int, int]], item_features: torch.Tensor | None,
+                   user_features: torch.Tensor | None, num_items: int, k_values: Iterable[int],
+                   faiss_search_k: int = 80) -> tuple[dict[int, list[int]], dict[int, set[int]]]:
+    """training.py:917-1043 with FAISS resources (exact IP over all items): per validation user,
+    predictions exclude the user's train positives."""
+    max_k = max(k_values)
+    items = encode_item_embeddings(model, num_items=num_items, item_features=item_features).numpy()
+    groups: dict[int, list[int]] = {}
+    for u, i in val_pairs:
+        groups.setdefault(int(u), []).append(int(i))
+    preds: dict[int, list[int]] = {}
+    truth: dict[int, set[int]] = {}
+    with torch.no_grad():
+        for u in sorted(groups):  # DataFrame.groupby("user_idx") iterates users in sorted order
+            gt = set(groups[u])
+            if not gt:
+                continue
+            truth[u] = gt
+            idx = torch.tensor([u], dtype=torch.long)
+            feats = user_features.index_select(0, idx) if user_features is not None else None
+            emb = tower_forward(model.user_encoder, idx, feats, training=False)
+            if model.adaptive_mimic is not None:
+                emb = gather_aug(model.adaptive_mimic.user_augmented, idx, emb)[0]
+            preds[u] = retrieve_with_faiss(items, emb[0].numpy(), set(train_positive_map.get(u, set())), gt,
+                                           max_k=max_k, faiss_search_k=faiss_search_k)
+    return preds, truth

@@ -1,6 +1,7 @@
 """The CPU oracle against (1) the reference's own known-answer / property tests, restated,
 and (2) the committed golden fixtures (regression guard for the oracle itself)."""
 
+import numpy as np
 import pytest
 import torch
 
@@ -86,3 +87,26 @@ def test_oracle_reproduces_golden(name):
     sm, so, sres = run_oracle(prob, steps=3)
     for k, v in sm.state_dict().items():
         assert torch.allclose(v, torch.from_numpy(arr[f"steps3/param/{k}"]), rtol=1e-6, atol=1e-8), k
+
+
+# ---- exact-IP retrieval restatement (training.py:613-679, :944-970) ----------------------
+def test_flat_ip_search_known_answer():
+    items = np.array([[1, 0], [0, 1], [1, 1], [2, 0], [-1, 0]], dtype=np.float32)
+    q = np.array([[1, 0], [0, 0]], dtype=np.float32)
+    s, i = ref.flat_ip_search(items, q, 7)
+    # query 0: scores [1, 0, 1, 2, -1] -> 3 (2), 0 (1), 2 (1), 1 (0), 4 (-1); ties by lower id
+    assert i[0].tolist() == [3, 0, 2, 1, 4, -1, -1]
+    assert s[0, :5].tolist() == [2, 1, 1, 0, -1]
+    # query 1: all scores 0 -> id order
+    assert i[1, :5].tolist() == [0, 1, 2, 3, 4]
+
+
+def test_retrieve_with_faiss_filters_blocked_and_appends_truth():
+    items = np.eye(6, dtype=np.float32)[:, :4] * np.arange(6, 0, -1, dtype=np.float32)[:, None]
+    user = np.ones(4, dtype=np.float32)
+    # scores: 6, 5, 4, 3, 0, 0 for items 0..5
+    got = ref.retrieve_with_faiss(items, user, blocked={0, 2}, ground_truth={5}, max_k=3, faiss_search_k=80)
+    assert got == [1, 3, 4]
+    # only 2 unblocked candidates exist beyond the block: the ground truth is appended
+    got = ref.retrieve_with_faiss(items[:4], user, blocked={0, 1}, ground_truth={9}, max_k=3, faiss_search_k=2)
+    assert got == [2, 3, 9]

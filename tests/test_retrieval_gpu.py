@@ -1,0 +1,140 @@
+"""Exact inner-product retrieval + top-k on the MI355X against the oracle's
+restatement of the FAISS branch (oracle/cpu_reference.py: flat_ip_search, evaluate_model).
+
+* Integer-valued embeddings make every fp32 score exact whatever the summation order, so ids
+  and scores must match the oracle BIT-EXACTLY — including ties (equal scores are ordered by
+  item id) and blocked items; ragged sizes, k past the unblocked corpus, k up to 192.
+* Real-valued embeddings: the returned scores equal the exact (fp64) top-k scores within
+  fp32 rounding (1e-5 relative), and any id difference is a near tie.
+* C3 shapes (64K queries x 2M items x 96): size-independent properties (ordering, blocked
+  items never returned, a sampled subset of queries checked against fp64 scores).
+* Recall@20 of the same trained model: ttamm's evaluate_model vs the oracle's, ±0.002
+  (SURVEY §8 c)."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import torch
+
+import ttamm
+from helpers import LOSS_WEIGHTS, Shape, make_problem, run_oracle
+from oracle import cpu_reference as ref
+from ttamm.retrieval import blocked_csr, evaluate_model, retrieve_topk
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_topk(items, queries, k, blocked):
+    scores = queries.astype(np.float64) @ items.astype(np.float64).T
+    nq, ni = scores.shape
+    ids = np.full((nq, k), -1, dtype=np.int64)
+    out = np.full((nq, k), -np.inf, dtype=np.float64)
+    for q in range(nq):
+        order = np.lexsort((np.arange(ni), -scores[q]))
+        order = [i for i in order if i not in blocked[q]][:k]
+        ids[q, : len(order)] = order
+        out[q, : len(order)] = scores[q, order]
+    return out, ids
+
+
+@pytest.mark.parametrize("nq,ni,D,k", [(300, 5000, 96, 20), (65, 4097, 128, 80), (7, 70, 8, 192),
+                                        (130, 1000, 256, 1), (64, 10, 16, 20)])
+def test_topk_bit_exact_on_exact_scores(nq, ni, D, k):
+    g = torch.Generator().manual_seed(nq * 7 + ni)
+    items = torch.randint(-3, 4, (ni, D), generator=g).float()
+    queries = torch.randint(-2, 3, (nq, D), generator=g).float()
+    blocked = [set(torch.randint(0, ni, (int(torch.randint(0, 30, (1,), generator=g)),), generator=g).tolist())
+               for _ in range(nq)]
+    want_s, want_i = _oracle_topk(items.numpy(), queries.numpy(), k, blocked)
+    boff, bval = blocked_csr(range(nq), dict(enumerate(blocked)), torch.device("cuda"))
+    s, i = retrieve_topk(queries.cuda(), items.cuda(), k, blocked_offsets=boff, blocked_values=bval)
+    assert torch.equal(i.cpu(), torch.from_numpy(want_i))
+    assert torch.equal(s.cpu().double(), torch.from_numpy(want_s))
+
+
+def test_topk_matches_faiss_restatement_without_blocking():
+    g = torch.Generator().manual_seed(3)
+    items = torch.randint(-3, 4, (3000, 96), generator=g).float()
+    queries = torch.randint(-3, 4, (100, 96), generator=g).float()
+    want_s, want_i = ref.flat_ip_search(items.numpy(), queries.numpy(), 80)
+    s, i = retrieve_topk(queries.cuda(), items.cuda(), 80)
+    assert torch.equal(i.cpu(), torch.from_numpy(want_i))
+    assert torch.equal(s.cpu(), torch.from_numpy(want_s))
+
+
+def test_topk_real_valued_scores():
+    g = torch.Generator().manual_seed(11)
+    items = torch.randn((20000, 96), generator=g)
+    queries = torch.randn((500, 96), generator=g)
+    k = 50
+    s, i = retrieve_topk(queries.cuda(), items.cuda(), k)
+    exact = queries.double() @ items.double().T
+    ws, wi = torch.topk(exact, k, dim=1)
+    assert torch.allclose(s.cpu().double(), ws, rtol=1e-5, atol=1e-5)
+    got = exact.gather(1, i.cpu())  # the exact scores of what was returned
+    assert torch.allclose(got, ws, rtol=1e-5, atol=1e-5)  # differences only among near ties
+
+
+def test_topk_edge_cases():
+    q = torch.randn((3, 8)).cuda()
+    s, i = retrieve_topk(q, torch.empty((0, 8)).cuda(), 5)
+    assert (i == -1).all() and torch.isinf(s).all()
+    s, i = retrieve_topk(torch.empty((0, 8)).cuda(), torch.randn((10, 8)).cuda(), 5)
+    assert s.shape == (0, 5)
+    with pytest.raises(ValueError, match="k must be"):
+        retrieve_topk(q, torch.randn((10, 8)).cuda(), 193)
+    with pytest.raises(ValueError, match="multiple of 8"):
+        retrieve_topk(torch.randn((3, 12)).cuda(), torch.randn((10, 12)).cuda(), 5)
+
+
+def test_topk_c3_properties():
+    """C3 shapes: 65,536 queries x 2M items x 96, K = 80, 20 blocked items per query."""
+    torch.manual_seed(0)
+    nq, ni, D, k = 65536, 2_000_000, 96, 80
+    items = torch.randn((ni, D), device="cuda")
+    queries = torch.randn((nq, D), device="cuda")
+    boff = torch.arange(0, 20 * nq + 1, 20, device="cuda")
+    bval = torch.randint(0, ni, (nq, 20), device="cuda").sort(dim=1).values.reshape(-1)
+    s, i = retrieve_topk(queries, items, k, blocked_offsets=boff, blocked_values=bval)
+    torch.cuda.synchronize()
+    assert (i >= 0).all() and (i < ni).all()
+    assert (s[:, :-1] >= s[:, 1:]).all()
+    blocked = bval.view(nq, 20)
+    assert not (i.unsqueeze(2) == blocked.unsqueeze(1)).any()
+    assert all(len(set(row)) == k for row in i[:256].tolist())
+    rows = torch.randint(0, nq, (64,), device="cuda")
+    exact = queries[rows].double() @ items.double().T
+    exact.scatter_(1, blocked[rows], float("-inf"))
+    ws, _ = torch.topk(exact, k, dim=1)
+    assert torch.allclose(s[rows].double(), ws, rtol=1e-5, atol=1e-4)
+
+
+def test_recall_at_20_matches_oracle_evaluation():
+    """The same trained weights evaluated by the oracle's _evaluate_model restatement (exact IP
+    over all items, train positives blocked) and by ttamm.retrieval.evaluate_model."""
+    from gpu_helpers import ttamm_model_from
+
+    shape = Shape(U=96, I=400, B=64)
+    prob = make_problem(shape, seed=5, steps=3, positives_per_user=6)
+    model_o, _, _ = run_oracle(prob, steps=3)
+    prob.model = model_o  # evaluate the trained weights on both sides
+    model_t = ttamm_model_from(prob).eval()
+    # validation pairs: one held-out item per user; train positives are blocked
+    g = torch.Generator().manual_seed(9)
+    val = [(u, int(torch.randint(0, shape.I, (1,), generator=g))) for u in range(shape.U)]
+    preds_o, truth_o = ref.evaluate_model(model_o, train_positive_map=prob.positives, val_pairs=val,
+                                          item_features=prob.item_features, user_features=prob.user_features,
+                                          num_items=shape.I, k_values=[10, 20])
+    preds_t, truth_t = evaluate_model(model_t, train_positive_map=prob.positives, val_interactions=val,
+                                      item_feature_tensor=prob.item_features.cuda(),
+                                      user_feature_tensor=prob.user_features.cuda(), device=torch.device("cuda"),
+                                      num_items=shape.I, k_values=[10, 20])
+    assert truth_o == truth_t
+    for u, p in preds_t.items():
+        assert not set(p) & prob.positives.get(u, set())
+    mo = ref.ranking_metrics(preds_o, truth_o, [20])
+    mt = ref.ranking_metrics(preds_t, truth_t, [20])
+    assert abs(mo.recall[20] - mt.recall[20]) <= 0.002
+    same = sum(preds_o[u] == preds_t[u] for u in preds_o)
+    assert same >= 0.9 * len(preds_o)  # identical lists except near ties

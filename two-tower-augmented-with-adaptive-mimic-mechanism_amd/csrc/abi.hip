@@ -51,6 +51,19 @@ TTAMM_API int ttamm_flush_tables(const ttamm_step_args* args, void* stream) {
     return flush_tables(*args, (hipStream_t)stream);
 }
 
+TTAMM_API size_t ttamm_retrieval_topk_workspace_size(int64_t n_queries, int64_t n_items, int32_t dim, int32_t k) {
+    return retrieval_workspace_bytes(n_queries, n_items, dim, k);
+}
+
+TTAMM_API int ttamm_retrieval_topk(const float* queries, int64_t n_queries, int64_t ldq, const float* items,
+                                   int64_t n_items, int64_t ldi, int32_t dim, const int64_t* blocked_offsets,
+                                   const int64_t* blocked_values, int32_t k, float* out_scores, int64_t* out_ids,
+                                   void* workspace, size_t workspace_bytes, void* stream) {
+    g_last_error.clear();
+    return launch_retrieval_topk(queries, n_queries, ldq, items, n_items, ldi, dim, blocked_offsets, blocked_values, k,
+                                 out_scores, out_ids, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
 TTAMM_API int ttamm_train_step(const ttamm_step_args* args, void* stream) {
     if (!args) return fail(TTAMM_E_INVALID, "null step args");
     g_last_error.clear();

@@ -149,6 +149,30 @@ int launch_loss_finalize(const float* partials, int blocks, int64_t B, int64_t B
                          hipStream_t s);
 
 // ------------------------------------------------------------------------------------
+// Exact inner-product retrieval + top-k (retrieval.hip)
+// ------------------------------------------------------------------------------------
+struct RetrievalArgs {
+    const float* Q;
+    int64_t ldq, nq;
+    const float* X;
+    int64_t ldx, ni;
+    int D;
+    const int64_t* boff;  // blocked items per query: CSR offsets [nq + 1] (null: none)
+    const int64_t* bval;  // sorted ascending within each query
+    int k;
+    int parts;            // item partitions (grid.y)
+    int64_t items_per_part;
+    float* buf_s;         // candidate buffers [blocks, 64, 256]
+    int* buf_i;
+    float* part_s;        // per-partition top-k [nq, parts, k]
+    int* part_i;
+};
+size_t retrieval_workspace_bytes(int64_t nq, int64_t ni, int dim, int k);
+int launch_retrieval_topk(const float* Q, int64_t nq, int64_t ldq, const float* X, int64_t ni, int64_t ldx, int dim,
+                          const int64_t* boff, const int64_t* bval, int k, float* out_s, int64_t* out_i, void* ws,
+                          size_t ws_bytes, hipStream_t s);
+
+// ------------------------------------------------------------------------------------
 // Coalesce + optimizers (optim.hip)
 // ------------------------------------------------------------------------------------
 struct CoalesceWs {

@@ -1,0 +1,308 @@
+// Exact inner-product retrieval with per-query blocked items and top-k.
+//
+// Replaces the FAISS IndexFlatIP search + the candidate filter of `_evaluate_model`
+// (training.py:944-970, index built at :645-679): for every query q, the k items with the
+// highest <Q[q], X[i]> that are not in q's blocked set, ordered by score (descending) then item
+// id (ascending).  FAISS's own tie order is an implementation detail of its heaps; this
+// kernel's is the total order above.
+//
+// Pass 1 (retrieval_partial_kernel): a block owns 64 queries and one partition of the items.
+// Four waves: (query half, item half) of each 64-item tile.  Scores come from fp32 MFMA
+// 32x32x2 with items as M and queries as N, so every lane holds ONE query and 16 items of the
+// tile.  A lane appends (score, id) to its query's candidate buffer only when the score reaches
+// the query's running threshold (the k-th best so far) and the item is not blocked; a wave
+// compacts a query's buffer (bitonic sort in registers, keep k) before it could overflow.
+// Pass 2 (retrieval_merge_kernel): one wave per query merges the partitions' top-k lists.
+#include <cfloat>
+#include <cstring>
+
+#include "kernels.h"
+
+namespace ttamm {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kRQ = 64;      // queries per block
+constexpr int kRI = 64;      // items per tile
+constexpr int kRCap = 256;   // candidate slots per query: k + kRI <= kRCap
+constexpr int kMergeJ = 8;   // merge: up to 64 * 8 = 512 candidates per query
+
+__device__ __forceinline__ bool better(float sa, int ia, float sb, int ib) {
+    return sa > sb || (sa == sb && (unsigned)ia < (unsigned)ib);
+}
+
+// Sort the 64*J (score, id) pairs of a wave — element e = lane*J + j — best first.
+template <int J>
+__device__ void wave_bitonic_sort(float (&s)[J], int (&id)[J]) {
+    const int lane = threadIdx.x & 63;
+    constexpr int N = 64 * J;
+#pragma unroll
+    for (int size = 2; size <= N; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= J) {
+                const int ls = stride / J;
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                    const int e = lane * J + j;
+                    const float ps = __shfl_xor(s[j], ls, 64);
+                    const int pi = __shfl_xor(id[j], ls, 64);
+                    const bool dir = (e & size) == 0;       // block sorted best-first
+                    const bool lower = (e & stride) == 0;
+                    const bool mine_better = better(s[j], id[j], ps, pi);
+                    if (mine_better != (lower == dir)) {
+                        s[j] = ps;
+                        id[j] = pi;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < J; ++j) {
+                    if (j & stride) continue;
+                    const int e = lane * J + j;
+                    const bool dir = (e & size) == 0;
+                    const int k = j | stride;
+                    if (better(s[k], id[k], s[j], id[j]) == dir) {
+                        const float ts = s[j];
+                        const int ti = id[j];
+                        s[j] = s[k];
+                        id[j] = id[k];
+                        s[k] = ts;
+                        id[k] = ti;
+                    }
+                }
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ bool is_blocked(const int64_t* __restrict__ vals, int64_t lo, int64_t hi, int64_t item) {
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        const int64_t v = vals[mid];
+        if (v == item) return true;
+        if (v < item)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return false;
+}
+
+// Sort query q's buffered candidates, keep the best `keep`, update its threshold.
+__device__ void compact_query(float* __restrict__ bs, int* __restrict__ bi, int* cnt, float* tau, int q, int k,
+                              float* out_s, int* out_i, int out_k) {
+    const int lane = threadIdx.x & 63;
+    const int n = cnt[q];
+    float s[4];
+    int id[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int e = lane * 4 + j;
+        s[j] = e < n ? bs[q * kRCap + e] : -INFINITY;
+        id[j] = e < n ? bi[q * kRCap + e] : -1;
+    }
+    wave_bitonic_sort<4>(s, id);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int e = lane * 4 + j;
+        if (e < k && e < n) {
+            bs[q * kRCap + e] = s[j];
+            bi[q * kRCap + e] = id[j];
+        }
+        if (e == k - 1) tau[q] = e < n ? s[j] : -INFINITY;
+        if (out_s && e < out_k) {
+            out_s[e] = e < n ? s[j] : -INFINITY;
+            out_i[e] = e < n ? id[j] : -1;
+        }
+    }
+    if (lane == 0) cnt[q] = n < k ? n : k;
+}
+
+__global__ __launch_bounds__(256) void retrieval_partial_kernel(RetrievalArgs A) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ int cnt[kRQ];
+    __shared__ float tau[kRQ];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int qw = w & 1, iw = w >> 1, h = lane >> 5;
+    const int D = A.D, LD = D + 4, D4 = D >> 2, Dh = D >> 1;
+    const int64_t q0 = (int64_t)blockIdx.x * kRQ;
+    const int64_t i_begin = (int64_t)blockIdx.y * A.items_per_part;
+    const int64_t i_end = i_begin + A.items_per_part < A.ni ? i_begin + A.items_per_part : A.ni;
+    float* Qs = lds;
+    float* Xs = lds + kRQ * LD;
+    for (int e = tid; e < kRQ * D4; e += 256) {
+        const int r = e / D4, c = (e - r * D4) * 4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (q0 + r < A.nq) v = *reinterpret_cast<const float4*>(A.Q + (q0 + r) * A.ldq + c);
+        *reinterpret_cast<float4*>(Qs + r * LD + c) = v;
+    }
+    if (tid < kRQ) {
+        cnt[tid] = 0;
+        tau[tid] = -INFINITY;
+    }
+    const int64_t blk = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    float* bs = A.buf_s + blk * kRQ * kRCap;
+    int* bi = A.buf_i + blk * kRQ * kRCap;
+    const int myq = qw * 32 + (lane & 31);
+    const int64_t gq = q0 + myq;
+    const bool qvalid = gq < A.nq;
+    int64_t blo = 0, bhi = 0;
+    if (A.boff && qvalid) {
+        blo = A.boff[gq];
+        bhi = A.boff[gq + 1];
+    }
+    const float* qb = Qs + myq * LD + h * Dh;
+    for (int64_t t0 = i_begin; t0 < i_end; t0 += kRI) {
+        __syncthreads();  // previous tile's readers and compactions are done
+        for (int e = tid; e < kRI * D4; e += 256) {
+            const int r = e / D4, c = (e - r * D4) * 4;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (t0 + r < i_end) v = *reinterpret_cast<const float4*>(A.X + (t0 + r) * A.ldx + c);
+            *reinterpret_cast<float4*>(Xs + r * LD + c) = v;
+        }
+        __syncthreads();
+        const float my_tau = tau[myq];
+        f32x16 acc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        // lane half h sums k in [h*D/2, (h+1)*D/2) — the same k order for both operands
+        const float* xa = Xs + (iw * 32 + (lane & 31)) * LD + h * Dh;
+        for (int kk = 0; kk < Dh; kk += 4) {
+            const float4 a4 = *reinterpret_cast<const float4*>(xa + kk);
+            const float4 b4 = *reinterpret_cast<const float4*>(qb + kk);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, b4.x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, b4.y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, b4.z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, b4.w, acc, 0, 0, 0);
+        }
+        if (qvalid) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t item = t0 + iw * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const float sc = acc[r];
+                if (item < i_end && sc >= my_tau && !(bhi > blo && is_blocked(A.bval, blo, bhi, item))) {
+                    const int slot = atomicAdd(&cnt[myq], 1);
+                    bs[myq * kRCap + slot] = sc;  // slot < kRCap: cnt <= kRCap - kRI before the tile
+                    bi[myq * kRCap + slot] = (int)item;
+                }
+            }
+        }
+        __syncthreads();
+        for (int q = w; q < kRQ; q += 4)
+            if (cnt[q] > kRCap - kRI) compact_query(bs, bi, cnt, tau, q, A.k, nullptr, nullptr, 0);
+    }
+    __syncthreads();
+    for (int q = w; q < kRQ; q += 4) {
+        const int64_t g = q0 + q;
+        if (g >= A.nq) continue;
+        float* os = A.part_s + (g * A.parts + blockIdx.y) * A.k;
+        int* oi = A.part_i + (g * A.parts + blockIdx.y) * A.k;
+        compact_query(bs, bi, cnt, tau, q, A.k, os, oi, A.k);
+    }
+}
+
+__global__ __launch_bounds__(64) void retrieval_merge_kernel(RetrievalArgs A, float* __restrict__ out_s,
+                                                             int64_t* __restrict__ out_i) {
+    const int lane = threadIdx.x;
+    const int64_t q = blockIdx.x;
+    const int n = A.parts * A.k;
+    float s[kMergeJ];
+    int id[kMergeJ];
+#pragma unroll
+    for (int j = 0; j < kMergeJ; ++j) {
+        const int e = lane * kMergeJ + j;
+        s[j] = e < n ? A.part_s[q * n + e] : -INFINITY;
+        id[j] = e < n ? A.part_i[q * n + e] : -1;
+        if (id[j] < 0) s[j] = -INFINITY;  // empty slots sort last
+    }
+    wave_bitonic_sort<kMergeJ>(s, id);
+#pragma unroll
+    for (int j = 0; j < kMergeJ; ++j) {
+        const int e = lane * kMergeJ + j;
+        if (e < A.k) {
+            const bool ok = id[j] >= 0;
+            out_s[q * A.k + e] = ok ? s[j] : -INFINITY;
+            out_i[q * A.k + e] = ok ? (int64_t)id[j] : -1;
+        }
+    }
+}
+
+int pick_parts(int64_t nq, int64_t ni, int k) {
+    const int64_t qtiles = (nq + kRQ - 1) / kRQ;
+    int64_t parts = (2048 + qtiles - 1) / qtiles;  // aim for >= 2048 blocks (8 per CU)
+    const int64_t by_items = (ni + 4 * kRI - 1) / (4 * kRI);  // >= 4 tiles per partition
+    if (parts > by_items) parts = by_items;
+    const int64_t by_merge = (64 * kMergeJ) / k;
+    if (parts > by_merge) parts = by_merge;
+    return parts < 1 ? 1 : (int)parts;
+}
+
+}  // namespace
+
+size_t retrieval_workspace_bytes(int64_t nq, int64_t ni, int dim, int k) {
+    (void)dim;
+    if (nq <= 0 || k <= 0) return 256;
+    const int parts = pick_parts(nq, ni, k);
+    const int64_t blocks = ((nq + kRQ - 1) / kRQ) * parts;
+    const size_t buf = (size_t)blocks * kRQ * kRCap * (sizeof(float) + sizeof(int));
+    const size_t part = (size_t)nq * parts * k * (sizeof(float) + sizeof(int));
+    return buf + part + 4 * 256;
+}
+
+int launch_retrieval_topk(const float* Q, int64_t nq, int64_t ldq, const float* X, int64_t ni, int64_t ldx, int dim,
+                          const int64_t* boff, const int64_t* bval, int k, float* out_s, int64_t* out_i, void* ws,
+                          size_t ws_bytes, hipStream_t s) {
+    TTAMM_REQUIRE(nq >= 0 && ni >= 0, "retrieval: negative sizes");
+    TTAMM_REQUIRE(k >= 1 && k <= kRCap - kRI, "retrieval: k must be in [1, 192]");
+    TTAMM_REQUIRE(dim > 0 && dim % 8 == 0 && dim <= 256, "retrieval: embedding dim must be a multiple of 8, <= 256");
+    TTAMM_REQUIRE(ldq >= dim && ldx >= dim && ldq % 4 == 0 && ldx % 4 == 0 &&
+                      ((uintptr_t)Q | (uintptr_t)X) % 16 == 0,
+                  "retrieval: rows must be 16-byte aligned (leading dims % 4 == 0)");
+    TTAMM_REQUIRE(ni < (int64_t(1) << 31), "retrieval: at most 2^31 - 1 items");
+    if (nq == 0) return TTAMM_OK;
+    TTAMM_REQUIRE(out_s && out_i, "retrieval: outputs missing");
+    TTAMM_REQUIRE(ws_bytes >= retrieval_workspace_bytes(nq, ni, dim, k), "retrieval: workspace too small");
+    RetrievalArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.Q = Q;
+    A.ldq = ldq;
+    A.nq = nq;
+    A.X = X;
+    A.ldx = ldx;
+    A.ni = ni;
+    A.D = dim;
+    A.boff = boff;
+    A.bval = bval;
+    A.k = k;
+    A.parts = pick_parts(nq, ni, k);
+    A.items_per_part = ni > 0 ? ((ni + A.parts - 1) / A.parts + kRI - 1) / kRI * kRI : 0;
+    const int64_t qtiles = (nq + kRQ - 1) / kRQ;
+    const int64_t blocks = qtiles * A.parts;
+    char* p = static_cast<char*>(ws);
+    auto take = [&](size_t bytes) {
+        char* r = p;
+        p += (bytes + 255) / 256 * 256;
+        return r;
+    };
+    A.buf_s = reinterpret_cast<float*>(take((size_t)blocks * kRQ * kRCap * sizeof(float)));
+    A.buf_i = reinterpret_cast<int*>(take((size_t)blocks * kRQ * kRCap * sizeof(int)));
+    A.part_s = reinterpret_cast<float*>(take((size_t)nq * A.parts * k * sizeof(float)));
+    A.part_i = reinterpret_cast<int*>(take((size_t)nq * A.parts * k * sizeof(int)));
+    const size_t lds = (size_t)(kRQ + kRI) * (dim + 4) * sizeof(float);
+    static bool attr_set = false;
+    if (!attr_set) {
+        TTAMM_HIP(hipFuncSetAttribute((const void*)retrieval_partial_kernel,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024));
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(retrieval_partial_kernel, dim3((unsigned)qtiles, (unsigned)A.parts), dim3(256), lds, s, A);
+    TTAMM_LAUNCH_CHECK();
+    hipLaunchKernelGGL(retrieval_merge_kernel, dim3((unsigned)nq), dim3(64), 0, s, A, out_s, out_i);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+}  // namespace ttamm

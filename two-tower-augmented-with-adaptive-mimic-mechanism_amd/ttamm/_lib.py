@@ -144,7 +144,7 @@ class StepArgs(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 4  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 5  # ttamm.h TTAMM_ABI_VERSION
 
 # ttamm.h TTAMM_PHASE_*
 PHASE_ALL = 0
@@ -165,6 +165,11 @@ SIGNATURES = {
     "ttamm_train_step": (ctypes.c_int, [ctypes.POINTER(StepArgs), c_vp]),
     "ttamm_dense_grad_floats": (c_i64, [ctypes.POINTER(StepArgs)]),
     "ttamm_adam_history_entry_bytes": (ctypes.c_size_t, []),
+    "ttamm_retrieval_topk_workspace_size": (ctypes.c_size_t, [c_i64, c_i64, c_i32, c_i32]),
+    "ttamm_retrieval_topk": (
+        ctypes.c_int,
+        [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, ctypes.c_size_t, c_vp],
+    ),
     "ttamm_flush_tables": (ctypes.c_int, [ctypes.POINTER(StepArgs), c_vp]),
     "ttamm_gather_rows": (ctypes.c_int, [c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "ttamm_tower_forward_workspace_size": (ctypes.c_size_t, [ctypes.POINTER(Tower), c_i64]),
