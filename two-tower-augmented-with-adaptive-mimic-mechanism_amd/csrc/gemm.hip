@@ -238,7 +238,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
             kidx[k] = P.a_idx ? P.a_idx[k_begin + k] : (int64_t)(k_begin + k);
         __syncthreads();
     }
-    float4 ra[CF::A_LOADS], rb[CF::B_LOADS];
+    // two register sets: the k-tile two ahead is in flight while the next one is written to LDS
+    float4 ra[2][CF::A_LOADS], rb[2][CF::B_LOADS];
 
     // Interior blocks with whole k-tiles take the FAST variant of the main loop: pointers
     // resolved once, plain float4 loads, no masking.  Edge blocks take the masked variant.
@@ -263,33 +264,36 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
 
     auto mainloop = [&](auto fast_tag) {
         constexpr bool FAST = decltype(fast_tag)::value;
-        auto load_tile = [&](int k0) {
+        auto load_tile = [&](auto S, int k0) {
+            constexpr int R = decltype(S)::value;
 #pragma unroll
             for (int it = 0; it < CF::A_LOADS; ++it) {
                 if (!AK) {
-                    ra[it] = FAST ? *reinterpret_cast<const float4*>(a_rp[it] + k0 + a_c[it])
+                    ra[R][it] = FAST ? *reinterpret_cast<const float4*>(a_rp[it] + k0 + a_c[it])
                                   : raw4(a_rp[it], k0 + a_c[it], P.lda);
                 } else {
                     const int k = FAST ? k0 + a_r[it] : min(k0 + a_r[it], k_end - 1);
                     const float* rp = P.A + kidx[k - k_begin] * P.lda;
-                    ra[it] = FAST ? *reinterpret_cast<const float4*>(rp + m0 + a_c[it]) : raw4(rp, m0 + a_c[it], P.lda);
+                    ra[R][it] = FAST ? *reinterpret_cast<const float4*>(rp + m0 + a_c[it]) : raw4(rp, m0 + a_c[it], P.lda);
                 }
             }
 #pragma unroll
             for (int it = 0; it < CF::B_LOADS; ++it) {
                 const int lin = tid + it * kThreads;
                 if (!BKM) {
-                    rb[it] = FAST ? *reinterpret_cast<const float4*>(b_rp[it] + k0)
-                                  : raw4(b_rp[it] - (lin & 3) * 4, k0 + (lin & 3) * 4, P.ldb);
+                    rb[R][it] = FAST ? *reinterpret_cast<const float4*>(b_rp[it] + k0)
+                                     : raw4(b_rp[it] - (lin & 3) * 4, k0 + (lin & 3) * 4, P.ldb);
                 } else if (FAST) {
-                    rb[it] = *reinterpret_cast<const float4*>(b_rp[it] + (int64_t)k0 * P.ldb);
+                    rb[R][it] = *reinterpret_cast<const float4*>(b_rp[it] + (int64_t)k0 * P.ldb);
                 } else {
                     const int k = min(k0 + lin / (BN / 4), k_end - 1);
-                    rb[it] = raw4(P.B + (int64_t)k * P.ldb, n0 + (lin % (BN / 4)) * 4, P.ldb);
+                    rb[R][it] = raw4(P.B + (int64_t)k * P.ldb, n0 + (lin % (BN / 4)) * 4, P.ldb);
                 }
             }
         };
-        auto store_tile = [&](int buf, int k0) {
+        auto store_tile = [&](auto S, auto Buf, int k0) {
+            constexpr int R = decltype(S)::value;  // register set
+            constexpr int buf = decltype(Buf)::value;
             float* as = As + buf * CF::A_STAGE;
             float* bs = Bs + buf * CF::B_STAGE;
 #pragma unroll
@@ -297,11 +301,11 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
                 const int lin = tid + it * kThreads;
                 if (lin >= CF::A_F4) continue;
                 if (!AK) {
-                    const float4 v = FAST ? ra[it] : mask4(ra[it], k0 + a_c[it], k_end, P.lda, -1, a_ok[it]);
+                    const float4 v = FAST ? ra[R][it] : mask4(ra[R][it], k0 + a_c[it], k_end, P.lda, -1, a_ok[it]);
                     *reinterpret_cast<float4*>(as + a_r[it] * SK + a_c[it]) = v;
                 } else {
-                    const float4 v = FAST ? ra[it]
-                                          : mask4(ra[it], m0 + a_c[it], P.a_cols, P.lda, P.a_ones_col,
+                    const float4 v = FAST ? ra[R][it]
+                                          : mask4(ra[R][it], m0 + a_c[it], P.a_cols, P.lda, P.a_ones_col,
                                                   k0 + a_r[it] < k_end);
                     *reinterpret_cast<float4*>(as + a_r[it] * BM + a_c[it]) = v;
                 }
@@ -313,28 +317,20 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
                 if (!BKM) {
                     const int n = n0 + (lin >> 2), c = k0 + (lin & 3) * 4;
                     *reinterpret_cast<float4*>(bs + (lin >> 2) * SK + (lin & 3) * 4) =
-                        FAST ? rb[it] : mask4(rb[it], c, k_end, P.ldb, -1, n < N);
+                        FAST ? rb[R][it] : mask4(rb[R][it], c, k_end, P.ldb, -1, n < N);
                 } else {
                     const int kr = lin / (BN / 4), nc = (lin % (BN / 4)) * 4;
                     *reinterpret_cast<float4*>(bs + kr * BN + nc) =
-                        FAST ? rb[it] : mask4(rb[it], n0 + nc, N, P.ldb, -1, k0 + kr < k_end);
+                        FAST ? rb[R][it] : mask4(rb[R][it], n0 + nc, N, P.ldb, -1, k0 + kr < k_end);
                 }
             }
         };
 
         const int nk = k_end > k_begin ? (k_end - k_begin + BK - 1) / BK : 0;
-        if (nk > 0) {
-            load_tile(k_begin);
-            store_tile(0, k_begin);
-        }
-        __syncthreads();
-        for (int kt = 0; kt < nk; ++kt) {
-            const int buf = kt & 1;
-#if TTAMM_GEMM_ABLATE == 1  // developer ablation: no k-loop traffic (measures the MFMA/LDS loop)
-            if (false) load_tile(k_begin + (kt + 1) * BK);
-#else
-            if (kt + 1 < nk) load_tile(k_begin + (kt + 1) * BK);
-#endif
+        auto kof = [&](int kt) { return k_begin + kt * BK; };
+        // k-tile kt lives in LDS buffer kt & 1 and passes through register set kt & 1
+        auto compute = [&](auto S) {
+            constexpr int buf = decltype(S)::value;
             const float* as = As + buf * CF::A_STAGE;
             const float* bs = Bs + buf * CF::B_STAGE;
 #pragma unroll
@@ -369,15 +365,48 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
                             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(af[i], q), f4get(bf[j], q),
                                                                              acc[i][j], 0, 0, 0);
             }
-#if TTAMM_GEMM_ABLATE == 1
-            if (false) store_tile(buf ^ 1, k_begin + (kt + 1) * BK);
-#else
-            if (kt + 1 < nk) store_tile(buf ^ 1, k_begin + (kt + 1) * BK);
-#endif
-#if TTAMM_GEMM_ABLATE != 2
-            __syncthreads();
-#endif
+        };
+        using S0 = std::integral_constant<int, 0>;
+        using S1 = std::integral_constant<int, 1>;
+        // Prefetch depth: MN-major A (forward / dgrad) keeps two k-tiles in flight through two
+        // register sets; the K-major gathered A of the weight gradients keeps one (measured
+        // faster: the second set costs occupancy there).
+        constexpr bool DEEP = !AK;
+        if (nk > 0) {
+            load_tile(S0{}, kof(0));
+            store_tile(S0{}, S0{}, kof(0));
         }
+        if (DEEP && nk > 1) load_tile(S1{}, kof(1));
+        __syncthreads();
+        // one step on LDS buffer B: DEEP — prefetch k-tile kt+2 into register set B (its LDS
+        // buffer is free after the barrier), compute kt, write kt+1 (set NB) to buffer NB;
+        // shallow — prefetch kt+1 into set 0, compute kt, write set 0 to buffer NB
+        auto step = [&](auto Bf, auto NB, int kt) {
+            if constexpr (DEEP) {
+#if TTAMM_GEMM_ABLATE != 1  // developer ablation 1: no k-loop traffic (measures the MFMA/LDS loop)
+                if (kt + 2 < nk) load_tile(Bf, kof(kt + 2));
+#endif
+                compute(Bf);
+#if TTAMM_GEMM_ABLATE != 1
+                if (kt + 1 < nk) store_tile(NB, NB, kof(kt + 1));
+#endif
+            } else {
+#if TTAMM_GEMM_ABLATE != 1
+                if (kt + 1 < nk) load_tile(S0{}, kof(kt + 1));
+#endif
+                compute(Bf);
+#if TTAMM_GEMM_ABLATE != 1
+                if (kt + 1 < nk) store_tile(S0{}, NB, kof(kt + 1));
+#endif
+            }
+            __syncthreads();
+        };
+        int kt = 0;
+        for (; kt + 1 < nk; kt += 2) {
+            step(S0{}, S1{}, kt);
+            step(S1{}, S0{}, kt + 1);
+        }
+        if (kt < nk) step(S0{}, S1{}, kt);
     };
     if (fast) mainloop(std::true_type{});
     else mainloop(std::false_type{});

@@ -121,7 +121,13 @@ __device__ void compact_query(float* __restrict__ bs, int* __restrict__ bi, int*
     if (lane == 0) cnt[q] = n < k ? n : k;
 }
 
+// IT items per tile: wave (qw, iw) scores queries [32 qw, 32 qw + 32) against items
+// [iw IT/2, (iw+1) IT/2) of the tile — IT/64 MFMA tiles sharing the query fragments.  The next
+// tile's rows are loaded into registers while the current one is scored (PF float4 per thread).
+template <int IT, int DMAX>
 __global__ __launch_bounds__(256) void retrieval_partial_kernel(RetrievalArgs A) {
+    constexpr int MT = IT / 64;                       // 32x32 MFMA tiles per wave
+    constexpr int PF = (IT * DMAX / 4 + 255) / 256;   // prefetch float4 per thread
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ int cnt[kRQ];
     __shared__ float tau[kRQ];
@@ -155,44 +161,68 @@ __global__ __launch_bounds__(256) void retrieval_partial_kernel(RetrievalArgs A)
         bhi = A.boff[gq + 1];
     }
     const float* qb = Qs + myq * LD + h * Dh;
-    for (int64_t t0 = i_begin; t0 < i_end; t0 += kRI) {
-        __syncthreads();  // previous tile's readers and compactions are done
-        for (int e = tid; e < kRI * D4; e += 256) {
-            const int r = e / D4, c = (e - r * D4) * 4;
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (t0 + r < i_end) v = *reinterpret_cast<const float4*>(A.X + (t0 + r) * A.ldx + c);
-            *reinterpret_cast<float4*>(Xs + r * LD + c) = v;
-        }
-        __syncthreads();
-        const float my_tau = tau[myq];
-        f32x16 acc;
+    float4 pf[PF];
+    auto load_tile = [&](int64_t t0) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        for (int it = 0; it < PF; ++it) {
+            const int e = tid + it * 256;
+            const int r = e / D4, c = (e - r * D4) * 4;
+            pf[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e < IT * D4 && t0 + r < i_end) pf[it] = *reinterpret_cast<const float4*>(A.X + (t0 + r) * A.ldx + c);
+        }
+    };
+    auto store_tile = [&]() {
+#pragma unroll
+        for (int it = 0; it < PF; ++it) {
+            const int e = tid + it * 256;
+            const int r = e / D4, c = (e - r * D4) * 4;
+            if (e < IT * D4) *reinterpret_cast<float4*>(Xs + r * LD + c) = pf[it];
+        }
+    };
+    if (i_begin < i_end) {
+        load_tile(i_begin);
+        store_tile();
+    }
+    for (int64_t t0 = i_begin; t0 < i_end; t0 += IT) {
+        __syncthreads();  // tile t0 is in LDS; thresholds and counts are current
+        if (t0 + IT < i_end) load_tile(t0 + IT);
+        const float my_tau = tau[myq];
+        f32x16 acc[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
         // lane half h sums k in [h*D/2, (h+1)*D/2) — the same k order for both operands
-        const float* xa = Xs + (iw * 32 + (lane & 31)) * LD + h * Dh;
+        const float* xa = Xs + (iw * (IT / 2) + (lane & 31)) * LD + h * Dh;
         for (int kk = 0; kk < Dh; kk += 4) {
-            const float4 a4 = *reinterpret_cast<const float4*>(xa + kk);
             const float4 b4 = *reinterpret_cast<const float4*>(qb + kk);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, b4.x, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, b4.y, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, b4.z, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, b4.w, acc, 0, 0, 0);
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                const float4 a4 = *reinterpret_cast<const float4*>(xa + m * 32 * LD + kk);
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, b4.x, acc[m], 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, b4.y, acc[m], 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, b4.z, acc[m], 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, b4.w, acc[m], 0, 0, 0);
+            }
         }
         if (qvalid) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int64_t item = t0 + iw * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const float sc = acc[r];
-                if (item < i_end && sc >= my_tau && !(bhi > blo && is_blocked(A.bval, blo, bhi, item))) {
-                    const int slot = atomicAdd(&cnt[myq], 1);
-                    bs[myq * kRCap + slot] = sc;  // slot < kRCap: cnt <= kRCap - kRI before the tile
-                    bi[myq * kRCap + slot] = (int)item;
+            for (int m = 0; m < MT; ++m)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t item = t0 + iw * (IT / 2) + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const float sc = acc[m][r];
+                    if (item < i_end && sc >= my_tau && !(bhi > blo && is_blocked(A.bval, blo, bhi, item))) {
+                        const int slot = atomicAdd(&cnt[myq], 1);
+                        bs[myq * kRCap + slot] = sc;  // slot < kRCap: cnt <= kRCap - IT before the tile
+                        bi[myq * kRCap + slot] = (int)item;
+                    }
                 }
-            }
         }
-        __syncthreads();
+        __syncthreads();  // all scores of the tile are in; Xs is free
         for (int q = w; q < kRQ; q += 4)
-            if (cnt[q] > kRCap - kRI) compact_query(bs, bi, cnt, tau, q, A.k, nullptr, nullptr, 0);
+            if (cnt[q] > kRCap - IT) compact_query(bs, bi, cnt, tau, q, A.k, nullptr, nullptr, 0);
+        if (t0 + IT < i_end) store_tile();
     }
     __syncthreads();
     for (int q = w; q < kRQ; q += 4) {
@@ -278,7 +308,7 @@ int launch_retrieval_topk(const float* Q, int64_t nq, int64_t ldq, const float* 
     A.bval = bval;
     A.k = k;
     A.parts = pick_parts(nq, ni, k);
-    A.items_per_part = ni > 0 ? ((ni + A.parts - 1) / A.parts + kRI - 1) / kRI * kRI : 0;
+    A.items_per_part = ni > 0 ? ((ni + A.parts - 1) / A.parts + 127) / 128 * 128 : 0;
     const int64_t qtiles = (nq + kRQ - 1) / kRQ;
     const int64_t blocks = qtiles * A.parts;
     char* p = static_cast<char*>(ws);
@@ -291,14 +321,22 @@ int launch_retrieval_topk(const float* Q, int64_t nq, int64_t ldq, const float* 
     A.buf_i = reinterpret_cast<int*>(take((size_t)blocks * kRQ * kRCap * sizeof(int)));
     A.part_s = reinterpret_cast<float*>(take((size_t)nq * A.parts * k * sizeof(float)));
     A.part_i = reinterpret_cast<int*>(take((size_t)nq * A.parts * k * sizeof(int)));
-    const size_t lds = (size_t)(kRQ + kRI) * (dim + 4) * sizeof(float);
-    static bool attr_set = false;
-    if (!attr_set) {
-        TTAMM_HIP(hipFuncSetAttribute((const void*)retrieval_partial_kernel,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024));
-        attr_set = true;
+    // 128-item tiles (twice the MFMA work per barrier) when the LDS and the buffer allow
+    const bool wide = dim <= 128 && k <= kRCap - 128;
+    const int IT = wide ? 128 : kRI;
+    const size_t lds = (size_t)(kRQ + IT) * (dim + 4) * sizeof(float);
+    auto kern = wide ? (const void*)retrieval_partial_kernel<128, 128> : (const void*)retrieval_partial_kernel<64, 256>;
+    static bool attr_set[2] = {false, false};
+    if (!attr_set[wide]) {
+        TTAMM_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024));
+        attr_set[wide] = true;
     }
-    hipLaunchKernelGGL(retrieval_partial_kernel, dim3((unsigned)qtiles, (unsigned)A.parts), dim3(256), lds, s, A);
+    if (wide)
+        hipLaunchKernelGGL((retrieval_partial_kernel<128, 128>), dim3((unsigned)qtiles, (unsigned)A.parts), dim3(256),
+                           lds, s, A);
+    else
+        hipLaunchKernelGGL((retrieval_partial_kernel<64, 256>), dim3((unsigned)qtiles, (unsigned)A.parts), dim3(256),
+                           lds, s, A);
     TTAMM_LAUNCH_CHECK();
     hipLaunchKernelGGL(retrieval_merge_kernel, dim3((unsigned)nq), dim3(64), 0, s, A, out_s, out_i);
     TTAMM_LAUNCH_CHECK();
