@@ -525,13 +525,49 @@ int launch_gemm(GemmBatch& b, hipStream_t s) {
     return dispatch_epi<Cfg<128, 96, 4, 1, false, false>>(b, s);
 }
 
-int wgrad_rows_per_split(int R) {
-    (void)R;
-    return 512;
+namespace {
+// Resident blocks of a wgrad launch config on this device (CUs x occupancy), cached.
+int wgrad_slots(bool wide) {
+    static int cached[2] = {0, 0};
+    if (cached[wide]) return cached[wide];
+    int dev = 0, cus = 256, per_cu = 1;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const void* k = wide ? (const void*)gemm_kernel<Cfg<128, 192, 2, 2, true, true>, EPI_STORE>
+                         : (const void*)gemm_kernel<Cfg<128, 96, 4, 1, true, true>, EPI_STORE>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    cached[wide] = cus * per_cu;
+    return cached[wide];
+}
+}  // namespace
+
+// Rows per split-K chunk for a step's weight gradients: a multiple of BK in [512, 2048]
+// minimising the launches' makespan, (rounds of resident blocks) x (rows per block), so the
+// tile count lands just under a multiple of the device's block slots instead of spilling a
+// nearly empty extra round.
+int wgrad_rows_per_split(const WgradShape* shapes, int n) {
+    int best = 512;
+    double best_cost = -1.0;
+    for (int rps = 512; rps <= 2048; rps += BK) {
+        int64_t tiles[2] = {0, 0};
+        for (int i = 0; i < n; ++i) {
+            if (shapes[i].R <= 0) continue;
+            const bool wide = shapes[i].M > 96;
+            const int tm = (int)ceil_div(shapes[i].N + 1, 128);
+            const int tn = (int)ceil_div(shapes[i].M, wide ? 192 : 96);
+            tiles[wide] += (int64_t)tm * tn * ceil_div(shapes[i].R, rps);
+        }
+        double cost = 0.0;
+        for (int w = 0; w < 2; ++w)
+            if (tiles[w]) cost += (double)ceil_div(tiles[w], wgrad_slots(w == 1)) * rps;
+        if (best_cost < 0.0 || cost < best_cost) {
+            best_cost = cost;
+            best = rps;
+        }
+    }
+    return best;
 }
 
-size_t wgrad_slab_floats(int R, int M, int N) {
-    const int rps = wgrad_rows_per_split(R);
+size_t wgrad_slab_floats(int R, int M, int N, int rps) {
     const int splits = R > 0 ? (int)ceil_div(R, rps) : 1;
     return (size_t)splits * M * (N + 1);
 }
@@ -552,7 +588,7 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s) {
     int64_t total = 0;
     for (int i = 0; i < wb.count; ++i) {
         WgradProblem& w = wb.p[i];
-        w.rows_per_split = wgrad_rows_per_split(w.R);
+        TTAMM_REQUIRE(w.rows_per_split > 0 && w.rows_per_split % BK == 0, "wgrad: rows_per_split must be a multiple of 16");
         w.splits = w.R > 0 ? (int)ceil_div(w.R, w.rows_per_split) : 1;
         total += (int64_t)w.M * (w.N + 1);
         if (w.R <= 0) {  // no rows: the slab (one split) is zero

@@ -98,8 +98,12 @@ struct WgradBatch {
     int count;
     int total_blocks;
 };
-int wgrad_rows_per_split(int R);
-size_t wgrad_slab_floats(int R, int M, int N);
+struct WgradShape {
+    int64_t R;  // rows
+    int M, N;   // out features, in features
+};
+int wgrad_rows_per_split(const WgradShape* shapes, int n);
+size_t wgrad_slab_floats(int R, int M, int N, int rows_per_split);
 int launch_wgrad(WgradBatch& batch, hipStream_t s);
 
 // ------------------------------------------------------------------------------------

@@ -194,16 +194,20 @@ __global__ __launch_bounds__(256) void retrieval_partial_kernel(RetrievalArgs A)
             for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
         // lane half h sums k in [h*D/2, (h+1)*D/2) — the same k order for both operands
         const float* xa = Xs + (iw * (IT / 2) + (lane & 31)) * LD + h * Dh;
+#pragma unroll 4
         for (int kk = 0; kk < Dh; kk += 4) {
             const float4 b4 = *reinterpret_cast<const float4*>(qb + kk);
+            float4 a4[MT];
 #pragma unroll
-            for (int m = 0; m < MT; ++m) {
-                const float4 a4 = *reinterpret_cast<const float4*>(xa + m * 32 * LD + kk);
-                acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, b4.x, acc[m], 0, 0, 0);
-                acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, b4.y, acc[m], 0, 0, 0);
-                acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, b4.z, acc[m], 0, 0, 0);
-                acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, b4.w, acc[m], 0, 0, 0);
-            }
+            for (int m = 0; m < MT; ++m) a4[m] = *reinterpret_cast<const float4*>(xa + m * 32 * LD + kk);
+            // accumulators interleaved: consecutive MFMAs never depend on each other
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int m = 0; m < MT; ++m)
+                    acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(q == 0 ? a4[m].x : q == 1 ? a4[m].y : q == 2 ? a4[m].z : a4[m].w,
+                                                                  q == 0 ? b4.x : q == 1 ? b4.y : q == 2 ? b4.z : b4.w,
+                                                                  acc[m], 0, 0, 0);
         }
         if (qvalid) {
 #pragma unroll

@@ -67,6 +67,7 @@ struct TowerWs {
     float* piece_e = nullptr;
     float* piece_a = nullptr;
     float* wpad = nullptr;  // first feature layer weight, in_features padded to a multiple of 4
+    int wgrad_rps = 512;    // split-K rows of the weight gradients (shared by the step's launches)
 };
 
 struct StepWs {
@@ -159,12 +160,28 @@ void carve_grads(const ttamm_tower& T, TowerWs& w, float*& cur) {
 
 // Workspace layout.  Deterministic in the arguments, so every phase call of a sharded step
 // finds the previous phases' activations where it left them.
+// The weight-gradient problems of one tower (tower_backward's list), for the split choice.
+int wgrad_shapes(const ttamm_tower& T, int64_t R, WgradShape* out) {
+    int n = 0;
+    if (T.fusion == TTAMM_FUSION_IDENTITY) return 0;
+    for (int l = 0; l < T.n_linear; ++l) out[n++] = WgradShape{R, T.linear[l].out_features, T.linear[l].in_features};
+    if (T.fusion == TTAMM_FUSION_GATED)
+        for (int q = 0; q < 2; ++q) out[n++] = WgradShape{R, T.gate[q].out_features, T.gate[q].in_features};
+    return n;
+}
+
 int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
     const int64_t B = A.b.batch;
     const int N = A.b.num_neg;
     const int D = A.user.id.dim;
     const bool mimic = A.mimic_enabled != 0;
     const bool shard = sharded(A);
+    {
+        WgradShape shapes[2 * (TTAMM_MAX_LINEAR + 2)];
+        int n = wgrad_shapes(A.user, B, shapes);
+        n += wgrad_shapes(A.item, shard ? A.item_rows_capacity : B * (1 + N), shapes + n);
+        ws.user.wgrad_rps = ws.item.wgrad_rps = wgrad_rows_per_split(shapes, n);
+    }
     // ext_io: the item tower's t / a / dT / dA live in the caller's exchange buffers
     auto tower = [&](const ttamm_tower& T, TowerWs& w, int64_t R, bool own_idx, bool ext_io, int64_t dA_rows) {
         w.R = R;
@@ -201,13 +218,14 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         if (T.fusion != TTAMM_FUSION_IDENTITY) {
             for (int l = 0; l < T.n_linear; ++l) {
                 const ttamm_linear& L = T.linear[l];
-                w.slab[l] = ar.take<float>(wgrad_slab_floats((int)R, L.out_features, L.in_features));
+                w.slab[l] = ar.take<float>(wgrad_slab_floats((int)R, L.out_features, L.in_features, w.wgrad_rps));
             }
         }
         if (T.fusion == TTAMM_FUSION_GATED) {
             for (int q = 0; q < 2; ++q) {
                 const ttamm_linear& L = T.gate[q];
-                w.slab[TTAMM_MAX_LINEAR + q] = ar.take<float>(wgrad_slab_floats((int)R, L.out_features, L.in_features));
+                w.slab[TTAMM_MAX_LINEAR + q] =
+                    ar.take<float>(wgrad_slab_floats((int)R, L.out_features, L.in_features, w.wgrad_rps));
             }
         }
         w.co.keys_in = ar.take<int32_t>(R);
@@ -521,6 +539,7 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
             g2.grad_w = w.ggw[1];
             g2.grad_b = w.ggb[1];
             g2.slab = w.slab[TTAMM_MAX_LINEAR + 1];
+            g2.rows_per_split = w.wgrad_rps;
             wb.p[wb.count++] = g2;
             WgradProblem g1{};
             g1.dY = w.dz;
@@ -533,6 +552,7 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
             g1.grad_w = w.ggw[0];
             g1.grad_b = w.ggb[0];
             g1.slab = w.slab[TTAMM_MAX_LINEAR];
+            g1.rows_per_split = w.wgrad_rps;
             wb.p[wb.count++] = g1;
         }
         for (int l = t.n_linear - 1; l >= 0; --l) {
@@ -559,6 +579,7 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
             p.grad_w = w.gw[l];
             p.grad_b = w.gb[l];
             p.slab = w.slab[l];
+            p.rows_per_split = w.wgrad_rps;
             wb.p[wb.count++] = p;
         }
     }

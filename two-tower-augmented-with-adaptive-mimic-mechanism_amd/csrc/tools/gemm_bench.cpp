@@ -110,6 +110,8 @@ int main() {
         WgradProblem w{};
         w.dY = dY, w.ld_dy = H, w.X = X, w.x_idx = idx, w.ld_x = F, w.R = R, w.M = H, w.N = F - 3;
         w.grad_w = gw, w.grad_b = gb, w.slab = slab;
+        const WgradShape sh{w.R, w.M, w.N};
+        w.rows_per_split = wgrad_rows_per_split(&sh, 1);
         wb.p[0] = w, wb.count = 1;
         launch_wgrad(wb, 0);
     });
@@ -119,6 +121,8 @@ int main() {
         WgradProblem w{};
         w.dY = dF, w.ld_dy = D, w.X = Hb, w.ld_x = H, w.R = R, w.M = D, w.N = H;
         w.grad_w = gw, w.grad_b = gb, w.slab = slab;
+        const WgradShape sh{w.R, w.M, w.N};
+        w.rows_per_split = wgrad_rows_per_split(&sh, 1);
         wb.p[0] = w, wb.count = 1;
         launch_wgrad(wb, 0);
     });
