@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 5
+#define TTAMM_ABI_VERSION 6
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -198,6 +198,11 @@ typedef struct ttamm_step_args {
     int32_t history_capacity;     /* > replay_slices                                         */
     int32_t replay_slices;        /* every row is replayed at least once per replay_slices
                                      steps (bounds the lag a read has to catch up)           */
+    /* ---- optional second HIP stream (NULL = everything on `stream`) ---------------------
+     * The row coalesce (sort of the batch's rows) and the deferred catch-up of the rows a
+     * tower reads depend only on the indices; with an aux stream they run there, overlapping
+     * the feature-MLP GEMMs, and `stream` waits for them before the first table read. */
+    void* aux_stream;
 } ttamm_step_args;
 
 /* ---------------------------------------------------------------------------------- */

@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parents[1]
 
 
-def _engine(prob, *, deferred: bool, slices: int, sparse: bool = True):
+def _engine(prob, *, deferred: bool, slices: int, sparse: bool = True, overlap: bool = True):
     from gpu_helpers import ttamm_model_from
 
     model = ttamm_model_from(prob)
@@ -34,7 +34,7 @@ def _engine(prob, *, deferred: bool, slices: int, sparse: bool = True):
     eng = ttamm.FusedTrainStep(model, opts, negatives_per_positive=prob.shape.N, positives=prob.positives,
                                user_features=prob.user_features.cuda(), item_features=prob.item_features.cuda(),
                                loss_weights=LOSS_WEIGHTS, max_batch=prob.shape.B, seed=11,
-                               deferred_adamw=deferred, replay_slices=slices)
+                               deferred_adamw=deferred, replay_slices=slices, overlap=overlap)
     return model, opts, eng
 
 
@@ -48,8 +48,8 @@ def _state(model, opts):
     return out
 
 
-def _run(prob, steps, *, deferred, slices, sparse=True, flush_at=None, lr_change_at=None):
-    model, opts, eng = _engine(prob, deferred=deferred, slices=slices, sparse=sparse)
+def _run(prob, steps, *, deferred, slices, sparse=True, flush_at=None, lr_change_at=None, overlap=True):
+    model, opts, eng = _engine(prob, deferred=deferred, slices=slices, sparse=sparse, overlap=overlap)
     gen = torch.Generator().manual_seed(3)
     losses = []
     for k in range(steps):
@@ -77,6 +77,18 @@ def test_deferred_equals_eager_bitwise(slices, steps, sparse):
     assert eager.keys() == lazy.keys()
     for k in eager:
         assert torch.equal(eager[k], lazy[k]), k
+
+
+@pytest.mark.parametrize("deferred,sparse", [(True, True), (False, True), (True, False)])
+def test_aux_stream_overlap_bitwise(deferred, sparse):
+    """The index-only prologue on the aux stream (ttamm_step_args.aux_stream) changes no bit:
+    same losses, parameters and moments as the one-stream step."""
+    prob = make_problem(Shape(), seed=5)
+    one, l1 = _run(prob, 9, deferred=deferred, slices=3, sparse=sparse, overlap=False)
+    two, l2 = _run(prob, 9, deferred=deferred, slices=3, sparse=sparse, overlap=True)
+    assert l1 == l2
+    for k in one:
+        assert torch.equal(one[k], two[k]), k
 
 
 def test_deferred_c2_equals_eager():

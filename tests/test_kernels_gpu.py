@@ -24,7 +24,10 @@ def _lib():
     return _lib, _lib.load()
 
 
-@pytest.mark.parametrize("rows,dim,n", [(1000, 96, 5000), (7, 8, 33), (513, 12, 1), (300, 5, 77), (64, 128, 0)])
+@pytest.mark.parametrize("rows,dim,n", [(1000, 96, 5000), (7, 8, 33), (513, 12, 1), (300, 5, 77), (64, 128, 0),
+                                        # every width of the wide kernel, with ragged row tails
+                                        (999, 32, 4097), (999, 64, 1234), (999, 128, 70001), (999, 192, 4099),
+                                        (999, 256, 3333), (999, 96, 70001), (50, 128, 7)])
 def test_gather_rows_bit_exact(rows, dim, n):
     L, lib = _lib()
     table = torch.randn(rows, dim, device="cuda")

@@ -65,6 +65,17 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
+// Streaming (non-temporal) 16-byte store, for outputs a LATER kernel reads: the line is not
+// kept dirty in this XCD's L2, so the end-of-kernel L2 write-back does not serialise behind
+// the launch.  Measured on a 49,152 x 512 B row gather: 22 us with plain stores, 6.8 us with
+// these (csrc/tools/gather_bench.cpp, profiles/r01_gather_variants.txt).
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_nt(float4* p, float4 v) {
+    const f32x4_t x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<f32x4_t*>(p));
+}
+__device__ __forceinline__ void store_nt(float* p, float4 v) { store_nt(reinterpret_cast<float4*>(p), v); }
+
 // Philox4x32-10 counter-based RNG (Salmon et al., SC'11).
 struct u32x4 {
     uint32_t x, y, z, w;

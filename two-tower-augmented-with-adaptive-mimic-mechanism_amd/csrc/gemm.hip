@@ -103,7 +103,9 @@ struct Cfg {
 // N % 4 == 0 (every layer width is a multiple of 4), so a column group is always whole and
 // every operand access is one float4.  `bias4` is the group's bias (zero if none).
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+// epilogue outputs are read by later kernels: streaming stores (common.h store_nt; measured
+// neutral on the step, a plain-store build ran within noise of it)
+__device__ __forceinline__ void st4(float* p, float4 v) { store_nt(p, v); }
 
 template <int E>
 __device__ __forceinline__ void epilogue4(const KArg(GemmProblem) & P, float4 v, float4 bias4, int split, int row,

@@ -20,6 +20,50 @@ __global__ void gather_rows_vec4(const float* __restrict__ table, int d4, const 
     }
 }
 
+// Whole-row gather, rows of D4 float4: a wave takes RPW rows per iteration, their
+// RPW x D4 float4 flattened over I = RPW*D4/64 wave instructions (no idle lanes for any D4,
+// e.g. 96-wide rows: 8 rows in 3 instructions; 128-wide: 8 rows in 4).  Each lane issues its
+// I row indices, then its I row loads, so a CU keeps I x 16 B x 2048 lanes of HBM reads in
+// flight — what random rows of a table far larger than the caches need to approach the HBM
+// rate (MI355X_MICROARCH.md, "Indexed rows").  Rows are written with streaming stores (the
+// consumer is a later kernel).  Bit-exact copy.
+constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
+template <int D4>
+struct WideGather {
+    static constexpr int RPW0 = 64 / cgcd(64, D4);  // fewest rows filling whole instructions
+    static constexpr int I0 = RPW0 * D4 / 64;
+    static constexpr int MUL = I0 >= 4 ? 1 : (4 + I0 - 1) / I0;
+    static constexpr int RPW = RPW0 * MUL, I = I0 * MUL;
+};
+
+template <int D4>
+__global__ __launch_bounds__(256) void gather_rows_wide(const float4* __restrict__ table,
+                                                         const int64_t* __restrict__ idx, int64_t n,
+                                                         float4* __restrict__ out, int64_t out_ld4) {
+    constexpr int RPW = WideGather<D4>::RPW, I = WideGather<D4>::I;
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t r0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW; r0 < n;
+         r0 += nwaves * RPW) {
+        int64_t src[I];
+#pragma unroll
+        for (int u = 0; u < I; ++u) {
+            const int64_t r = r0 + (u * 64 + lane) / D4;
+            src[u] = r < n ? idx[r] : -1;
+        }
+        float4 v[I];
+#pragma unroll
+        for (int u = 0; u < I; ++u)
+            if (src[u] >= 0) v[u] = table[src[u] * D4 + (u * 64 + lane) % D4];
+#pragma unroll
+        for (int u = 0; u < I; ++u) {
+            const int e = u * 64 + lane;
+            const int64_t r = r0 + e / D4;
+            if (r < n) store_nt(out + r * out_ld4 + e % D4, v[u]);
+        }
+    }
+}
+
 __global__ void gather_rows_scalar(const float* __restrict__ table, int dim, const int64_t* __restrict__ idx,
                                    int64_t n, float* __restrict__ out, int64_t out_ld) {
     const int64_t total = n * dim;
@@ -266,7 +310,30 @@ int launch_gather_rows(const float* table, int dim, const int64_t* idx, int64_t 
     if (n <= 0) return TTAMM_OK;
     const bool vec = (dim % 4 == 0) && (out_ld % 4 == 0) && ((uintptr_t)table % 16 == 0) &&
                      ((uintptr_t)out % 16 == 0);
-    if (vec) {
+    const int d4 = dim / 4;
+    auto wide = [&](auto K) {
+        constexpr int D4 = decltype(K)::value;
+        const int64_t rows_per_block = (int64_t)WideGather<D4>::RPW * 4;
+        int64_t blocks = ceil_div(n, rows_per_block);
+        if (blocks > 8192) blocks = 8192;  // grid-stride beyond ~4 resident rounds
+        hipLaunchKernelGGL(gather_rows_wide<D4>, dim3((unsigned)blocks), dim3(256), 0, s,
+                           reinterpret_cast<const float4*>(table), idx, n, reinterpret_cast<float4*>(out),
+                           out_ld / 4);
+    };
+    auto try_wide = [&]() -> bool {
+        switch (d4) {  // the row widths of the supported configurations (D, 2D, H up to 256 floats)
+            case 8: wide(std::integral_constant<int, 8>{}); return true;
+            case 16: wide(std::integral_constant<int, 16>{}); return true;
+            case 24: wide(std::integral_constant<int, 24>{}); return true;
+            case 32: wide(std::integral_constant<int, 32>{}); return true;
+            case 48: wide(std::integral_constant<int, 48>{}); return true;
+            case 64: wide(std::integral_constant<int, 64>{}); return true;
+            default: return false;
+        }
+    };
+    if (vec && try_wide()) {
+        // launched
+    } else if (vec) {
         hipLaunchKernelGGL(gather_rows_vec4, dim3(grid_for(n * (dim / 4))), dim3(256), 0, s, table, dim / 4, idx, n,
                            out, out_ld);
     } else {

@@ -304,77 +304,82 @@ void set_keys(GemmProblem& p, const TowerWs& w) {
 }
 
 // ---- forward -------------------------------------------------------------------------------
+// part FWD_MLP: ID-row gather + feature encoder; FWD_FUSION: gate / combine (reads the mimic rows)
+enum { FWD_MLP = 1, FWD_FUSION = 2, FWD_ALL = 3 };
 int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt, int D, bool mimic, hipStream_t s,
-                  int ntowers, void* const* l0_events = nullptr) {
+                  int ntowers, void* const* l0_events = nullptr, int part = FWD_ALL) {
     int rc;
-    // ID rows -> e (ef[:, :D] when gated)
-    for (int k = 0; k < ntowers; ++k) {
-        const ttamm_tower& t = *T[k];
-        TowerWs& w = *W[k];
-        float* dst = t.fusion == TTAMM_FUSION_GATED ? w.ef : w.e;
-        const int64_t ld = t.fusion == TTAMM_FUSION_GATED ? 2 * D : D;
-        if ((rc = launch_gather_rows(t.id.weight, D, w.idx, w.R, dst, ld, s))) return rc;
-    }
-    // feature encoder layers
-    int maxL = 0;
-    for (int k = 0; k < ntowers; ++k)
-        if (T[k]->fusion != TTAMM_FUSION_IDENTITY) maxL = T[k]->n_linear > maxL ? T[k]->n_linear : maxL;
-    for (int l = 0; l < maxL; ++l) {
-        Batcher bb;
+    if (part & FWD_MLP) {
+        // ID rows -> e (ef[:, :D] when gated)
         for (int k = 0; k < ntowers; ++k) {
             const ttamm_tower& t = *T[k];
             TowerWs& w = *W[k];
-            if (t.fusion == TTAMM_FUSION_IDENTITY || l >= t.n_linear) continue;
-            const ttamm_linear& L = t.linear[l];
-            GemmProblem p = gp_base();
-            if (l == 0) {
-                p.A = t.features;
-                p.a_idx = w.fidx;
-                p.lda = t.feat_ld;
-            } else {
-                p.A = w.hid[l - 1];
-                p.lda = t.linear[l - 1].out_features;
-            }
-            p.B = L.weight;
-            p.ldb = L.in_features;
-            if (l == 0 && w.wpad) {
-                if ((rc = launch_pad_rows(L.weight, L.out_features, L.in_features, L.in_features, w.wpad,
-                                          round4(L.in_features), s)))
-                    return rc;
-                p.B = w.wpad;
-                p.ldb = round4(L.in_features);
-            }
-            p.b_kn = 0;
-            p.M = (int)w.R;
-            p.N = L.out_features;
-            p.K = L.in_features;
-            // the feature rows and the padded weight are zero beyond F: run K to the padded
-            // width so every k-tile is whole (fast GEMM path)
-            if (l == 0 && w.wpad && t.feat_ld >= round4(L.in_features)) p.K = round4(L.in_features);
-            p.bias = L.bias;
-            if (l + 1 < t.n_linear) {
-                p.epi = EPI_HIDDEN;
-                p.C = w.hid[l];
-                p.ldc = L.out_features;
-                set_dropout(p, t, bt, w.role, l, w.role == ROLE_USER ? bt.user_keep_mask[l] : bt.item_keep_mask[l]);
-                set_keys(p, w);
-            } else {
-                p.epi = EPI_STORE;
-                if (t.fusion == TTAMM_FUSION_GATED) {
-                    p.C = w.ef + D;
-                    p.ldc = 2 * D;
-                } else {
-                    p.C = w.f;
-                    p.ldc = D;
-                }
-            }
-            bb.add(p);
+            float* dst = t.fusion == TTAMM_FUSION_GATED ? w.ef : w.e;
+            const int64_t ld = t.fusion == TTAMM_FUSION_GATED ? 2 * D : D;
+            if ((rc = launch_gather_rows(t.id.weight, D, w.idx, w.R, dst, ld, s))) return rc;
         }
-        const bool timed = l == 0 && l0_events && l0_events[0] && l0_events[1];
-        if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)l0_events[0], s));
-        if ((rc = bb.run(s))) return rc;
-        if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)l0_events[1], s));
+        // feature encoder layers
+        int maxL = 0;
+        for (int k = 0; k < ntowers; ++k)
+            if (T[k]->fusion != TTAMM_FUSION_IDENTITY) maxL = T[k]->n_linear > maxL ? T[k]->n_linear : maxL;
+        for (int l = 0; l < maxL; ++l) {
+            Batcher bb;
+            for (int k = 0; k < ntowers; ++k) {
+                const ttamm_tower& t = *T[k];
+                TowerWs& w = *W[k];
+                if (t.fusion == TTAMM_FUSION_IDENTITY || l >= t.n_linear) continue;
+                const ttamm_linear& L = t.linear[l];
+                GemmProblem p = gp_base();
+                if (l == 0) {
+                    p.A = t.features;
+                    p.a_idx = w.fidx;
+                    p.lda = t.feat_ld;
+                } else {
+                    p.A = w.hid[l - 1];
+                    p.lda = t.linear[l - 1].out_features;
+                }
+                p.B = L.weight;
+                p.ldb = L.in_features;
+                if (l == 0 && w.wpad) {
+                    if ((rc = launch_pad_rows(L.weight, L.out_features, L.in_features, L.in_features, w.wpad,
+                                              round4(L.in_features), s)))
+                        return rc;
+                    p.B = w.wpad;
+                    p.ldb = round4(L.in_features);
+                }
+                p.b_kn = 0;
+                p.M = (int)w.R;
+                p.N = L.out_features;
+                p.K = L.in_features;
+                // the feature rows and the padded weight are zero beyond F: run K to the padded
+                // width so every k-tile is whole (fast GEMM path)
+                if (l == 0 && w.wpad && t.feat_ld >= round4(L.in_features)) p.K = round4(L.in_features);
+                p.bias = L.bias;
+                if (l + 1 < t.n_linear) {
+                    p.epi = EPI_HIDDEN;
+                    p.C = w.hid[l];
+                    p.ldc = L.out_features;
+                    set_dropout(p, t, bt, w.role, l, w.role == ROLE_USER ? bt.user_keep_mask[l] : bt.item_keep_mask[l]);
+                    set_keys(p, w);
+                } else {
+                    p.epi = EPI_STORE;
+                    if (t.fusion == TTAMM_FUSION_GATED) {
+                        p.C = w.ef + D;
+                        p.ldc = 2 * D;
+                    } else {
+                        p.C = w.f;
+                        p.ldc = D;
+                    }
+                }
+                bb.add(p);
+            }
+            const bool timed = l == 0 && l0_events && l0_events[0] && l0_events[1];
+            if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)l0_events[0], s));
+            if ((rc = bb.run(s))) return rc;
+            if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)l0_events[1], s));
+        }
     }
+    if (!(part & FWD_FUSION)) return TTAMM_OK;
     // feature encoder "identity" (no Linear): f = feature rows
     for (int k = 0; k < ntowers; ++k) {
         const ttamm_tower& t = *T[k];
@@ -642,6 +647,61 @@ int tower_prepare(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred& 
     return launch_replay(ra, s);
 }
 
+// Fork / join events of the aux stream, one pair per host thread and device (reused across
+// steps: a wait binds to the record that precedes it).
+int aux_events(hipEvent_t* fork, hipEvent_t* join) {
+    struct Pair {
+        int dev;
+        hipEvent_t f, j;
+    };
+    thread_local std::vector<Pair> cache;
+    int dev = 0;
+    TTAMM_HIP(hipGetDevice(&dev));
+    for (const Pair& p : cache)
+        if (p.dev == dev) {
+            *fork = p.f;
+            *join = p.j;
+            return TTAMM_OK;
+        }
+    Pair p{dev, nullptr, nullptr};
+    TTAMM_HIP(hipEventCreateWithFlags(&p.f, hipEventDisableTiming));
+    TTAMM_HIP(hipEventCreateWithFlags(&p.j, hipEventDisableTiming));
+    cache.push_back(p);
+    *fork = p.f;
+    *join = p.j;
+    return TTAMM_OK;
+}
+
+// tower_prepare of `n` towers, then their forward.  With an aux stream the prepare work (sort
+// + deferred catch-up: index-only inputs) runs there while `s` gathers ID rows and runs the
+// feature MLP; `s` joins before the fusion, whose epilogue reads the mimic rows.  A deferred
+// dense ID table is read by the first gather, so that case stays serial.
+int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_batch& bt, int D, bool mimic,
+                    const Deferred& df, hipStream_t s, hipStream_t aux, void* const* l0_events) {
+    int rc;
+    bool overlap = aux != nullptr && aux != s;
+    for (int k = 0; k < n; ++k)
+        if (df.on && T[k]->id.optimizer == TTAMM_OPT_DENSE) overlap = false;
+    if (!overlap) {
+        for (int k = 0; k < n; ++k)
+            if ((rc = tower_prepare(*T[k], *W[k], mimic, df, s))) return rc;
+        return tower_forward(T, W, bt, D, mimic, s, n, l0_events, FWD_ALL);
+    }
+    // The MLP launches are enqueued first: the prologue is ~25 small launches (radix sort,
+    // scan, catch-up) whose host-side enqueue alone outlasts their GPU time, so issuing them
+    // first would hold the GEMMs back behind the host.
+    hipEvent_t fork, join;
+    if ((rc = aux_events(&fork, &join))) return rc;
+    TTAMM_HIP(hipEventRecord(fork, s));
+    if ((rc = tower_forward(T, W, bt, D, mimic, s, n, l0_events, FWD_MLP))) return rc;
+    TTAMM_HIP(hipStreamWaitEvent(aux, fork, 0));
+    for (int k = 0; k < n; ++k)
+        if ((rc = tower_prepare(*T[k], *W[k], mimic, df, aux))) return rc;
+    TTAMM_HIP(hipEventRecord(join, aux));
+    TTAMM_HIP(hipStreamWaitEvent(s, join, 0));
+    return tower_forward(T, W, bt, D, mimic, s, n, l0_events, FWD_FUSION);
+}
+
 int tower_optimizer_rows(const ttamm_tower& t, TowerWs& w, int D, bool mimic, const SparseConsts& sp,
                          const AdamConsts& ad, const Deferred& df, hipStream_t s) {
     RowUpdateArgs ru;
@@ -906,22 +966,21 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         }
     }
     // ---- forward ----------------------------------------------------------------------------
+    hipStream_t aux = static_cast<hipStream_t>(A.aux_stream);
     if (!shard) {
-        if ((rc = tower_prepare(A.user, U, mimic, df, s))) return rc;
-        if ((rc = tower_prepare(A.item, I, mimic, df, s))) return rc;
-        if ((rc = tower_forward(T, W, A.b, D, mimic, s, 2, A.timing_events + 2))) return rc;
+        if ((rc = prepare_forward(T, W, 2, A.b, D, mimic, df, s, aux, A.timing_events + 2))) return rc;
     } else {
         const ttamm_tower* Ti[2] = {&A.item, nullptr};
         TowerWs* Wi[2] = {&I, nullptr};
         if (ph & TTAMM_PHASE_ITEM_FWD) {
-            if ((rc = tower_prepare(A.item, I, mimic, df, s))) return rc;
-            if (I.R > 0)
-                if ((rc = tower_forward(Ti, Wi, A.b, D, mimic, s, 1, A.timing_events + 2))) return rc;
+            if (I.R > 0) {
+                if ((rc = prepare_forward(Ti, Wi, 1, A.b, D, mimic, df, s, aux, A.timing_events + 2))) return rc;
+            } else if ((rc = tower_prepare(A.item, I, mimic, df, s))) {
+                return rc;
+            }
         }
-        if (ph & TTAMM_PHASE_USER_FWD) {
-            if ((rc = tower_prepare(A.user, U, mimic, df, s))) return rc;
-            if ((rc = tower_forward(T, W, A.b, D, mimic, s, 1))) return rc;
-        }
+        if (ph & TTAMM_PHASE_USER_FWD)
+            if ((rc = prepare_forward(T, W, 1, A.b, D, mimic, df, s, aux, nullptr))) return rc;
     }
     // ---- score + loss (fwd + bwd seeds), user-side backward ---------------------------------
     if (ph & TTAMM_PHASE_USER) {

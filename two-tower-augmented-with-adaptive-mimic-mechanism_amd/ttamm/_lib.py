@@ -141,10 +141,11 @@ class StepArgs(ctypes.Structure):
         ("adam_history", c_vp),
         ("history_capacity", c_i32),
         ("replay_slices", c_i32),
+        ("aux_stream", c_vp),
     ]
 
 
-ABI_VERSION = 5  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 6  # ttamm.h TTAMM_ABI_VERSION
 
 # ttamm.h TTAMM_PHASE_*
 PHASE_ALL = 0

@@ -122,6 +122,7 @@ class FusedTrainStep:
         num_items: int | None = None,
         deferred_adamw: bool = True,
         replay_slices: int = 64,
+        overlap: bool = True,
     ) -> None:
         if negatives_per_positive <= 0:
             raise ValueError("num_negatives must be greater than zero.")
@@ -271,6 +272,10 @@ class FusedTrainStep:
                 args.adam_history = self.adam_history.data_ptr()
                 args.history_capacity = cap
                 args.replay_slices = replay_slices
+        # second HIP stream for the index-only prologue (row sort + deferred catch-up),
+        # overlapping the feature MLP (ttamm.h ttamm_step_args.aux_stream)
+        self.aux_stream = torch.cuda.Stream(device=self.device) if overlap else None
+        args.aux_stream = self.aux_stream.cuda_stream if self.aux_stream is not None else None
         self._configure(args)
         self.ws_bytes = int(self.lib.ttamm_train_step_workspace_size(ctypes.byref(args)))
         self.workspace = torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
