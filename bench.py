@@ -43,9 +43,14 @@ import torch  # noqa: E402
 METRIC = "training interactions/sec at 1/2/4/8 MI355X; Recall@20 parity vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 matrix (v_mfma_f32_32x32x2_f32), dense
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 MFMA ~2.5 PF dense (no sparsity)
 
 CONFIGS = {
     "c2": dict(U=200_000, I=2_000_000, D=96, H=192, F=605, B=8192, N=5, dropout=0.15, pos_per_user=20),
+    # BASELINE configs[4] per GPU: bf16 towers, 256-dim embeddings, 512-wide MLP, gate on
+    # (weak scaling: each of N ranks holds a shard of this size; at --gpus 8 the 8-GPU C5)
+    "c5": dict(U=200_000, I=2_000_000, D=256, H=512, F=605, B=8192, N=5, dropout=0.15, pos_per_user=20,
+               matmul="bf16"),
     # small sanity config (not a bench line)
     "tiny": dict(U=2_000, I=20_000, D=96, H=192, F=605, B=1024, N=5, dropout=0.15, pos_per_user=20),
 }
@@ -59,6 +64,7 @@ def tower_cfg(c: dict) -> dict:
                             "dropout": c["dropout"]},
         "fusion": "gated",
         "output_dim": c["D"],
+        "matmul_dtype": c.get("matmul", "fp32"),
     }
 
 
@@ -311,6 +317,8 @@ def main() -> None:
         l1_rows = (getattr(eng, "item_rows_seen", 0) - rows0) / args.steps
     l1_flops = 2.0 * l1_rows * F * H
     tflops = l1_flops / (gemm_ms * 1e-3) / 1e12
+    bf16 = c.get("matmul", "fp32") == "bf16"
+    mfma_peak = MFMA_BF16_PEAK_TFLOPS if bf16 else MFMA_FP32_PEAK_TFLOPS
     traffic = load_traffic(args.config)
     deferred = not args.eager_adamw
     if deferred:
@@ -336,12 +344,13 @@ def main() -> None:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
-        "data": "synthetic: C2 shapes, Zipf(1.05) positives (20/user), features shaped like features.py, "
-                "random-init weights",
+        "dtype": "bf16 GEMM operands, fp32 accumulate/state" if bf16 else "fp32",
+        "data": f"synthetic: {args.config.upper()} shapes, Zipf(1.05) positives (20/user), features shaped like "
+                "features.py, random-init weights",
         "config": {
             "workload": f"{args.config.upper()}: {I * world} items x {U * world} users, D={D}, "
                         f"MLP {F}->{H}->{D} (ReLU, dropout {c['dropout']}), gated fusion, adaptive mimic, "
+                        f"{'bf16' if bf16 else 'fp32'} tower GEMMs, "
                         f"B={B} per GPU, N={N} sampled negatives, AdamW + SparseAdam",
             "global_batch": B * world,
             "negatives_per_positive": N,
@@ -352,12 +361,12 @@ def main() -> None:
         "final_loss": round(loss, 6),
         "roofline": {
             "bound": "mfma",
-            "kernel": "gemm_kernel first feature layer forward (Linear 605->192 + ReLU + dropout, user and item "
-                      "rows grouped), fp32 MFMA 32x32x2",
+            "kernel": f"gemm_kernel first feature layer forward (Linear {F}->{H} + ReLU + dropout, user and item "
+                      f"rows grouped), {'bf16 MFMA 32x32x16' if bf16 else 'fp32 MFMA 32x32x2'}",
             "achieved": round(tflops, 2),
-            "peak": MFMA_FP32_PEAK_TFLOPS,
+            "peak": mfma_peak,
             "unit": "TFLOP/s",
-            "frac": round(tflops / MFMA_FP32_PEAK_TFLOPS, 4),
+            "frac": round(tflops / mfma_peak, 4),
             "traffic": (traffic or {}).get("l1_forward_gemm_bytes_per_launch"),
             "algorithmic_flops_per_launch": l1_flops,
             "avg_launch_ms": round(gemm_ms, 4),

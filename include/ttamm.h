@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 6
+#define TTAMM_ABI_VERSION 7
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -120,6 +120,11 @@ typedef struct ttamm_tower {
     float dropout;         /* Dropout p after each hidden ReLU (encoders.py:132-138)    */
     ttamm_linear linear[TTAMM_MAX_LINEAR];
     ttamm_linear gate[2];  /* FeatureFusionGate.gate_network.{0,2} (encoders.py:157-162) */
+    int32_t matmul_bf16;   /* 0: fp32 GEMMs (the reference).  1: "bf16 towers" (BASELINE config
+                              C5): every feature-MLP / gate GEMM (forward, input and weight
+                              gradients) rounds both operands to bf16 (RNE) and accumulates in
+                              fp32; activations, losses, tables, weights and optimizer state stay
+                              fp32.  Both towers of a step must agree.                      */
 } ttamm_tower;
 
 /* Optimizer hyper-parameters for one step, as the Python floats torch holds (double).

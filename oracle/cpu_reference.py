@@ -36,8 +36,10 @@ class FeatureFusionGate(nn.Module):  # encoders.py:149-168
 
 
 class OracleTower(nn.Module):  # encoders.py:171-219 (constructor) — forward is tower_forward below
-    def __init__(self, embedding: nn.Embedding, feature_encoder, fusion: str, gate) -> None:
+    def __init__(self, embedding: nn.Embedding, feature_encoder, fusion: str, gate, matmul_dtype: str = "fp32") -> None:
         super().__init__()
+        # not in the reference: the "bf16 towers" precision of BASELINE config C5 (see _bf16_linear)
+        self.matmul_dtype = matmul_dtype
         self.embedding = embedding
         self.feature_encoder = feature_encoder
         self.fusion = "identity" if feature_encoder is None else fusion
@@ -106,7 +108,8 @@ def build_tower(cfg: Mapping[str, Any], *, num_embeddings: int, feature_dim: int
     if fusion in ("gated", "adaptive_mimic"):
         gate = FeatureFusionGate(emb.embedding_dim, (cfg.get("adaptive_mimic") or {}).get("hidden_dim"))
         fusion = "gated"
-    return OracleTower(emb, fe, fusion, gate)
+    mm = str(cfg.get("matmul_dtype", "fp32")).lower()
+    return OracleTower(emb, fe, fusion, gate, "bf16" if mm in ("bf16", "bfloat16") else "fp32")
 
 
 def build_model(
@@ -133,17 +136,46 @@ def _dropout(x: torch.Tensor, p: float, keep: torch.Tensor | None, training: boo
     return x * noise
 
 
+def _round_bf16(x: torch.Tensor) -> torch.Tensor:
+    return x.to(torch.bfloat16).to(torch.float32)  # round to nearest even
+
+
+class _BF16Linear(torch.autograd.Function):
+    """nn.Linear with bf16 operands and fp32 accumulation — the definition of ttamm's
+    matmul_dtype="bf16" (not reference behaviour; BASELINE config C5 "bf16 towers").  Every
+    product of the forward and of both gradients rounds its two operands to bf16:
+    y = bf(x) bf(W)^T + b,  dx = bf(dy) bf(W),  dW = bf(dy)^T bf(x),  db = sum bf(dy)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        xr, wr = _round_bf16(x), _round_bf16(w)
+        ctx.save_for_backward(xr, wr)
+        return xr @ wr.t() + b
+
+    @staticmethod
+    def backward(ctx, dy):
+        xr, wr = ctx.saved_tensors
+        dyr = _round_bf16(dy)
+        return dyr @ wr, dyr.t() @ xr, dyr.sum(0)
+
+
+def _linear(lin: nn.Linear, x: torch.Tensor, bf16: bool) -> torch.Tensor:
+    return _BF16Linear.apply(x, lin.weight, lin.bias) if bf16 else lin(x)
+
+
 def feature_forward(fe: FeatureEncoderWrapper, x: torch.Tensor, keep_masks: Sequence[torch.Tensor] | None,
-                    training: bool) -> torch.Tensor:
+                    training: bool, bf16: bool = False) -> torch.Tensor:
     net = fe.network
     if isinstance(net, nn.Linear):
-        return net(x)
+        return _linear(net, x, bf16)
     hidden = 0
     for m in net:
         if isinstance(m, nn.Dropout):
             keep = keep_masks[hidden] if keep_masks is not None else None
             x = _dropout(x, m.p, keep, training)
             hidden += 1
+        elif isinstance(m, nn.Linear):
+            x = _linear(m, x, bf16)
         else:
             x = m(x)
     return x
@@ -154,10 +186,12 @@ def tower_forward(tower: OracleTower, idx: torch.Tensor, feats: torch.Tensor | N
     e = tower.embedding(idx)  # encoders.py:223
     if tower.fusion == "identity" or tower.feature_encoder is None or feats is None:
         return e
-    f = feature_forward(tower.feature_encoder, feats, keep_masks, training)  # :233
+    bf16 = tower.matmul_dtype == "bf16"
+    f = feature_forward(tower.feature_encoder, feats, keep_masks, training, bf16)  # :233
     if tower.fusion == "sum":
         return e + f  # :240
-    gate = tower.adaptive_mimic.gate_network(torch.cat([e, f], dim=-1))  # :164-168
+    g1, _, g2, _ = tower.adaptive_mimic.gate_network  # Linear, ReLU, Linear, Sigmoid (:157-162)
+    gate = torch.sigmoid(_linear(g2, torch.relu(_linear(g1, torch.cat([e, f], dim=-1), bf16)), bf16))  # :164-168
     return gate * e + (1.0 - gate) * f
 
 

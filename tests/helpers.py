@@ -26,10 +26,12 @@ class Shape:
     mimic: bool = True
     sparse: bool = True
     hidden_dims: tuple = (16,)
+    matmul_dtype: str = "fp32"
 
     def tower_cfg(self) -> dict:
         return {
             "type": "tower",
+            "matmul_dtype": self.matmul_dtype,
             "id_embedding": {"params": {"embedding_dim": self.D, "sparse": self.sparse},
                              "init": {"type": "normal", "std": 0.02}},
             "feature_encoder": {"type": "mlp", "hidden_dims": list(self.hidden_dims), "activation": "relu",

@@ -71,3 +71,45 @@ def test_three_steps_match_oracle(shape):
         assert rel_err(tst[n]["exp_avg"], ost[n]["exp_avg"]) <= 1e-4, n
         assert rel_err(tst[n]["exp_avg_sq"], ost[n]["exp_avg_sq"]) <= 1e-4, n
         assert float(tst[n]["step"]) == float(ost[n]["step"]), n
+
+
+# bf16 towers (ttamm.h ttamm_tower.matmul_bf16; BASELINE config C5): checked against the
+# oracle's bf16 restatement (oracle/cpu_reference.py _BF16Linear: operands rounded to bf16,
+# fp32 accumulation).  Both sides round the SAME definition, but an fp32 activation that differs
+# by one ulp (summation order) can round to the neighbouring bf16 value, so the tolerance is the
+# bf16 one: max-norm relative 2e-3 per tensor, and the mean error stays at fp32 level.
+BF16_TOL = 2e-3
+
+
+@pytest.mark.parametrize(
+    "shape",
+    [
+        Shape(matmul_dtype="bf16"),
+        Shape(U=50, I=300, F=37, H=24, D=12, B=40, N=3, gate_hidden=20, hidden_dims=(24,), matmul_dtype="bf16"),
+        Shape(U=96, I=768, F=605, H=512, D=256, B=48, N=5, hidden_dims=(512,), matmul_dtype="bf16"),
+    ],
+    ids=["tiny", "odd", "c5-dims"],
+)
+def test_bf16_step_gradients_match_bf16_oracle(shape):
+    from gpu_helpers import run_ttamm
+
+    prob = make_problem(shape, steps=1)
+    om, oo, ores = run_oracle(prob, lr=0.0, betas=(0.0, 0.999))
+    tm, to, tres = run_ttamm(prob, lr=0.0, betas=(0.0, 0.999))
+    for key in ("total", "bce", "mimic_user", "mimic_item"):
+        assert abs(tres[0][key] - getattr(ores[0], key)) <= 1e-4 * abs(getattr(ores[0], key)), key
+    og, tg = _grads_by_name(om, oo), _grads_by_name(tm, to)
+    assert set(og) == set(tg)
+    for name in og:
+        err = rel_err(tg[name], og[name])
+        mean = ((tg[name].double() - og[name].double()).abs().mean() / og[name].double().abs().max().clamp_min(1e-30)).item()
+        assert err <= BF16_TOL, f"{name}: rel err {err:.3e}"
+        assert mean <= 2e-5, f"{name}: mean rel err {mean:.3e}"
+    # the bf16 path really rounds: fp32 GEMMs on the same inputs give gradients measurably
+    # farther from the bf16 oracle than ttamm's bf16 step is
+    prob32 = make_problem(Shape(**{**shape.__dict__, "matmul_dtype": "fp32"}), steps=1)
+    m32, o32, _ = run_oracle(prob32, lr=0.0, betas=(0.0, 0.999))
+    g32 = _grads_by_name(m32, o32)
+    far = max(rel_err(g32[n], og[n]) for n in og)
+    near = max(rel_err(tg[n], og[n]) for n in og)
+    assert far > 5e-4 and far > 4 * near, (far, near)

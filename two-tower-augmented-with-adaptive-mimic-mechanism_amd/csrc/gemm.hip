@@ -14,6 +14,11 @@
 //
 // Matrix core: v_mfma_f32_32x32x2_f32 (exact fp32: one rounding per product, like an fma
 // chain).  Lane half h = lane>>5 owns k-slot h; inside a BK = 16 tile it walks k = 8h..8h+7.
+// bf16 variant (BF = true; ttamm_tower.matmul_bf16, BASELINE config C5): the same LDS image
+// and fragment reads — a lane's 8 k values 8h..8h+7 are exactly the A/B fragment of
+// v_mfma_f32_32x32x16_bf16 (lane l: row l&31, k = 8(l>>5) + j) — rounded to bf16 (RNE,
+// v_cvt_pk_bf16_f32) in registers; one bf16 MFMA replaces the eight fp32 ones per k-tile.
+// Accumulation, epilogues and every stored tensor stay fp32.
 //
 // Epilogue: the accumulators go through LDS (in row slices) and 256 threads apply the fused
 // elementwise tail with float4 loads/stores: bias, ReLU, dropout (encoders.py:132-138),
@@ -35,6 +40,8 @@
 namespace ttamm {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 namespace {
 
@@ -47,6 +54,11 @@ constexpr int kThreads = 256;
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 __device__ __forceinline__ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+// 8 consecutive k values of one lane -> one bf16 MFMA fragment (round to nearest even)
+__device__ __forceinline__ bf16x8 pack_bf16(float4 a, float4 b) {
+    const f32x8 v = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    return __builtin_convertvector(v, bf16x8);
+}
 __device__ __forceinline__ float f4get(const float4& v, int q) {
     return q == 0 ? v.x : q == 1 ? v.y : q == 2 ? v.z : v.w;
 }
@@ -181,7 +193,7 @@ __device__ __forceinline__ void epilogue4(const KArg(GemmProblem) & P, float4 v,
     st4(P.C + (int64_t)split * P.slab_stride + (int64_t)row * P.ldc + col, make_float4(x[0], x[1], x[2], x[3]));
 }
 
-template <class CF, int E>
+template <class CF, int E, bool BF>
 __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
     constexpr int BM = CF::BM, BN = CF::BN, TM = CF::TM, TN = CF::TN, I = CF::I, J = CF::J;
     constexpr bool AK = CF::A_KMAJ, BKM = CF::B_KMAJ;
@@ -335,37 +347,47 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
             constexpr int buf = decltype(S)::value;
             const float* as = As + buf * CF::A_STAGE;
             const float* bs = Bs + buf * CF::B_STAGE;
+            // the lane's 4 k values 8h + 4*s4 .. +3 of A row m / B column n
+            auto frag_a = [&](int i, int s4) -> float4 {
+                const int m = wm * TM + i * 32 + li;
+                if (!AK) return *reinterpret_cast<const float4*>(as + m * SK + 8 * h + 4 * s4);
+                const float* c = as + (8 * h + 4 * s4) * BM + m;
+                return make_float4(c[0], c[BM], c[2 * BM], c[3 * BM]);
+            };
+            auto frag_b = [&](int j, int s4) -> float4 {
+                const int n = wn * TN + j * 32 + li;
+                if (!BKM) return *reinterpret_cast<const float4*>(bs + n * SK + 8 * h + 4 * s4);
+                const float* c = bs + (8 * h + 4 * s4) * BN + n;
+                return make_float4(c[0], c[BN], c[2 * BN], c[3 * BN]);
+            };
+            if constexpr (BF) {
+                bf16x8 a8[I], b8[J];
 #pragma unroll
-            for (int s4 = 0; s4 < 2; ++s4) {
-                float4 af[I], bf[J];
+                for (int i = 0; i < I; ++i) a8[i] = pack_bf16(frag_a(i, 0), frag_a(i, 1));
 #pragma unroll
-                for (int i = 0; i < I; ++i) {
-                    const int m = wm * TM + i * 32 + li;
-                    if (!AK) {
-                        af[i] = *reinterpret_cast<const float4*>(as + m * SK + 8 * h + 4 * s4);
-                    } else {
-                        const float* c = as + (8 * h + 4 * s4) * BM + m;
-                        af[i] = make_float4(c[0], c[BM], c[2 * BM], c[3 * BM]);
-                    }
+                for (int j = 0; j < J; ++j) b8[j] = pack_bf16(frag_b(j, 0), frag_b(j, 1));
+#pragma unroll
+                for (int i = 0; i < I; ++i)
+#pragma unroll
+                    for (int j = 0; j < J; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a8[i], b8[j], acc[i][j], 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int s4 = 0; s4 < 2; ++s4) {
+                    float4 af[I], bf[J];
+#pragma unroll
+                    for (int i = 0; i < I; ++i) af[i] = frag_a(i, s4);
+#pragma unroll
+                    for (int j = 0; j < J; ++j) bf[j] = frag_b(j, s4);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+#pragma unroll
+                        for (int i = 0; i < I; ++i)
+#pragma unroll
+                            for (int j = 0; j < J; ++j)
+                                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(af[i], q), f4get(bf[j], q),
+                                                                                 acc[i][j], 0, 0, 0);
                 }
-#pragma unroll
-                for (int j = 0; j < J; ++j) {
-                    const int n = wn * TN + j * 32 + li;
-                    if (!BKM) {
-                        bf[j] = *reinterpret_cast<const float4*>(bs + n * SK + 8 * h + 4 * s4);
-                    } else {
-                        const float* c = bs + (8 * h + 4 * s4) * BN + n;
-                        bf[j] = make_float4(c[0], c[BN], c[2 * BN], c[3 * BN]);
-                    }
-                }
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-#pragma unroll
-                    for (int i = 0; i < I; ++i)
-#pragma unroll
-                        for (int j = 0; j < J; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4get(af[i], q), f4get(bf[j], q),
-                                                                             acc[i][j], 0, 0, 0);
             }
         };
         using S0 = std::integral_constant<int, 0>;
@@ -470,7 +492,7 @@ __global__ void wgrad_reduce_kernel(WgradBatch batch, int64_t total) {
     else if (P.grad_b) P.grad_b[m] = s;
 }
 
-template <class CF, int E>
+template <class CF, int E, bool BF>
 int launch_one(GemmBatch& b, hipStream_t s) {
     int tiles = 0;
     for (int i = 0; i < b.count; ++i) {
@@ -483,23 +505,27 @@ int launch_one(GemmBatch& b, hipStream_t s) {
     }
     b.total_tiles = tiles;
     if (tiles == 0) return TTAMM_OK;
-    hipLaunchKernelGGL((gemm_kernel<CF, E>), dim3(tiles), dim3(kThreads), 0, s, b);
+    hipLaunchKernelGGL((gemm_kernel<CF, E, BF>), dim3(tiles), dim3(kThreads), 0, s, b);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }
 
-template <class CF>
-int dispatch_epi(GemmBatch& b, hipStream_t s) {
+template <class CF, bool BF>
+int dispatch_epi_t(GemmBatch& b, hipStream_t s) {
     switch (b.p[0].epi) {
-        case EPI_STORE: return launch_one<CF, EPI_STORE>(b, s);
-        case EPI_HIDDEN: return launch_one<CF, EPI_HIDDEN>(b, s);
-        case EPI_GATE_HIDDEN: return launch_one<CF, EPI_GATE_HIDDEN>(b, s);
-        case EPI_GATE_OUT: return launch_one<CF, EPI_GATE_OUT>(b, s);
-        case EPI_DGRAD_RELU: return launch_one<CF, EPI_DGRAD_RELU>(b, s);
-        case EPI_DGRAD_GATE_EF: return launch_one<CF, EPI_DGRAD_GATE_EF>(b, s);
-        case EPI_DGRAD_HIDDEN: return launch_one<CF, EPI_DGRAD_HIDDEN>(b, s);
+        case EPI_STORE: return launch_one<CF, EPI_STORE, BF>(b, s);
+        case EPI_HIDDEN: return launch_one<CF, EPI_HIDDEN, BF>(b, s);
+        case EPI_GATE_HIDDEN: return launch_one<CF, EPI_GATE_HIDDEN, BF>(b, s);
+        case EPI_GATE_OUT: return launch_one<CF, EPI_GATE_OUT, BF>(b, s);
+        case EPI_DGRAD_RELU: return launch_one<CF, EPI_DGRAD_RELU, BF>(b, s);
+        case EPI_DGRAD_GATE_EF: return launch_one<CF, EPI_DGRAD_GATE_EF, BF>(b, s);
+        case EPI_DGRAD_HIDDEN: return launch_one<CF, EPI_DGRAD_HIDDEN, BF>(b, s);
         default: return fail(TTAMM_E_INVALID, "gemm: unknown epilogue");
     }
+}
+template <class CF>
+int dispatch_epi(GemmBatch& b, hipStream_t s) {
+    return b.p[0].bf16 ? dispatch_epi_t<CF, true>(b, s) : dispatch_epi_t<CF, false>(b, s);
 }
 
 }  // namespace
@@ -511,7 +537,8 @@ int launch_gemm(GemmBatch& b, hipStream_t s) {
     for (int i = 0; i < b.count; ++i) {
         GemmProblem& p = b.p[i];
         TTAMM_REQUIRE(p.M >= 0 && p.N > 0 && p.K > 0, "gemm: bad shape");
-        TTAMM_REQUIRE(p.epi == b.p[0].epi && p.b_kn == bkn && !p.a_kmaj, "gemm: grouped problems must share a variant");
+        TTAMM_REQUIRE(p.epi == b.p[0].epi && p.b_kn == bkn && !p.a_kmaj && p.bf16 == b.p[0].bf16,
+                      "gemm: grouped problems must share a variant");
         TTAMM_REQUIRE(p.lda % 4 == 0 && p.ldb % 4 == 0 && ((uintptr_t)p.A | (uintptr_t)p.B) % 16 == 0,
                       "gemm: operands must be 16-byte aligned with leading dims % 4 == 0");
         TTAMM_REQUIRE(p.N % 4 == 0 && p.ldc % 4 == 0 && (uintptr_t)p.C % 16 == 0, "gemm: output must be float4-aligned");
@@ -534,8 +561,8 @@ int wgrad_slots(bool wide) {
     if (cached[wide]) return cached[wide];
     int dev = 0, cus = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* k = wide ? (const void*)gemm_kernel<Cfg<128, 192, 2, 2, true, true>, EPI_STORE>
-                         : (const void*)gemm_kernel<Cfg<128, 96, 4, 1, true, true>, EPI_STORE>;
+    const void* k = wide ? (const void*)gemm_kernel<Cfg<128, 192, 2, 2, true, true>, EPI_STORE, false>
+                         : (const void*)gemm_kernel<Cfg<128, 96, 4, 1, true, true>, EPI_STORE, false>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu < 1) per_cu = 1;
     cached[wide] = cus * per_cu;
     return cached[wide];
@@ -580,10 +607,14 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s) {
     GemmBatch wide, narrow;  // m_out > 96 / <= 96
     std::memset(&wide, 0, sizeof(wide));
     std::memset(&narrow, 0, sizeof(narrow));
+    const bool bf = wb.count > 0 && wb.p[0].bf16;
     auto flush = [&](GemmBatch& g, bool is_wide) -> int {
         if (g.count == 0) return TTAMM_OK;
-        const int rc = is_wide ? launch_one<Cfg<128, 192, 2, 2, true, true>, EPI_STORE>(g, s)
-                               : launch_one<Cfg<128, 96, 4, 1, true, true>, EPI_STORE>(g, s);
+        using Wide = Cfg<128, 192, 2, 2, true, true>;
+        using Narrow = Cfg<128, 96, 4, 1, true, true>;
+        const int rc = is_wide ? (bf ? launch_one<Wide, EPI_STORE, true>(g, s) : launch_one<Wide, EPI_STORE, false>(g, s))
+                               : (bf ? launch_one<Narrow, EPI_STORE, true>(g, s)
+                                     : launch_one<Narrow, EPI_STORE, false>(g, s));
         std::memset(&g, 0, sizeof(g));
         return rc;
     };
@@ -591,6 +622,7 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s) {
     for (int i = 0; i < wb.count; ++i) {
         WgradProblem& w = wb.p[i];
         TTAMM_REQUIRE(w.rows_per_split > 0 && w.rows_per_split % BK == 0, "wgrad: rows_per_split must be a multiple of 16");
+        TTAMM_REQUIRE(w.bf16 == wb.p[0].bf16, "wgrad: the batch must share one matmul precision");
         w.splits = w.R > 0 ? (int)ceil_div(w.R, w.rows_per_split) : 1;
         total += (int64_t)w.M * (w.N + 1);
         if (w.R <= 0) {  // no rows: the slab (one split) is zero
@@ -620,6 +652,7 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s) {
         p.slab_stride = (int64_t)(w.N + 1) * w.M;
         p.keep_prob = 1.f;
         p.inv_keep = 1.f;
+        p.bf16 = w.bf16;
         const bool is_wide = w.M > 96;
         GemmBatch& g = is_wide ? wide : narrow;
         if (g.count == kMaxGemmProblems) {

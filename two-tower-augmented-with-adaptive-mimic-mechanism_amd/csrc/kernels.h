@@ -64,6 +64,7 @@ struct GemmProblem {
     int64_t slab_stride;
     int tile_begin;     // filled by the launcher
     int tiles_m, tiles_n;
+    int bf16;           // 1: operands rounded to bf16 (RNE), fp32 accumulation (grouped problems agree)
 };
 
 constexpr int kMaxGemmProblems = 8;
@@ -91,6 +92,7 @@ struct WgradProblem {
     int rows_per_split;
     int tile_begin;
     int tiles_m, tiles_n;
+    int bf16;              // 1: operands rounded to bf16, fp32 accumulation (the batch agrees)
 };
 constexpr int kMaxWgradProblems = 16;
 struct WgradBatch {

@@ -330,6 +330,7 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
                 if (t.fusion == TTAMM_FUSION_IDENTITY || l >= t.n_linear) continue;
                 const ttamm_linear& L = t.linear[l];
                 GemmProblem p = gp_base();
+                p.bf16 = t.matmul_bf16;
                 if (l == 0) {
                     p.A = t.features;
                     p.a_idx = w.fidx;
@@ -395,6 +396,7 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
         if (t.fusion == TTAMM_FUSION_GATED) {
             const int Hg = t.gate[0].out_features;
             GemmProblem p = gp_base();
+            p.bf16 = t.matmul_bf16;
             p.A = w.ef;
             p.lda = 2 * D;
             p.B = t.gate[0].weight;
@@ -408,6 +410,7 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
             p.ldc = Hg;
             g1.add(p);
             GemmProblem q = gp_base();
+            q.bf16 = t.matmul_bf16;
             q.A = w.z;
             q.lda = Hg;
             q.B = t.gate[1].weight;
@@ -452,6 +455,7 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
         const int Hg = t.gate[0].out_features;
         if ((rc = launch_gate_dq(w.dT, w.dT_ld, w.ef, w.g, w.R, D, w.dq, s))) return rc;
         GemmProblem p = gp_base();  // dz = (dq . G2) * (z > 0)
+        p.bf16 = t.matmul_bf16;
         p.A = w.dq;
         p.lda = D;
         p.B = t.gate[1].weight;  // [D, Hg] = [K, N]
@@ -467,6 +471,7 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
         p.ld_aux0 = Hg;
         b1.add(p);
         GemmProblem q = gp_base();  // [de | df] = dz . G1 + gate-mix terms
+        q.bf16 = t.matmul_bf16;
         q.A = w.dz;
         q.lda = Hg;
         q.B = t.gate[0].weight;  // [Hg, 2D] = [K, N]
@@ -500,6 +505,7 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
             if (l < 1) continue;
             const ttamm_linear& L = t.linear[l];
             GemmProblem p = gp_base();
+            p.bf16 = t.matmul_bf16;
             if (l == t.n_linear - 1) {
                 p.A = t.fusion == TTAMM_FUSION_GATED ? w.dEF + D : w.dT;
                 p.lda = t.fusion == TTAMM_FUSION_GATED ? 2 * D : w.dT_ld;
@@ -534,6 +540,7 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
         if (t.fusion == TTAMM_FUSION_GATED) {
             const int Hg = t.gate[0].out_features;
             WgradProblem g2{};
+            g2.bf16 = t.matmul_bf16;
             g2.dY = w.dq;
             g2.ld_dy = D;
             g2.X = w.z;
@@ -547,6 +554,7 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
             g2.rows_per_split = w.wgrad_rps;
             wb.p[wb.count++] = g2;
             WgradProblem g1{};
+            g1.bf16 = t.matmul_bf16;
             g1.dY = w.dz;
             g1.ld_dy = Hg;
             g1.X = w.ef;
@@ -563,6 +571,7 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
         for (int l = t.n_linear - 1; l >= 0; --l) {
             const ttamm_linear& L = t.linear[l];
             WgradProblem p{};
+            p.bf16 = t.matmul_bf16;
             if (l == t.n_linear - 1) {
                 p.dY = t.fusion == TTAMM_FUSION_GATED ? w.dEF + D : w.dT;
                 p.ld_dy = t.fusion == TTAMM_FUSION_GATED ? 2 * D : w.dT_ld;
@@ -861,6 +870,7 @@ int validate_step(const ttamm_step_args& A) {
     int rc;
     if ((rc = validate_tower(A.user, "user_encoder", D, true))) return rc;
     if ((rc = validate_tower(A.item, "item_encoder", D, true))) return rc;
+    TTAMM_REQUIRE(A.user.matmul_bf16 == A.item.matmul_bf16, "user and item towers must share one matmul precision");
     TTAMM_REQUIRE(A.b.batch > 0, "empty batch");
     TTAMM_REQUIRE(A.b.num_neg > 0, "num_negatives must be greater than zero.");
     const int64_t num_items = A.num_items_global > 0 ? A.num_items_global : A.item.id.rows;

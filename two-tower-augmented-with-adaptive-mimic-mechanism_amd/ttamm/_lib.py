@@ -71,6 +71,7 @@ class Tower(ctypes.Structure):
         ("dropout", c_f),
         ("linear", Linear * MAX_LINEAR),
         ("gate", Linear * 2),
+        ("matmul_bf16", c_i32),
     ]
 
 
@@ -145,7 +146,7 @@ class StepArgs(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 6  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 7  # ttamm.h TTAMM_ABI_VERSION
 
 # ttamm.h TTAMM_PHASE_*
 PHASE_ALL = 0

@@ -167,9 +167,14 @@ class TowerEncoder(nn.Module):
         fusion: str,
         output_dim: int | None,
         adaptive_mimic: FeatureFusionGate | None,
+        matmul_dtype: str = "fp32",
     ) -> None:
         super().__init__()
         self.embedding = embedding
+        # ttamm extension (BASELINE config C5, "bf16 towers"): the precision of the
+        # feature-MLP / gate GEMMs — "fp32" (the reference) or "bf16" (operands rounded to
+        # bf16, fp32 accumulation; ttamm.h ttamm_tower.matmul_bf16)
+        self.matmul_dtype = _matmul_dtype(matmul_dtype)
         self.feature_encoder = feature_encoder
         self.adaptive_mimic = adaptive_mimic
         self.num_embeddings = embedding.num_embeddings
@@ -249,6 +254,7 @@ def build_tower_encoder(
         fusion=fusion,
         output_dim=cfg.get("output_dim"),
         adaptive_mimic=gate,
+        matmul_dtype=str(cfg.get("matmul_dtype", "fp32")),
     )
     return tower.to(device) if device is not None else tower
 
@@ -257,6 +263,15 @@ def build_tower_encoder(
 # Mapping of a TowerEncoder onto the libttamm tower descriptor
 # ---------------------------------------------------------------------------------------
 _FUSION_CODE = {"identity": _lib.FUSION_IDENTITY, "sum": _lib.FUSION_SUM, "gated": _lib.FUSION_GATED}
+
+
+def _matmul_dtype(name: str) -> str:
+    key = str(name).lower()
+    if key in ("fp32", "float32", "float"):
+        return "fp32"
+    if key in ("bf16", "bfloat16"):
+        return "bf16"
+    raise ValueError(f"Unsupported matmul_dtype: {name} (fp32 or bf16)")
 
 
 def feature_layers(tower: TowerEncoder) -> tuple[list[nn.Linear], float]:
@@ -331,6 +346,7 @@ def describe_tower(
             s.mimic.exp_avg = st["exp_avg"].data_ptr()
             s.mimic.exp_avg_sq = st["exp_avg_sq"].data_ptr()
     s.fusion = _FUSION_CODE[tower.fusion]
+    s.matmul_bf16 = 1 if getattr(tower, "matmul_dtype", "fp32") == "bf16" else 0
     linears, p = feature_layers(tower)
     if s.fusion != _lib.FUSION_IDENTITY:
         if features is None:

@@ -396,6 +396,7 @@ class _IdentityView(nn.Module):
         self.fusion = "identity"
         self.feature_encoder = None
         self.embedding = tower.embedding
+        self.matmul_dtype = tower.matmul_dtype
 
 
 def train_one_epoch(
