@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 7
+#define TTAMM_ABI_VERSION 8
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -139,6 +139,8 @@ typedef struct ttamm_hparams {
     int64_t sparse_step; /* SparseAdam per-tensor step after increment (>= 1)         */
     double lambda_mimic_user; /* loss_weights.mimic_user (training.py:722,800-801)    */
     double lambda_mimic_item; /* loss_weights.mimic_item (training.py:723,802-803)    */
+    double lambda_category_alignment; /* loss_weights.category_alignment (training.py:724,805-820);
+                                         used when ttamm_step_args.item_categories is set */
 } ttamm_hparams;
 
 /* One batch of the training loop (training.py:726-736). */
@@ -167,7 +169,7 @@ typedef struct ttamm_step_args {
     int32_t mimic_enabled;
     ttamm_hparams hp;
     ttamm_batch b;
-    float* loss_out;      /* [4]: total, bce, mimic_user, mimic_item of this step     */
+    float* loss_out;      /* [5]: total, bce, mimic_user, mimic_item, category_alignment */
     double* loss_accum;   /* [2]: += total*batch, += batch  (training.py:829-831)      */
     uint32_t* status;     /* device status word (TTAMM_STATUS_* bits), OR-ed          */
     void* workspace;
@@ -208,6 +210,12 @@ typedef struct ttamm_step_args {
      * tower reads depend only on the indices; with an aux stream they run there, overlapping
      * the feature-MLP GEMMs, and `stream` waits for them before the first table read. */
     void* aux_stream;
+    /* ---- category-alignment loss (training.py:530-579, :805-820; one-process step only) ----
+     * item_categories: [item.id.rows] int64 category id per item, each in [0, num_categories)
+     * (_build_item_category_tensor, training.py:582-610); NULL (or lambda 0) = no L_cal.       */
+    const int64_t* item_categories;
+    int64_t num_categories;
+    int64_t major_category;       /* major_category_id                                       */
 } ttamm_step_args;
 
 /* ---------------------------------------------------------------------------------- */

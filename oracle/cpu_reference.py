@@ -272,6 +272,46 @@ def build_optimizers(model: OracleModel, *, lr: float = 1e-3, weight_decay: floa
 
 
 # ---------------------------------------------------------------------------------------
+# category-alignment loss (training.py:530-579)
+# ---------------------------------------------------------------------------------------
+def compute_covariance(matrix: torch.Tensor) -> torch.Tensor:  # training.py:530-538
+    if matrix.shape[0] <= 1:
+        return torch.zeros((matrix.shape[1], matrix.shape[1]), device=matrix.device, dtype=matrix.dtype)
+    centered = matrix - matrix.mean(dim=0, keepdim=True)
+    return centered.T @ centered / (matrix.shape[0] - 1)
+
+
+def category_alignment_loss(item_indices: torch.Tensor, item_embeddings: torch.Tensor, *,
+                            category_tensor: torch.Tensor | None, major_category_id: int | None) -> torch.Tensor:
+    """training.py:541-579: sum over non-major categories with >= 2 rows in the batch of
+    ||cov_c - cov_major||_F^2, divided by the number compared (ascending category order)."""
+    if category_tensor is None or major_category_id is None or item_indices.numel() == 0:
+        return item_embeddings.new_zeros(())
+    batch_categories = category_tensor.index_select(0, item_indices)
+    unique_categories = batch_categories.unique()
+    if unique_categories.numel() <= 1:
+        return item_embeddings.new_zeros(())
+    major_mask = batch_categories == major_category_id
+    if major_mask.sum() < 2:
+        return item_embeddings.new_zeros(())
+    major_cov = compute_covariance(item_embeddings[major_mask])
+    loss = item_embeddings.new_zeros(())
+    compared = 0
+    for cat_id in unique_categories.tolist():
+        if cat_id == major_category_id:
+            continue
+        mask = batch_categories == cat_id
+        if mask.sum() < 2:
+            continue
+        diff = compute_covariance(item_embeddings[mask]) - major_cov
+        loss = loss + torch.sum(diff * diff)
+        compared += 1
+    if compared == 0:
+        return item_embeddings.new_zeros(())
+    return loss / compared
+
+
+# ---------------------------------------------------------------------------------------
 # one training step (training.py:726-831)
 # ---------------------------------------------------------------------------------------
 @dataclass
@@ -280,6 +320,7 @@ class StepResult:
     bce: float
     mimic_user: float
     mimic_item: float
+    category_alignment: float = 0.0
 
 
 def train_step(
@@ -294,6 +335,8 @@ def train_step(
     loss_weights: Mapping[str, float] | None = None,
     user_keep_masks: Sequence[torch.Tensor] | None = None,
     item_keep_masks: Sequence[torch.Tensor] | None = None,
+    item_category_tensor: torch.Tensor | None = None,
+    major_category_id: int | None = None,
 ) -> StepResult:
     """One iteration of _train_one_epoch's body.  item_keep_masks rows are ordered
     [positives; negatives] (the two item_encoder calls, training.py:750 and :776)."""
@@ -335,6 +378,13 @@ def train_step(
         total = total + lam_u * loss_u
     if loss_i is not None and lam_i > 0:
         total = total + lam_i * loss_i
+    lam_cal = float(lw.get("category_alignment", 0.0))
+    cal = None
+    if lam_cal > 0:  # :805-820
+        cal = category_alignment_loss(torch.cat([pos_items, neg_flat], dim=0),
+                                      torch.cat([p, n.reshape(-1, u.shape[-1])], dim=0),
+                                      category_tensor=item_category_tensor, major_category_id=major_category_id)
+        total = total + lam_cal * cal
     total.backward()  # :822
     for opt in optimizers:  # :826-827
         opt.step()
@@ -342,6 +392,7 @@ def train_step(
         float(total.item()), float(bce.item()),
         float(loss_u.item()) if loss_u is not None else 0.0,
         float(loss_i.item()) if loss_i is not None else 0.0,
+        float(cal.item()) if cal is not None else 0.0,
     )
 
 

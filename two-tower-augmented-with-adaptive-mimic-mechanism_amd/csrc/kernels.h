@@ -151,8 +151,8 @@ struct ScoreArgs {
 int score_blocks(int64_t B);
 int launch_score_loss(const ScoreArgs& a, hipStream_t s);
 int launch_loss_finalize(const float* partials, int blocks, int64_t B, int64_t Bg, int N, int D, float lambda_u,
-                         float lambda_i, int mimic, float* loss_out, double* loss_accum,
-                         hipStream_t s);
+                         float lambda_i, int mimic, const float* cal, float lambda_cal, float* loss_out,
+                         double* loss_accum, hipStream_t s);
 
 // ------------------------------------------------------------------------------------
 // Exact inner-product retrieval + top-k (retrieval.hip)
@@ -196,6 +196,44 @@ struct CoalesceWs {
 size_t coalesce_temp_bytes(int64_t n);
 // sort rows by index; unique rows + segment starts
 int launch_coalesce(const int64_t* idx, int64_t n, int64_t table_rows, CoalesceWs& ws, hipStream_t s);
+
+// ------------------------------------------------------------------------------------
+// Category-alignment loss + gradient (cal.hip; training.py:530-579, :805-820)
+// ------------------------------------------------------------------------------------
+struct CalArgs {
+    const float* x;             // augmented item rows [R, ld_x] = cat[positives; negatives]
+    int64_t ld_x;
+    const int64_t* idx;         // item id of row r
+    const int64_t* categories;  // [items] category id (training.py:582-610)
+    int64_t num_categories;
+    int64_t major;              // major_category_id
+    int64_t R;
+    int D;
+    float lambda;               // loss_weights.category_alignment
+    int64_t* catrow;            // [R]
+    CoalesceWs co;              // sort of the rows by category
+    int nseg_max;               // min(R, num_categories)
+    int32_t* pcount;            // [nseg_max] pieces per category segment
+    int32_t* pstart;            // [nseg_max] exclusive scan
+    void* scan_temp;
+    size_t scan_temp_bytes;
+    float* psum;                // [pieces, D]
+    float* mean;                // [nseg_max, D]
+    float* pslab;               // [pieces, D, D]
+    float* cov;                 // [nseg_max, D, D]
+    float* part;                // [nseg_max]
+    int32_t* flag;              // [nseg_max]
+    float* gmajor;              // [D, D]
+    float* out;                 // [2]: L_cal, compared
+    float* dT;                  // item rows' dT [R, ld_d] (+= lambda dX); null: loss only
+    float* dA;                  // positive rows' dA [dA_rows, ld_d] (+=), may be null
+    int64_t ld_d;
+    int64_t dA_rows;
+};
+int cal_max_pieces(int64_t R, int64_t nseg_max);
+size_t cal_scan_temp_bytes(int64_t nseg_max);
+int launch_category_alignment(const CalArgs& a, hipStream_t s);
+
 
 // Optimizer constants, derived on the host in double precision the way torch does and
 // rounded to fp32 once (adam.py:419-547 single-tensor path; _functional.py:24-84).

@@ -247,8 +247,8 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
 
 // Deterministic final reduction of the per-block partials; total loss as in training.py:798-803.
 __global__ void loss_finalize_kernel(const float* __restrict__ partials, int blocks, int64_t B, int64_t Bg, int N, int D,
-                                     float lu, float li, int mimic, float* __restrict__ loss_out,
-                                     double* __restrict__ loss_accum) {
+                                     float lu, float li, int mimic, const float* __restrict__ cal, float lcal,
+                                     float* __restrict__ loss_out, double* __restrict__ loss_accum) {
     __shared__ float red[3][256];
     float s[3] = {0.f, 0.f, 0.f};
     for (int i = threadIdx.x; i < blocks; i += blockDim.x)
@@ -268,10 +268,13 @@ __global__ void loss_finalize_kernel(const float* __restrict__ partials, int blo
         float total = bce;
         if (mimic && lu > 0.f) total = total + lu * mu;
         if (mimic && li > 0.f) total = total + li * mi;
+        const float lc = cal ? cal[0] : 0.f;  // category alignment (training.py:805-820)
+        if (cal && lcal > 0.f) total = total + lcal * lc;
         loss_out[0] = total;
         loss_out[1] = bce;
         loss_out[2] = mimic ? mu : 0.f;
         loss_out[3] = mimic ? mi : 0.f;
+        loss_out[4] = lc;
         if (loss_accum) {
             loss_accum[0] += (double)total * (double)Bg;
             loss_accum[1] += (double)B;
@@ -390,9 +393,9 @@ int launch_score_loss(const ScoreArgs& a, hipStream_t s) {
 int score_blocks(int64_t B) { return (int)ceil_div(B, kScoreWaves); }
 
 int launch_loss_finalize(const float* partials, int blocks, int64_t B, int64_t Bg, int N, int D, float lu, float li,
-                         int mimic, float* loss_out, double* loss_accum, hipStream_t s) {
+                         int mimic, const float* cal, float lcal, float* loss_out, double* loss_accum, hipStream_t s) {
     hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, partials, blocks, B, Bg, N, D, lu, li, mimic,
-                       loss_out, loss_accum);
+                       cal, lcal, loss_out, loss_accum);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

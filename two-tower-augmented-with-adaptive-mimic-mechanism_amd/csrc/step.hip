@@ -15,6 +15,7 @@
 // A row-sharded multi-GPU step runs the same pieces as phases (ttamm.h TTAMM_PHASE_*): the
 // item tower of a rank runs over the item rows it owns, for whoever requested them; the
 // host moves (t | a) and (dT | dA) rows between phases and all-reduces the gradient arena.
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -74,7 +75,15 @@ struct StepWs {
     TowerWs user, item;
     float* partials = nullptr;
     int score_blocks = 0;
+    bool cal_on = false;  // category-alignment loss this step
+    CalArgs cal{};
 };
+
+// The category-alignment loss runs when categories are given and its weight is positive
+// (training.py:805: `if lambda_cal > 0`; _category_alignment_loss returns 0 without them).
+bool cal_enabled(const ttamm_step_args& A) {
+    return A.item_categories != nullptr && A.hp.lambda_category_alignment > 0.0;
+}
 
 int tower_in_dim(const ttamm_tower& T, int l) { return l == 0 ? T.feat_dim : T.linear[l - 1].out_features; }
 inline int round4(int x) { return (x + 3) / 4 * 4; }
@@ -253,6 +262,38 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         tower(A.item, ws.item, B * (1 + N), true, false, B);
     ws.score_blocks = score_blocks(B);
     ws.partials = ar.take<float>((size_t)ws.score_blocks * 3);
+    if (cal_enabled(A) && !shard) {
+        CalArgs& c = ws.cal;
+        ws.cal_on = true;
+        const int64_t R = B * (1 + N);
+        c.R = R;
+        c.D = D;
+        c.nseg_max = (int)std::min<int64_t>(R, std::max<int64_t>(1, std::min<int64_t>(A.num_categories, 65535)));
+        const int pieces = cal_max_pieces(R, c.nseg_max);
+        c.catrow = ar.take<int64_t>(R);
+        c.co.keys_in = ar.take<int32_t>(R);
+        c.co.vals_in = ar.take<int32_t>(R);
+        c.co.keys_out = ar.take<int32_t>(R);
+        c.co.vals_out = ar.take<int32_t>(R);
+        c.co.flags = ar.take<int32_t>(R);
+        c.co.uid = ar.take<int32_t>(R);
+        c.co.seg_start = ar.take<int32_t>(R + 1);
+        c.co.n_unique = ar.take<int32_t>(1);
+        c.co.temp_bytes = coalesce_temp_bytes(R);
+        c.co.temp = ar.take<char>(c.co.temp_bytes);
+        c.pcount = ar.take<int32_t>(c.nseg_max);
+        c.pstart = ar.take<int32_t>(c.nseg_max);
+        c.scan_temp_bytes = cal_scan_temp_bytes(c.nseg_max);
+        c.scan_temp = ar.take<char>(c.scan_temp_bytes);
+        c.psum = ar.take<float>((size_t)pieces * D);
+        c.mean = ar.take<float>((size_t)c.nseg_max * D);
+        c.pslab = ar.take<float>((size_t)pieces * D * D);
+        c.cov = ar.take<float>((size_t)c.nseg_max * D * D);
+        c.part = ar.take<float>(c.nseg_max);
+        c.flag = ar.take<int32_t>(c.nseg_max);
+        c.gmajor = ar.take<float>((size_t)D * D);
+        c.out = ar.take<float>(2);
+    }
     // gradient arena: the caller's all-reduce buffer when sharded, else workspace
     float* arena = shard ? A.dense_grads : ar.take<float>(tower_grad_floats(A.user) + tower_grad_floats(A.item));
     carve_grads(A.user, ws.user, arena);
@@ -872,6 +913,14 @@ int validate_step(const ttamm_step_args& A) {
     if ((rc = validate_tower(A.item, "item_encoder", D, true))) return rc;
     TTAMM_REQUIRE(A.user.matmul_bf16 == A.item.matmul_bf16, "user and item towers must share one matmul precision");
     TTAMM_REQUIRE(A.b.batch > 0, "empty batch");
+    if (cal_enabled(A)) {
+        TTAMM_REQUIRE(!sharded(A), "the category-alignment loss is not implemented in the row-sharded step");
+        TTAMM_REQUIRE(A.num_categories > 0 && A.num_categories <= 65535,
+                      "category alignment: num_categories must be in [1, 65535]");
+        TTAMM_REQUIRE(A.major_category >= 0 && A.major_category < A.num_categories,
+                      "category alignment: major_category out of range");
+        TTAMM_REQUIRE(A.user.id.dim <= 256, "category alignment: embedding dim must be <= 256");
+    }
     TTAMM_REQUIRE(A.b.num_neg > 0, "num_negatives must be greater than zero.");
     const int64_t num_items = A.num_items_global > 0 ? A.num_items_global : A.item.id.rows;
     TTAMM_REQUIRE(num_items > 1, "num_items must be greater than one.");
@@ -1029,8 +1078,24 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         sa.partials = ws.partials;
         sa.blocks = ws.score_blocks;
         if ((rc = launch_score_loss(sa, s))) return rc;
+        if (ws.cal_on) {  // + lambda * L_cal over cat[positives; negatives] (training.py:805-820)
+            CalArgs& c = ws.cal;
+            c.x = I.aug;
+            c.ld_x = D;
+            c.idx = I.idx;
+            c.categories = A.item_categories;
+            c.num_categories = A.num_categories;
+            c.major = A.major_category;
+            c.lambda = (float)A.hp.lambda_category_alignment;
+            c.dT = I.dT_own;
+            c.dA = mimic ? I.dA_own : nullptr;
+            c.ld_d = D;
+            c.dA_rows = B;
+            if ((rc = launch_category_alignment(c, s))) return rc;
+        }
         if (A.loss_out) {
             if ((rc = launch_loss_finalize(ws.partials, ws.score_blocks, B, Bg, N, D, sa.lambda_u, sa.lambda_i, sa.mimic,
+                                           ws.cal_on ? ws.cal.out : nullptr, (float)A.hp.lambda_category_alignment,
                                            A.loss_out, A.loss_accum, s)))
                 return rc;
         }

@@ -91,6 +91,7 @@ class HParams(ctypes.Structure):
         ("sparse_step", c_i64),
         ("lambda_mimic_user", c_d),
         ("lambda_mimic_item", c_d),
+        ("lambda_category_alignment", c_d),
     ]
 
 
@@ -143,10 +144,13 @@ class StepArgs(ctypes.Structure):
         ("history_capacity", c_i32),
         ("replay_slices", c_i32),
         ("aux_stream", c_vp),
+        ("item_categories", c_vp),
+        ("num_categories", c_i64),
+        ("major_category", c_i64),
     ]
 
 
-ABI_VERSION = 7  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 8  # ttamm.h TTAMM_ABI_VERSION
 
 # ttamm.h TTAMM_PHASE_*
 PHASE_ALL = 0

@@ -123,6 +123,8 @@ class FusedTrainStep:
         deferred_adamw: bool = True,
         replay_slices: int = 64,
         overlap: bool = True,
+        item_category_tensor: torch.Tensor | None = None,
+        major_category_id: int | None = None,
     ) -> None:
         if negatives_per_positive <= 0:
             raise ValueError("num_negatives must be greater than zero.")
@@ -228,6 +230,24 @@ class FusedTrainStep:
         lw = dict(loss_weights or {})
         args.hp.lambda_mimic_user = float(lw.get("mimic_user", 0.0))
         args.hp.lambda_mimic_item = float(lw.get("mimic_item", 0.0))
+        # category-alignment loss (training.py:530-579, :805-820): the reference returns 0
+        # without a category tensor / major id, so the fused step runs it only with both
+        args.hp.lambda_category_alignment = float(lw.get("category_alignment", 0.0))
+        self.item_categories = None
+        if item_category_tensor is not None and major_category_id is not None and \
+                args.hp.lambda_category_alignment > 0:
+            cats = item_category_tensor.to(self.device, torch.long).contiguous()
+            if cats.numel() != ie.num_embeddings:
+                raise ValueError("ttamm: item_category_tensor must hold one category per item")
+            ncat = int(cats.max().item()) + 1 if cats.numel() else 0
+            if int(cats.min().item()) < 0 or not 0 <= int(major_category_id) < ncat:
+                raise ValueError("ttamm: category ids must be >= 0 and major_category_id must occur")
+            if ncat > 65535:
+                raise NotImplementedError("ttamm: at most 65535 item categories")
+            self.item_categories = cats
+            args.item_categories = cats.data_ptr()
+            args.num_categories = ncat
+            args.major_category = int(major_category_id)
         args.b.num_neg = self.num_neg
         self.csr = None
         if positives is not None:
@@ -237,7 +257,7 @@ class FusedTrainStep:
             args.b.pos_offsets = self.csr.offsets.data_ptr()
             args.b.pos_values = self.csr.values.data_ptr()
         args.b.seed = draw_seed() if seed is None else int(seed)
-        self.loss_out = torch.zeros(4, dtype=torch.float32, device=self.device)
+        self.loss_out = torch.zeros(5, dtype=torch.float32, device=self.device)
         self.loss_accum = torch.zeros(2, dtype=torch.float64, device=self.device)
         self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
         args.loss_out = self.loss_out.data_ptr()
@@ -384,7 +404,7 @@ class FusedTrainStep:
 
     def last_losses(self) -> dict[str, float]:
         v = self.loss_out.tolist()
-        return {"total": v[0], "bce": v[1], "mimic_user": v[2], "mimic_item": v[3]}
+        return {"total": v[0], "bce": v[1], "mimic_user": v[2], "mimic_item": v[3], "category_alignment": v[4]}
 
 
 class _IdentityView(nn.Module):
@@ -424,8 +444,6 @@ def train_one_epoch(
     if gradient_clip_norm is not None and gradient_clip_norm > 0:
         raise NotImplementedError("ttamm: gradient clipping is not implemented in the fused step")
     lw = dict(loss_weights or {})
-    if float(lw.get("category_alignment", 0.0)) > 0 and item_category_tensor is not None and major_category_id is not None:
-        raise NotImplementedError("ttamm: the category-alignment loss (training.py:530-579) is not implemented yet")
     if num_items != model.item_encoder.num_embeddings:
         raise ValueError("num_items does not match the item embedding table")
     device = torch.device(device)
@@ -440,6 +458,7 @@ def train_one_epoch(
                 model, optimizers, negatives_per_positive=negatives_per_positive, positives=user_positive_items,
                 user_features=user_features, item_features=item_features, loss_weights=lw,
                 max_batch=max(int(size), users.numel()),
+                item_category_tensor=item_category_tensor, major_category_id=major_category_id,
             )
         engine.step(users, pos)  # stream-ordered: the caching allocator recycles inputs safely
     if engine is None:
