@@ -76,6 +76,20 @@ __device__ __forceinline__ void store_nt(float4* p, float4 v) {
 }
 __device__ __forceinline__ void store_nt(float* p, float4 v) { store_nt(reinterpret_cast<float4*>(p), v); }
 
+// x / c correctly rounded (== IEEE x / c, bit for bit) for a per-step constant c > 0 with
+// inv_c = RN(1/c), when x is +0 or a normal number and x / c stays normal: two Markstein
+// refinements of x * inv_c — the first makes the quotient faithful, so the second residual
+// fma(-c, q, x) is exact and q + r * inv_c rounds to the correctly rounded quotient.  Used
+// for sqrt(v) / sqrt(bc2): sqrt of any fp32 v >= 0 is 0 or >= 2^-75, bc2_sqrt is in (0, 1].
+// 5 VALU ops instead of the ~11 of the general IEEE division sequence.
+__device__ __forceinline__ float div_by_const(float x, float c, float inv_c) {
+    float q = x * inv_c;
+    float r = fmaf(-c, q, x);
+    q = fmaf(r, inv_c, q);
+    r = fmaf(-c, q, x);
+    return fmaf(r, inv_c, q);
+}
+
 // Philox4x32-10 counter-based RNG (Salmon et al., SC'11).
 struct u32x4 {
     uint32_t x, y, z, w;

@@ -245,6 +245,7 @@ struct AdamConsts {
     float eps;
     float neg_step;  // -lr / bias_correction1
     float bc2_sqrt;  // sqrt(bias_correction2)
+    float inv_bc2_sqrt;  // RN(1 / bc2_sqrt): the correctly rounded reciprocal (div_by_const)
     float wd;        // weight_decay (Adam L2 form)
     int decoupled;
 };
@@ -352,6 +353,7 @@ int launch_dense_adam(const DenseAdamArgs& a, hipStream_t s);
 int launch_sparse_adam_rows(float* w, float* m, float* v, int dim, const int64_t* rows,
                             const float* grad, int64_t n, SparseConsts sp, hipStream_t s);
 
+float correctly_rounded_reciprocal(float c);  // RN(1/c), c > 0 normal
 AdamConsts make_adam_consts(double lr, double beta1, double beta2, double eps, double wd,
                             int decoupled, int64_t step);
 SparseConsts make_sparse_consts(double lr, double beta1, double beta2, double eps, int64_t step);

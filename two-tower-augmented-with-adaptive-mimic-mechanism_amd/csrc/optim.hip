@@ -14,6 +14,8 @@
 // The result equals one dense AdamW step over the full dense gradient.
 #include <hipcub/hipcub.hpp>
 
+#include <cmath>
+
 #include "kernels.h"
 
 #pragma clang fp contract(off)
@@ -25,17 +27,24 @@ namespace {
 // torch single-tensor Adam/AdamW (adam.py:419-547):
 //   p *= 1 - lr*wd ; m.lerp_(g, 1-b1) ; v = v*b2 + (1-b2)*g*g ;
 //   p += -step * m / (sqrt(v)/sqrt(bc2) + eps)
-template <bool DECOUPLED>
+// G0: the gradient is the literal 0 (an untouched dense-table row): lerp(m, 0, w) =
+// m + w*(0 - m) == fma(w, -m, m) and v*b2 + (1-b2)*0*0 == v*b2 (v >= +0), bit for bit.
+template <bool DECOUPLED, bool G0 = false>
 __device__ __forceinline__ void adam_elem_t(float& p, float& m, float& v, float g, const AdamConsts& c) {
     if (DECOUPLED) {
         p = p * c.decay;
     } else if (c.wd != 0.f) {
         g = g + p * c.wd;
     }
-    m = fmaf(c.w1, g - m, m);  // ATen lerp (|w| < 0.5): self + w * (end - self), vectorised as fmadd
-    v = v * c.b2;
-    v = v + c.w2 * g * g;
-    const float denom = sqrtf(v) / c.bc2_sqrt + c.eps;
+    if (G0 && DECOUPLED) {
+        m = fmaf(c.w1, -m, m);
+        v = v * c.b2;
+    } else {
+        m = fmaf(c.w1, g - m, m);  // ATen lerp (|w| < 0.5): self + w * (end - self), vectorised as fmadd
+        v = v * c.b2;
+        v = v + c.w2 * g * g;
+    }
+    const float denom = div_by_const(sqrtf(v), c.bc2_sqrt, c.inv_bc2_sqrt) + c.eps;
     p = p + c.neg_step * (m / denom);
 }
 
@@ -44,6 +53,12 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
         adam_elem_t<true>(p, m, v, g, c);
     else
         adam_elem_t<false>(p, m, v, g, c);
+}
+__device__ __forceinline__ void adam_elem_g0(float& p, float& m, float& v, const AdamConsts& c) {
+    if (c.decoupled)
+        adam_elem_t<true, true>(p, m, v, 0.f, c);
+    else
+        adam_elem_t<false, true>(p, m, v, 0.f, c);
 }
 
 // torch SparseAdam on one coalesced element (_functional.py:61-84).
@@ -213,10 +228,10 @@ __global__ __launch_bounds__(256) void dense_sweep_kernel(SweepArgs A) {
         const int64_t stride = (int64_t)gridDim.x * blockDim.x;
         for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
             float4 p = P[i], m = Mm[i], v = V[i];
-            adam_elem(p.x, m.x, v.x, 0.f, A.ad);
-            adam_elem(p.y, m.y, v.y, 0.f, A.ad);
-            adam_elem(p.z, m.z, v.z, 0.f, A.ad);
-            adam_elem(p.w, m.w, v.w, 0.f, A.ad);
+            adam_elem_g0(p.x, m.x, v.x, A.ad);
+            adam_elem_g0(p.y, m.y, v.y, A.ad);
+            adam_elem_g0(p.z, m.z, v.z, A.ad);
+            adam_elem_g0(p.w, m.w, v.w, A.ad);
             P[i] = p;
             Mm[i] = m;
             V[i] = v;
@@ -224,7 +239,7 @@ __global__ __launch_bounds__(256) void dense_sweep_kernel(SweepArgs A) {
         // scalar tail
         for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < S.n; i += stride) {
             float p = S.p[i], m = S.m[i], v = S.v[i];
-            adam_elem(p, m, v, 0.f, A.ad);
+            adam_elem_g0(p, m, v, A.ad);
             S.p[i] = p;
             S.m[i] = m;
             S.v[i] = v;
@@ -269,10 +284,10 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
         int j = (int)((l + 1) % cap);
         for (int32_t t = l + 1; t <= target; ++t) {
             const AdamConsts c = H[j];
-            adam_elem_t<DECOUPLED>(p.x, m.x, v.x, 0.f, c);
-            adam_elem_t<DECOUPLED>(p.y, m.y, v.y, 0.f, c);
-            adam_elem_t<DECOUPLED>(p.z, m.z, v.z, 0.f, c);
-            adam_elem_t<DECOUPLED>(p.w, m.w, v.w, 0.f, c);
+            adam_elem_t<DECOUPLED, true>(p.x, m.x, v.x, 0.f, c);
+            adam_elem_t<DECOUPLED, true>(p.y, m.y, v.y, 0.f, c);
+            adam_elem_t<DECOUPLED, true>(p.z, m.z, v.z, 0.f, c);
+            adam_elem_t<DECOUPLED, true>(p.w, m.w, v.w, 0.f, c);
             j = j + 1 == cap ? 0 : j + 1;
         }
         *reinterpret_cast<float4*>(S.p + o) = p;
@@ -358,6 +373,23 @@ inline int end_bit_for(int64_t rows) {
 
 }  // namespace
 
+// RN(1/c) for a positive normal fp32 c: the double quotient rounded to fp32 may be off by one
+// ulp (double rounding), so pick among it and its neighbours the one with the smallest
+// |1 - y*c|, evaluated exactly in double (24-bit x 24-bit products fit in 53 bits).
+float correctly_rounded_reciprocal(float c) {
+    const float y0 = (float)(1.0 / (double)c);
+    float best = y0;
+    double err = std::fabs(1.0 - (double)y0 * (double)c);
+    for (float y : {std::nextafter(y0, 0.f), std::nextafter(y0, INFINITY)}) {
+        const double e = std::fabs(1.0 - (double)y * (double)c);
+        if (e < err) {
+            err = e;
+            best = y;
+        }
+    }
+    return best;
+}
+
 AdamConsts make_adam_consts(double lr, double beta1, double beta2, double eps, double wd, int decoupled,
                             int64_t step) {
     AdamConsts c;
@@ -370,6 +402,7 @@ AdamConsts make_adam_consts(double lr, double beta1, double beta2, double eps, d
     c.eps = (float)eps;
     c.neg_step = (float)(-(lr / bc1));
     c.bc2_sqrt = (float)std::pow(bc2, 0.5);
+    c.inv_bc2_sqrt = correctly_rounded_reciprocal(c.bc2_sqrt);
     c.wd = (float)wd;
     c.decoupled = decoupled;
     return c;

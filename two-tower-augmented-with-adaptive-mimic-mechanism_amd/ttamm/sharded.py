@@ -257,7 +257,7 @@ class ShardedTrainStep(FusedTrainStep):
         args.num_items_global = self.num_items
         n_grad = int(self.lib.ttamm_dense_grad_floats(ctypes.byref(args)))
         # gradient arena + this rank's loss share: one all-reduce carries both
-        self.arena = torch.zeros(n_grad + 4, dtype=torch.float32, device=self.device)
+        self.arena = torch.zeros(n_grad + 5, dtype=torch.float32, device=self.device)  # + loss_out[5]
         self.n_grad = n_grad
         self.loss_out = self.arena[n_grad:]
         args.loss_out = self.loss_out.data_ptr()
