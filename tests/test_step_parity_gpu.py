@@ -113,3 +113,35 @@ def test_bf16_step_gradients_match_bf16_oracle(shape):
     far = max(rel_err(g32[n], og[n]) for n in og)
     near = max(rel_err(tg[n], og[n]) for n in og)
     assert far > 5e-4 and far > 4 * near, (far, near)
+
+
+# Fused gate kernel (csrc/gate.hip: fp32 towers with D == Hg in {32, 64, 96}) and the generic
+# two-GEMM gate path (TTAMM_GENERIC_GATE=1), both against the oracle at the fp32 tolerance.
+# Row counts are not multiples of the kernel's 16-row slabs (user rows = B, item rows = B(1+N)).
+GATE_SHAPES = [
+    Shape(U=64, I=256, F=40, H=48, D=32, B=45, N=5, hidden_dims=(48,)),
+    Shape(U=64, I=512, F=70, H=64, D=64, B=40, N=4, hidden_dims=(64,)),
+    Shape(U=96, I=768, F=605, H=192, D=96, B=37, N=5, hidden_dims=(192,)),
+    Shape(U=64, I=256, F=40, H=48, D=32, B=32, N=5, hidden_dims=(48,), mimic=False),
+    Shape(U=64, I=256, F=40, H=48, D=32, B=32, N=5, hidden_dims=(48,), sparse=False),
+]
+
+
+@pytest.mark.parametrize("generic", [False, True], ids=["fused", "generic"])
+@pytest.mark.parametrize("shape", GATE_SHAPES, ids=["d32", "d64", "d96-c2dims", "d32-nomimic", "d32-dense-id"])
+def test_gate_paths_match_oracle(shape, generic, monkeypatch):
+    from gpu_helpers import run_ttamm
+
+    if generic:
+        monkeypatch.setenv("TTAMM_GENERIC_GATE", "1")
+    else:
+        monkeypatch.delenv("TTAMM_GENERIC_GATE", raising=False)
+    prob = make_problem(shape, steps=1)
+    om, oo, ores = run_oracle(prob, lr=0.0, betas=(0.0, 0.999))
+    tm, to, tres = run_ttamm(prob, lr=0.0, betas=(0.0, 0.999))
+    assert abs(tres[0]["total"] - ores[0].total) <= GRAD_TOL * abs(ores[0].total)
+    og, tg = _grads_by_name(om, oo), _grads_by_name(tm, to)
+    assert set(og) == set(tg)
+    for name in og:
+        err = rel_err(tg[name], og[name])
+        assert err <= GRAD_TOL, f"{name}: rel err {err:.3e}"

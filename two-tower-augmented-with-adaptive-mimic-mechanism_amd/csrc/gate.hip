@@ -1,0 +1,338 @@
+// Fused FeatureFusionGate forward and backward for fp32 towers (encoders.py:149-168, applied
+// at :246-253; the adaptive-mimic augment of adaptive_mimic.py:88-95 rides in the forward
+// epilogue).  Per row, with ef = [e | f] (ID row | feature-MLP output):
+//
+//   forward   z = relu(ef G1^T + c1)            [Hg]
+//             g = sigmoid(z G2^T + c2)          [D]
+//             t = g e + (1 - g) f ; a = A[idx] ; aug = t + a
+//   backward  dq  = (dT e - dT f) (1 - g) g     (SigmoidBackward of the mix, as gate_dq_kernel)
+//             dz  = (dq G2) * (z > 0)
+//             dEF = dz G1 + [dT g | dT (1 - g)]
+//
+// The generic path runs these as two GEMM launches (forward) / an elementwise kernel and two
+// GEMM launches (backward) that round-trip z, dq and dz through HBM and re-read ef; here each
+// wave owns 16 rows and chains the two GEMMs in registers.  The gate matrices are small
+// (Hg x 2D, D x Hg), so one persistent block per CU stages them in LDS once and its 8 waves
+// stream 16-row slabs (the next slab's rows prefetched during the current one).
+//
+// MFMA orientation: v_mfma_f32_16x16x4_f32 computes OUT^T = W . X^T (the weights as the A
+// operand, the slab's 16 rows as the columns).  Lane l (li = l & 15, q = l >> 4) then holds
+// OUT[row li][feature 16*ob + 4q + r] in register r of output tile ob — four consecutive
+// features of one row, one float4 in memory — and that is exactly the B fragment of the next
+// GEMM when its k-steps are permuted so that step (t, r) covers k = 16t + 4q + r (lane group q
+// supplies k-slot q).  The A fragment of that step is W[16*ob + li][16t + 4q + r]: four
+// consecutive floats of an LDS row, one ds_read_b128 per four MFMAs.  All four r-steps of a
+// k-tile are issued across the output tiles, so consecutive MFMAs never share an accumulator.
+#include "kernels.h"
+
+namespace ttamm {
+
+namespace {
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+// 512 threads: 2 waves per SIMD with up to 256 VGPRs each — a wave keeps its slab's rows, the
+// next slab's prefetched rows and the MFMA operands of both chained GEMMs in registers
+constexpr int kGateWaves = 8;
+constexpr int kGateThreads = 64 * kGateWaves;
+
+__device__ __forceinline__ f4v ldg4(const float* p) { return *reinterpret_cast<const f4v*>(p); }
+__device__ __forceinline__ f4v lds4(const float* p) { return *reinterpret_cast<const f4v*>(p); }
+__device__ __forceinline__ void stg4(float* p, f4v v) { store_nt(p, make_float4(v[0], v[1], v[2], v[3])); }
+__device__ __forceinline__ float sigmoid_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+// acc[ob] += W[16 (ob0 + ob) + li][16 t + 4 q + r] * b[t][r] over k-tiles t < NK
+template <int NO, int NK, int LD>
+__device__ __forceinline__ void tile_gemm(const float* w_lds, int ob0, const f4v (&b)[NK], f4v (&acc)[NO], int li,
+                                          int q) {
+#pragma unroll
+    for (int t = 0; t < NK; ++t) {
+        f4v w[NO];
+#pragma unroll
+        for (int ob = 0; ob < NO; ++ob) w[ob] = lds4(w_lds + (16 * (ob0 + ob) + li) * LD + 16 * t + 4 * q);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int ob = 0; ob < NO; ++ob)
+                acc[ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[ob][r], b[t][r], acc[ob], 0, 0, 0);
+        // keep the scheduler from hoisting every k-tile's LDS reads to the top (register spills)
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void zero(f4v (&a)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) a[i] = f4v{0.f, 0.f, 0.f, 0.f};
+}
+
+// lane (li, q)'s part of row `row` of a [*, ld] matrix: columns 16 t + 4 q .. + 3, t < N
+template <int N>
+__device__ __forceinline__ void load_row(f4v (&v)[N], const float* base, int64_t ld, int64_t row, int q) {
+    const float* p = base + row * ld + 4 * q;
+#pragma unroll
+    for (int t = 0; t < N; ++t) v[t] = ldg4(p + 16 * t);
+}
+
+template <int D, int HG>
+struct GateCfg {
+    static constexpr int TD = D / 16, TH = HG / 16, TE = 2 * D / 16;  // 16-feature tiles
+    // forward LDS: G1 [HG][2D] and G2 [D][HG] as stored, rows padded by 4 floats, then c1, c2
+    static constexpr int F_LD1 = 2 * D + 4, F_LD2 = HG + 4;
+    static constexpr int F_LDS = HG * F_LD1 + D * F_LD2 + HG + D;
+    // backward LDS: G2^T [HG][D] and G1^T [2D][HG]
+    static constexpr int B_LD1 = D + 4, B_LD2 = HG + 4;
+    static constexpr int B_LDS = HG * B_LD1 + 2 * D * B_LD2;
+    static_assert(D % 16 == 0 && HG % 16 == 0, "16-feature tiles");
+    static_assert(F_LDS * 4 <= 163840 && B_LDS * 4 <= 163840, "the gate matrices must fit one CU's LDS");
+};
+
+// this block's tower and its index among the tower's blocks
+__device__ __forceinline__ int gate_tower(const KArg(GateArgs) * ka, int& bidx) {
+    bidx = blockIdx.x;
+    if (ka->count > 1 && bidx >= ka->tw[0].blocks) {
+        bidx -= ka->tw[0].blocks;
+        return 1;
+    }
+    return 0;
+}
+
+template <int D, int HG>
+__global__ __launch_bounds__(kGateThreads) void gate_fwd_kernel(GateArgs) {
+    using C = GateCfg<D, HG>;
+    __shared__ __attribute__((aligned(16))) float lds[C::F_LDS];
+    const KArg(GateArgs)* ka = (const KArg(GateArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
+    int bidx;
+    const KArg(GateTower)& T = ka->tw[gate_tower(ka, bidx)];
+    float* g1s = lds;
+    float* g2s = g1s + HG * C::F_LD1;
+    float* c1s = g2s + D * C::F_LD2;
+    float* c2s = c1s + HG;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int li = lane & 15, q = lane >> 4;
+    const int64_t R = T.R;
+    const int64_t nslab = (R + 15) / 16;
+    const int64_t stride = (int64_t)T.blocks * kGateWaves;
+    int64_t s = (int64_t)bidx * kGateWaves + wave;
+    // the first slab's rows are in flight while the block stages the gate matrices
+    f4v ef[C::TE];
+    int64_t arow = 0;  // the slab row's mimic-table row
+    if (s < nslab) {
+        const int64_t r0 = s * 16 + li < R ? s * 16 + li : R - 1;
+        load_row(ef, T.ef, 2 * D, r0, q);
+        if (T.table) arow = T.idx[r0];
+    }
+    constexpr int N1 = HG * (2 * D / 4), N2 = D * (HG / 4);
+#pragma unroll
+    for (int e0 = 0; e0 < N1; e0 += kGateThreads) {
+        const int e = e0 + (int)threadIdx.x;
+        if (e < N1) {
+            const int i = e / (2 * D / 4), c = 4 * (e % (2 * D / 4));
+            *reinterpret_cast<f4v*>(g1s + i * C::F_LD1 + c) = ldg4(T.G1 + (int64_t)i * 2 * D + c);
+        }
+    }
+#pragma unroll
+    for (int e0 = 0; e0 < N2; e0 += kGateThreads) {
+        const int e = e0 + (int)threadIdx.x;
+        if (e < N2) {
+            const int i = e / (HG / 4), c = 4 * (e % (HG / 4));
+            *reinterpret_cast<f4v*>(g2s + i * C::F_LD2 + c) = ldg4(T.G2 + (int64_t)i * HG + c);
+        }
+    }
+    for (int e = threadIdx.x; e < HG + D; e += kGateThreads) c1s[e] = e < HG ? T.c1[e] : T.c2[e - HG];
+    __syncthreads();
+    for (; s < nslab; s += stride) {
+        const int64_t row = s * 16 + li;
+        const bool ok = row < R;
+        const int64_t rr = ok ? row : R - 1;
+        f4v a[C::TD];  // mimic rows for the epilogue, requested before the MFMA chain
+        if (T.table) load_row(a, T.table, D, arow, q);
+        f4v z[C::TH];
+        zero(z);
+        tile_gemm<C::TH, C::TE, C::F_LD1>(g1s, 0, ef, z, li, q);  // z^T = G1 . ef^T
+        // the next slab's rows, in flight during the rest of this one
+        f4v nx[C::TE];
+        int64_t arow_n = 0;
+        const int64_t sn = s + stride;
+        if (sn < nslab) {
+            const int64_t rn = sn * 16 + li < R ? sn * 16 + li : R - 1;
+            load_row(nx, T.ef, 2 * D, rn, q);
+            if (T.table) arow_n = T.idx[rn];
+        }
+#pragma unroll
+        for (int ob = 0; ob < C::TH; ++ob) {
+            const f4v c1 = lds4(c1s + 16 * ob + 4 * q);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float v = z[ob][r] + c1[r];
+                z[ob][r] = v > 0.f ? v : 0.f;
+            }
+            if (ok) stg4(T.z + row * HG + 16 * ob + 4 * q, z[ob]);
+        }
+        f4v x[C::TD];
+        zero(x);
+        tile_gemm<C::TD, C::TH, C::F_LD2>(g2s, 0, z, x, li, q);  // (pre-sigmoid)^T = G2 . z^T
+        if (ok) {
+#pragma unroll
+            for (int ob = 0; ob < C::TD; ++ob) {
+                const int col = 16 * ob + 4 * q;
+                const f4v c2 = lds4(c2s + col);
+                const f4v e = ef[ob], f = ef[C::TD + ob];  // this lane's columns of e and f
+                f4v g, tt;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    g[r] = sigmoid_(x[ob][r] + c2[r]);
+                    tt[r] = g[r] * e[r] + (1.0f - g[r]) * f[r];
+                }
+                stg4(T.g + row * D + col, g);
+                stg4(T.t + row * T.ld_t + col, tt);
+                f4v aug = tt;
+                if (T.table) {
+                    stg4(T.a + row * T.ld_t + col, a[ob]);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) aug[r] = tt[r] + a[ob][r];
+                }
+                if (T.aug) stg4(T.aug + row * D + col, aug);
+            }
+        }
+        if (sn < nslab) {
+#pragma unroll
+            for (int t = 0; t < C::TE; ++t) ef[t] = nx[t];
+            arow = arow_n;
+        }
+    }
+}
+
+template <int D, int HG>
+__global__ __launch_bounds__(kGateThreads) void gate_bwd_kernel(GateArgs) {
+    using C = GateCfg<D, HG>;
+    __shared__ __attribute__((aligned(16))) float lds[C::B_LDS];
+    const KArg(GateArgs)* ka = (const KArg(GateArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
+    int bidx;
+    const KArg(GateTower)& T = ka->tw[gate_tower(ka, bidx)];
+    float* g2t = lds;                  // G2^T [HG][D]
+    float* g1t = lds + HG * C::B_LD1;  // G1^T [2D][HG]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int li = lane & 15, q = lane >> 4;
+    const int64_t R = T.R;
+    const int64_t nslab = (R + 15) / 16;
+    const int64_t stride = (int64_t)T.blocks * kGateWaves;
+    // transposed staging: float4 reads along a row, four scalar LDS writes down a column
+    constexpr int N2 = D * (HG / 4), N1 = HG * (2 * D / 4);
+#pragma unroll
+    for (int e0 = 0; e0 < N2; e0 += kGateThreads) {
+        const int e = e0 + (int)threadIdx.x;
+        if (e < N2) {
+            const int d = e / (HG / 4), j = 4 * (e % (HG / 4));  // G2 [D][HG]
+            const f4v v = ldg4(T.G2 + (int64_t)d * HG + j);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) g2t[(j + i) * C::B_LD1 + d] = v[i];
+        }
+    }
+#pragma unroll
+    for (int e0 = 0; e0 < N1; e0 += kGateThreads) {
+        const int e = e0 + (int)threadIdx.x;
+        if (e < N1) {
+            const int j = e / (2 * D / 4), c = 4 * (e % (2 * D / 4));  // G1 [HG][2D]
+            const f4v v = ldg4(T.G1 + (int64_t)j * 2 * D + c);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) g1t[(c + i) * C::B_LD2 + j] = v[i];
+        }
+    }
+    __syncthreads();
+    for (int64_t s = (int64_t)bidx * kGateWaves + wave; s < nslab; s += stride) {
+        const int64_t row = s * 16 + li;
+        const bool ok = row < R;
+        const int64_t rr = ok ? row : R - 1;
+        // every operand of the slab requested at once
+        f4v d[C::TD], ef[C::TE], g[C::TD], zr[C::TH];
+        load_row(d, T.dT, T.ld_dT, rr, q);
+        load_row(ef, T.ef, 2 * D, rr, q);
+        load_row(g, T.g, D, rr, q);
+        load_row(zr, T.z, HG, rr, q);
+        f4v dz[C::TH];
+        {
+            f4v dq[C::TD];  // dq = (dT e - dT f) (1 - g) g
+#pragma unroll
+            for (int t = 0; t < C::TD; ++t) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float dg = d[t][r] * ef[t][r] - d[t][r] * ef[C::TD + t][r];
+                    dq[t][r] = dg * (1.0f - g[t][r]) * g[t][r];
+                }
+                if (ok) stg4(T.dq + row * D + 16 * t + 4 * q, dq[t]);
+            }
+            zero(dz);
+            tile_gemm<C::TH, C::TD, C::B_LD1>(g2t, 0, dq, dz, li, q);  // dz^T = G2^T . dq^T
+        }
+#pragma unroll
+        for (int ob = 0; ob < C::TH; ++ob) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dz[ob][r] = zr[ob][r] > 0.f ? dz[ob][r] : 0.f;
+            if (ok) stg4(T.dz + row * HG + 16 * ob + 4 * q, dz[ob]);
+        }
+        // dEF^T = G1^T . dz^T + [dT g | dT (1 - g)], in two halves (e part, f part)
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            f4v de[C::TD];
+            zero(de);
+            tile_gemm<C::TD, C::TH, C::B_LD2>(g1t, half * C::TD, dz, de, li, q);
+            if (ok) {
+#pragma unroll
+                for (int ob = 0; ob < C::TD; ++ob) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        de[ob][r] += half == 0 ? d[ob][r] * g[ob][r] : d[ob][r] * (1.0f - g[ob][r]);
+                    stg4(T.dEF + row * 2 * D + half * D + 16 * ob + 4 * q, de[ob]);
+                }
+            }
+        }
+    }
+}
+
+// persistent grid: about one block per CU, split between the towers by row count
+int gate_blocks(GateArgs& a) {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0, n = 0;
+        cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+            cus = n;
+    }
+    int64_t total = 0;
+    for (int i = 0; i < a.count; ++i) total += a.tw[i].R;
+    int sum = 0;
+    for (int i = 0; i < a.count; ++i) {
+        const int64_t need = ceil_div(ceil_div(a.tw[i].R, 16), kGateWaves);  // blocks with a slab per wave
+        int64_t share = (cus * a.tw[i].R + total - 1) / total;
+        if (share > need) share = need;
+        a.tw[i].blocks = (int)(share < 1 ? 1 : share);
+        sum += a.tw[i].blocks;
+    }
+    return sum;
+}
+
+template <int D, int HG>
+int launch_gate_t(GateArgs& a, bool backward, hipStream_t s) {
+    const int blocks = gate_blocks(a);
+    if (backward) hipLaunchKernelGGL((gate_bwd_kernel<D, HG>), dim3(blocks), dim3(kGateThreads), 0, s, a);
+    else hipLaunchKernelGGL((gate_fwd_kernel<D, HG>), dim3(blocks), dim3(kGateThreads), 0, s, a);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+}  // namespace
+
+bool gate_fused_supported(int D, int HG) { return D == HG && (D == 32 || D == 64 || D == 96); }
+
+int launch_gate(GateArgs& a, bool backward, hipStream_t s) {
+    TTAMM_REQUIRE(a.count >= 1 && a.count <= 2 && gate_fused_supported(a.D, a.HG), "fused gate: unsupported shape");
+    for (int i = 0; i < a.count; ++i) TTAMM_REQUIRE(a.tw[i].R > 0, "fused gate: empty tower");
+    switch (a.D) {
+        case 32: return launch_gate_t<32, 32>(a, backward, s);
+        case 64: return launch_gate_t<64, 64>(a, backward, s);
+        default: return launch_gate_t<96, 96>(a, backward, s);
+    }
+}
+
+}  // namespace ttamm

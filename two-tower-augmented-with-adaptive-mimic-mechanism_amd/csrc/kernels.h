@@ -109,6 +109,39 @@ size_t wgrad_slab_floats(int R, int M, int N, int rows_per_split);
 int launch_wgrad(WgradBatch& batch, hipStream_t s);
 
 // ------------------------------------------------------------------------------------
+// Fused gate forward / backward (gate.hip): fp32 towers with D == Hg in {32, 64, 96}
+// ------------------------------------------------------------------------------------
+struct GateTower {
+    int64_t R;
+    const float* ef;     // [R, 2D] = [e | f]
+    const float* G1;     // gate_network.0.weight [Hg, 2D]
+    const float* c1;     // [Hg]
+    const float* G2;     // gate_network.2.weight [D, Hg]
+    const float* c2;     // [D]
+    float* z;            // [R, Hg]
+    float* g;            // [R, D]
+    float* t;            // [R, ld_t]
+    float* a;            // [R, ld_t] mimic rows (written when table)
+    int64_t ld_t;
+    const float* table;  // mimic table or null
+    const int64_t* idx;  // its rows
+    float* aug;          // [R, D] or null (sharded item owner)
+    const float* dT;     // backward: [R, ld_dT]
+    int64_t ld_dT;
+    float* dq;           // [R, D]
+    float* dz;           // [R, Hg]
+    float* dEF;          // [R, 2D]
+    int blocks;          // filled by the launcher
+};
+struct GateArgs {
+    GateTower tw[2];
+    int count;
+    int D, HG;
+};
+bool gate_fused_supported(int D, int HG);
+int launch_gate(GateArgs& a, bool backward, hipStream_t s);
+
+// ------------------------------------------------------------------------------------
 // Row kernels (rows.hip)
 // ------------------------------------------------------------------------------------
 int launch_gather_rows(const float* table, int dim, const int64_t* idx, int64_t n, float* out,

@@ -16,6 +16,7 @@
 // item tower of a rank runs over the item rows it owns, for whoever requested them; the
 // host moves (t | a) and (dT | dA) rows between phases and all-reduces the gradient arena.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -344,6 +345,57 @@ void set_keys(GemmProblem& p, const TowerWs& w) {
     p.key_split = w.key_split;
 }
 
+// ---- fused gate (gate.hip) ------------------------------------------------------------------
+// Used when every gated tower of a grouped launch is fp32 with a supported D == Hg; any other
+// configuration (bf16 towers, other widths) runs the generic GEMM path.  TTAMM_GENERIC_GATE=1
+// forces the generic path (the tests run both).
+bool generic_gate_forced() {
+    const char* v = std::getenv("TTAMM_GENERIC_GATE");
+    return v && v[0] == '1';
+}
+
+bool gate_group(const ttamm_tower* const* T, TowerWs* const* W, int ntowers, int D, bool mimic, GateArgs& ga) {
+    std::memset(&ga, 0, sizeof(ga));
+    if (generic_gate_forced()) return false;
+    int hg = -1;
+    for (int k = 0; k < ntowers; ++k) {
+        const ttamm_tower& t = *T[k];
+        if (t.fusion != TTAMM_FUSION_GATED) continue;
+        const int h = t.gate[0].out_features;
+        if (t.matmul_bf16 || !gate_fused_supported(D, h) || (hg >= 0 && h != hg)) return false;
+        hg = h;
+    }
+    if (hg < 0) return false;
+    for (int k = 0; k < ntowers; ++k) {
+        const ttamm_tower& t = *T[k];
+        const TowerWs& w = *W[k];
+        if (t.fusion != TTAMM_FUSION_GATED || w.R <= 0) continue;
+        GateTower& g = ga.tw[ga.count++];
+        g.R = w.R;
+        g.ef = w.ef;
+        g.G1 = t.gate[0].weight;
+        g.c1 = t.gate[0].bias;
+        g.G2 = t.gate[1].weight;
+        g.c2 = t.gate[1].bias;
+        g.z = w.z;
+        g.g = w.g;
+        g.t = w.t;
+        g.a = w.a;
+        g.ld_t = w.t_ld;
+        g.table = mimic ? t.mimic.weight : nullptr;
+        g.idx = w.idx;
+        g.aug = w.aug;
+        g.dT = w.dT;
+        g.ld_dT = w.dT_ld;
+        g.dq = w.dq;
+        g.dz = w.dz;
+        g.dEF = w.dEF;
+    }
+    ga.D = D;
+    ga.HG = hg;
+    return true;
+}
+
 // ---- forward -------------------------------------------------------------------------------
 // part FWD_MLP: ID-row gather + feature encoder; FWD_FUSION: gate / combine (reads the mimic rows)
 enum { FWD_MLP = 1, FWD_FUSION = 2, FWD_ALL = 3 };
@@ -429,12 +481,17 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
             return fail(TTAMM_E_INVALID, "identity feature encoder is not supported by the fused step");
     }
     // fusion
+    GateArgs ga;
+    const bool fused_gate = gate_group(T, W, ntowers, D, mimic, ga);
+    if (fused_gate && ga.count > 0)
+        if ((rc = launch_gate(ga, false, s))) return rc;
     Batcher g1, g2;
     for (int k = 0; k < ntowers; ++k) {
         const ttamm_tower& t = *T[k];
         TowerWs& w = *W[k];
         const float* table = mimic ? t.mimic.weight : nullptr;
         if (t.fusion == TTAMM_FUSION_GATED) {
+            if (fused_gate) continue;
             const int Hg = t.gate[0].out_features;
             GemmProblem p = gp_base();
             p.bf16 = t.matmul_bf16;
@@ -488,11 +545,15 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
 int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s, int ntowers) {
     int rc;
     // gate: dq, dz, dEF
+    GateArgs ga;
+    const bool fused_gate = gate_group(T, W, ntowers, D, false, ga);
+    if (fused_gate && ga.count > 0)
+        if ((rc = launch_gate(ga, true, s))) return rc;
     Batcher b1, b2;
     for (int k = 0; k < ntowers; ++k) {
         const ttamm_tower& t = *T[k];
         TowerWs& w = *W[k];
-        if (t.fusion != TTAMM_FUSION_GATED) continue;
+        if (t.fusion != TTAMM_FUSION_GATED || fused_gate) continue;
         const int Hg = t.gate[0].out_features;
         if ((rc = launch_gate_dq(w.dT, w.dT_ld, w.ef, w.g, w.R, D, w.dq, s))) return rc;
         GemmProblem p = gp_base();  // dz = (dq . G2) * (z > 0)
