@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 8
+#define TTAMM_ABI_VERSION 9
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -248,6 +248,12 @@ int ttamm_retrieval_topk(const float* queries, int64_t n_queries, int64_t ldq, c
                          int64_t ldi, int32_t dim, const int64_t* blocked_offsets, const int64_t* blocked_values,
                          int32_t k, float* out_scores, int64_t* out_ids, void* workspace, size_t workspace_bytes,
                          void* stream);
+
+/* faiss.normalize_L2 on device rows, in place (training.py:670-672 on the item matrix and
+ * :954-955 on the queries when the model's similarity is cosine): row r of the [n, dim] matrix
+ * with leading dim ld is scaled by 1 / sqrt(sum of its squares); rows of norm 0 are left as
+ * they are.  Replaces faiss::fvec_renorm_L2 (faiss/utils/distances.cpp). */
+int ttamm_normalize_rows(float* rows, int64_t n, int32_t dim, int64_t ld, void* stream);
 
 /* Deferred AdamW(g = 0): bytes of one adam_history entry, and the flush that brings every row
  * of every dense-group table with last_step up to hp.dense_step (call before the tables or

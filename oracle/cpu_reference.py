@@ -514,6 +514,19 @@ def flat_ip_search(items: np.ndarray, queries: np.ndarray, k: int) -> tuple[np.n
     return out, ids
 
 
+def normalize_l2(x: np.ndarray) -> np.ndarray:
+    """faiss.normalize_L2 (called at training.py:670-672 on the index matrix and :954-955 on each
+    query).  faiss is not installed here (third-party, unpinned by the reference); its published
+    algorithm (faiss/utils/distances.cpp fvec_renorm_L2): per row nr = sum x^2 in fp32, and if
+    nr > 0 every element is multiplied by the fp32 value of 1 / sqrt(nr).  Returns a new array."""
+    x = np.array(x, dtype=np.float32, copy=True)
+    nr = np.einsum("ij,ij->i", x.astype(np.float64), x.astype(np.float64)).astype(np.float32)
+    root = np.sqrt(np.where(nr > 0, nr, np.float32(1.0)))  # sqrtf, fp32
+    inv = np.where(nr > 0, (1.0 / root.astype(np.float64)).astype(np.float32), np.float32(1.0))  # 1.0 / sqrtf(nr)
+    x *= inv[:, None]
+    return x
+
+
 def retrieve_with_faiss(items: np.ndarray, user_embedding: np.ndarray, blocked: set[int], ground_truth: set[int],
                         *, max_k: int, faiss_search_k: int) -> list[int]:
     """training.py:944-970 (_retrieve_with_faiss), dot-product index."""
@@ -538,11 +551,15 @@ def retrieve_with_faiss(items: np.ndarray, user_embedding: np.ndarray, blocked: 
 def evaluate_model(model: OracleModel, *, train_positive_map: Mapping[int, set[int]],
                    val_pairs: Sequence[tuple[int, int]], item_features: torch.Tensor | None,
                    user_features: torch.Tensor | None, num_items: int, k_values: Iterable[int],
-                   faiss_search_k: int = 80) -> tuple[dict[int, list[int]], dict[int, set[int]]]:
+                   faiss_search_k: int = 80, normalize: bool = False
+                   ) -> tuple[dict[int, list[int]], dict[int, set[int]]]:
     """training.py:917-1043 with FAISS resources (exact IP over all items): per validation user,
-    predictions exclude the user's train positives."""
+    predictions exclude the user's train positives.  ``normalize``: the model's similarity is
+    cosine, so the index and the queries are L2-normalised (:670-672, :954-955)."""
     max_k = max(k_values)
     items = encode_item_embeddings(model, num_items=num_items, item_features=item_features).numpy()
+    if normalize:
+        items = normalize_l2(items)
     groups: dict[int, list[int]] = {}
     for u, i in val_pairs:
         groups.setdefault(int(u), []).append(int(i))
@@ -559,6 +576,7 @@ def evaluate_model(model: OracleModel, *, train_positive_map: Mapping[int, set[i
             emb = tower_forward(model.user_encoder, idx, feats, training=False)
             if model.adaptive_mimic is not None:
                 emb = gather_aug(model.adaptive_mimic.user_augmented, idx, emb)[0]
-            preds[u] = retrieve_with_faiss(items, emb[0].numpy(), set(train_positive_map.get(u, set())), gt,
+            query = normalize_l2(emb.numpy())[0] if normalize else emb[0].numpy()
+            preds[u] = retrieve_with_faiss(items, query, set(train_positive_map.get(u, set())), gt,
                                            max_k=max_k, faiss_search_k=faiss_search_k)
     return preds, truth

@@ -110,3 +110,14 @@ def test_retrieve_with_faiss_filters_blocked_and_appends_truth():
     # only 2 unblocked candidates exist beyond the block: the ground truth is appended
     got = ref.retrieve_with_faiss(items[:4], user, blocked={0, 1}, ground_truth={9}, max_k=3, faiss_search_k=2)
     assert got == [2, 3, 9]
+
+
+def test_normalize_l2_known_answer():
+    """faiss.normalize_L2 restatement (training.py:670-672): unit rows, zero rows untouched."""
+    x = np.array([[3, 4], [0, 0], [0, -2], [1, 1]], dtype=np.float32)
+    y = ref.normalize_l2(x)
+    assert y[0].tolist() == [np.float32(0.6), np.float32(0.8)]
+    assert y[1].tolist() == [0.0, 0.0]
+    assert y[2].tolist() == [0.0, -1.0]
+    assert abs(float(y[3, 0]) - 2 ** -0.5) < 1e-7 and y[3, 0] == y[3, 1]
+    assert x[0].tolist() == [3, 4]  # input not modified

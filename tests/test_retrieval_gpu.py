@@ -138,3 +138,58 @@ def test_recall_at_20_matches_oracle_evaluation():
     assert abs(mo.recall[20] - mt.recall[20]) <= 0.002
     same = sum(preds_o[u] == preds_t[u] for u in preds_o)
     assert same >= 0.9 * len(preds_o)  # identical lists except near ties
+
+
+def test_normalize_rows_matches_faiss_restatement():
+    """faiss.normalize_L2 (training.py:670-672, :954-955) on the device vs the oracle's
+    restatement: within 2 fp32 ulp per element (the sum of squares is order-dependent); rows of
+    norm 0 untouched; a leading dim wider than the row is respected."""
+    from ttamm.retrieval import normalize_rows
+
+    g = torch.Generator().manual_seed(4)
+    full = torch.randn((1000, 104), generator=g) * torch.rand((1000, 1), generator=g) * 10
+    full[::97, :] = 0.0
+    want = ref.normalize_l2(full[:, :96].numpy())
+    dev = full.cuda()
+    normalize_rows(dev[:, :96])
+    got = dev.cpu()
+    assert torch.equal(got[:, 96:], full[:, 96:])  # padding columns untouched
+    assert torch.equal(got[::97], full[::97])  # zero rows stay zero
+    assert torch.allclose(got[:, :96], torch.from_numpy(want), rtol=2.5e-7, atol=1e-9)
+    norms = got[:, :96].double().norm(dim=1)
+    nz = full[:, :96].abs().sum(dim=1) > 0
+    assert torch.allclose(norms[nz], torch.ones_like(norms[nz]), atol=1e-6)
+
+
+def test_recall_at_20_cosine_model_matches_oracle():
+    """The reference default (configs/default.yaml:59, similarity: cosine): the index and the
+    queries are L2-normalised before the inner-product search on both sides."""
+    from gpu_helpers import ttamm_model_from
+    from torch import nn
+
+    shape = Shape(U=96, I=400, B=64)
+    prob = make_problem(shape, seed=6, steps=2, positives_per_user=6)
+    model_o, _, _ = run_oracle(prob, steps=2)
+    prob.model = model_o
+    model_t = ttamm_model_from(prob).eval()
+    model_t.similarity = nn.CosineSimilarity(dim=-1)
+    g = torch.Generator().manual_seed(10)
+    val = [(u, int(torch.randint(0, shape.I, (1,), generator=g))) for u in range(shape.U)]
+    preds_o, truth_o = ref.evaluate_model(model_o, train_positive_map=prob.positives, val_pairs=val,
+                                          item_features=prob.item_features, user_features=prob.user_features,
+                                          num_items=shape.I, k_values=[10, 20], normalize=True)
+    preds_t, truth_t = evaluate_model(model_t, train_positive_map=prob.positives, val_interactions=val,
+                                      item_feature_tensor=prob.item_features.cuda(),
+                                      user_feature_tensor=prob.user_features.cuda(), device=torch.device("cuda"),
+                                      num_items=shape.I, k_values=[10, 20])
+    assert truth_o == truth_t
+    mo = ref.ranking_metrics(preds_o, truth_o, [20])
+    mt = ref.ranking_metrics(preds_t, truth_t, [20])
+    assert abs(mo.recall[20] - mt.recall[20]) <= 0.002
+    same = sum(preds_o[u] == preds_t[u] for u in preds_o)
+    assert same >= 0.9 * len(preds_o)
+    # cosine changes the ranking: the dot-product oracle gives different lists
+    preds_dot, _ = ref.evaluate_model(model_o, train_positive_map=prob.positives, val_pairs=val,
+                                      item_features=prob.item_features, user_features=prob.user_features,
+                                      num_items=shape.I, k_values=[10, 20])
+    assert sum(preds_dot[u] != preds_o[u] for u in preds_o) > 0

@@ -64,6 +64,11 @@ TTAMM_API int ttamm_retrieval_topk(const float* queries, int64_t n_queries, int6
                                  out_scores, out_ids, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
+TTAMM_API int ttamm_normalize_rows(float* rows, int64_t n, int32_t dim, int64_t ld, void* stream) {
+    g_last_error.clear();
+    return launch_normalize_rows(rows, n, dim, ld, (hipStream_t)stream);
+}
+
 TTAMM_API int ttamm_train_step(const ttamm_step_args* args, void* stream) {
     if (!args) return fail(TTAMM_E_INVALID, "null step args");
     g_last_error.clear();

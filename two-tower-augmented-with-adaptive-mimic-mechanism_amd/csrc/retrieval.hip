@@ -274,7 +274,35 @@ int pick_parts(int64_t nq, int64_t ni, int k) {
     return parts < 1 ? 1 : (int)parts;
 }
 
+// faiss.normalize_L2 (faiss/utils/distances.cpp fvec_renorm_L2), applied to the item matrix
+// and the queries when the model's similarity is cosine (training.py:670-672, :954-955): each
+// row is scaled by 1 / sqrt(sum x^2) in fp32; rows of norm 0 stay as they are.  One wave per
+// row, the squares summed lane-strided then by a butterfly.
+__global__ __launch_bounds__(256) void normalize_rows_kernel(float* __restrict__ x, int64_t n, int dim, int64_t ld) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n) return;
+    float* r = x + row * ld;
+    float ss = 0.f;
+    for (int c = lane; c < dim; c += 64) ss = fmaf(r[c], r[c], ss);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    if (ss > 0.f) {
+        const float inv = 1.0f / sqrtf(ss);
+        for (int c = lane; c < dim; c += 64) r[c] *= inv;
+    }
+}
+
 }  // namespace
+
+int launch_normalize_rows(float* x, int64_t n, int dim, int64_t ld, hipStream_t s) {
+    TTAMM_REQUIRE(n >= 0 && dim > 0 && ld >= dim, "normalize_rows: bad shape");
+    if (n == 0) return TTAMM_OK;
+    TTAMM_REQUIRE(x != nullptr, "normalize_rows: null rows");
+    hipLaunchKernelGGL(normalize_rows_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, s, x, n, dim, ld);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
 
 size_t retrieval_workspace_bytes(int64_t nq, int64_t ni, int dim, int k) {
     (void)dim;

@@ -150,7 +150,7 @@ class StepArgs(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 8  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 9  # ttamm.h TTAMM_ABI_VERSION
 
 # ttamm.h TTAMM_PHASE_*
 PHASE_ALL = 0
@@ -172,6 +172,7 @@ SIGNATURES = {
     "ttamm_dense_grad_floats": (c_i64, [ctypes.POINTER(StepArgs)]),
     "ttamm_adam_history_entry_bytes": (ctypes.c_size_t, []),
     "ttamm_retrieval_topk_workspace_size": (ctypes.c_size_t, [c_i64, c_i64, c_i32, c_i32]),
+    "ttamm_normalize_rows": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i64, c_vp]),
     "ttamm_retrieval_topk": (
         ctypes.c_int,
         [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, ctypes.c_size_t, c_vp],

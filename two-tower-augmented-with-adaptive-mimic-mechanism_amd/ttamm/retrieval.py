@@ -63,9 +63,22 @@ class _NoFeatures(nn.Module):
         self.embedding = tower.embedding
 
 
-def _check_eval(model: nn.Module) -> None:
-    if isinstance(getattr(model, "similarity", None), nn.CosineSimilarity):
-        raise NotImplementedError("ttamm retrieval: cosine similarity (FAISS normalize_L2) is not implemented")
+def _uses_cosine(model: nn.Module) -> bool:
+    """training.py:670 / :942: the FAISS index and the queries are L2-normalised when the model's
+    similarity module is nn.CosineSimilarity (the default, configs/default.yaml:59)."""
+    return isinstance(getattr(model, "similarity", None), nn.CosineSimilarity)
+
+
+def normalize_rows(x: torch.Tensor) -> torch.Tensor:
+    """faiss.normalize_L2 (training.py:670-672, :954-955) on a device matrix, in place: each row
+    scaled by 1 / sqrt(sum of squares); all-zero rows unchanged.  Returns ``x``."""
+    _lib.require_rocm(x, "normalize_rows")
+    if x.dtype != torch.float32 or x.dim() != 2 or x.stride(1) != 1:
+        raise ValueError("ttamm normalize_rows: a float32 [n, dim] matrix with unit column stride is required")
+    if x.numel():
+        _lib.check(_lib.load().ttamm_normalize_rows(x.data_ptr(), x.shape[0], x.shape[1], x.stride(0),
+                                                     _lib.stream_handle(x.device)))
+    return x
 
 
 def encode_item_embeddings(model, *, num_items: int, item_features: torch.Tensor | None, device: torch.device,
@@ -160,8 +173,9 @@ def evaluate_model(
     faiss_search_k: int = 0,
     item_embeddings: torch.Tensor | None = None,
 ) -> tuple[dict[int, list[int]], dict[int, set[int]]]:
-    """_evaluate_model (training.py:917-1043), exact inner-product branch, for every validation
-    user at once.  ``val_interactions``: a DataFrame with user_idx / item_idx columns or an
+    """_evaluate_model (training.py:917-1043), exact inner-product branch (cosine models: on
+    L2-normalised items and queries, as the FAISS index is built), for every validation user at
+    once.  ``val_interactions``: a DataFrame with user_idx / item_idx columns or an
     iterable of (user, item) pairs.  ``candidate_samples`` / ``rng`` / ``faiss_resources`` are
     accepted for signature compatibility; retrieval is always the exact full-corpus search
     (the FAISS branch).
@@ -169,7 +183,6 @@ def evaluate_model(
     Semantics kept from :944-970: a user's train positives are never returned; predictions are
     the best max(k_values) remaining items; if fewer exist, the user's ground-truth items not
     already listed are appended (set iteration order) and the list is cut to max_k."""
-    _check_eval(model)
     groups = _group_pairs(val_interactions)
     if not groups:
         return {}, {}
@@ -182,6 +195,9 @@ def evaluate_model(
                                                  device=device)
     q = encode_user_embeddings(model, torch.tensor(users, dtype=torch.long, device=device),
                                user_features=user_feature_tensor)
+    if _uses_cosine(model):  # normalize_L2 on the index (:670-672) and on every query (:954-955)
+        item_embeddings = normalize_rows(item_embeddings.clone())
+        normalize_rows(q)
     boff, bval = blocked_csr(users, train_positive_map, device)
     _, ids = retrieve_topk(q, item_embeddings, max_k, blocked_offsets=boff, blocked_values=bval)
     preds: dict[int, list[int]] = {}
