@@ -28,6 +28,7 @@
 // Weight gradients: dW^T[n_in, m_out] = X^T . dY, split over row chunks, written to fp32
 // slabs and summed in a fixed order by wgrad_reduce_kernel; the bias gradient rides along as
 // an implicit all-ones column of X.
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 
@@ -88,12 +89,16 @@ __device__ __forceinline__ uint32_t keep_threshold(float keep_prob) {
     return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
 }
 
-template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KMAJ_, bool B_KMAJ_>
+// MF: MFMA block edge — 32 (v_mfma_f32_32x32x2_f32 / 32x32x16_bf16) or 16
+// (v_mfma_f32_16x16x4_f32, fp32 only): the 16-row granularity lets a tile height divide the
+// step's row count into exactly two tiles per CU (C2: 57344 = 512 x 112).
+template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KMAJ_, bool B_KMAJ_, int MF_ = 32>
 struct Cfg {
-    static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_;
+    static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_, MF = MF_;
     static constexpr bool A_KMAJ = A_KMAJ_, B_KMAJ = B_KMAJ_;
     static constexpr int TM = BM / WAVES_M, TN = BN / WAVES_N;
-    static constexpr int I = TM / 32, J = TN / 32;
+    static constexpr int I = TM / MF, J = TN / MF;
+    static constexpr int NR = MF == 32 ? 16 : 4;  // accumulator registers per MFMA block
     static constexpr int A_F4 = BM * BK / 4, B_F4 = BN * BK / 4;
     static constexpr int A_LOADS = (A_F4 + kThreads - 1) / kThreads;
     static constexpr int B_LOADS = (B_F4 + kThreads - 1) / kThreads;
@@ -101,14 +106,17 @@ struct Cfg {
     static constexpr int B_STAGE = B_KMAJ ? BK * BN : BN * SK;
     static constexpr int STAGE = 2 * (A_STAGE + B_STAGE);
     static constexpr int CLD = BN + 4;                           // epilogue tile row stride
-    static constexpr int EPI_PHASES = WAVES_M >= 2 ? 2 : 1;     // row slices of the epilogue
-    static constexpr int EPI_ROWS = BM / EPI_PHASES;
+    // epilogue row slices (whole MFMA row blocks): halves of the tile by wave rows, or by
+    // row blocks when one wave row spans the tile
+    static constexpr int EPI_ROWS = WAVES_M >= 2 ? BM / 2 : (I > 1 ? (I + 1) / 2 * MF : BM);
+    static constexpr int EPI_PHASES = (BM + EPI_ROWS - 1) / EPI_ROWS;
     static constexpr int EPI = EPI_ROWS * CLD;
     static constexpr int KIDX = A_KMAJ ? 2 * 512 : 0;              // int64 gather rows (floats)
     static constexpr int LDS = (STAGE + KIDX) > EPI ? (STAGE + KIDX) : EPI;
     static_assert(WAVES_M * WAVES_N == 4, "4 waves per block");
-    static_assert(TM % 32 == 0 && TN % 32 == 0, "wave tile must be a multiple of 32");
-    static_assert(WAVES_M % EPI_PHASES == 0, "epilogue slices must hold whole wave rows");
+    static_assert(MF == 32 || MF == 16, "MFMA block edge");
+    static_assert(TM % MF == 0 && TN % MF == 0, "wave tile must be a multiple of the MFMA block");
+    static_assert(WAVES_M == 1 || WAVES_M % EPI_PHASES == 0, "epilogue slices must hold whole wave rows");
 };
 
 // ---- the fused elementwise tail on 4 consecutive columns of one row ----------------------
@@ -219,7 +227,10 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / CF::WAVES_N, wn = wave % CF::WAVES_N;
-    const int li = lane & 31, h = lane >> 5;
+    constexpr int MF = CF::MF;
+    // lane -> (row/column in an MFMA block, k slot): 32x32x2 has 2 k slots of 32 lanes,
+    // 16x16x4 has 4 k slots of 16 lanes
+    const int li = lane & (MF - 1), h = lane / MF;
     float* As = lds;
     float* Bs = lds + 2 * CF::A_STAGE;
 
@@ -268,13 +279,14 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
         else b_rp[it] = P.B + (int64_t)(lin / (BN / 4)) * P.ldb + n0 + (lin % (BN / 4)) * 4;
     }
 
-    f32x16 acc[I][J];
+    using Acc = std::conditional_t<MF == 32, f32x16, f32x4_t>;
+    Acc acc[I][J];
 #pragma unroll
     for (int i = 0; i < I; ++i)
 #pragma unroll
         for (int j = 0; j < J; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+            for (int r = 0; r < CF::NR; ++r) acc[i][j][r] = 0.f;
 
     auto mainloop = [&](auto fast_tag) {
         constexpr bool FAST = decltype(fast_tag)::value;
@@ -347,20 +359,37 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
             constexpr int buf = decltype(S)::value;
             const float* as = As + buf * CF::A_STAGE;
             const float* bs = Bs + buf * CF::B_STAGE;
-            // the lane's 4 k values 8h + 4*s4 .. +3 of A row m / B column n
+            // the lane's 4 k values kb .. kb+3 of A row m / B column n, kb = 8h + 4*s4 (32x32:
+            // lane half h walks k = 8h..8h+7) or 4h (16x16: k slot h walks k = 4h..4h+3)
+            auto kbase = [&](int s4) { return MF == 32 ? 8 * h + 4 * s4 : 4 * h; };
             auto frag_a = [&](int i, int s4) -> float4 {
-                const int m = wm * TM + i * 32 + li;
-                if (!AK) return *reinterpret_cast<const float4*>(as + m * SK + 8 * h + 4 * s4);
-                const float* c = as + (8 * h + 4 * s4) * BM + m;
+                const int m = wm * TM + i * MF + li;
+                if (!AK) return *reinterpret_cast<const float4*>(as + m * SK + kbase(s4));
+                const float* c = as + kbase(s4) * BM + m;
                 return make_float4(c[0], c[BM], c[2 * BM], c[3 * BM]);
             };
             auto frag_b = [&](int j, int s4) -> float4 {
-                const int n = wn * TN + j * 32 + li;
-                if (!BKM) return *reinterpret_cast<const float4*>(bs + n * SK + 8 * h + 4 * s4);
-                const float* c = bs + (8 * h + 4 * s4) * BN + n;
+                const int n = wn * TN + j * MF + li;
+                if (!BKM) return *reinterpret_cast<const float4*>(bs + n * SK + kbase(s4));
+                const float* c = bs + kbase(s4) * BN + n;
                 return make_float4(c[0], c[BN], c[2 * BN], c[3 * BN]);
             };
-            if constexpr (BF) {
+            if constexpr (MF == 16) {
+                static_assert(!BF, "16x16 blocks are fp32 only");
+                float4 af[I], bf[J];
+#pragma unroll
+                for (int i = 0; i < I; ++i) af[i] = frag_a(i, 0);
+#pragma unroll
+                for (int j = 0; j < J; ++j) bf[j] = frag_b(j, 0);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int i = 0; i < I; ++i)
+#pragma unroll
+                        for (int j = 0; j < J; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4get(af[i], q), f4get(bf[j], q),
+                                                                             acc[i][j], 0, 0, 0);
+            } else if constexpr (BF) {
                 bf16x8 a8[I], b8[J];
 #pragma unroll
                 for (int i = 0; i < I; ++i) a8[i] = pack_bf16(frag_a(i, 0), frag_a(i, 1));
@@ -439,16 +468,18 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
     float* Cs = lds;
     for (int ph = 0; ph < CF::EPI_PHASES; ++ph) {
         const int row_lo = ph * CF::EPI_ROWS;
-        if (wm * TM >= row_lo && wm * TM < row_lo + CF::EPI_ROWS) {
+        const int rows_here = min(CF::EPI_ROWS, BM - row_lo);
 #pragma unroll
-            for (int i = 0; i < I; ++i)
+        for (int i = 0; i < I; ++i) {
+            const int br = wm * TM + i * MF;  // first tile row of MFMA row block i
+            if (br < row_lo || br >= row_lo + CF::EPI_ROWS) continue;
 #pragma unroll
-                for (int j = 0; j < J; ++j)
+            for (int j = 0; j < J; ++j)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int rr = wm * TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h - row_lo;
-                        Cs[rr * CF::CLD + wn * TN + j * 32 + li] = acc[i][j][r];
-                    }
+                for (int r = 0; r < CF::NR; ++r) {
+                    const int rr = br - row_lo + (MF == 32 ? (r & 3) + 8 * (r >> 2) + 4 * h : 4 * h + r);
+                    Cs[rr * CF::CLD + wn * TN + j * MF + li] = acc[i][j][r];
+                }
         }
         __syncthreads();
         // each thread owns one 4-column group (bias loaded once) and walks rows
@@ -461,7 +492,7 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
                                   P.bias != nullptr;
             const float4 bias4 = has_bias ? ld4(P.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 4
-            for (int rr = r0; rr < CF::EPI_ROWS; rr += RSTEP) {
+            for (int rr = r0; rr < rows_here; rr += RSTEP) {
                 const int row = m0 + row_lo + rr;
                 if (row < M) epilogue4<E>(P, ld4(Cs + rr * CF::CLD + c4 * 4), bias4, split, row, col);
             }
@@ -525,7 +556,20 @@ int dispatch_epi_t(GemmBatch& b, hipStream_t s) {
 }
 template <class CF>
 int dispatch_epi(GemmBatch& b, hipStream_t s) {
-    return b.p[0].bf16 ? dispatch_epi_t<CF, true>(b, s) : dispatch_epi_t<CF, false>(b, s);
+    if constexpr (CF::MF == 16) return dispatch_epi_t<CF, false>(b, s);
+    else return b.p[0].bf16 ? dispatch_epi_t<CF, true>(b, s) : dispatch_epi_t<CF, false>(b, s);
+}
+
+// Wide fp32 forward (the first feature layer, N = 192 at C2): 112 x 192 tiles on 16x16x4
+// blocks — four waves side by side, each 112 x 48 — so the step's R = 57344 rows make 512
+// tiles, exactly two per CU (128-row tiles make 448: 1.75 per CU, a quarter of the chip idle
+// in the second round).  TTAMM_GEMM_WIDE32=1 selects the 128 x 192 32x32 tiles instead.
+bool wide16_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("TTAMM_GEMM_WIDE32");
+        return !(e && e[0] == '1');
+    }();
+    return on;
 }
 
 }  // namespace
@@ -548,6 +592,7 @@ int launch_gemm(GemmBatch& b, hipStream_t s) {
     }
     if (maxN > 96) {
         if (bkn) return dispatch_epi<Cfg<128, 192, 2, 2, false, true>>(b, s);
+        if (!b.p[0].bf16 && wide16_enabled()) return dispatch_epi<Cfg<112, 192, 1, 4, false, false, 16>>(b, s);
         return dispatch_epi<Cfg<128, 192, 2, 2, false, false>>(b, s);
     }
     if (bkn) return dispatch_epi<Cfg<128, 96, 4, 1, false, true>>(b, s);

@@ -86,6 +86,24 @@ int main() {
         b.p[0] = p, b.count = 1;
         launch_gemm(b, 0);
     });
+    time_it("fwd L1 (no dropout)", 2.0 * R * F * H, [&] {
+        GemmBatch b;
+        std::memset(&b, 0, sizeof(b));
+        GemmProblem p = base();
+        p.A = X, p.a_idx = idx, p.lda = F, p.B = W1, p.ldb = F, p.M = R, p.N = H, p.K = F;
+        p.epi = EPI_HIDDEN, p.C = C, p.ldc = H, p.bias = b1;
+        b.p[0] = p, b.count = 1;
+        launch_gemm(b, 0);
+    });
+    time_it("fwd L1 (no gather, no dropout)", 2.0 * R * F * H, [&] {
+        GemmBatch b;
+        std::memset(&b, 0, sizeof(b));
+        GemmProblem p = base();
+        p.A = X, p.lda = F, p.B = W1, p.ldb = F, p.M = R, p.N = H, p.K = F;
+        p.epi = EPI_HIDDEN, p.C = C, p.ldc = H, p.bias = b1;
+        b.p[0] = p, b.count = 1;
+        launch_gemm(b, 0);
+    });
     time_it("fwd L2 R x 192 -> 96", 2.0 * R * H * D, [&] {
         GemmBatch b;
         std::memset(&b, 0, sizeof(b));
