@@ -563,11 +563,14 @@ int dispatch_epi(GemmBatch& b, hipStream_t s) {
 // Wide fp32 forward (the first feature layer, N = 192 at C2): 112 x 192 tiles on 16x16x4
 // blocks — four waves side by side, each 112 x 48 — so the step's R = 57344 rows make 512
 // tiles, exactly two per CU (128-row tiles make 448: 1.75 per CU, a quarter of the chip idle
-// in the second round).  TTAMM_GEMM_WIDE32=1 selects the 128 x 192 32x32 tiles instead.
+// in the second round).  Opt-in only (TTAMM_GEMM_WIDE16=1): it wins in isolation (146.7 vs
+// 163.6 us) but inside the full C2 step it measured 214 us/launch against 151 us for the
+// 128 x 192 32x32x2 tiles (profiles/r01_c2_bench_kernel_stats_session4_wide16.csv), so the 32x32
+// tiles stay the default.
 bool wide16_enabled() {
     static const bool on = [] {
-        const char* e = std::getenv("TTAMM_GEMM_WIDE32");
-        return !(e && e[0] == '1');
+        const char* e = std::getenv("TTAMM_GEMM_WIDE16");
+        return e && e[0] == '1';
     }();
     return on;
 }
