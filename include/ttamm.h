@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 9
+#define TTAMM_ABI_VERSION 10
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -72,8 +72,14 @@ extern "C" {
 #define TTAMM_PHASE_ITEM_BWD 16
 #define TTAMM_PHASE_DENSE 32
 
-/* Device-side status word bits (written by kernels, read by the host at epoch end). */
-#define TTAMM_STATUS_SAMPLER_EXHAUSTED 1u /* samplers.py:78-81 */
+/* Device-side status word bits (written by kernels, read by the host at epoch end).  Once a
+ * bit is set, every later step on that status word is skipped on the device (no parameter,
+ * optimizer-state or loss-accumulator write), so the state the host finds is the state after
+ * the last good step — as the reference, which raises inside the failing batch before its
+ * backward, leaves it. */
+#define TTAMM_STATUS_SAMPLER_EXHAUSTED 1u    /* samplers.py:78-81 -> RuntimeError            */
+#define TTAMM_STATUS_INDEX_OUT_OF_RANGE 2u   /* a batch id < 0 or >= table rows -> IndexError
+                                                (nn.Embedding, encoders.py:222-223)         */
 
 /* ---------------------------------------------------------------------------------- */
 /* Parameter descriptors                                                               */
@@ -216,6 +222,11 @@ typedef struct ttamm_step_args {
     const int64_t* item_categories;
     int64_t num_categories;
     int64_t major_category;       /* major_category_id                                       */
+    /* ---- error recovery ---------------------------------------------------------------------
+     * steps_applied: optional device counter, += 1 by every step that ran (status clean when it
+     * began).  After a status error the host flushes the deferred tables to, and writes back
+     * optimizer step counts of, the steps that ran.                                           */
+    int64_t* steps_applied;
 } ttamm_step_args;
 
 /* ---------------------------------------------------------------------------------- */
@@ -262,7 +273,10 @@ size_t ttamm_adam_history_entry_bytes(void);
 int ttamm_flush_tables(const ttamm_step_args* args, void* stream);
 
 /* nn.Embedding forward / AdaptiveMimicMechanism._gather_and_reshape
- * (encoders.py:222-223, adaptive_mimic.py:97-105): out[r, :] = table[idx[r], :]. */
+ * (encoders.py:222-223, adaptive_mimic.py:97-105): out[r, :] = table[idx[r], :].
+ * Every row-indexed entry point below never reads outside its table: an id outside
+ * [0, table_rows) yields a zero row (the Python mirror raises IndexError before the call, as
+ * nn.Embedding does).  The training step reports such ids through TTAMM_STATUS_INDEX_OUT_OF_RANGE. */
 int ttamm_gather_rows(const float* table, int64_t table_rows, int32_t dim, const int64_t* idx,
                       int64_t n, float* out, int64_t out_ld, void* stream);
 

@@ -78,7 +78,7 @@ TTAMM_API int ttamm_train_step(const ttamm_step_args* args, void* stream) {
 TTAMM_API int ttamm_gather_rows(const float* table, int64_t table_rows, int32_t dim, const int64_t* idx, int64_t n,
                                 float* out, int64_t out_ld, void* stream) {
     if (n < 0 || dim <= 0 || out_ld < dim || table_rows <= 0) return fail(TTAMM_E_INVALID, "gather_rows: bad shape");
-    return launch_gather_rows(table, dim, idx, n, out, out_ld, (hipStream_t)stream);
+    return launch_gather_rows(table, table_rows, dim, idx, n, out, out_ld, (hipStream_t)stream);
 }
 
 TTAMM_API size_t ttamm_tower_forward_workspace_size(const ttamm_tower* tower, int64_t n) {
@@ -95,7 +95,7 @@ TTAMM_API int ttamm_tower_forward(const ttamm_tower* tower, const int64_t* idx, 
 TTAMM_API int ttamm_mimic_augment(const float* table, int64_t table_rows, int32_t dim, const int64_t* idx, int64_t n,
                                   const float* base, float* out, float* aug_out, void* stream) {
     if (n < 0 || dim <= 0 || table_rows <= 0) return fail(TTAMM_E_INVALID, "mimic_augment: bad shape");
-    return launch_combine(base, dim, nullptr, 0, table, idx, n, dim, nullptr, aug_out, dim, out, (hipStream_t)stream);
+    return launch_combine(base, dim, nullptr, 0, table, table_rows, idx, n, dim, nullptr, aug_out, dim, out, (hipStream_t)stream);
 }
 
 TTAMM_API int ttamm_mse_loss(const float* input, const float* target, int64_t n, float* out, void* stream) {

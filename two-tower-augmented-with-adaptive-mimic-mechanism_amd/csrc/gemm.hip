@@ -560,21 +560,6 @@ int dispatch_epi(GemmBatch& b, hipStream_t s) {
     else return b.p[0].bf16 ? dispatch_epi_t<CF, true>(b, s) : dispatch_epi_t<CF, false>(b, s);
 }
 
-// Wide fp32 forward (the first feature layer, N = 192 at C2): 112 x 192 tiles on 16x16x4
-// blocks — four waves side by side, each 112 x 48 — so the step's R = 57344 rows make 512
-// tiles, exactly two per CU (128-row tiles make 448: 1.75 per CU, a quarter of the chip idle
-// in the second round).  Opt-in only (TTAMM_GEMM_WIDE16=1): it wins in isolation (146.7 vs
-// 163.6 us) but inside the full C2 step it measured 214 us/launch against 151 us for the
-// 128 x 192 32x32x2 tiles (profiles/r01_c2_bench_kernel_stats_session4_wide16.csv), so the 32x32
-// tiles stay the default.
-bool wide16_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("TTAMM_GEMM_WIDE16");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-
 }  // namespace
 
 int launch_gemm(GemmBatch& b, hipStream_t s) {
@@ -595,7 +580,6 @@ int launch_gemm(GemmBatch& b, hipStream_t s) {
     }
     if (maxN > 96) {
         if (bkn) return dispatch_epi<Cfg<128, 192, 2, 2, false, true>>(b, s);
-        if (!b.p[0].bf16 && wide16_enabled()) return dispatch_epi<Cfg<112, 192, 1, 4, false, false, 16>>(b, s);
         return dispatch_epi<Cfg<128, 192, 2, 2, false, false>>(b, s);
     }
     if (bkn) return dispatch_epi<Cfg<128, 96, 4, 1, false, true>>(b, s);

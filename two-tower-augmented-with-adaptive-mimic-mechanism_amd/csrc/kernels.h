@@ -144,12 +144,35 @@ int launch_gate(GateArgs& a, bool backward, hipStream_t s);
 // ------------------------------------------------------------------------------------
 // Row kernels (rows.hip)
 // ------------------------------------------------------------------------------------
-int launch_gather_rows(const float* table, int dim, const int64_t* idx, int64_t n, float* out,
+// ids outside [0, table_rows) give zero rows (never an out-of-table read)
+int launch_gather_rows(const float* table, int64_t table_rows, int dim, const int64_t* idx, int64_t n, float* out,
                        int64_t out_ld, hipStream_t s);
+
+// Index staging (training step prologue): out[i] = in[i] if 0 <= in[i] < rows, else 0 and
+// TTAMM_STATUS_INDEX_OUT_OF_RANGE is OR-ed into *status.  out == null: check only.
+struct StageSeg {
+    const int64_t* in;
+    int64_t* out;
+    int64_t n;
+    int64_t rows;
+};
+constexpr int kMaxStageSegs = 3;
+struct StageArgs {
+    StageSeg seg[kMaxStageSegs];
+    int count;
+    uint32_t* status;
+};
+int launch_stage_rows(const StageArgs& a, hipStream_t s);
+
+// Status bits that stop every later step (ttamm.h TTAMM_STATUS_*).
+constexpr uint32_t kStatusPoison = TTAMM_STATUS_SAMPLER_EXHAUSTED | TTAMM_STATUS_INDEX_OUT_OF_RANGE;
+__device__ __forceinline__ bool step_poisoned(const uint32_t* status) {
+    return status != nullptr && (*status & kStatusPoison) != 0u;
+}
 // t = e (+ f); a = table[idx]; aug = t + a   (non-gated fusion)
 // t = e (+ f); a = table[idx]; aug = t (+ a).  t / a rows at stride ld_ta; aug may be null.
 int launch_combine(const float* e, int64_t ld_e, const float* f, int64_t ld_f, const float* table,
-                   const int64_t* idx, int64_t n, int dim, float* t, float* a, int64_t ld_ta, float* aug,
+                   int64_t table_rows, const int64_t* idx, int64_t n, int dim, float* t, float* a, int64_t ld_ta, float* aug,
                    hipStream_t s);
 int launch_pad_rows(const float* src, int64_t rows, int cols, int64_t ld_src, float* dst, int ld_dst,
                     hipStream_t s);
@@ -185,7 +208,7 @@ int score_blocks(int64_t B);
 int launch_score_loss(const ScoreArgs& a, hipStream_t s);
 int launch_loss_finalize(const float* partials, int blocks, int64_t B, int64_t Bg, int N, int D, float lambda_u,
                          float lambda_i, int mimic, const float* cal, float lambda_cal, float* loss_out,
-                         double* loss_accum, hipStream_t s);
+                         double* loss_accum, const uint32_t* status, hipStream_t s);
 
 // ------------------------------------------------------------------------------------
 // Exact inner-product retrieval + top-k (retrieval.hip)
@@ -317,6 +340,7 @@ struct RowUpdateArgs {
     AdamConsts ad;
     int32_t dense_step;     // deferred mode (table.last_step): rows are updated in place and
                             // stamped current to this step
+    const uint32_t* status; // step_poisoned(status): no write (ttamm.h TTAMM_STATUS_*)
 };
 int launch_row_update(const RowUpdateArgs& a, hipStream_t s);
 
@@ -325,7 +349,10 @@ int launch_row_update(const RowUpdateArgs& a, hipStream_t s);
 // brought to step T replays adam_elem(g = 0) with history[l+1 .. T] — the same operations the
 // eager sweep would have applied, so the bits agree.
 constexpr int kMaxAdamHistory = 512;
-int launch_history_put(AdamConsts* hist, int cap, int64_t step, const AdamConsts& c, hipStream_t s);
+// First kernel of a step that may write state: unless the status word is poisoned, count the
+// step in *applied (may be null) and store its constants in hist[step % cap] (hist may be null).
+int launch_step_begin(const uint32_t* status, int64_t* applied, AdamConsts* hist, int cap, int64_t step,
+                      const AdamConsts& c, hipStream_t s);
 struct ReplaySeg {
     float* p;
     float* m;
@@ -348,6 +375,7 @@ struct ReplayArgs {
     int32_t target;   // replay every row up to this dense step
     int stamp;        // write last = target afterwards (row ranges only)
     int decoupled;    // AdamW (decoupled weight decay) vs Adam (L2): the optimizer's, every step
+    const uint32_t* status;  // poisoned: no write (null for the flush)
 };
 int launch_replay(const ReplayArgs& a, hipStream_t s);
 
@@ -362,12 +390,14 @@ struct SweepArgs {
     SweepSeg seg[kMaxSweepSegs];
     int count;
     AdamConsts ad;
+    const uint32_t* status;
 };
 // AdamW with g = 0 over whole tables (adam.py:419-547 for rows the batch did not touch)
 int launch_dense_sweep(const SweepArgs& a, hipStream_t s);
 // write back side-buffer rows: table[key[u]] = side[u]
 int launch_side_scatter(const int32_t* n_unique, const int32_t* keys, const int32_t* seg_start,
-                        const float* side, int64_t n, int dim, ttamm_table t, hipStream_t s);
+                        const float* side, int64_t n, int dim, ttamm_table t, const uint32_t* status,
+                        hipStream_t s);
 
 struct DenseTensor {
     float* p;
@@ -381,6 +411,7 @@ struct DenseAdamArgs {
     DenseTensor t[kMaxDenseTensors];
     int count;
     AdamConsts ad;
+    const uint32_t* status;
 };
 int launch_dense_adam(const DenseAdamArgs& a, hipStream_t s);
 

@@ -162,7 +162,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void piece_sum_kernel(RowUpdateArgs
 __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArgs A) {
     const int lane = threadIdx.x & 63;
     const int64_t u = (int64_t)blockIdx.x * kRowWaves + (threadIdx.x >> 6);
-    if (u >= A.n || u >= (int64_t)A.n_unique[0]) return;
+    if (u >= A.n || u >= (int64_t)A.n_unique[0] || step_poisoned(A.status)) return;
     const int64_t k0 = A.seg_start[u], k1 = A.seg_start[u + 1];
     const int64_t key = A.keys[k0];
     const int D = A.dim;
@@ -219,6 +219,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArg
 
 // Streaming AdamW(g = 0) over whole tables: 12 B read + 12 B written per element.
 __global__ __launch_bounds__(256) void dense_sweep_kernel(SweepArgs A) {
+    if (step_poisoned(A.status)) return;
     for (int s = 0; s < A.count; ++s) {
         const SweepSeg& S = A.seg[s];
         const int64_t n4 = S.n >> 2;
@@ -250,8 +251,11 @@ __global__ __launch_bounds__(256) void dense_sweep_kernel(SweepArgs A) {
 // ---- deferred exact AdamW(g = 0) ----------------------------------------------------------
 constexpr int kMaxHistory = kMaxAdamHistory;
 
-__global__ void history_put_kernel(AdamConsts* hist, int cap, int64_t step, AdamConsts c) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) hist[step % cap] = c;
+__global__ void step_begin_kernel(const uint32_t* status, int64_t* applied, AdamConsts* hist, int cap, int64_t step,
+                                  AdamConsts c) {
+    if (threadIdx.x != 0 || blockIdx.x != 0 || step_poisoned(status)) return;
+    if (applied) applied[0] += 1;
+    if (hist) hist[step % cap] = c;
 }
 
 // One thread per 4 consecutive elements of a row (dim % 4 == 0: four independent dependency
@@ -262,6 +266,7 @@ template <bool DECOUPLED>
 __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
     const KArg(ReplayArgs)* ka = (const KArg(ReplayArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
     const KArg(ReplaySeg)& S = ka->seg[blockIdx.y];
+    if (step_poisoned(ka->status)) return;
     __shared__ AdamConsts H[kMaxHistory];
     const int cap = ka->cap;
     for (int i = threadIdx.x; i < cap; i += blockDim.x) H[i] = ka->hist[i];
@@ -299,6 +304,7 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
 __global__ void stamp_kernel(ReplayArgs) {
     const KArg(ReplayArgs)* ka = (const KArg(ReplayArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
     const KArg(ReplaySeg)& S = ka->seg[blockIdx.y];
+    if (step_poisoned(ka->status)) return;
     for (int64_t r = S.row_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < S.row_hi;
          r += (int64_t)gridDim.x * blockDim.x)
         S.last[r] = ka->target;
@@ -306,7 +312,8 @@ __global__ void stamp_kernel(ReplayArgs) {
 
 __global__ void side_scatter_kernel(const int32_t* __restrict__ n_unique, const int32_t* __restrict__ keys,
                                     const int32_t* __restrict__ seg_start, const float* __restrict__ side, int64_t n,
-                                    int dim, ttamm_table t) {
+                                    int dim, ttamm_table t, const uint32_t* __restrict__ status) {
+    if (step_poisoned(status)) return;
     const int64_t total = n * dim;
     const int64_t nu = n_unique[0];
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
@@ -324,6 +331,7 @@ __global__ void side_scatter_kernel(const int32_t* __restrict__ n_unique, const 
 }
 
 __global__ void dense_adam_kernel(DenseAdamArgs A, int64_t total) {
+    if (step_poisoned(A.status)) return;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
         int64_t off = i;
@@ -474,9 +482,11 @@ int launch_dense_sweep(const SweepArgs& a, hipStream_t s) {
     return TTAMM_OK;
 }
 
-int launch_history_put(AdamConsts* hist, int cap, int64_t step, const AdamConsts& c, hipStream_t s) {
-    TTAMM_REQUIRE(hist && cap > 1 && cap <= kMaxHistory, "adam history: capacity must be in [2, 512]");
-    hipLaunchKernelGGL(history_put_kernel, dim3(1), dim3(64), 0, s, hist, cap, step, c);
+int launch_step_begin(const uint32_t* status, int64_t* applied, AdamConsts* hist, int cap, int64_t step,
+                      const AdamConsts& c, hipStream_t s) {
+    TTAMM_REQUIRE(!hist || (cap > 1 && cap <= kMaxHistory), "adam history: capacity must be in [2, 512]");
+    if (!hist && !applied) return TTAMM_OK;
+    hipLaunchKernelGGL(step_begin_kernel, dim3(1), dim3(64), 0, s, status, applied, hist, hist ? cap : 2, step, c);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }
@@ -510,10 +520,10 @@ int launch_replay(const ReplayArgs& a, hipStream_t s) {
 }
 
 int launch_side_scatter(const int32_t* n_unique, const int32_t* keys, const int32_t* seg_start, const float* side,
-                        int64_t n, int dim, ttamm_table t, hipStream_t s) {
+                        int64_t n, int dim, ttamm_table t, const uint32_t* status, hipStream_t s) {
     if (n <= 0) return TTAMM_OK;
     hipLaunchKernelGGL(side_scatter_kernel, dim3(grid_for(n * dim)), dim3(256), 0, s, n_unique, keys, seg_start, side,
-                       n, dim, t);
+                       n, dim, t, status);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

@@ -6,16 +6,22 @@ namespace ttamm {
 
 namespace {
 
+// Row id r of a table with `rows` rows, or -1 when it is outside the table (the gathers then
+// write a zero row instead of reading outside it; the step reports such ids via its status).
+__device__ __forceinline__ int64_t checked_row(int64_t r, int64_t rows) { return (r >= 0 && r < rows) ? r : -1; }
+
 // out[r, :] = table[idx[r], :]   (nn.Embedding forward, encoders.py:222-223).
 // One float4 per thread, flat over n * dim/4; bit-exact copy.
-__global__ void gather_rows_vec4(const float* __restrict__ table, int d4, const int64_t* __restrict__ idx,
-                                 int64_t n, float* __restrict__ out, int64_t out_ld) {
+__global__ void gather_rows_vec4(const float* __restrict__ table, int64_t rows, int d4,
+                                 const int64_t* __restrict__ idx, int64_t n, float* __restrict__ out, int64_t out_ld) {
     const int64_t total = n * d4;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = i / d4;
         const int c = (int)(i - r * d4);
-        const float4 v = reinterpret_cast<const float4*>(table + idx[r] * (int64_t)d4 * 4)[c];
+        const int64_t src = checked_row(idx[r], rows);
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (src >= 0) v = reinterpret_cast<const float4*>(table + src * (int64_t)d4 * 4)[c];
         reinterpret_cast<float4*>(out + r * out_ld)[c] = v;
     }
 }
@@ -37,7 +43,7 @@ struct WideGather {
 };
 
 template <int D4>
-__global__ __launch_bounds__(256) void gather_rows_wide(const float4* __restrict__ table,
+__global__ __launch_bounds__(256) void gather_rows_wide(const float4* __restrict__ table, int64_t rows,
                                                          const int64_t* __restrict__ idx, int64_t n,
                                                          float4* __restrict__ out, int64_t out_ld4) {
     constexpr int RPW = WideGather<D4>::RPW, I = WideGather<D4>::I;
@@ -49,12 +55,14 @@ __global__ __launch_bounds__(256) void gather_rows_wide(const float4* __restrict
 #pragma unroll
         for (int u = 0; u < I; ++u) {
             const int64_t r = r0 + (u * 64 + lane) / D4;
-            src[u] = r < n ? idx[r] : -1;
+            src[u] = r < n ? checked_row(idx[r], rows) : -1;
         }
         float4 v[I];
 #pragma unroll
-        for (int u = 0; u < I; ++u)
+        for (int u = 0; u < I; ++u) {
+            v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (src[u] >= 0) v[u] = table[src[u] * D4 + (u * 64 + lane) % D4];
+        }
 #pragma unroll
         for (int u = 0; u < I; ++u) {
             const int e = u * 64 + lane;
@@ -64,20 +72,38 @@ __global__ __launch_bounds__(256) void gather_rows_wide(const float4* __restrict
     }
 }
 
-__global__ void gather_rows_scalar(const float* __restrict__ table, int dim, const int64_t* __restrict__ idx,
-                                   int64_t n, float* __restrict__ out, int64_t out_ld) {
+__global__ void gather_rows_scalar(const float* __restrict__ table, int64_t rows, int dim,
+                                   const int64_t* __restrict__ idx, int64_t n, float* __restrict__ out, int64_t out_ld) {
     const int64_t total = n * dim;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = i / dim;
         const int c = (int)(i - r * dim);
-        out[r * out_ld + c] = table[idx[r] * (int64_t)dim + c];
+        const int64_t src = checked_row(idx[r], rows);
+        out[r * out_ld + c] = src >= 0 ? table[src * (int64_t)dim + c] : 0.f;
     }
+}
+
+// Index staging of a training step (kernels.h StageArgs); blockIdx.y = segment.
+__global__ void stage_rows_kernel(StageArgs) {
+    const KArg(StageArgs)* ka = (const KArg(StageArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
+    const KArg(StageSeg)& S = ka->seg[blockIdx.y];
+    const int64_t n = S.n, rows = S.rows;
+    bool bad = false;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t v = S.in[i];
+        const bool ok = v >= 0 && v < rows;
+        bad |= !ok;
+        if (S.out) S.out[i] = ok ? v : 0;
+    }
+    if (ka->status && __ballot(bad) != 0ull && (threadIdx.x & 63) == 0)
+        atomicOr(ka->status, TTAMM_STATUS_INDEX_OUT_OF_RANGE);
 }
 
 // t = e (+ f) ; a = table[idx] ; aug = t + a      (encoders.py:225-240, adaptive_mimic.py:88-95)
 __global__ void combine_kernel(const float* __restrict__ e, int64_t ld_e, const float* __restrict__ f,
-                               int64_t ld_f, const float* __restrict__ table, const int64_t* __restrict__ idx,
+                               int64_t ld_f, const float* __restrict__ table, int64_t table_rows,
+                               const int64_t* __restrict__ idx,
                                int64_t n, int dim, float* __restrict__ t, float* __restrict__ a, int64_t ld_ta,
                                float* __restrict__ aug) {
     const int64_t total = n * dim;
@@ -90,7 +116,8 @@ __global__ void combine_kernel(const float* __restrict__ e, int64_t ld_e, const 
         if (t) t[r * ld_ta + c] = tv;
         float av = tv;
         if (table) {
-            const float am = table[idx[r] * (int64_t)dim + c];
+            const int64_t src = checked_row(idx[r], table_rows);
+            const float am = src >= 0 ? table[src * (int64_t)dim + c] : 0.f;
             if (a) a[r * ld_ta + c] = am;
             av = tv + am;
         }
@@ -248,7 +275,8 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
 // Deterministic final reduction of the per-block partials; total loss as in training.py:798-803.
 __global__ void loss_finalize_kernel(const float* __restrict__ partials, int blocks, int64_t B, int64_t Bg, int N, int D,
                                      float lu, float li, int mimic, const float* __restrict__ cal, float lcal,
-                                     float* __restrict__ loss_out, double* __restrict__ loss_accum) {
+                                     float* __restrict__ loss_out, double* __restrict__ loss_accum,
+                                     const uint32_t* __restrict__ status) {
     __shared__ float red[3][256];
     float s[3] = {0.f, 0.f, 0.f};
     for (int i = threadIdx.x; i < blocks; i += blockDim.x)
@@ -275,7 +303,7 @@ __global__ void loss_finalize_kernel(const float* __restrict__ partials, int blo
         loss_out[2] = mimic ? mu : 0.f;
         loss_out[3] = mimic ? mi : 0.f;
         loss_out[4] = lc;
-        if (loss_accum) {
+        if (loss_accum && !step_poisoned(status)) {
             loss_accum[0] += (double)total * (double)Bg;
             loss_accum[1] += (double)B;
         }
@@ -308,8 +336,8 @@ inline unsigned grid_for(int64_t work, int threads = 256) {
 
 }  // namespace
 
-int launch_gather_rows(const float* table, int dim, const int64_t* idx, int64_t n, float* out, int64_t out_ld,
-                       hipStream_t s) {
+int launch_gather_rows(const float* table, int64_t table_rows, int dim, const int64_t* idx, int64_t n, float* out,
+                       int64_t out_ld, hipStream_t s) {
     if (n <= 0) return TTAMM_OK;
     const bool vec = (dim % 4 == 0) && (out_ld % 4 == 0) && ((uintptr_t)table % 16 == 0) &&
                      ((uintptr_t)out % 16 == 0);
@@ -320,7 +348,7 @@ int launch_gather_rows(const float* table, int dim, const int64_t* idx, int64_t 
         int64_t blocks = ceil_div(n, rows_per_block);
         if (blocks > 8192) blocks = 8192;  // grid-stride beyond ~4 resident rounds
         hipLaunchKernelGGL(gather_rows_wide<D4>, dim3((unsigned)blocks), dim3(256), 0, s,
-                           reinterpret_cast<const float4*>(table), idx, n, reinterpret_cast<float4*>(out),
+                           reinterpret_cast<const float4*>(table), table_rows, idx, n, reinterpret_cast<float4*>(out),
                            out_ld / 4);
     };
     auto try_wide = [&]() -> bool {
@@ -337,21 +365,21 @@ int launch_gather_rows(const float* table, int dim, const int64_t* idx, int64_t 
     if (vec && try_wide()) {
         // launched
     } else if (vec) {
-        hipLaunchKernelGGL(gather_rows_vec4, dim3(grid_for(n * (dim / 4))), dim3(256), 0, s, table, dim / 4, idx, n,
-                           out, out_ld);
+        hipLaunchKernelGGL(gather_rows_vec4, dim3(grid_for(n * (dim / 4))), dim3(256), 0, s, table, table_rows,
+                           dim / 4, idx, n, out, out_ld);
     } else {
-        hipLaunchKernelGGL(gather_rows_scalar, dim3(grid_for(n * dim)), dim3(256), 0, s, table, dim, idx, n, out,
-                           out_ld);
+        hipLaunchKernelGGL(gather_rows_scalar, dim3(grid_for(n * dim)), dim3(256), 0, s, table, table_rows, dim, idx,
+                           n, out, out_ld);
     }
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }
 
 int launch_combine(const float* e, int64_t ld_e, const float* f, int64_t ld_f, const float* table,
-                   const int64_t* idx, int64_t n, int dim, float* t, float* a, int64_t ld_ta, float* aug,
+                   int64_t table_rows, const int64_t* idx, int64_t n, int dim, float* t, float* a, int64_t ld_ta, float* aug,
                    hipStream_t s) {
     if (n <= 0) return TTAMM_OK;
-    hipLaunchKernelGGL(combine_kernel, dim3(grid_for(n * dim)), dim3(256), 0, s, e, ld_e, f, ld_f, table, idx, n,
+    hipLaunchKernelGGL(combine_kernel, dim3(grid_for(n * dim)), dim3(256), 0, s, e, ld_e, f, ld_f, table, table_rows, idx, n,
                        dim, t, a, ld_ta, aug);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
@@ -393,9 +421,24 @@ int launch_score_loss(const ScoreArgs& a, hipStream_t s) {
 int score_blocks(int64_t B) { return (int)ceil_div(B, kScoreWaves); }
 
 int launch_loss_finalize(const float* partials, int blocks, int64_t B, int64_t Bg, int N, int D, float lu, float li,
-                         int mimic, const float* cal, float lcal, float* loss_out, double* loss_accum, hipStream_t s) {
+                         int mimic, const float* cal, float lcal, float* loss_out, double* loss_accum,
+                         const uint32_t* status, hipStream_t s) {
     hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, partials, blocks, B, Bg, N, D, lu, li, mimic,
-                       cal, lcal, loss_out, loss_accum);
+                       cal, lcal, loss_out, loss_accum, status);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+}  // namespace ttamm
+
+namespace ttamm {
+
+int launch_stage_rows(const StageArgs& a, hipStream_t s) {
+    TTAMM_REQUIRE(a.count >= 0 && a.count <= kMaxStageSegs, "stage_rows: bad arguments");
+    int64_t most = 0;
+    for (int i = 0; i < a.count; ++i) most = a.seg[i].n > most ? a.seg[i].n : most;
+    if (most == 0) return TTAMM_OK;
+    hipLaunchKernelGGL(stage_rows_kernel, dim3(grid_for(most), a.count), dim3(256), 0, s, a);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

@@ -33,7 +33,8 @@ struct TowerWs {
     int64_t R = 0;
     const int64_t* idx = nullptr;   // ID / mimic table rows
     const int64_t* fidx = nullptr;  // feature rows (null: row r)
-    int64_t* idx_own = nullptr;     // 1-process item tower: [pos; neg]
+    int64_t* idx_own = nullptr;     // staged (range-checked) rows: users / 1-process items [pos; neg] /
+                                    // sharded owner's requested local item rows
     // dropout stream key of row r (see GemmProblem::row_key)
     const int64_t* row_key = nullptr;
     int64_t key_base0 = 0, key_base1 = 0, key_split = 0;
@@ -100,6 +101,7 @@ int validate_tower(const ttamm_tower& T, const char* name, int D, bool training)
     TTAMM_REQUIRE(T.id.dim == D, n + ": embedding dim mismatch");
     TTAMM_REQUIRE(D % 4 == 0, n + ": ttamm requires embedding_dim % 4 == 0");
     TTAMM_REQUIRE(T.id.rows > 0, n + ": empty embedding table");
+    TTAMM_REQUIRE(T.id.rows < (int64_t(1) << 31), n + ": tables of 2^31 rows or more are not supported (int32 row keys)");
     TTAMM_REQUIRE(T.n_linear >= 0 && T.n_linear <= TTAMM_MAX_LINEAR, n + ": too many feature-encoder layers");
     TTAMM_REQUIRE(T.fusion >= TTAMM_FUSION_IDENTITY && T.fusion <= TTAMM_FUSION_GATED, n + ": unsupported fusion");
     if (T.fusion != TTAMM_FUSION_IDENTITY) {
@@ -193,9 +195,9 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         ws.user.wgrad_rps = ws.item.wgrad_rps = wgrad_rows_per_split(shapes, n);
     }
     // ext_io: the item tower's t / a / dT / dA live in the caller's exchange buffers
-    auto tower = [&](const ttamm_tower& T, TowerWs& w, int64_t R, bool own_idx, bool ext_io, int64_t dA_rows) {
+    auto tower = [&](const ttamm_tower& T, TowerWs& w, int64_t R, bool ext_io, int64_t dA_rows) {
         w.R = R;
-        if (own_idx) w.idx_own = ar.take<int64_t>(R);
+        w.idx_own = ar.take<int64_t>(R);
         for (int l = 0; l + 1 < T.n_linear; ++l) {
             w.hid[l] = ar.take<float>((size_t)R * T.linear[l].out_features);
             w.dhid[l] = ar.take<float>((size_t)R * T.linear[l].out_features);
@@ -256,11 +258,11 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
     };
     ws.user.role = ROLE_USER;
     ws.item.role = ROLE_ITEM;
-    tower(A.user, ws.user, B, false, false, B);
+    tower(A.user, ws.user, B, false, B);
     if (shard)
-        tower(A.item, ws.item, A.item_rows_capacity, false, true, 0);
+        tower(A.item, ws.item, A.item_rows_capacity, true, 0);
     else
-        tower(A.item, ws.item, B * (1 + N), true, false, B);
+        tower(A.item, ws.item, B * (1 + N), false, B);
     ws.score_blocks = score_blocks(B);
     ws.partials = ar.take<float>((size_t)ws.score_blocks * 3);
     if (cal_enabled(A) && !shard) {
@@ -409,7 +411,7 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
             TowerWs& w = *W[k];
             float* dst = t.fusion == TTAMM_FUSION_GATED ? w.ef : w.e;
             const int64_t ld = t.fusion == TTAMM_FUSION_GATED ? 2 * D : D;
-            if ((rc = launch_gather_rows(t.id.weight, D, w.idx, w.R, dst, ld, s))) return rc;
+            if ((rc = launch_gather_rows(t.id.weight, t.id.rows, D, w.idx, w.R, dst, ld, s))) return rc;
         }
         // feature encoder layers
         int maxL = 0;
@@ -531,8 +533,8 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
             q.ld_out2 = w.t_ld;
             g2.add(q);
         } else {
-            if ((rc = launch_combine(w.e, D, t.fusion == TTAMM_FUSION_SUM ? w.f : nullptr, D, table, w.idx, w.R, D, w.t,
-                                     w.a, w.t_ld, w.aug, s)))
+            if ((rc = launch_combine(w.e, D, t.fusion == TTAMM_FUSION_SUM ? w.f : nullptr, D, table, t.mimic.rows, w.idx,
+                                     w.R, D, w.t, w.a, w.t_ld, w.aug, s)))
                 return rc;
         }
     }
@@ -711,6 +713,7 @@ struct Deferred {
     int slices = 1;
     int32_t step = 0;  // the dense step this call executes
     int decoupled = 1;
+    const uint32_t* status = nullptr;  // poisoned: the step writes nothing
 };
 
 // The tables of a tower that belong to the dense (AdamW) group.
@@ -743,6 +746,7 @@ int tower_prepare(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred& 
     ra.hist = df.hist;
     ra.cap = df.cap;
     ra.decoupled = df.decoupled;
+    ra.status = df.status;
     ra.target = df.step - 1;
     const ttamm_table* tabs[2];
     const int n = dense_tables(t, mimic, tabs);
@@ -845,6 +849,7 @@ int tower_optimizer_rows(const ttamm_tower& t, TowerWs& w, int D, bool mimic, co
     ru.sp = sp;
     ru.ad = ad;
     ru.dense_step = df.step;
+    ru.status = df.status;
     return launch_row_update(ru, s);
 }
 void add_seg(SweepArgs& sw, const ttamm_table& tb) {
@@ -869,6 +874,7 @@ int table_updates(const ttamm_tower* T[2], TowerWs* W[2], int n, int D, bool mim
         ra.hist = df.hist;
         ra.cap = df.cap;
         ra.decoupled = df.decoupled;
+        ra.status = df.status;
         ra.target = df.step;
         ra.stamp = 1;
         const int slice = df.step % df.slices;
@@ -891,6 +897,7 @@ int table_updates(const ttamm_tower* T[2], TowerWs* W[2], int n, int D, bool mim
     SweepArgs sw;
     std::memset(&sw, 0, sizeof(sw));
     sw.ad = ad;
+    sw.status = df.status;
     if (mimic)
         for (int k = 0; k < n; ++k) add_seg(sw, T[k]->mimic);
     for (int k = 0; k < n; ++k)
@@ -903,19 +910,21 @@ int table_updates(const ttamm_tower* T[2], TowerWs* W[2], int n, int D, bool mim
         TowerWs& w = *W[k];
         if (mimic)
             if ((rc = launch_side_scatter(w.co.n_unique, w.co.keys_out, w.co.seg_start, w.side_mimic, w.R, D, t.mimic,
-                                          s)))
+                                          df.status, s)))
                 return rc;
         if (t.id.optimizer == TTAMM_OPT_DENSE)
-            if ((rc = launch_side_scatter(w.co.n_unique, w.co.keys_out, w.co.seg_start, w.side_id, w.R, D, t.id, s)))
+            if ((rc = launch_side_scatter(w.co.n_unique, w.co.keys_out, w.co.seg_start, w.side_id, w.R, D, t.id,
+                                          df.status, s)))
                 return rc;
     }
     return TTAMM_OK;
 }
 
-int dense_update(const ttamm_tower* T[2], TowerWs* W[2], const AdamConsts& ad, hipStream_t s) {
+int dense_update(const ttamm_tower* T[2], TowerWs* W[2], const AdamConsts& ad, const uint32_t* status, hipStream_t s) {
     DenseAdamArgs da;
     std::memset(&da, 0, sizeof(da));
     da.ad = ad;
+    da.status = status;
     auto add_dense = [&](float* p, float* m, float* v, const float* g, int64_t n) {
         da.t[da.count++] = DenseTensor{p, m, v, g, n};
     };
@@ -1031,13 +1040,13 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     // ---- row bindings -----------------------------------------------------------------------
     TowerWs& U = ws.user;
     TowerWs& I = ws.item;
-    U.idx = U.fidx = A.b.users;
+    U.idx = U.fidx = U.idx_own;  // staged copy of A.b.users
     U.key_split = B;
     U.key_base0 = A.row_base;
     int64_t* neg = nullptr;
     if (shard) {
         I.R = A.n_item_rows;
-        I.idx = I.fidx = A.item_rows;
+        I.idx = I.fidx = I.idx_own;  // staged copy of A.item_rows
         I.row_key = A.item_row_keys;
         I.t = A.item_fwd_out;
         I.a = mimic && A.item_fwd_out ? A.item_fwd_out + D : nullptr;
@@ -1067,23 +1076,46 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
                                                hp.sparse_step);
     Deferred df;
     if ((rc = deferred_of(A, df))) return rc;
-    if (df.on && (ph & (TTAMM_PHASE_ITEM_FWD | TTAMM_PHASE_USER_FWD)))
-        if ((rc = launch_history_put(df.hist, df.cap, df.step, ad, s))) return rc;
+    df.status = A.status;
 
-    // ---- negatives --------------------------------------------------------------------------
+    // ---- indices and negatives ---------------------------------------------------------------
     if (ph & TTAMM_PHASE_SAMPLE) {
-        if (!shard)
-            TTAMM_HIP(hipMemcpyAsync(I.idx_own, A.b.pos_items, B * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+        // range-checked copies of the batch's ids (nn.Embedding raises IndexError,
+        // encoders.py:222-223): an out-of-range id sets TTAMM_STATUS_INDEX_OUT_OF_RANGE, is
+        // replaced by row 0 so no kernel reads outside a table, and the step writes nothing
+        StageArgs st;
+        std::memset(&st, 0, sizeof(st));
+        st.status = A.status;
+        st.seg[st.count++] = StageSeg{A.b.users, U.idx_own, B, A.user.id.rows};
+        if (!shard) {
+            st.seg[st.count++] = StageSeg{A.b.pos_items, I.idx_own, B, A.item.id.rows};
+            if (!A.b.sample_negatives) {
+                TTAMM_REQUIRE(A.b.neg_items != nullptr, "negatives must be given when sample_negatives == 0");
+                st.seg[st.count++] = StageSeg{A.b.neg_items, neg, B * N, A.item.id.rows};
+            }
+        } else {  // requester: global item ids, checked only (the owners stage their local rows)
+            st.seg[st.count++] = StageSeg{A.b.pos_items, nullptr, B, num_items};
+            if (!A.b.sample_negatives && A.b.neg_items) st.seg[st.count++] = StageSeg{A.b.neg_items, nullptr, B * N, num_items};
+        }
+        TTAMM_REQUIRE(A.status != nullptr, "the training step needs a status word");
+        if ((rc = launch_stage_rows(st, s))) return rc;
         if (A.b.sample_negatives) {
-            if ((rc = launch_sample_negatives(A.b.users, B, N, num_items, A.b.pos_offsets, A.b.pos_values, A.b.seed,
+            if ((rc = launch_sample_negatives(U.idx_own, B, N, num_items, A.b.pos_offsets, A.b.pos_values, A.b.seed,
                                               A.b.counter, A.row_base * N, neg, A.status, s)))
                 return rc;
             if (!shard && A.b.neg_items)
                 TTAMM_HIP(hipMemcpyAsync(A.b.neg_items, neg, B * N * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
-        } else if (!shard) {
-            TTAMM_REQUIRE(A.b.neg_items != nullptr, "negatives must be given when sample_negatives == 0");
-            TTAMM_HIP(hipMemcpyAsync(neg, A.b.neg_items, B * N * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
         }
+        // count the step and publish its AdamW constants, unless a status error stops it
+        if ((rc = launch_step_begin(A.status, A.steps_applied, df.on ? df.hist : nullptr, df.cap, df.step, ad, s)))
+            return rc;
+    }
+    if (shard && (ph & TTAMM_PHASE_ITEM_FWD) && I.R > 0) {  // owner: stage the requested local rows
+        StageArgs st;
+        std::memset(&st, 0, sizeof(st));
+        st.status = A.status;
+        st.seg[st.count++] = StageSeg{A.item_rows, I.idx_own, I.R, A.item.id.rows};
+        if ((rc = launch_stage_rows(st, s))) return rc;
     }
     // ---- forward ----------------------------------------------------------------------------
     hipStream_t aux = static_cast<hipStream_t>(A.aux_stream);
@@ -1157,14 +1189,14 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         if (A.loss_out) {
             if ((rc = launch_loss_finalize(ws.partials, ws.score_blocks, B, Bg, N, D, sa.lambda_u, sa.lambda_i, sa.mimic,
                                            ws.cal_on ? ws.cal.out : nullptr, (float)A.hp.lambda_category_alignment,
-                                           A.loss_out, A.loss_accum, s)))
+                                           A.loss_out, A.loss_accum, A.status, s)))
                 return rc;
         }
         if (!shard) {
             // ---- the whole backward + optimizers in one process --------------------------------
             if ((rc = tower_backward(T, W, D, s, 2))) return rc;
             if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, s))) return rc;
-            return dense_update(T, W, ad, s);
+            return dense_update(T, W, ad, A.status, s);
         }
         if ((rc = tower_backward(T, W, D, s, 1))) return rc;
         if ((rc = table_updates(T, W, 1, D, mimic, sp, ad, df, nullptr, s))) return rc;
@@ -1183,7 +1215,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         if ((rc = table_updates(Ti, Wi, 1, D, mimic, sp, ad, df, A.timing_events, s))) return rc;
     }
     if (ph & TTAMM_PHASE_DENSE)
-        if ((rc = dense_update(T, W, ad, s))) return rc;
+        if ((rc = dense_update(T, W, ad, A.status, s))) return rc;
     return TTAMM_OK;
 }
 
@@ -1236,6 +1268,7 @@ size_t tower_forward_workspace_size(const ttamm_tower& T, int64_t n) {
     ar.take<float>((size_t)n * D);      // f
     if (T.fusion == TTAMM_FUSION_GATED) ar.take<float>((size_t)n * T.gate[0].out_features);
     for (int q = 0; q < 3; ++q) ar.take<float>((size_t)n * D);  // g, t, a
+    ar.take<int64_t>(n);                                         // range-checked ids
     if (needs_wpad(T)) ar.take<float>((size_t)T.linear[0].out_features * round4(T.linear[0].in_features));
     return ar.off + 256;
 }
@@ -1245,6 +1278,8 @@ int tower_forward_eval(const ttamm_tower& T, const int64_t* idx, const int64_t* 
     const int D = T.id.dim;
     int rc;
     if ((rc = validate_tower(T, "tower", D, false))) return rc;
+    if (augment && T.mimic.weight)
+        TTAMM_REQUIRE(T.mimic.rows == T.id.rows && T.mimic.dim == D, "tower: mimic table shape does not match the tower");
     if (n <= 0) return TTAMM_OK;
     Arena ar{static_cast<char*>(wsp), ws_bytes, 0, false};
     TowerWs w;
@@ -1258,8 +1293,19 @@ int tower_forward_eval(const ttamm_tower& T, const int64_t* idx, const int64_t* 
     float* gbuf = ar.take<float>((size_t)n * D);
     float* tbuf = ar.take<float>((size_t)n * D);
     float* abuf = ar.take<float>((size_t)n * D);
+    int64_t* idxc = ar.take<int64_t>(n);
     if (needs_wpad(T)) w.wpad = ar.take<float>((size_t)T.linear[0].out_features * round4(T.linear[0].in_features));
     TTAMM_REQUIRE(ar.ok(), "workspace too small for tower forward");
+    {  // ids outside the tables read row 0 (the Python mirror raises IndexError before calling)
+        StageArgs st;
+        std::memset(&st, 0, sizeof(st));
+        st.seg[st.count++] = StageSeg{idx, idxc, n, T.id.rows};
+        if ((rc = launch_stage_rows(st, s))) return rc;
+        if (fidx == idx) fidx = idxc;
+        idx = idxc;
+        w.idx = idx;
+        w.fidx = fidx;
+    }
     if (T.fusion == TTAMM_FUSION_GATED) {
         w.ef = efbuf;
         w.z = zbuf;

@@ -22,6 +22,7 @@ MAX_LINEAR = 4
 FUSION_IDENTITY, FUSION_SUM, FUSION_GATED = 0, 1, 2
 OPT_SPARSE_ADAM, OPT_DENSE = 0, 1
 STATUS_SAMPLER_EXHAUSTED = 1
+STATUS_INDEX_OUT_OF_RANGE = 2
 
 _NATIVE_DIR = Path(__file__).resolve().parent / "_native"
 LIB_PATH = _NATIVE_DIR / "libttamm.so"
@@ -147,10 +148,11 @@ class StepArgs(ctypes.Structure):
         ("item_categories", c_vp),
         ("num_categories", c_i64),
         ("major_category", c_i64),
+        ("steps_applied", c_vp),
     ]
 
 
-ABI_VERSION = 9  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 10  # ttamm.h TTAMM_ABI_VERSION
 
 # ttamm.h TTAMM_PHASE_*
 PHASE_ALL = 0
@@ -245,6 +247,17 @@ def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
 
 def stream_handle(device: torch.device | None = None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def check_index_range(idx: torch.Tensor, rows: int) -> None:
+    """nn.Embedding's check (encoders.py:222-223 runs F.embedding): an id outside [0, rows)
+    raises IndexError("index out of range in self").  One device->host read; used by the module
+    (eval) entry points, while the fused step reports bad ids through its status word."""
+    if idx.numel() == 0:
+        return
+    lo, hi = torch.aminmax(idx.reshape(-1))
+    if int(lo) < 0 or int(hi) >= rows:
+        raise IndexError("index out of range in self")
 
 
 def require_rocm(t: torch.Tensor, what: str) -> None:

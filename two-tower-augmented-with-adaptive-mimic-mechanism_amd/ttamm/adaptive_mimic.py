@@ -70,6 +70,7 @@ class AdaptiveMimicMechanism(nn.Module):
                 "use ttamm.train_one_epoch or torch.no_grad()"
             )
         flat = indices.reshape(-1).contiguous()
+        _lib.check_index_range(flat, table.num_embeddings)
         base = reference.reshape(flat.numel(), -1)
         if base.shape[1] != self.embedding_dim:
             raise ValueError("Adaptive mimic: embedding width does not match the augmentation tables.")

@@ -389,6 +389,7 @@ def tower_forward(
         features = None
     use_features = tower.fusion != "identity" and features is not None
     idx = indices.reshape(-1).contiguous()
+    _lib.check_index_range(idx, tower.num_embeddings)
     n = idx.numel()
     out = torch.empty((n, tower.id_dim), dtype=torch.float32, device=idx.device)
     if not use_features and tower.fusion != "identity":

@@ -32,6 +32,7 @@ def _encode(tower: TowerEncoder, mimic_table: torch.Tensor | None, rows: torch.T
     out = torch.empty((n, D), dtype=torch.float32, device=dev)
     if n == 0:
         return out
+    _lib.check_index_range(rows, tower.num_embeddings)
     feats = _pad_features(features) if tower.fusion != "identity" else None
     if tower.fusion != "identity" and feats is None:
         # no features: the reference falls back to the ID embedding (encoders.py:228-231)

@@ -91,6 +91,13 @@ def sample_negative_items(
     users = user_indices.to(device=device, dtype=torch.long).reshape(-1).contiguous()
     _lib.require_rocm(users, "sample_negative_items")
     need = int(users.max().item()) + 1 if users.numel() else 0
+    if users.numel() and int(users.min().item()) < 0:
+        # positives.get(u, set()) in the reference: an id with no entry has no positives; point
+        # negative ids at an empty CSR row past the largest user
+        need = max(need, (max(positives) + 1) if isinstance(positives, Mapping) and positives else 0,
+                   positives.num_users if isinstance(positives, PositivesCSR) else 0)
+        users = torch.where(users < 0, torch.full_like(users, need), users)
+        need += 1
     csr = positives_csr(positives, device=device, num_users=need)
     if csr.max_degree >= num_items:
         degrees = (csr.offsets[1:] - csr.offsets[:-1]).index_select(0, users.clamp(max=csr.num_users - 1))

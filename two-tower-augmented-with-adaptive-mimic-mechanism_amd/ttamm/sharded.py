@@ -339,7 +339,12 @@ class ShardedTrainStep(FusedTrainStep):
         self.comm.run(self.program(users, pos_items, neg_items, keep_masks=keep_masks, timing_events=timing_events))
 
     def finish_program(self) -> Program:
-        """Collective finish: global epoch loss (sum of the ranks' shares)."""
+        """Collective finish: global epoch loss (sum of the ranks' shares).  A status error on
+        any rank (an out-of-range id, sampler exhaustion) raises on every rank; each rank's own
+        tables hold the state after its last good step."""
+        flags = torch.stack([(self.status & b) != 0 for b in (1, 2)]).reshape(-1).to(torch.float32)
+        yield AllReduce(flags)
+        self.status.bitwise_or_((flags[0] > 0).to(torch.int32) + 2 * (flags[1] > 0).to(torch.int32))
         yield AllReduce(self.loss_accum)
         return FusedTrainStep.finish(self)
 

@@ -201,6 +201,13 @@ class FusedTrainStep:
                     for i in (0, 2):
                         dense_param(tower.adaptive_mimic.gate_network[i].weight)
                         dense_param(tower.adaptive_mimic.gate_network[i].bias)
+            elif tower.fusion != "identity":
+                # no feature rows: the reference's tower falls back to the ID embedding
+                # (encoders.py:228-231), so these parameters get no gradient and torch's
+                # optimizers skip them (no state, no step) — as here
+                for p in tower.parameters():
+                    if p is not emb:
+                        handled.add(id(p))
             self.towers[name] = (tower, feats if uses_features else None, id_opt)
         self.mimic_tables = {}
         if mimic is not None:
@@ -260,9 +267,11 @@ class FusedTrainStep:
         self.loss_out = torch.zeros(5, dtype=torch.float32, device=self.device)
         self.loss_accum = torch.zeros(2, dtype=torch.float64, device=self.device)
         self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.steps_applied = torch.zeros(1, dtype=torch.int64, device=self.device)
         args.loss_out = self.loss_out.data_ptr()
         args.loss_accum = self.loss_accum.data_ptr()
         args.status = self.status.data_ptr()
+        args.steps_applied = self.steps_applied.data_ptr()
         self.max_batch = int(max_batch)
         args.b.batch = self.max_batch
         self.lib = _lib.load()
@@ -387,18 +396,32 @@ class FusedTrainStep:
         self.args.hp.dense_step = self.dense_step0 + self.steps_done
         _lib.check(self.lib.ttamm_flush_tables(ctypes.byref(self.args), _lib.stream_handle(self.device)))
 
+    def _status_error(self) -> int:
+        """Synchronise and return the device status bits.  After an error the device skipped
+        every later step (ttamm.h TTAMM_STATUS_*): count only the steps that ran."""
+        torch.cuda.current_stream(self.device).synchronize()
+        status = int(self.status.item())
+        if status:
+            self.steps_done = int(self.steps_applied.item())
+        return status
+
     def finish(self) -> float:
         """Flush deferred table updates, synchronise, surface device-side errors, write the
         optimizer step counters back, and return the epoch's mean loss weighted by positives
-        (training.py:829-833)."""
+        (training.py:829-833).  A batch id outside its table raises IndexError (nn.Embedding,
+        encoders.py:222-223), sampler exhaustion RuntimeError (samplers.py:78-81); either way the
+        parameters and optimizer state are those after the last good step."""
+        status = self._status_error()
         self.flush()
         torch.cuda.current_stream(self.device).synchronize()
-        if int(self.status.item()) & _lib.STATUS_SAMPLER_EXHAUSTED:
-            raise RuntimeError("Exceeded resampling attempts while drawing negatives.")
         for st in self._adam_steps:
             st["step"].fill_(float(self.dense_step0 + self.steps_done))
         for st in self._sparse_steps:
             st["step"] = self.sparse_step0 + self.steps_done
+        if status & _lib.STATUS_INDEX_OUT_OF_RANGE:
+            raise IndexError("index out of range in self")
+        if status & _lib.STATUS_SAMPLER_EXHAUSTED:
+            raise RuntimeError("Exceeded resampling attempts while drawing negatives.")
         total, count = self.loss_accum.tolist()
         return total / max(count, 1.0)
 
