@@ -260,6 +260,16 @@ int ttamm_retrieval_topk(const float* queries, int64_t n_queries, int64_t ldq, c
                          int32_t k, float* out_scores, int64_t* out_ids, void* workspace, size_t workspace_bytes,
                          void* stream);
 
+/* The no-FAISS branch of _evaluate_model, _retrieve_with_sampling (training.py:974-1009): query q
+ * scores its candidate list — items rows cand_rows[cand_offsets[q] .. cand_offsets[q+1]), at most
+ * max_candidates (<= 4096) per query — by inner product, or by cosine similarity of the
+ * F.normalize'd vectors when cosine != 0 (:999-1003), and returns the k best LIST POSITIONS
+ * (torch.topk(scores, k), sorted; equal scores by list position), -1 / -inf past the list. */
+int ttamm_candidate_topk(const float* queries, int64_t n_queries, int64_t ldq, const float* items, int64_t n_items,
+                         int64_t ldi, int32_t dim, const int64_t* cand_offsets, const int64_t* cand_rows,
+                         int32_t max_candidates, int32_t cosine, int32_t k, float* out_scores, int64_t* out_positions,
+                         void* stream);
+
 /* faiss.normalize_L2 on device rows, in place (training.py:670-672 on the item matrix and
  * :954-955 on the queries when the model's similarity is cosine): row r of the [n, dim] matrix
  * with leading dim ld is scaled by 1 / sqrt(sum of its squares); rows of norm 0 are left as

@@ -207,7 +207,7 @@ def gather_aug(table: nn.Embedding, idx: torch.Tensor, reference: torch.Tensor):
 # sampler (samplers.py:11-85)
 # ---------------------------------------------------------------------------------------
 def sample_negative_items(users: torch.Tensor, *, num_items: int, positives: Mapping[int, set[int]],
-                          num_negatives: int) -> torch.Tensor:
+                          num_negatives: int, generator: torch.Generator | None = None) -> torch.Tensor:
     if num_negatives <= 0:
         raise ValueError("num_negatives must be greater than zero.")
     if num_items <= 1:
@@ -224,12 +224,12 @@ def sample_negative_items(users: torch.Tensor, *, num_items: int, positives: Map
             if pt is None:
                 pt = torch.tensor(sorted(pos), dtype=torch.long)
                 cache[int(u)] = pt
-        draw = torch.randint(0, num_items, (num_negatives,), dtype=torch.long)
+        draw = torch.randint(0, num_items, (num_negatives,), dtype=torch.long, generator=generator)
         if pt is not None:
             bad = torch.isin(draw, pt)
             rounds = 0
             while bad.any():
-                draw[bad] = torch.randint(0, num_items, (int(bad.sum().item()),), dtype=torch.long)
+                draw[bad] = torch.randint(0, num_items, (int(bad.sum().item()),), dtype=torch.long, generator=generator)
                 bad = torch.isin(draw, pt)
                 rounds += 1
                 if rounds > 10:
@@ -398,16 +398,27 @@ def train_step(
 
 def train_one_epoch(model, batches: Iterable, optimizers, *, negatives_per_positive: int, num_items: int,
                     positives: Mapping[int, set[int]], user_features, item_features,
-                    loss_weights: Mapping[str, float] | None = None, max_steps: int | None = None) -> tuple[float, int, float]:
+                    loss_weights: Mapping[str, float] | None = None, max_steps: int | None = None,
+                    item_category_tensor: torch.Tensor | None = None, major_category_id: int | None = None,
+                    batch_hook=None, step_losses: list | None = None) -> tuple[float, int, float]:
     """training.py:700-833 with the reference's per-row sampler; returns
-    (mean loss, interactions, seconds)."""
+    (mean loss, interactions, seconds).  ``batch_hook(step, users, pos) -> (negatives | None,
+    {"user": masks, "item": masks} | None)`` injects the RNG streams (the same hook ttamm's
+    train_one_epoch takes); ``step_losses`` collects each step's StepResult."""
     running, seen, steps = 0.0, 0, 0
     t0 = time.perf_counter()
     for users, pos in batches:
-        neg = sample_negative_items(users, num_items=num_items, positives=positives,
-                                    num_negatives=negatives_per_positive)
-        res = train_step(model, optimizers, users, pos, neg, user_features=user_features,
-                         item_features=item_features, loss_weights=loss_weights)
+        neg, masks = batch_hook(steps, users, pos) if batch_hook is not None else (None, None)
+        if neg is None:
+            neg = sample_negative_items(users, num_items=num_items, positives=positives,
+                                        num_negatives=negatives_per_positive)
+        masks = masks or {}
+        res = train_step(model, optimizers, users, pos, neg.reshape(users.shape[0], -1), user_features=user_features,
+                         item_features=item_features, loss_weights=loss_weights,
+                         user_keep_masks=masks.get("user"), item_keep_masks=masks.get("item"),
+                         item_category_tensor=item_category_tensor, major_category_id=major_category_id)
+        if step_losses is not None:
+            step_losses.append(res)
         running += res.total * users.shape[0]
         seen += users.shape[0]
         steps += 1
@@ -579,4 +590,52 @@ def evaluate_model(model: OracleModel, *, train_positive_map: Mapping[int, set[i
             query = normalize_l2(emb.numpy())[0] if normalize else emb[0].numpy()
             preds[u] = retrieve_with_faiss(items, query, set(train_positive_map.get(u, set())), gt,
                                            max_k=max_k, faiss_search_k=faiss_search_k)
+    return preds, truth
+
+
+def evaluate_model_sampled(model: OracleModel, *, train_positive_map: Mapping[int, set[int]],
+                           val_pairs: Sequence[tuple[int, int]], item_features: torch.Tensor | None,
+                           user_features: torch.Tensor | None, num_items: int, k_values: Iterable[int],
+                           candidate_samples: int, rng: np.random.Generator, cosine: bool = True
+                           ) -> tuple[dict[int, list[int]], dict[int, set[int]]]:
+    """training.py:917-1043 without FAISS: _retrieve_with_sampling (:974-1009) per validation user,
+    users ascending (DataFrame.groupby), the Python set / rng.choice calls as the reference makes
+    them; scores by CosineSimilarity of F.normalize'd vectors (cosine model) or the dot product."""
+    max_k = max(k_values)
+    groups: dict[int, list[int]] = {}
+    for u, i in val_pairs:
+        groups.setdefault(int(u), []).append(int(i))
+    preds: dict[int, list[int]] = {}
+    truth: dict[int, set[int]] = {}
+    model.eval()
+    with torch.no_grad():
+        for u in sorted(groups):
+            gt = set(groups[u])
+            if not gt:
+                continue
+            truth[u] = gt
+            idx = torch.tensor([u], dtype=torch.long)
+            feats = user_features.index_select(0, idx) if user_features is not None else None
+            ue = tower_forward(model.user_encoder, idx, feats, training=False)
+            if model.adaptive_mimic is not None:
+                ue = gather_aug(model.adaptive_mimic.user_augmented, idx, ue)[0]
+            blocked = set(train_positive_map.get(u, set()))
+            candidates = set(gt)
+            available = list(set(range(num_items)) - blocked)
+            if available:
+                budget = max(0, min(candidate_samples, len(available)))
+                if budget > 0:
+                    candidates.update(int(n) for n in rng.choice(available, size=budget, replace=False).tolist())
+            cand = list(candidates)
+            ct = torch.tensor(cand, dtype=torch.long)
+            cf = item_features.index_select(0, ct) if item_features is not None else None
+            ce = tower_forward(model.item_encoder, ct, cf, training=False)
+            if model.adaptive_mimic is not None:
+                ce = gather_aug(model.adaptive_mimic.item_augmented, ct, ce)[0]
+            if cosine:
+                scores = F.cosine_similarity(F.normalize(ue, dim=-1), F.normalize(ce, dim=-1), dim=-1)
+            else:
+                scores = (ue * ce).sum(dim=-1)
+            top = torch.topk(scores.reshape(-1), k=min(max_k, len(cand)))
+            preds[u] = [cand[i] for i in top.indices.tolist()]
     return preds, truth

@@ -64,6 +64,15 @@ TTAMM_API int ttamm_retrieval_topk(const float* queries, int64_t n_queries, int6
                                  out_scores, out_ids, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
+TTAMM_API int ttamm_candidate_topk(const float* queries, int64_t n_queries, int64_t ldq, const float* items,
+                                   int64_t n_items, int64_t ldi, int32_t dim, const int64_t* cand_offsets,
+                                   const int64_t* cand_rows, int32_t max_candidates, int32_t cosine, int32_t k,
+                                   float* out_scores, int64_t* out_positions, void* stream) {
+    g_last_error.clear();
+    return launch_candidate_topk(queries, n_queries, ldq, items, n_items, ldi, dim, cand_offsets, cand_rows,
+                                 max_candidates, cosine, k, out_scores, out_positions, (hipStream_t)stream);
+}
+
 TTAMM_API int ttamm_normalize_rows(float* rows, int64_t n, int32_t dim, int64_t ld, void* stream) {
     g_last_error.clear();
     return launch_normalize_rows(rows, n, dim, ld, (hipStream_t)stream);

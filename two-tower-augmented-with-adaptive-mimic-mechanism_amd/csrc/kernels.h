@@ -231,6 +231,9 @@ struct RetrievalArgs {
 };
 size_t retrieval_workspace_bytes(int64_t nq, int64_t ni, int dim, int k);
 int launch_normalize_rows(float* x, int64_t n, int dim, int64_t ld, hipStream_t s);
+int launch_candidate_topk(const float* Q, int64_t nq, int64_t ldq, const float* X, int64_t ni, int64_t ldx, int dim,
+                          const int64_t* coff, const int64_t* crow, int max_candidates, int cosine, int k, float* out_s,
+                          int64_t* out_p, hipStream_t s);
 int launch_retrieval_topk(const float* Q, int64_t nq, int64_t ldq, const float* X, int64_t ni, int64_t ldx, int dim,
                           const int64_t* boff, const int64_t* bval, int k, float* out_s, int64_t* out_i, void* ws,
                           size_t ws_bytes, hipStream_t s);

@@ -293,7 +293,80 @@ __global__ __launch_bounds__(256) void normalize_rows_kernel(float* __restrict__
     }
 }
 
+// Sampled-candidate retrieval (_retrieve_with_sampling, training.py:974-1009): one block per
+// query scores its candidates (one wave per candidate, lanes over D), cosine when `cosine`
+// (F.normalize on both sides, :999-1003), then ranks them: a candidate's rank is the number of
+// candidates with a larger score, or an equal score at an earlier list position (torch.topk
+// order, sorted=True); ranks < k are written.  Candidate lists are at most kCandCap long.
+constexpr int kCandCap = 4096;
+
+__global__ __launch_bounds__(256) void candidate_topk_kernel(const float* __restrict__ Q, int64_t ldq,
+                                                             const float* __restrict__ X, int64_t ni, int64_t ldx,
+                                                             int dim, const int64_t* __restrict__ coff,
+                                                             const int64_t* __restrict__ crow, int cosine, int k,
+                                                             float* __restrict__ out_s, int64_t* __restrict__ out_p) {
+    __shared__ float sc[kCandCap];
+    __shared__ float qn;
+    const int64_t q = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t c0 = coff[q];
+    const int nc = (int)(coff[q + 1] - c0);
+    const float* qr = Q + q * ldq;
+    if (wave == 0) {  // ||query||
+        float ss = 0.f;
+        for (int d = lane; d < dim; d += 64) ss = fmaf(qr[d], qr[d], ss);
+        ss = wave_sum(ss);
+        if (lane == 0) qn = fmaxf(sqrtf(ss), 1e-12f);
+    }
+    __syncthreads();
+    for (int c = wave; c < nc; c += 4) {
+        const int64_t r = crow[c0 + c];
+        float dot = 0.f, ss = 0.f;
+        if (r >= 0 && r < ni) {
+            const float* xr = X + r * ldx;
+            for (int d = lane; d < dim; d += 64) {
+                dot = fmaf(qr[d], xr[d], dot);
+                ss = fmaf(xr[d], xr[d], ss);
+            }
+        }
+        dot = wave_sum(dot);
+        ss = wave_sum(ss);
+        if (lane == 0) sc[c] = cosine ? dot / (qn * fmaxf(sqrtf(ss), 1e-12f)) : dot;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
+        const float v = sc[c];
+        int rank = 0;
+        for (int o = 0; o < nc; ++o) {
+            const float w = sc[o];
+            rank += (w > v || (w == v && o < c)) ? 1 : 0;
+        }
+        if (rank < k) {
+            out_s[q * k + rank] = v;
+            out_p[q * k + rank] = c;
+        }
+    }
+    for (int r = nc + threadIdx.x; r < k; r += blockDim.x) {  // fewer candidates than k
+        out_s[q * k + r] = -INFINITY;
+        out_p[q * k + r] = -1;
+    }
+}
+
 }  // namespace
+
+int launch_candidate_topk(const float* Q, int64_t nq, int64_t ldq, const float* X, int64_t ni, int64_t ldx, int dim,
+                          const int64_t* coff, const int64_t* crow, int max_candidates, int cosine, int k, float* out_s,
+                          int64_t* out_p, hipStream_t s) {
+    TTAMM_REQUIRE(nq >= 0 && ni >= 0 && dim > 0 && ldq >= dim && ldx >= dim, "candidate_topk: bad shape");
+    TTAMM_REQUIRE(k >= 1, "candidate_topk: k must be >= 1");
+    TTAMM_REQUIRE(max_candidates >= 0 && max_candidates <= kCandCap, "candidate_topk: at most 4096 candidates per query");
+    if (nq == 0) return TTAMM_OK;
+    TTAMM_REQUIRE(Q && coff && out_s && out_p && (crow || max_candidates == 0), "candidate_topk: null pointer");
+    hipLaunchKernelGGL(candidate_topk_kernel, dim3((unsigned)nq), dim3(256), 0, s, Q, ldq, X, ni, ldx, dim, coff, crow,
+                       cosine, k, out_s, out_p);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
 
 int launch_normalize_rows(float* x, int64_t n, int dim, int64_t ld, hipStream_t s) {
     TTAMM_REQUIRE(n >= 0 && dim > 0 && ld >= dim, "normalize_rows: bad shape");

@@ -13,6 +13,7 @@ from .encoders import (
     build_id_embedding,
     build_tower_encoder,
 )
+from .retrieval import encode_item_embeddings, evaluate_model, prepare_faiss_resources
 from .samplers import PositivesCSR, sample_negative_items
 from .training import DotProductSimilarity, FusedTrainStep, _collect_parameter_groups, train_one_epoch
 from .two_tower import TwoTowerModel
@@ -30,6 +31,9 @@ __all__ = [
     "build_feature_encoder",
     "build_id_embedding",
     "build_tower_encoder",
+    "encode_item_embeddings",
+    "evaluate_model",
+    "prepare_faiss_resources",
     "sample_negative_items",
     "train_one_epoch",
 ]

@@ -175,6 +175,10 @@ SIGNATURES = {
     "ttamm_adam_history_entry_bytes": (ctypes.c_size_t, []),
     "ttamm_retrieval_topk_workspace_size": (ctypes.c_size_t, [c_i64, c_i64, c_i32, c_i32]),
     "ttamm_normalize_rows": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i64, c_vp]),
+    "ttamm_candidate_topk": (
+        ctypes.c_int,
+        [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],
+    ),
     "ttamm_retrieval_topk": (
         ctypes.c_int,
         [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, ctypes.c_size_t, c_vp],

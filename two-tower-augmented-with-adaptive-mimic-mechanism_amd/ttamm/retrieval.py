@@ -13,6 +13,7 @@ from __future__ import annotations
 import ctypes
 from typing import Any, Iterable, Mapping, Sequence
 
+import numpy as np
 import torch
 from torch import nn
 
@@ -147,6 +148,80 @@ def retrieve_topk(queries: torch.Tensor, items: torch.Tensor, k: int, *,
     return scores, ids
 
 
+def prepare_faiss_resources(model, *, num_items: int, item_features: torch.Tensor | None, device: torch.device,
+                            similarity_module: nn.Module | None = None, batch_size: int = 262_144,
+                            retain_embeddings: bool = False) -> dict[str, Any] | None:
+    """_prepare_faiss_resources (training.py:646-679): the item matrix of the exact inner-product
+    index — kept in HBM instead of a faiss.IndexFlatIP — L2-normalised when the similarity is
+    cosine.  Pass the result as ``faiss_resources`` to evaluate_model."""
+    if num_items == 0:
+        return None
+    emb = encode_item_embeddings(model, num_items=num_items, item_features=item_features, device=device,
+                                 batch_size=batch_size)
+    sim = similarity_module if similarity_module is not None else getattr(model, "similarity", None)
+    normalize = isinstance(sim, nn.CosineSimilarity)
+    if normalize:
+        normalize_rows(emb)
+    out: dict[str, Any] = {"index": emb, "normalize": normalize}
+    if retain_embeddings:
+        out["embeddings"] = emb
+    return out
+
+
+def sampled_candidates(users: Sequence[int], truth: Mapping[int, set[int]], blocked: Mapping[int, Iterable[int]],
+                       *, num_items: int, candidate_samples: int, rng: np.random.Generator) -> list[list[int]]:
+    """Candidate lists of _retrieve_with_sampling (training.py:979-987), drawing from ``rng`` in
+    the reference's order (one rng.choice per user, users ascending as DataFrame.groupby yields
+    them): the user's ground truth plus up to ``candidate_samples`` distinct unblocked items.
+    ``list(set(range(n)) - blocked)`` iterates in ascending order (CPython stores small ints at
+    their own hash slot, and the set's table is larger than n), so the sorted setdiff is the same
+    array and rng.choice picks the same items.  The list order is the reference's set order."""
+    everything = np.arange(num_items, dtype=np.int64)
+    lists: list[list[int]] = []
+    for u in users:
+        cands = set(truth[u])
+        b = blocked.get(int(u), ())
+        avail = everything if not b else np.setdiff1d(everything, np.fromiter(b, dtype=np.int64), assume_unique=False)
+        if avail.size:
+            budget = max(0, min(int(candidate_samples), int(avail.size)))
+            if budget > 0:
+                cands.update(int(n) for n in rng.choice(avail, size=budget, replace=False).tolist())
+        lists.append(list(cands))
+    return lists
+
+
+def _evaluate_sampled(model, users: list[int], truth: dict[int, set[int]], blocked: Mapping[int, Iterable[int]], *,
+                      item_features, user_features, device, num_items: int, candidate_samples: int, max_k: int,
+                      rng: np.random.Generator) -> dict[int, list[int]]:
+    """_retrieve_with_sampling for every user in one launch (ttamm_candidate_topk)."""
+    lists = sampled_candidates(users, truth, blocked, num_items=num_items, candidate_samples=candidate_samples, rng=rng)
+    flat = np.fromiter((i for c in lists for i in c), dtype=np.int64)
+    offsets = np.zeros(len(lists) + 1, dtype=np.int64)
+    np.cumsum([len(c) for c in lists], out=offsets[1:])
+    most = max((len(c) for c in lists), default=0)
+    uniq, rows = np.unique(flat, return_inverse=True)
+    mimic = getattr(model, "adaptive_mimic", None)
+    with torch.no_grad():
+        items = _encode(model.item_encoder, mimic.item_augmented.weight if mimic is not None else None,
+                        torch.from_numpy(uniq).to(device), item_features, 262_144)
+        q = encode_user_embeddings(model, torch.tensor(users, dtype=torch.long, device=device), user_features=user_features)
+    k = max(1, max_k)
+    scores = torch.empty((len(users), k), dtype=torch.float32, device=device)
+    pos = torch.empty((len(users), k), dtype=torch.long, device=device)
+    off_d = torch.from_numpy(offsets).to(device)
+    rows_d = torch.from_numpy(rows.astype(np.int64)).to(device)
+    cosine = 1 if isinstance(getattr(model, "similarity", None), nn.CosineSimilarity) else 0
+    _lib.check(_lib.load().ttamm_candidate_topk(
+        q.data_ptr(), len(users), q.stride(0), items.data_ptr() if items.numel() else None, items.shape[0],
+        items.stride(0) if items.numel() else q.shape[1], q.shape[1], off_d.data_ptr(),
+        rows_d.data_ptr() if rows_d.numel() else None, most, cosine, k, scores.data_ptr(), pos.data_ptr(),
+        _lib.stream_handle(device)))
+    preds: dict[int, list[int]] = {}
+    for u, cand, prow in zip(users, lists, pos.cpu().tolist()):
+        preds[u] = [cand[p] for p in prow[: min(max_k, len(cand))]]
+    return preds
+
+
 def _group_pairs(val_interactions: Any) -> dict[int, list[int]]:
     groups: dict[int, list[int]] = {}
     if hasattr(val_interactions, "groupby"):  # pandas DataFrame (training.py:999)
@@ -174,16 +249,19 @@ def evaluate_model(
     faiss_search_k: int = 0,
     item_embeddings: torch.Tensor | None = None,
 ) -> tuple[dict[int, list[int]], dict[int, set[int]]]:
-    """_evaluate_model (training.py:917-1043), exact inner-product branch (cosine models: on
-    L2-normalised items and queries, as the FAISS index is built), for every validation user at
-    once.  ``val_interactions``: a DataFrame with user_idx / item_idx columns or an
-    iterable of (user, item) pairs.  ``candidate_samples`` / ``rng`` / ``faiss_resources`` are
-    accepted for signature compatibility; retrieval is always the exact full-corpus search
-    (the FAISS branch).
+    """_evaluate_model (training.py:917-1043) for every validation user at once.
+    ``val_interactions``: a DataFrame with user_idx / item_idx columns or an iterable of
+    (user, item) pairs.  Branches, as the reference picks them (:940, :1029-1040):
 
-    Semantics kept from :944-970: a user's train positives are never returned; predictions are
-    the best max(k_values) remaining items; if fewer exist, the user's ground-truth items not
-    already listed are appended (set iteration order) and the list is cut to max_k."""
+      * ``faiss_resources`` given (``prepare_faiss_resources``: the HBM item matrix standing in
+        for faiss.IndexFlatIP) — exact inner-product search, on L2-normalised items and queries
+        for a cosine model.  A user's train positives are never returned; predictions are the
+        best max(k_values) remaining items; if fewer exist, the user's ground-truth items not
+        already listed are appended (set iteration order) and the list is cut to max_k (:944-972);
+      * no ``faiss_resources`` and an ``rng`` — the sampled-candidate branch the reference takes
+        without faiss (:974-1009): ground truth + ``candidate_samples`` random unblocked items
+        per user drawn from ``rng`` in the reference's order, ranked by the model's similarity;
+      * neither — the exact search (the item matrix is built here)."""
     groups = _group_pairs(val_interactions)
     if not groups:
         return {}, {}
@@ -191,6 +269,17 @@ def evaluate_model(
     max_k = max(k_values)
     users = [u for u, items in groups.items() if items]
     truth = {u: set(groups[u]) for u in users}
+    if faiss_resources is None and rng is not None and item_embeddings is None:
+        return _evaluate_sampled(model, users, truth, train_positive_map, item_features=item_feature_tensor,
+                                 user_features=user_feature_tensor, device=device, num_items=num_items,
+                                 candidate_samples=candidate_samples, max_k=max_k, rng=rng), truth
+    if faiss_resources is not None and item_embeddings is None:
+        item_embeddings = faiss_resources["index"]
+        if faiss_resources.get("normalize"):  # already normalised; the queries still need it
+            q = encode_user_embeddings(model, torch.tensor(users, dtype=torch.long, device=device),
+                                       user_features=user_feature_tensor)
+            normalize_rows(q)
+            return _exact(users, truth, q, item_embeddings, train_positive_map, max_k, device), truth
     if item_embeddings is None:
         item_embeddings = encode_item_embeddings(model, num_items=num_items, item_features=item_feature_tensor,
                                                  device=device)
@@ -199,6 +288,10 @@ def evaluate_model(
     if _uses_cosine(model):  # normalize_L2 on the index (:670-672) and on every query (:954-955)
         item_embeddings = normalize_rows(item_embeddings.clone())
         normalize_rows(q)
+    return _exact(users, truth, q, item_embeddings, train_positive_map, max_k, device), truth
+
+
+def _exact(users, truth, q, item_embeddings, train_positive_map, max_k, device) -> dict[int, list[int]]:
     boff, bval = blocked_csr(users, train_positive_map, device)
     _, ids = retrieve_topk(q, item_embeddings, max_k, blocked_offsets=boff, blocked_values=bval)
     preds: dict[int, list[int]] = {}
@@ -208,4 +301,4 @@ def evaluate_model(
             seen = set(got)
             got.extend(i for i in truth[u] if i not in seen)
         preds[u] = got[:max_k]
-    return preds, truth
+    return preds

@@ -18,7 +18,7 @@ their format.
 from __future__ import annotations
 
 import ctypes
-from typing import Any, Iterable, Mapping, Sequence
+from typing import Any, Callable, Iterable, Mapping, Sequence
 
 import torch
 from torch import nn
@@ -458,8 +458,18 @@ def train_one_epoch(
     loss_weights: Mapping[str, Any] | None = None,
     item_category_tensor: torch.Tensor | None = None,
     major_category_id: int | None = None,
+    batch_hook: Callable[[int, torch.Tensor, torch.Tensor], tuple[Any, Any]] | None = None,
+    step_losses: list | None = None,
 ) -> float:
-    """Drop-in for ``_train_one_epoch`` (training.py:700-833) executed on the MI355X."""
+    """Drop-in for ``_train_one_epoch`` (training.py:700-833) executed on the MI355X.
+
+    Two keyword-only extras (absent from the reference, default off) make a run reproducible
+    against a CPU run of the reference loop:
+      batch_hook(step, users, pos) -> (negatives [B, N] | None, {"user": [...], "item": [...]} |
+          None): injects the batch's negatives (instead of the on-device sampler) and dropout
+          keep-masks (instead of the Philox stream) — the RNG streams a CPU run draws differently;
+      step_losses: receives each step's device loss vector [total, bce, mimic_user, mimic_item,
+          category_alignment] (no host synchronisation inside the loop)."""
     model.train()
     if not isinstance(criterion, nn.BCEWithLogitsLoss) or criterion.reduction != "mean" or \
             criterion.weight is not None or criterion.pos_weight is not None:
@@ -472,9 +482,10 @@ def train_one_epoch(
     device = torch.device(device)
     batches = iter(dataloader)
     engine = None
-    for users, pos in batches:
-        users = users.to(device, non_blocking=True).reshape(-1)
-        pos = pos.to(device, non_blocking=True).reshape(-1)
+    step = 0
+    for users_in, pos_in in batches:
+        users = users_in.to(device, non_blocking=True).reshape(-1)
+        pos = pos_in.to(device, non_blocking=True).reshape(-1)
         if engine is None:
             size = getattr(dataloader, "batch_size", None) or users.numel()
             engine = FusedTrainStep(
@@ -483,7 +494,17 @@ def train_one_epoch(
                 max_batch=max(int(size), users.numel()),
                 item_category_tensor=item_category_tensor, major_category_id=major_category_id,
             )
-        engine.step(users, pos)  # stream-ordered: the caching allocator recycles inputs safely
+        neg = masks = None
+        if batch_hook is not None:
+            neg, masks = batch_hook(step, users_in, pos_in)
+            if neg is not None:
+                neg = neg.to(device, torch.long).reshape(-1)
+            if masks:
+                masks = {k: [m.to(device) for m in v] for k, v in masks.items()}
+        engine.step(users, pos, neg, keep_masks=masks)  # stream-ordered: inputs are recycled safely
+        if step_losses is not None:
+            step_losses.append(engine.loss_out.clone())
+        step += 1
     if engine is None:
         return 0.0
     return engine.finish()
