@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 10
+#define TTAMM_ABI_VERSION 11
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -71,6 +71,16 @@ extern "C" {
 #define TTAMM_PHASE_USER 8
 #define TTAMM_PHASE_ITEM_BWD 16
 #define TTAMM_PHASE_DENSE 32
+/* In-batch negatives in a sharded step (ttamm_step_args.in_batch): after USER_FWD and the (t | a)
+ * exchange,
+ *   INBATCH_SRC requester: its augmented positives (t + a)                 -> inbatch_local
+ *               [all-gather: inbatch_local -> inbatch_items, rank-major]
+ *   INBATCH     requester: S = U P^T over the global positives; dU kept in the workspace,
+ *               its share of dP for every global positive                -> inbatch_dp_all
+ *               [reduce-scatter (sum): inbatch_dp_all -> inbatch_dp, this rank's positives]
+ * then USER adds the sampled negatives (if any) and the mimic terms. */
+#define TTAMM_PHASE_INBATCH_SRC 64
+#define TTAMM_PHASE_INBATCH 128
 
 /* Device-side status word bits (written by kernels, read by the host at epoch end).  Once a
  * bit is set, every later step on that status word is skipped on the device (no parameter,
@@ -227,6 +237,17 @@ typedef struct ttamm_step_args {
      * began).  After a status error the host flushes the deferred tables to, and writes back
      * optimizer step counts of, the steps that ran.                                           */
     int64_t* steps_applied;
+    /* ---- in-batch negatives (BASELINE configs C2 / C4).  Not reference behaviour (the reference
+     * scores b.num_neg sampled negatives per positive, training.py:770-798); ttamm's definition
+     * (oracle/cpu_reference.py train_step(in_batch=True)): user b is scored against every positive
+     * of the global batch, S = U P^T with label 1 where the positive is b's own, followed by its
+     * b.num_neg (>= 0) sampled negatives; one BCE mean over global_batch x (global_batch + num_neg)
+     * logits.  S is never stored: a fused fp32-MFMA kernel forms it, its BCE and dU / dP. ---- */
+    int32_t in_batch;
+    float* inbatch_local;         /* sharded: [batch, dim] this rank's augmented positives        */
+    const float* inbatch_items;   /* sharded: [global_batch, dim] all ranks' (all-gathered)       */
+    float* inbatch_dp_all;        /* sharded: [global_batch, dim] this rank's share of dP         */
+    const float* inbatch_dp;      /* sharded: [batch, dim] summed dP of this rank's positives     */
 } ttamm_step_args;
 
 /* ---------------------------------------------------------------------------------- */

@@ -337,16 +337,24 @@ def train_step(
     item_keep_masks: Sequence[torch.Tensor] | None = None,
     item_category_tensor: torch.Tensor | None = None,
     major_category_id: int | None = None,
+    in_batch: bool = False,
 ) -> StepResult:
     """One iteration of _train_one_epoch's body.  item_keep_masks rows are ordered
-    [positives; negatives] (the two item_encoder calls, training.py:750 and :776)."""
+    [positives; negatives] (the two item_encoder calls, training.py:750 and :776).
+
+    ``in_batch`` — NOT reference behaviour (the reference scores sampled negatives only,
+    training.py:770-798); this is the definition of ttamm's in-batch mode (BASELINE configs C2/C4
+    "in-batch negatives"): every user is scored against every positive of the batch,
+    logits_ib = u @ p^T [B, B] with label 1 on the diagonal, followed by its own sampled negatives
+    (``neg_items`` may have 0 columns); one BCEWithLogits mean over all B(B + N) logits.  Mimic
+    losses and L_cal are unchanged (L_cal still over cat[positives; sampled negatives])."""
     model.train()
     lw = dict(loss_weights or {})
     lam_u = float(lw.get("mimic_user", 0.0))
     lam_i = float(lw.get("mimic_item", 0.0))
     mimic = model.adaptive_mimic
     B = users.shape[0]
-    N = neg_items.shape[1]
+    N = neg_items.shape[1] if neg_items.dim() == 2 else 0
     for opt in optimizers:  # :738-739
         opt.zero_grad()
     uf = user_features.index_select(0, users) if user_features is not None and user_features.numel() else None
@@ -365,13 +373,22 @@ def train_step(
         u, p = t_u, t_p
     pos_logits = (u * p).sum(dim=-1)  # :770
     neg_flat = neg_items.reshape(-1)
-    nf = item_features.index_select(0, neg_flat) if item_features is not None and item_features.numel() else None
-    t_n = tower_forward(model.item_encoder, neg_flat, nf, neg_masks)  # :776
-    n = gather_aug(mimic.item_augmented, neg_flat, t_n)[0] if mimic is not None else t_n
-    n = n.view(-1, N, u.shape[-1])
-    neg_logits = (u.unsqueeze(1) * n).sum(dim=-1)  # :786-787
-    logits = torch.cat([pos_logits, neg_logits.reshape(-1)], dim=0)
-    labels = torch.cat([torch.ones_like(pos_logits), torch.zeros_like(neg_logits.reshape(-1))], dim=0)
+    if N > 0:
+        nf = item_features.index_select(0, neg_flat) if item_features is not None and item_features.numel() else None
+        t_n = tower_forward(model.item_encoder, neg_flat, nf, neg_masks)  # :776
+        n = gather_aug(mimic.item_augmented, neg_flat, t_n)[0] if mimic is not None else t_n
+        n = n.view(-1, N, u.shape[-1])
+        neg_logits = (u.unsqueeze(1) * n).sum(dim=-1)  # :786-787
+    else:
+        n = u.new_zeros((B, 0, u.shape[-1]))
+        neg_logits = u.new_zeros((B, 0))
+    if in_batch:
+        ib = u @ p.t()
+        logits = torch.cat([ib.reshape(-1), neg_logits.reshape(-1)], dim=0)
+        labels = torch.cat([torch.eye(B, dtype=u.dtype).reshape(-1), torch.zeros_like(neg_logits.reshape(-1))], dim=0)
+    else:
+        logits = torch.cat([pos_logits, neg_logits.reshape(-1)], dim=0)
+        labels = torch.cat([torch.ones_like(pos_logits), torch.zeros_like(neg_logits.reshape(-1))], dim=0)
     bce = nn.BCEWithLogitsLoss()(logits, labels)  # :798, criterion :1366
     total = bce
     if loss_u is not None and lam_u > 0:
@@ -400,7 +417,7 @@ def train_one_epoch(model, batches: Iterable, optimizers, *, negatives_per_posit
                     positives: Mapping[int, set[int]], user_features, item_features,
                     loss_weights: Mapping[str, float] | None = None, max_steps: int | None = None,
                     item_category_tensor: torch.Tensor | None = None, major_category_id: int | None = None,
-                    batch_hook=None, step_losses: list | None = None) -> tuple[float, int, float]:
+                    batch_hook=None, step_losses: list | None = None, in_batch: bool = False) -> tuple[float, int, float]:
     """training.py:700-833 with the reference's per-row sampler; returns
     (mean loss, interactions, seconds).  ``batch_hook(step, users, pos) -> (negatives | None,
     {"user": masks, "item": masks} | None)`` injects the RNG streams (the same hook ttamm's
@@ -409,6 +426,8 @@ def train_one_epoch(model, batches: Iterable, optimizers, *, negatives_per_posit
     t0 = time.perf_counter()
     for users, pos in batches:
         neg, masks = batch_hook(steps, users, pos) if batch_hook is not None else (None, None)
+        if neg is None and negatives_per_positive == 0:
+            neg = torch.empty((users.shape[0], 0), dtype=torch.long)
         if neg is None:
             neg = sample_negative_items(users, num_items=num_items, positives=positives,
                                         num_negatives=negatives_per_positive)
@@ -416,7 +435,8 @@ def train_one_epoch(model, batches: Iterable, optimizers, *, negatives_per_posit
         res = train_step(model, optimizers, users, pos, neg.reshape(users.shape[0], -1), user_features=user_features,
                          item_features=item_features, loss_weights=loss_weights,
                          user_keep_masks=masks.get("user"), item_keep_masks=masks.get("item"),
-                         item_category_tensor=item_category_tensor, major_category_id=major_category_id)
+                         item_category_tensor=item_category_tensor, major_category_id=major_category_id,
+                         in_batch=in_batch)
         if step_losses is not None:
             step_losses.append(res)
         running += res.total * users.shape[0]

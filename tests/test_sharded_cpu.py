@@ -13,7 +13,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from ttamm.sharded import AllReduce, AllToAll, RowOwnership, TorchComm, Wait, route_requests, run_loopback
+from ttamm.sharded import (AllGather, AllReduce, AllToAll, ReduceScatter, RowOwnership, TorchComm, Wait, route_requests,
+                           run_loopback)
 
 
 def test_row_ownership():
@@ -63,8 +64,12 @@ def _exchange_program(W: int, rank: int, case: str):
     to_owner = yield AllToAll(grads.index_select(0, route.order), route.send_counts, route.recv_counts)
     acc = torch.tensor([float(rank + 1), 2.0 ** -rank])
     yield AllReduce(acc)
+    # in-batch negatives: all-gather [2, 3] rows, reduce-scatter [2W, 3] rows
+    gathered = yield AllGather(torch.full((2, 3), float(rank)))
+    scattered = yield ReduceScatter(torch.arange(2 * W * 3, dtype=torch.float64).reshape(2 * W, 3) * (rank + 1))
     return {"items": items, "keys": keys, "fwd": fwd, "route_rows": route.rows, "route_keys": route.keys,
-            "to_owner": to_owner, "acc": acc, "recv": route.recv_counts}
+            "to_owner": to_owner, "acc": acc, "recv": route.recv_counts, "gathered": gathered,
+            "scattered": scattered}
 
 
 def _check(W: int, outs: list[dict], case: str):
@@ -80,6 +85,10 @@ def _check(W: int, outs: list[dict], case: str):
                                                   dtype=o["acc"].dtype))
         if case == "skewed" and rank > 0:
             assert o["route_rows"].numel() == 0
+        assert torch.equal(o["gathered"], torch.arange(W).repeat_interleave(2).double()[:, None].expand(2 * W, 3)
+                           .to(o["gathered"].dtype))
+        full = torch.arange(2 * W * 3, dtype=torch.float64).reshape(2 * W, 3) * (W * (W + 1) / 2)
+        assert torch.equal(o["scattered"], full[2 * rank:2 * rank + 2])
     total = sum(o["route_rows"].numel() for o in outs)
     assert total == sum(o["items"].numel() for o in outs)
 
@@ -128,8 +137,8 @@ def test_exchange_gloo_world2(case):
         assert p.exitcode == 0
     outs = [got[r] for r in range(W)]
     for o in outs:  # empty tensors lose their trailing shape in the round trip through lists
-        for k in ("fwd", "to_owner"):
-            o[k] = o[k].reshape(-1, 3 if k == "fwd" else 2)
+        for k in ("fwd", "to_owner", "gathered", "scattered"):
+            o[k] = o[k].reshape(-1, 2 if k == "to_owner" else 3)
     _check(W, outs, case)
     # identical to the loopback schedule
     ref = run_loopback([_exchange_program(W, r, case) for r in range(W)])

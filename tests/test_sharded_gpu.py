@@ -47,7 +47,7 @@ def _opts(model, lr, betas):
     return opts
 
 
-def _setup(shape: Shape, W: int, *, lr: float, betas, steps: int):
+def _setup(shape: Shape, W: int, *, lr: float, betas, steps: int, in_batch: bool = False):
     prob = make_problem(shape, seed=77)
     state = prob.model.state_dict()
     gen = torch.Generator().manual_seed(5)
@@ -66,7 +66,8 @@ def _setup(shape: Shape, W: int, *, lr: float, betas, steps: int):
     gopts = _opts(gm, lr, betas)
     geng = ttamm.FusedTrainStep(gm, gopts, negatives_per_positive=shape.N, positives=prob.positives,
                                 user_features=prob.user_features.cuda(), item_features=prob.item_features.cuda(),
-                                loss_weights=LOSS_WEIGHTS, max_batch=W * shape.B, seed=SEED)
+                                loss_weights=LOSS_WEIGHTS, max_batch=W * shape.B, seed=SEED,
+                                in_batch_negatives=in_batch)
     # W ranks
     ranks = []
     for r in range(W):
@@ -78,7 +79,7 @@ def _setup(shape: Shape, W: int, *, lr: float, betas, steps: int):
         eng = ShardedTrainStep(m, opts, world_size=W, rank=r, num_items=shape.I, negatives_per_positive=shape.N,
                                positives=local_pos, user_features=own.shard(prob.user_features).cuda(),
                                item_features=own.shard(prob.item_features).cuda(), loss_weights=LOSS_WEIGHTS,
-                               max_batch=shape.B, seed=SEED)
+                               max_batch=shape.B, seed=SEED, in_batch_negatives=in_batch)
         ranks.append((own, m, opts, eng))
     return prob, batches, (gm, gopts, geng), ranks
 
@@ -100,13 +101,16 @@ def _run(batches, g, ranks, W):
     return glosses, rlosses, negs, gavg, ravg
 
 
-@pytest.mark.parametrize("W,shape", [
-    (2, Shape()),
-    (3, Shape(hidden_dims=(16, 12))),
-    (2, Shape(dropout=0.0, gate_hidden=20)),
+@pytest.mark.parametrize("W,shape,in_batch", [
+    (2, Shape(), False),
+    (3, Shape(hidden_dims=(16, 12)), False),
+    (2, Shape(dropout=0.0, gate_hidden=20), False),
+    # in-batch negatives: all-gather of the positives + reduce-scatter of dP (ttamm.h INBATCH phases)
+    (2, Shape(N=2), True),
+    (3, Shape(U=300, I=900, N=0, B=70), True),
 ])
-def test_sharded_gradients_match_global_step(W, shape):
-    prob, batches, g, ranks = _setup(shape, W, lr=0.0, betas=(0.0, 0.999), steps=1)
+def test_sharded_gradients_match_global_step(W, shape, in_batch):
+    prob, batches, g, ranks = _setup(shape, W, lr=0.0, betas=(0.0, 0.999), steps=1, in_batch=in_batch)
     glosses, rlosses, negs, gavg, ravg = _run(batches, g, ranks, W)
     B, N = shape.B, shape.N
     gneg, rneg = negs[0]
@@ -128,9 +132,10 @@ def test_sharded_gradients_match_global_step(W, shape):
             assert rel_err(st["exp_avg"], want) <= 1e-5, (own.rank, name)
 
 
-def test_sharded_three_steps_match_global_step():
+@pytest.mark.parametrize("in_batch", [False, True], ids=["sampled", "in-batch"])
+def test_sharded_three_steps_match_global_step(in_batch):
     W, shape = 2, Shape()
-    prob, batches, g, ranks = _setup(shape, W, lr=1e-3, betas=(0.9, 0.999), steps=3)
+    prob, batches, g, ranks = _setup(shape, W, lr=1e-3, betas=(0.9, 0.999), steps=3, in_batch=in_batch)
     glosses, rlosses, _, _, _ = _run(batches, g, ranks, W)
     for s in range(3):
         assert abs(rlosses[s][0]["total"] - glosses[s]["total"]) <= 1e-5 * abs(glosses[s]["total"])

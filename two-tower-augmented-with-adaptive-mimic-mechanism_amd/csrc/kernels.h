@@ -163,6 +163,9 @@ struct StageArgs {
     uint32_t* status;
 };
 int launch_stage_rows(const StageArgs& a, hipStream_t s);
+// out = x (+ y) over [n, dim] rows (y may be null): an augmented row t + a (adaptive_mimic.py:88-95)
+int launch_add_rows(const float* x, int64_t ldx, const float* y, int64_t ldy, int64_t n, int dim, float* out,
+                    int64_t ldo, hipStream_t s);
 
 // Status bits that stop every later step (ttamm.h TTAMM_STATUS_*).
 constexpr uint32_t kStatusPoison = TTAMM_STATUS_SAMPLER_EXHAUSTED | TTAMM_STATUS_INDEX_OUT_OF_RANGE;
@@ -203,12 +206,45 @@ struct ScoreArgs {
     int64_t ld_dti;
     float* partials;  // [blocks, 3]
     int blocks;
+    float inv_numel;  // 1 / logits in the BCE mean: Bg (1 + N), or Bg (Bg + N) in-batch
+    // in-batch mode: the positive logit is part of the in-batch matrix; the rows' gradients
+    // start from its dU / dP (ib_du [B, D], ib_dp [B, ib_ld]) and the sampled negatives add on
+    const float* ib_du;
+    const float* ib_dp;
+    int64_t ib_ld;
 };
 int score_blocks(int64_t B);
 int launch_score_loss(const ScoreArgs& a, hipStream_t s);
-int launch_loss_finalize(const float* partials, int blocks, int64_t B, int64_t Bg, int N, int D, float lambda_u,
-                         float lambda_i, int mimic, const float* cal, float lambda_cal, float* loss_out,
-                         double* loss_accum, const uint32_t* status, hipStream_t s);
+// bce = (sum of the score partials + sum of ib_partials) / bce_count
+int launch_loss_finalize(const float* partials, int blocks, const float* ib_partials, int ib_blocks, int64_t bce_count,
+                         int64_t B, int64_t Bg, int D, float lambda_u, float lambda_i, int mimic, const float* cal,
+                         float lambda_cal, float* loss_out, double* loss_accum, const uint32_t* status, hipStream_t s);
+
+// ------------------------------------------------------------------------------------
+// In-batch negatives: S = U P^T with BCE, dU, dP (inbatch.hip)
+// ------------------------------------------------------------------------------------
+struct InBatchArgs {
+    const float* U;      // [B, ldu] augmented user rows (rows of S)
+    int64_t ldu, B;
+    const float* P;      // [Bc, ldp] augmented positive rows of the (global) batch (columns of S)
+    int64_t ldp, Bc;
+    int D;
+    int64_t row_base;    // column of user 0's own positive (global batch position of the rank)
+    float inv_T;         // 1 / logits in the BCE mean
+    float* slab_u;       // [splits_u, B, D]
+    float* slab_p;       // [splits_p, Bc, D]
+    float* loss_part;    // [rblk_u * splits_u] BCE sums of the user-role blocks
+    float* dU;           // [B, ld_du]  = dS P
+    int64_t ld_du;
+    float* dP;           // [Bc, ld_dp] = dS^T U
+    int64_t ld_dp;
+    // filled by inbatch_plan
+    int rblk_u, rblk_p, splits_u, splits_p;
+    int64_t cols_u, cols_p;
+};
+void inbatch_plan(int64_t B, int64_t Bc, InBatchArgs& a);
+size_t inbatch_workspace_floats(int64_t B, int64_t Bc, int D, size_t* slab_u, size_t* slab_p, size_t* parts);
+int launch_inbatch(InBatchArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------------------------------
 // Exact inner-product retrieval + top-k (retrieval.hip)

@@ -184,7 +184,8 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
     const int D = A.D, N = A.N;
     const int64_t B = A.B;
     const int64_t ldi = A.ld_dti;
-    const float inv_numel = 1.0f / (float)(A.Bg * (1 + N));
+    const float inv_numel = A.inv_numel;
+    const bool ib = A.ib_du != nullptr;
     float bce = 0.f, mse_u = 0.f, mse_i = 0.f;
     if (b < B) {
         const int nch = (D + 63) / 64;
@@ -201,15 +202,21 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
             }
         }
         const float sp = wave_sum(dot);
-        const float dsp = (1.0f / (1.0f + expf(-sp)) - 1.0f) * inv_numel;
-        bce += bce_logit(sp, 1.0f);
-        // positive item row: dT_pos = ds+ * u ; user: ds+ * p
+        float dsp = 0.f;
+        if (!ib) {
+            dsp = (1.0f / (1.0f + expf(-sp)) - 1.0f) * inv_numel;
+            bce += bce_logit(sp, 1.0f);
+        }
+        // positive item row: dT_pos = ds+ * u ; user: ds+ * p   (in-batch: the S = U P^T terms)
+        float dpos[kMaxDChunks];
 #pragma unroll
         for (int c = 0; c < kMaxDChunks; ++c) {
             const int d = c * 64 + lane;
+            dpos[c] = 0.f;
             if (c < nch && d < D) {
-                A.dT_item[b * ldi + d] = dsp * u[c];
-                du[c] = dsp * p[c];
+                dpos[c] = ib ? A.ib_dp[b * A.ib_ld + d] : dsp * u[c];
+                A.dT_item[b * ldi + d] = dpos[c];
+                du[c] = ib ? A.ib_du[b * D + d] : dsp * p[c];
             }
         }
         for (int j = 0; j < N; ++j) {
@@ -252,7 +259,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
                     mse_u += xu * xu;
                     mse_i += xi * xi;
                     A.dA_user[b * D + d] = du[c] + norm * xu * A.lambda_u;
-                    A.dA_item[b * ldi + d] = dsp * u[c] + norm * xi * A.lambda_i;
+                    A.dA_item[b * ldi + d] = dpos[c] + norm * xi * A.lambda_i;
                 }
             }
         }
@@ -273,7 +280,8 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
 }
 
 // Deterministic final reduction of the per-block partials; total loss as in training.py:798-803.
-__global__ void loss_finalize_kernel(const float* __restrict__ partials, int blocks, int64_t B, int64_t Bg, int N, int D,
+__global__ void loss_finalize_kernel(const float* __restrict__ partials, int blocks, const float* __restrict__ ib_partials,
+                                     int ib_blocks, int64_t bce_count, int64_t B, int64_t Bg, int D,
                                      float lu, float li, int mimic, const float* __restrict__ cal, float lcal,
                                      float* __restrict__ loss_out, double* __restrict__ loss_accum,
                                      const uint32_t* __restrict__ status) {
@@ -281,6 +289,7 @@ __global__ void loss_finalize_kernel(const float* __restrict__ partials, int blo
     float s[3] = {0.f, 0.f, 0.f};
     for (int i = threadIdx.x; i < blocks; i += blockDim.x)
         for (int k = 0; k < 3; ++k) s[k] += partials[i * 3 + k];
+    for (int i = threadIdx.x; i < ib_blocks; i += blockDim.x) s[0] += ib_partials[i];
     for (int k = 0; k < 3; ++k) red[k][threadIdx.x] = s[k];
     __syncthreads();
     for (int o = blockDim.x / 2; o > 0; o >>= 1) {
@@ -290,7 +299,7 @@ __global__ void loss_finalize_kernel(const float* __restrict__ partials, int blo
     }
     if (threadIdx.x == 0) {
         // sharded step: this rank's share of the global means (the host sums loss_out over ranks)
-        const float bce = red[0][0] / (float)(Bg * (1 + N));
+        const float bce = red[0][0] / (float)bce_count;
         const float mu = red[1][0] / (float)(Bg * D);
         const float mi = red[2][0] / (float)(Bg * D);
         float total = bce;
@@ -411,7 +420,7 @@ int launch_gate_dq(const float* dT, int64_t ld_dT, const float* ef, const float*
 
 int launch_score_loss(const ScoreArgs& a, hipStream_t s) {
     TTAMM_REQUIRE(a.D <= 64 * kMaxDChunks, "score: embedding dim too large (max 512)");
-    TTAMM_REQUIRE(a.N >= 1 && a.N <= kMaxNeg, "score: negatives_per_positive out of range");
+    TTAMM_REQUIRE(a.N >= (a.ib_du ? 0 : 1) && a.N <= kMaxNeg, "score: negatives_per_positive out of range");
     if (a.B <= 0) return TTAMM_OK;
     hipLaunchKernelGGL(score_loss_kernel, dim3(a.blocks), dim3(64 * kScoreWaves), 0, s, a);
     TTAMM_LAUNCH_CHECK();
@@ -420,11 +429,11 @@ int launch_score_loss(const ScoreArgs& a, hipStream_t s) {
 
 int score_blocks(int64_t B) { return (int)ceil_div(B, kScoreWaves); }
 
-int launch_loss_finalize(const float* partials, int blocks, int64_t B, int64_t Bg, int N, int D, float lu, float li,
-                         int mimic, const float* cal, float lcal, float* loss_out, double* loss_accum,
-                         const uint32_t* status, hipStream_t s) {
-    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, partials, blocks, B, Bg, N, D, lu, li, mimic,
-                       cal, lcal, loss_out, loss_accum, status);
+int launch_loss_finalize(const float* partials, int blocks, const float* ib_partials, int ib_blocks, int64_t bce_count,
+                         int64_t B, int64_t Bg, int D, float lu, float li, int mimic, const float* cal, float lcal,
+                         float* loss_out, double* loss_accum, const uint32_t* status, hipStream_t s) {
+    hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, partials, blocks, ib_partials, ib_blocks,
+                       bce_count, B, Bg, D, lu, li, mimic, cal, lcal, loss_out, loss_accum, status);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }
@@ -432,6 +441,28 @@ int launch_loss_finalize(const float* partials, int blocks, int64_t B, int64_t B
 }  // namespace ttamm
 
 namespace ttamm {
+
+namespace {
+// out = x (+ y), row-wise over [n, dim]
+__global__ void add_rows_kernel(const float* __restrict__ x, int64_t ldx, const float* __restrict__ y, int64_t ldy,
+                                int64_t n, int dim, float* __restrict__ out, int64_t ldo) {
+    const int64_t total = n * dim;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / dim;
+        const int c = (int)(i - r * dim);
+        const float v = x[r * ldx + c];
+        out[r * ldo + c] = y ? v + y[r * ldy + c] : v;
+    }
+}
+}  // namespace
+
+int launch_add_rows(const float* x, int64_t ldx, const float* y, int64_t ldy, int64_t n, int dim, float* out,
+                    int64_t ldo, hipStream_t s) {
+    if (n <= 0) return TTAMM_OK;
+    hipLaunchKernelGGL(add_rows_kernel, dim3(grid_for(n * dim)), dim3(256), 0, s, x, ldx, y, ldy, n, dim, out, ldo);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
 
 int launch_stage_rows(const StageArgs& a, hipStream_t s) {
     TTAMM_REQUIRE(a.count >= 0 && a.count <= kMaxStageSegs, "stage_rows: bad arguments");

@@ -77,6 +77,12 @@ struct StepWs {
     TowerWs user, item;
     float* partials = nullptr;
     int score_blocks = 0;
+    // in-batch negatives (ttamm_step_args.in_batch)
+    bool ib_on = false;
+    InBatchArgs ib{};
+    float* ib_du = nullptr;   // [B, D]
+    float* ib_dp = nullptr;   // [B, D] (one process; sharded: the caller's inbatch_dp)
+    int ib_parts = 0;
     bool cal_on = false;  // category-alignment loss this step
     CalArgs cal{};
 };
@@ -265,6 +271,18 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         tower(A.item, ws.item, B * (1 + N), false, B);
     ws.score_blocks = score_blocks(B);
     ws.partials = ar.take<float>((size_t)ws.score_blocks * 3);
+    if (A.in_batch) {
+        ws.ib_on = true;
+        const int64_t Bc = shard ? global_batch(A) : B;
+        size_t su, sp, parts;
+        inbatch_workspace_floats(B, Bc, D, &su, &sp, &parts);
+        ws.ib.slab_u = ar.take<float>(su);
+        ws.ib.slab_p = ar.take<float>(sp);
+        ws.ib.loss_part = ar.take<float>(parts);
+        ws.ib_parts = (int)parts;
+        ws.ib_du = ar.take<float>((size_t)B * D);
+        if (!shard) ws.ib_dp = ar.take<float>((size_t)B * D);
+    }
     if (cal_enabled(A) && !shard) {
         CalArgs& c = ws.cal;
         ws.cal_on = true;
@@ -991,7 +1009,12 @@ int validate_step(const ttamm_step_args& A) {
                       "category alignment: major_category out of range");
         TTAMM_REQUIRE(A.user.id.dim <= 256, "category alignment: embedding dim must be <= 256");
     }
-    TTAMM_REQUIRE(A.b.num_neg > 0, "num_negatives must be greater than zero.");
+    if (A.in_batch) {
+        TTAMM_REQUIRE(A.b.num_neg >= 0, "num_negatives must be >= 0 with in-batch negatives");
+        TTAMM_REQUIRE(D % 4 == 0 && D <= 128, "in-batch negatives: embedding dim must be <= 128");
+    } else {
+        TTAMM_REQUIRE(A.b.num_neg > 0, "num_negatives must be greater than zero.");
+    }
     const int64_t num_items = A.num_items_global > 0 ? A.num_items_global : A.item.id.rows;
     TTAMM_REQUIRE(num_items > 1, "num_items must be greater than one.");
     if (A.mimic_enabled) {
@@ -1005,7 +1028,9 @@ int validate_step(const ttamm_step_args& A) {
                   "row_base / global_batch out of range");
     if (!sharded(A)) return TTAMM_OK;
     const int ph = A.phase;
-    TTAMM_REQUIRE((ph & ~63) == 0, "unknown phase bits");
+    TTAMM_REQUIRE((ph & ~255) == 0, "unknown phase bits");
+    TTAMM_REQUIRE(A.in_batch || (ph & (TTAMM_PHASE_INBATCH_SRC | TTAMM_PHASE_INBATCH)) == 0,
+                  "INBATCH phases need in_batch");
     TTAMM_REQUIRE(A.item_rows_capacity >= 0 && A.n_item_rows >= 0 && A.n_item_rows <= A.item_rows_capacity,
                   "n_item_rows exceeds item_rows_capacity");
     if (ph & TTAMM_PHASE_SAMPLE)
@@ -1026,7 +1051,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     const int D = A.user.id.dim;
     const bool mimic = A.mimic_enabled != 0;
     const bool shard = sharded(A);
-    const int ph = shard ? A.phase : 63;
+    const int ph = shard ? A.phase : 255;
 
     Arena ar{static_cast<char*>(A.workspace), A.workspace_bytes, 0, false};
     StepWs ws;
@@ -1089,17 +1114,18 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         st.seg[st.count++] = StageSeg{A.b.users, U.idx_own, B, A.user.id.rows};
         if (!shard) {
             st.seg[st.count++] = StageSeg{A.b.pos_items, I.idx_own, B, A.item.id.rows};
-            if (!A.b.sample_negatives) {
+            if (!A.b.sample_negatives && N > 0) {
                 TTAMM_REQUIRE(A.b.neg_items != nullptr, "negatives must be given when sample_negatives == 0");
                 st.seg[st.count++] = StageSeg{A.b.neg_items, neg, B * N, A.item.id.rows};
             }
         } else {  // requester: global item ids, checked only (the owners stage their local rows)
             st.seg[st.count++] = StageSeg{A.b.pos_items, nullptr, B, num_items};
-            if (!A.b.sample_negatives && A.b.neg_items) st.seg[st.count++] = StageSeg{A.b.neg_items, nullptr, B * N, num_items};
+            if (!A.b.sample_negatives && A.b.neg_items && N > 0)
+                st.seg[st.count++] = StageSeg{A.b.neg_items, nullptr, B * N, num_items};
         }
         TTAMM_REQUIRE(A.status != nullptr, "the training step needs a status word");
         if ((rc = launch_stage_rows(st, s))) return rc;
-        if (A.b.sample_negatives) {
+        if (A.b.sample_negatives && N > 0) {
             if ((rc = launch_sample_negatives(U.idx_own, B, N, num_items, A.b.pos_offsets, A.b.pos_values, A.b.seed,
                                               A.b.counter, A.row_base * N, neg, A.status, s)))
                 return rc;
@@ -1133,6 +1159,37 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         }
         if (ph & TTAMM_PHASE_USER_FWD)
             if ((rc = prepare_forward(T, W, 1, A.b, D, mimic, df, s, aux, nullptr))) return rc;
+    }
+    // ---- in-batch negatives: S = U P^T, its BCE, dU and dP ------------------------------------
+    const int64_t ib_cols = ws.ib_on ? (shard ? Bg : B) : 0;  // positives every user is scored against
+    if (ws.ib_on && shard && (ph & TTAMM_PHASE_INBATCH_SRC)) {
+        TTAMM_REQUIRE(A.item_fwd_in && A.inbatch_local, "INBATCH_SRC needs item_fwd_in and inbatch_local");
+        if ((rc = launch_add_rows(A.item_fwd_in, 2 * D, mimic ? A.item_fwd_in + D : nullptr, 2 * D, B, D,
+                                  A.inbatch_local, D, s)))
+            return rc;
+    }
+    if (ws.ib_on && (ph & (shard ? TTAMM_PHASE_INBATCH : TTAMM_PHASE_USER))) {
+        InBatchArgs& a = ws.ib;
+        a.U = U.aug;
+        a.ldu = D;
+        a.B = B;
+        if (shard) {
+            TTAMM_REQUIRE(A.inbatch_items && A.inbatch_dp_all, "INBATCH needs inbatch_items and inbatch_dp_all");
+            a.P = A.inbatch_items;
+            a.dP = A.inbatch_dp_all;
+        } else {
+            a.P = I.aug;  // rows [0, B): the positives
+            a.dP = ws.ib_dp;
+        }
+        a.ldp = D;
+        a.ld_dp = D;
+        a.Bc = ib_cols;
+        a.D = D;
+        a.row_base = shard ? A.row_base : 0;
+        a.inv_T = 1.0f / (float)(Bg * (ib_cols + N));
+        a.dU = ws.ib_du;
+        a.ld_du = D;
+        if ((rc = launch_inbatch(a, s))) return rc;
     }
     // ---- score + loss (fwd + bwd seeds), user-side backward ---------------------------------
     if (ph & TTAMM_PHASE_USER) {
@@ -1170,6 +1227,14 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         }
         sa.partials = ws.partials;
         sa.blocks = ws.score_blocks;
+        const int64_t bce_count = Bg * ((ws.ib_on ? ib_cols : 1) + N);
+        sa.inv_numel = 1.0f / (float)bce_count;
+        if (ws.ib_on) {
+            TTAMM_REQUIRE(!shard || A.inbatch_dp, "sharded in-batch USER phase needs inbatch_dp");
+            sa.ib_du = ws.ib_du;
+            sa.ib_dp = shard ? A.inbatch_dp : ws.ib_dp;
+            sa.ib_ld = D;
+        }
         if ((rc = launch_score_loss(sa, s))) return rc;
         if (ws.cal_on) {  // + lambda * L_cal over cat[positives; negatives] (training.py:805-820)
             CalArgs& c = ws.cal;
@@ -1187,9 +1252,11 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
             if ((rc = launch_category_alignment(c, s))) return rc;
         }
         if (A.loss_out) {
-            if ((rc = launch_loss_finalize(ws.partials, ws.score_blocks, B, Bg, N, D, sa.lambda_u, sa.lambda_i, sa.mimic,
-                                           ws.cal_on ? ws.cal.out : nullptr, (float)A.hp.lambda_category_alignment,
-                                           A.loss_out, A.loss_accum, A.status, s)))
+            if ((rc = launch_loss_finalize(ws.partials, ws.score_blocks, ws.ib_on ? ws.ib.loss_part : nullptr,
+                                           ws.ib_on ? ws.ib_parts : 0, bce_count, B, Bg, D, sa.lambda_u, sa.lambda_i,
+                                           sa.mimic, ws.cal_on ? ws.cal.out : nullptr,
+                                           (float)A.hp.lambda_category_alignment, A.loss_out, A.loss_accum, A.status,
+                                           s)))
                 return rc;
         }
         if (!shard) {

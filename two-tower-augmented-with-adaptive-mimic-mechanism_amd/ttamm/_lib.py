@@ -149,10 +149,15 @@ class StepArgs(ctypes.Structure):
         ("num_categories", c_i64),
         ("major_category", c_i64),
         ("steps_applied", c_vp),
+        ("in_batch", c_i32),
+        ("inbatch_local", c_vp),
+        ("inbatch_items", c_vp),
+        ("inbatch_dp_all", c_vp),
+        ("inbatch_dp", c_vp),
     ]
 
 
-ABI_VERSION = 10  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 11  # ttamm.h TTAMM_ABI_VERSION
 
 # ttamm.h TTAMM_PHASE_*
 PHASE_ALL = 0
@@ -162,6 +167,8 @@ PHASE_USER_FWD = 4
 PHASE_USER = 8
 PHASE_ITEM_BWD = 16
 PHASE_DENSE = 32
+PHASE_INBATCH_SRC = 64
+PHASE_INBATCH = 128
 
 
 # Symbol table: name -> (restype, argtypes).  tests/ check every one is exported and that this

@@ -17,6 +17,8 @@ Per step (ttamm.h TTAMM_PHASE_*):
   ITEM_FWD  owner: item tower over the requested rows            -> (t | a) rows
   a2a       (t | a) rows -> requesters               (overlaps USER_FWD on the GPU)
   USER_FWD  user tower
+  (in-batch negatives only: INBATCH_SRC -> all-gather of the ranks' augmented positives
+   [B, D] -> [W B, D] -> INBATCH: S = U P^T over the global batch -> reduce-scatter of dP)
   USER      scores, losses, user backward + user-table updates   -> (dT | dA) rows
   a2a       (dT | dA) rows -> owners
   ITEM_BWD  owner: item backward + item-table updates
@@ -101,6 +103,20 @@ class AllReduce:
     tensor: torch.Tensor
 
 
+@dataclass
+class AllGather:
+    """Every rank's ``send`` (same shape on all ranks), concatenated rank-major."""
+
+    send: torch.Tensor
+
+
+@dataclass
+class ReduceScatter:
+    """``send`` holds W equal chunks along dim 0; rank r gets the sum over ranks of chunk r."""
+
+    send: torch.Tensor
+
+
 Program = Generator[Any, Any, Any]
 
 
@@ -135,6 +151,27 @@ class TorchComm:
             work, out = req.handle
             if work is not None:
                 work.wait()
+            return out
+        if isinstance(req, AllGather):
+            send = req.send.contiguous()
+            W = dist.get_world_size(self.group)
+            if self.staged:
+                host = send.cpu()
+                out = host.new_empty((W * host.shape[0],) + tuple(host.shape[1:]))
+                dist.all_gather(list(out.chunk(W)), host, group=self.group)
+                return out.to(send.device)
+            out = send.new_empty((W * send.shape[0],) + tuple(send.shape[1:]))
+            dist.all_gather_into_tensor(out, send, group=self.group)
+            return out
+        if isinstance(req, ReduceScatter):
+            send = req.send.contiguous()
+            W = dist.get_world_size(self.group)
+            if self.staged:  # gloo has no reduce-scatter: all-reduce the host copy, keep this rank's chunk
+                host = send.cpu()
+                dist.all_reduce(host, group=self.group)
+                return host.chunk(W)[dist.get_rank(self.group)].contiguous().to(send.device)
+            out = send.new_empty((send.shape[0] // W,) + tuple(send.shape[1:]))
+            dist.reduce_scatter_tensor(out, send, group=self.group)
             return out
         if isinstance(req, AllReduce):
             if self.staged and req.tensor.device.type != "cpu":
@@ -196,6 +233,16 @@ def run_loopback(programs: Sequence[Program]) -> list[Any]:
             for r in range(W):
                 reqs[r].tensor.copy_(total)
                 results[r] = reqs[r].tensor
+        elif kind is AllGather:
+            got = torch.cat([q.send for q in reqs])
+            for r in range(W):
+                results[r] = got.clone()
+        elif kind is ReduceScatter:
+            total = reqs[0].send.clone()
+            for r in range(1, W):
+                total += reqs[r].send
+            for r, chunk in enumerate(total.chunk(W)):
+                results[r] = chunk.contiguous()
         else:
             raise TypeError(f"unknown collective request {reqs[0]!r}")
     return values
@@ -265,6 +312,10 @@ class ShardedTrainStep(FusedTrainStep):
         D = self.model.user_encoder.embedding.weight.shape[1]
         self.D = D
         self.fwd_out = torch.empty((self.capacity, 2 * D), dtype=torch.float32, device=self.device)
+        if self.in_batch:  # all-gathered positives: the workspace is sized for the global batch
+            args.global_batch = W * self.max_batch
+            self.ib_local = torch.empty((self.max_batch, D), dtype=torch.float32, device=self.device)
+            self.ib_dp_all = torch.empty((W * self.max_batch, D), dtype=torch.float32, device=self.device)
         self.fwd_in = torch.empty((R, 2 * D), dtype=torch.float32, device=self.device)
         self.bwd_out = torch.empty((R, 2 * D), dtype=torch.float32, device=self.device)
 
@@ -318,6 +369,18 @@ class ShardedTrainStep(FusedTrainStep):
         fwd_in.index_copy_(0, route.order, back)
         a.item_fwd_in = fwd_in.data_ptr()
         a.item_bwd_out = self.bwd_out.data_ptr()
+        ib = ()
+        if self.in_batch:
+            # ---- in-batch: every rank's augmented positives, then dP summed back to its rank ------
+            a.inbatch_local = self.ib_local.data_ptr()
+            self._phase(_lib.PHASE_INBATCH_SRC)
+            gathered = yield AllGather(self.ib_local[:B])
+            a.inbatch_items = gathered.data_ptr()
+            a.inbatch_dp_all = self.ib_dp_all.data_ptr()
+            self._phase(_lib.PHASE_INBATCH)
+            dp = yield ReduceScatter(self.ib_dp_all[: W * B])
+            a.inbatch_dp = dp.data_ptr()
+            ib = (gathered, dp)
         self._phase(_lib.PHASE_USER)
         # ---- (dT | dA) to the owners -----------------------------------------------------------
         bwd_in = yield AllToAll(self.bwd_out[:R].index_select(0, route.order), route.send_counts,
@@ -330,7 +393,7 @@ class ShardedTrainStep(FusedTrainStep):
         self._phase(_lib.PHASE_DENSE)
         self.steps_done += 1
         # keep the step's device buffers alive until the stream has consumed them
-        self._live = (route, back, bwd_in, req, keys)
+        self._live = (route, back, bwd_in, req, keys) + ib
 
     def step(self, users, pos_items, neg_items=None, *, keep_masks=None, timing_events=None) -> None:
         if self.comm is None:

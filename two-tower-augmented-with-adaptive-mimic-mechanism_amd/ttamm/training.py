@@ -125,8 +125,12 @@ class FusedTrainStep:
         overlap: bool = True,
         item_category_tensor: torch.Tensor | None = None,
         major_category_id: int | None = None,
+        in_batch_negatives: bool = False,
     ) -> None:
-        if negatives_per_positive <= 0:
+        # in_batch_negatives: ttamm's in-batch mode (ttamm.h ttamm_step_args.in_batch; not the
+        # reference's behaviour): every user is also scored against every positive of the batch
+        self.in_batch = bool(in_batch_negatives)
+        if negatives_per_positive < 0 or (negatives_per_positive == 0 and not self.in_batch):
             raise ValueError("num_negatives must be greater than zero.")
         self.model = model
         self.num_neg = int(negatives_per_positive)
@@ -234,6 +238,7 @@ class FusedTrainStep:
             )
             setattr(args, name, desc)
         args.mimic_enabled = 1 if mimic is not None else 0
+        args.in_batch = 1 if self.in_batch else 0
         lw = dict(loss_weights or {})
         args.hp.lambda_mimic_user = float(lw.get("mimic_user", 0.0))
         args.hp.lambda_mimic_item = float(lw.get("mimic_item", 0.0))
@@ -371,7 +376,10 @@ class FusedTrainStep:
         a.b.users = users.data_ptr()
         a.b.pos_items = pos_items.data_ptr()
         a.b.batch = B
-        if neg_items is not None:
+        if self.num_neg == 0:  # in-batch negatives only
+            a.b.neg_items = None
+            a.b.sample_negatives = 0
+        elif neg_items is not None:
             if neg_items.numel() != B * self.num_neg or neg_items.dtype != torch.long:
                 raise ValueError("ttamm: negatives must be int64 [batch, negatives_per_positive]")
             a.b.neg_items = neg_items.data_ptr()
@@ -460,6 +468,7 @@ def train_one_epoch(
     major_category_id: int | None = None,
     batch_hook: Callable[[int, torch.Tensor, torch.Tensor], tuple[Any, Any]] | None = None,
     step_losses: list | None = None,
+    in_batch_negatives: bool = False,
 ) -> float:
     """Drop-in for ``_train_one_epoch`` (training.py:700-833) executed on the MI355X.
 
@@ -469,7 +478,9 @@ def train_one_epoch(
           None): injects the batch's negatives (instead of the on-device sampler) and dropout
           keep-masks (instead of the Philox stream) — the RNG streams a CPU run draws differently;
       step_losses: receives each step's device loss vector [total, bce, mimic_user, mimic_item,
-          category_alignment] (no host synchronisation inside the loop)."""
+          category_alignment] (no host synchronisation inside the loop).
+    ``in_batch_negatives`` selects ttamm's in-batch mode (FusedTrainStep; BASELINE C2/C4), with
+    ``negatives_per_positive`` sampled negatives on top (0 allowed)."""
     model.train()
     if not isinstance(criterion, nn.BCEWithLogitsLoss) or criterion.reduction != "mean" or \
             criterion.weight is not None or criterion.pos_weight is not None:
@@ -493,6 +504,7 @@ def train_one_epoch(
                 user_features=user_features, item_features=item_features, loss_weights=lw,
                 max_batch=max(int(size), users.numel()),
                 item_category_tensor=item_category_tensor, major_category_id=major_category_id,
+                in_batch_negatives=in_batch_negatives,
             )
         neg = masks = None
         if batch_hook is not None:
