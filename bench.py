@@ -1,13 +1,19 @@
 #!/usr/bin/env python3
 """Throughput benchmark of the fused two-tower training step on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4|c5|tiny]
+                    [--negatives sampled|in-batch] [--neg N]
 
 Workload (BASELINE.json configs[1], "C2"): 2M items x 200K users, 96-dim towers, feature
 MLP 605 -> 192 -> 96 (ReLU, dropout 0.15), gated fusion, adaptive mimic on, batch 8192,
 5 sampled negatives per positive (the reference's semantics), AdamW
 (lr 1e-3, wd 0.01) over the dense group incl. the full mimic tables + SparseAdam over the
 ID tables.  Synthetic data of that shape, random-init weights; inputs resident in HBM.
+--negatives in-batch switches to ttamm's in-batch mode (BASELINE C2/C4 "in-batch negatives":
+every user scored against every positive of the global batch, plus --neg sampled negatives,
+default 0).  --config c4 is BASELINE configs[3] per GPU: a 1/8 shard of 50M items x 200K
+users (6.25M x 25K), D = 128, MLP 605 -> 256 -> 128, in-batch negatives (all-gathered across
+ranks); at --gpus 8 the global model is the full C4.
 
 One step = one call of ttamm_train_step on one batch (sampling, forward, loss, backward,
 both optimizers).  `value` = interactions (positives) per second over all ranks.
@@ -18,8 +24,10 @@ the row-sharded step of ttamm/sharded.py on a C2 batch of its own users: item re
 all-reduce.
 
 The JSON line also carries
-  roofline:     the dominant kernel (the AdamW(g=0) sweep over the mimic tables) timed with
-                HIP events on the step's stream; algorithmic bytes 24 * (U+I) * D per launch.
+  roofline:     the dominant MFMA kernel — the first feature-layer forward GEMM (sampled mode),
+                or the in-batch scoring kernel when it takes longer — timed with HIP events on
+                the step's stream over the timed steps; algorithmic FLOPs per launch (2 R F H,
+                or 6 B Bg D for S = U P^T, dU = dS P, dP = dS^T U); `kernels` lists both.
   cpu_baseline: the CPU oracle (oracle/cpu_reference.py, the reference's step restated on
                 PyTorch-CPU incl. its per-row sampler loop) timed on this host, rank 0, N=1.
 """
@@ -51,6 +59,10 @@ CONFIGS = {
     # (weak scaling: each of N ranks holds a shard of this size; at --gpus 8 the 8-GPU C5)
     "c5": dict(U=200_000, I=2_000_000, D=256, H=512, F=605, B=8192, N=5, dropout=0.15, pos_per_user=20,
                matmul="bf16"),
+    # BASELINE configs[3] per GPU (weak scaling): 1/8 of 50M items x 200K users, D = 128, H = 256;
+    # in-batch negatives, all-gathered across ranks ("all-gather negatives")
+    "c4": dict(U=25_000, I=6_250_000, D=128, H=256, F=605, B=8192, N=0, dropout=0.15, pos_per_user=20,
+               negatives="in-batch"),
     # small sanity config (not a bench line)
     "tiny": dict(U=2_000, I=20_000, D=96, H=192, F=605, B=1024, N=5, dropout=0.15, pos_per_user=20),
 }
@@ -101,7 +113,7 @@ class Workload:
     """C2 data + model on one GPU, or rank `rank`'s C2-sized shard of an N x C2 model."""
 
     def __init__(self, c: dict, device, seed: int, world: int = 1, rank: int = 0, step_seed: int | None = None,
-                 deferred: bool = True, overlap: bool = True):
+                 deferred: bool = True, overlap: bool = True, in_batch: bool = False):
         import ttamm
         from ttamm.samplers import PositivesCSR
 
@@ -146,7 +158,7 @@ class Workload:
         self.opts = [torch.optim.AdamW(dense, lr=1e-3, weight_decay=0.01), torch.optim.SparseAdam(sparse, lr=1e-3)]
         kw = dict(negatives_per_positive=c["N"], positives=self.csr, user_features=self.user_features,
                   item_features=self.item_features, loss_weights={"mimic_user": 0.15, "mimic_item": 0.15},
-                  max_batch=c["B"], deferred_adamw=deferred, overlap=overlap)
+                  max_batch=c["B"], deferred_adamw=deferred, overlap=overlap, in_batch_negatives=in_batch)
         if world == 1:
             self.engine = ttamm.FusedTrainStep(self.model, self.opts, seed=seed, **kw)
         else:
@@ -170,7 +182,7 @@ class Workload:
 # ---------------------------------------------------------------------------------------
 # CPU baseline: the oracle's restatement of the reference step on this host
 # ---------------------------------------------------------------------------------------
-def cpu_baseline(c: dict, steps: int, warmup: int, seed: int) -> dict:
+def cpu_baseline(c: dict, steps: int, warmup: int, seed: int, in_batch: bool = False) -> dict:
     from oracle import cpu_reference as ref
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, len(os.sched_getaffinity(0)))
@@ -197,18 +209,19 @@ def cpu_baseline(c: dict, steps: int, warmup: int, seed: int) -> dict:
         batches.append((us, ps))
     lw = {"mimic_user": 0.15, "mimic_item": 0.15}
     ref.train_one_epoch(model, batches[:warmup], opts, negatives_per_positive=N, num_items=I, positives=positives,
-                        user_features=user_features, item_features=item_features, loss_weights=lw)
+                        user_features=user_features, item_features=item_features, loss_weights=lw, in_batch=in_batch)
     _, seen, secs = ref.train_one_epoch(model, batches[warmup:], opts, negatives_per_positive=N, num_items=I,
                                         positives=positives, user_features=user_features,
-                                        item_features=item_features, loss_weights=lw)
+                                        item_features=item_features, loss_weights=lw, in_batch=in_batch)
     return {
         "value": round(seen / secs, 1),
         "unit": "interactions/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{steps} timed steps (+{warmup} warm-up) of the C2-shaped step, batch {B}, on "
+        "sample": f"{steps} timed steps (+{warmup} warm-up) of the same-shaped step, batch {B}, on "
                   f"{threads} host threads: oracle/cpu_reference.py (reference per-row sampler, AdamW over the "
-                  f"full {U}x{c['D']} + {I}x{c['D']} mimic tables, SparseAdam)",
+                  f"full {U}x{c['D']} + {I}x{c['D']} mimic tables, SparseAdam"
+                  f"{', in-batch B x B logits' if in_batch else ''})",
     }
 
 
@@ -237,6 +250,10 @@ def main() -> None:
                     help="sweep AdamW(g=0) over the whole mimic tables every step instead of the deferred exact replay")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the step's index-only prologue on the main stream (no aux stream)")
+    ap.add_argument("--negatives", choices=["sampled", "in-batch"], default=None,
+                    help="sampled (the reference's, default for c2/c5) or ttamm's in-batch mode (default for c4)")
+    ap.add_argument("--neg", type=int, default=None,
+                    help="sampled negatives per positive (default: 5 sampled, 0 on top of in-batch)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -255,12 +272,15 @@ def main() -> None:
     # more ranks than GPUs only with --dist-backend gloo (RCCL needs one GPU per rank)
     device = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(device)
-    c = CONFIGS[args.config]
-
-    from ttamm import _lib
+    c = dict(CONFIGS[args.config])
+    in_batch = (args.negatives or c.get("negatives", "sampled")) == "in-batch"
+    if args.neg is not None:
+        c["N"] = args.neg
+    elif in_batch and args.negatives == "in-batch" and "negatives" not in c:
+        c["N"] = 0
 
     w = Workload(c, device, args.seed + rank, world=world, rank=rank, step_seed=args.seed,
-                 deferred=not args.eager_adamw, overlap=not args.no_overlap)
+                 deferred=not args.eager_adamw, overlap=not args.no_overlap, in_batch=in_batch)
     eng = w.engine
     for _ in range(args.warmup):
         u, p = w.batch()
@@ -270,7 +290,7 @@ def main() -> None:
 
     # per-step HIP event pairs on the step's stream (ttamm.h ttamm_step_args.timing_events):
     # [0,1] dense-group table maintenance, [2,3] the grouped first feature-layer forward GEMM
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(args.steps)]
     for quad in evs:  # materialise the hipEvent_t handles
         for e in quad:
             e.record()
@@ -304,6 +324,7 @@ def main() -> None:
     flush_ms = marks[1].elapsed_time(marks[2])
     maint_ms = sum(q[0].elapsed_time(q[1]) for q in evs) / args.steps
     gemm_ms = sum(q[2].elapsed_time(q[3]) for q in evs) / args.steps
+    ib_ms = sum(q[4].elapsed_time(q[5]) for q in evs) / args.steps if in_batch else 0.0
 
     B, U, I, D, F, H, N = c["B"], c["U"], c["I"], c["D"], c["F"], c["H"], c["N"]
     interactions = args.steps * B * world
@@ -333,6 +354,33 @@ def main() -> None:
                  "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                  "traffic": (traffic or {}).get("dense_sweep_kernel_bytes_per_launch"),
                  "algorithmic_bytes_per_launch": sweep_bytes, "avg_launch_ms": round(maint_ms, 4)}
+    kernels = [{
+        "bound": "mfma",
+        "kernel": f"gemm_kernel first feature layer forward (Linear {F}->{H} + ReLU + dropout, user and item "
+                  f"rows grouped), {'bf16 MFMA 32x32x16' if bf16 else 'fp32 MFMA 32x32x2'}",
+        "achieved": round(tflops, 2),
+        "peak": mfma_peak,
+        "unit": "TFLOP/s",
+        "frac": round(tflops / mfma_peak, 4),
+        "traffic": (traffic or {}).get("l1_forward_gemm_bytes_per_launch"),
+        "algorithmic_flops_per_launch": l1_flops,
+        "avg_launch_ms": round(gemm_ms, 4),
+    }]
+    if in_batch:
+        Bg = B * world
+        ib_flops = 6.0 * B * Bg * D  # S = U P^T, dU = dS P, dP = dS^T U (S recomputed: not counted)
+        ib_tf = ib_flops / (ib_ms * 1e-3) / 1e12
+        kernels.append({
+            "bound": "mfma",
+            "kernel": f"inbatch_kernel (S = U P^T [{B} x {Bg}] + BCE + dU + dP, fp32 MFMA 32x32x2) + ib_reduce",
+            "achieved": round(ib_tf, 2), "peak": MFMA_FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(ib_tf / MFMA_FP32_PEAK_TFLOPS, 4),
+            "traffic": (traffic or {}).get("inbatch_bytes_per_launch"),
+            "algorithmic_flops_per_launch": ib_flops, "avg_launch_ms": round(ib_ms, 4),
+        })
+    roof = max(kernels, key=lambda k: k["avg_launch_ms"])
+    neg_desc = (f"in-batch negatives (all {B * world} positives of the global batch)"
+                + (f" + {N} sampled" if N else "")) if in_batch else f"N={N} sampled negatives"
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -351,26 +399,17 @@ def main() -> None:
             "workload": f"{args.config.upper()}: {I * world} items x {U * world} users, D={D}, "
                         f"MLP {F}->{H}->{D} (ReLU, dropout {c['dropout']}), gated fusion, adaptive mimic, "
                         f"{'bf16' if bf16 else 'fp32'} tower GEMMs, "
-                        f"B={B} per GPU, N={N} sampled negatives, AdamW + SparseAdam",
+                        f"B={B} per GPU, {neg_desc}, AdamW + SparseAdam",
             "global_batch": B * world,
+            "negatives": "in-batch" if in_batch else "sampled",
             "negatives_per_positive": N,
             "parallelism": f"row-sharded tables x{world} (all-to-all) + replicated MLP (all-reduce)"
                            if world > 1 else "single",
             "adamw_tables": "deferred exact replay" if deferred else "eager sweep",
         },
         "final_loss": round(loss, 6),
-        "roofline": {
-            "bound": "mfma",
-            "kernel": f"gemm_kernel first feature layer forward (Linear {F}->{H} + ReLU + dropout, user and item "
-                      f"rows grouped), {'bf16 MFMA 32x32x16' if bf16 else 'fp32 MFMA 32x32x2'}",
-            "achieved": round(tflops, 2),
-            "peak": mfma_peak,
-            "unit": "TFLOP/s",
-            "frac": round(tflops / mfma_peak, 4),
-            "traffic": (traffic or {}).get("l1_forward_gemm_bytes_per_launch"),
-            "algorithmic_flops_per_launch": l1_flops,
-            "avg_launch_ms": round(gemm_ms, 4),
-        },
+        "roofline": roof,
+        "kernels": kernels,
         "table_maintenance": maint,
         "timeline": {"ms_per_step_excl_closing_flush": round(steps_only_ms, 4),
                      "closing_flush_ms": round(flush_ms, 4),
@@ -380,7 +419,7 @@ def main() -> None:
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(c, args.cpu_steps, 1, args.seed)
+            out["cpu_baseline"] = cpu_baseline(c, args.cpu_steps, 1, args.seed, in_batch=in_batch)
         except Exception as exc:  # reported, not fatal to the GPU measurement
             out["cpu_baseline"] = {"error": repr(exc)}
     if rank == 0:

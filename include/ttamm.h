@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 11
+#define TTAMM_ABI_VERSION 12
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -190,10 +190,11 @@ typedef struct ttamm_step_args {
     uint32_t* status;     /* device status word (TTAMM_STATUS_* bits), OR-ed          */
     void* workspace;
     size_t workspace_bytes;
-    void* timing_events[4]; /* optional hipEvent_t pairs (bench roofline), NULL = off:
+    void* timing_events[6]; /* optional hipEvent_t pairs (bench roofline), NULL = off:
                                [0],[1] around the dense-group table maintenance (eager
                                AdamW(g=0) sweep, or deferred slice replay); [2],[3] around
-                               the grouped first feature-layer forward GEMM              */
+                               the grouped first feature-layer forward GEMM; [4],[5] around
+                               the in-batch scoring kernel (in_batch)                    */
     /* ---- row-sharded multi-GPU step (phase != TTAMM_PHASE_ALL) ----------------------
      * The same workspace must be passed to every phase of a step.                        */
     int32_t phase;                /* TTAMM_PHASE_* bits                                      */

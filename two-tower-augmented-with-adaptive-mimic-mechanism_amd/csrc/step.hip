@@ -1189,7 +1189,10 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         a.inv_T = 1.0f / (float)(Bg * (ib_cols + N));
         a.dU = ws.ib_du;
         a.ld_du = D;
+        void* const* ev = A.timing_events + 4;
+        if (ev[0] && ev[1]) TTAMM_HIP(hipEventRecord((hipEvent_t)ev[0], s));
         if ((rc = launch_inbatch(a, s))) return rc;
+        if (ev[0] && ev[1]) TTAMM_HIP(hipEventRecord((hipEvent_t)ev[1], s));
     }
     // ---- score + loss (fwd + bwd seeds), user-side backward ---------------------------------
     if (ph & TTAMM_PHASE_USER) {

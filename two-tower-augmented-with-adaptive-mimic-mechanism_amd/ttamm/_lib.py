@@ -125,7 +125,7 @@ class StepArgs(ctypes.Structure):
         ("status", c_vp),
         ("workspace", c_vp),
         ("workspace_bytes", ctypes.c_size_t),
-        ("timing_events", c_vp * 4),
+        ("timing_events", c_vp * 6),
         # row-sharded multi-GPU step (ttamm.h TTAMM_PHASE_*)
         ("phase", c_i32),
         ("row_base", c_i64),
@@ -157,7 +157,7 @@ class StepArgs(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 11  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 12  # ttamm.h TTAMM_ABI_VERSION
 
 # ttamm.h TTAMM_PHASE_*
 PHASE_ALL = 0

@@ -337,8 +337,8 @@ class ShardedTrainStep(FusedTrainStep):
         Bg = W * B
         a.row_base = rank * B
         a.global_batch = Bg
-        ev = list(timing_events or []) + [None] * 4
-        for i in range(4):
+        ev = list(timing_events or []) + [None] * 6
+        for i in range(6):
             a.timing_events[i] = None
         self._hparams()
         negs = neg_items.reshape(-1) if neg_items is not None else self.neg_buffer[: B * N]
@@ -377,7 +377,9 @@ class ShardedTrainStep(FusedTrainStep):
             gathered = yield AllGather(self.ib_local[:B])
             a.inbatch_items = gathered.data_ptr()
             a.inbatch_dp_all = self.ib_dp_all.data_ptr()
+            a.timing_events[4], a.timing_events[5] = ev[4], ev[5]
             self._phase(_lib.PHASE_INBATCH)
+            a.timing_events[4] = a.timing_events[5] = None
             dp = yield ReduceScatter(self.ib_dp_all[: W * B])
             a.inbatch_dp = dp.data_ptr()
             ib = (gathered, dp)

@@ -355,7 +355,7 @@ class FusedTrainStep:
             return
         a = self.args
         ev = list(timing_events or [])
-        for i in range(4):
+        for i in range(6):
             a.timing_events[i] = ev[i] if i < len(ev) else None
         self._hparams()
         _lib.check(self.lib.ttamm_train_step(ctypes.byref(a), _lib.stream_handle(self.device)))
