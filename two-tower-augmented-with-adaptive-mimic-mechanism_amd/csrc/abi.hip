@@ -115,7 +115,7 @@ TTAMM_API int ttamm_sample_negatives(const int64_t* users, int64_t batch, int32_
                                      const int64_t* pos_offsets, const int64_t* pos_values, uint64_t seed,
                                      uint64_t counter, int64_t* out, uint32_t* status, void* stream) {
     return launch_sample_negatives(users, batch, num_neg, num_items, pos_offsets, pos_values, seed, counter, 0, out,
-                                   status, (hipStream_t)stream);
+                                   nullptr, status, (hipStream_t)stream);
 }
 
 TTAMM_API int ttamm_sparse_adam_rows(float* weight, float* exp_avg, float* exp_avg_sq, int32_t dim,

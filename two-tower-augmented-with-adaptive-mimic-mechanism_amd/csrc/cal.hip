@@ -17,8 +17,6 @@
 //   piece sums -> means -> piece centered scatter tiles (64 x 64 per block) -> covariances ->
 //   per-category squared distances -> loss -> G_major -> per-row gradients added into the
 //   item rows' dT (and dA for positives: the augmented embedding is t + a).
-#include <hipcub/hipcub.hpp>
-
 #include "kernels.h"
 
 namespace ttamm {
@@ -310,12 +308,6 @@ inline unsigned blocks_for(int64_t n, int t = 256) { return (unsigned)ceil_div(n
 
 int cal_max_pieces(int64_t R, int64_t nseg_max) { return (int)(ceil_div(R, kPiece) + nseg_max); }
 
-size_t cal_scan_temp_bytes(int64_t nseg_max) {
-    size_t bytes = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (int32_t*)nullptr, (int32_t*)nullptr, (int)nseg_max);
-    return bytes;
-}
-
 int launch_category_alignment(const CalArgs& a, hipStream_t s) {
     TTAMM_REQUIRE(a.D % 4 == 0 && a.D <= 256, "category alignment: embedding dim must be a multiple of 4, <= 256");
     TTAMM_REQUIRE(a.R > 0 && a.nseg_max > 0 && a.nseg_max <= 65535, "category alignment: bad batch / category count");
@@ -326,8 +318,7 @@ int launch_category_alignment(const CalArgs& a, hipStream_t s) {
     if ((rc = launch_coalesce(a.catrow, a.R, a.num_categories, co, s))) return rc;
     hipLaunchKernelGGL(cal_plan_kernel, dim3(blocks_for(a.nseg_max)), dim3(256), 0, s, a);
     TTAMM_LAUNCH_CHECK();
-    size_t bytes = a.scan_temp_bytes;
-    TTAMM_HIP(hipcub::DeviceScan::ExclusiveSum(a.scan_temp, bytes, a.pcount, a.pstart, (int)a.nseg_max, s));
+    if ((rc = launch_block_exclusive_scan(a.pcount, a.pstart, a.nseg_max, s))) return rc;
     const unsigned pieces = (unsigned)cal_max_pieces(a.R, a.nseg_max);
     const unsigned nt = (unsigned)ceil_div(a.D, kTile);
     hipLaunchKernelGGL(cal_piece_sum_kernel, dim3(pieces), dim3(256), 0, s, a);

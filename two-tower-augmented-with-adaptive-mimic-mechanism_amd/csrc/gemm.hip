@@ -517,8 +517,18 @@ __global__ void wgrad_reduce_kernel(WgradBatch batch, int64_t total) {
     const int Mo = P.M;
     const int64_t plane = (int64_t)(P.N + 1) * Mo;
     const int n = (int)(off / Mo), m = (int)(off - (int64_t)n * Mo);
+    // fixed summation order (split 0, 1, ...); the loads of 8 splits are issued before their adds
     float s = 0.f;
-    for (int sp = 0; sp < P.splits; ++sp) s += P.slab[sp * plane + off];
+    const float* src = P.slab + off;
+    int sp = 0;
+    for (; sp + 8 <= P.splits; sp += 8) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = src[(int64_t)(sp + i) * plane];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s += v[i];
+    }
+    for (; sp < P.splits; ++sp) s += src[(int64_t)sp * plane];
     if (n < P.N) P.grad_w[(int64_t)m * P.N + n] = s;
     else if (P.grad_b) P.grad_b[m] = s;
 }

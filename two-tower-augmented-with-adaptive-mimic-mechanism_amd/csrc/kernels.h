@@ -277,20 +277,35 @@ int launch_retrieval_topk(const float* Q, int64_t nq, int64_t ldq, const float* 
 // ------------------------------------------------------------------------------------
 // Coalesce + optimizers (optim.hip)
 // ------------------------------------------------------------------------------------
+// Grouping of a batch's row ids ("coalesce": duplicates summed in batch order, as torch's
+// index_add / sparse coalesce do).  Output: slots 0..n-1 hold the positions grouped by row —
+// segment u = slots [seg_start[u], seg_start[u+1]) is one row (keys_out), its positions
+// ascending.  Segment order: first occurrence in the batch, or ascending row id (`sorted`, for
+// small key ranges).  cnt / first / fill are per-row scratch of the table (key_range entries)
+// that must be zero between calls — the call leaves them zero again.
 struct CoalesceWs {
-    int32_t* keys_in;
-    int32_t* vals_in;
-    int32_t* keys_out;
-    int32_t* vals_out;
-    int32_t* flags;     // [n]
-    int32_t* uid;       // [n]   inclusive scan
-    int32_t* seg_start; // [n+1]
-    int32_t* n_unique;  // [1]
-    void* temp;
-    size_t temp_bytes;
+    int32_t* keys_out;   // [n]
+    int32_t* vals_out;   // [n] batch position of each slot
+    int32_t* vals_tmp;   // [n]
+    int32_t* lead;       // [n] leader flag -> segment index of a leader position
+    int32_t* lead_cnt;   // [max(n, 257)] scan scratch (tile totals)
+    int32_t* seglong;    // [max(n, 257)] 1: the slot's segment is longer than a row-update piece
+    int32_t* seg_start;  // [n + 1]
+    int32_t* n_unique;   // [1]
+    int32_t* cnt;        // [key_range] persistent, zero between calls
+    int32_t* first;      // [key_range]
+    int32_t* fill;       // [key_range]
+    int64_t key_range;
+    int sorted;          // 1: segments in ascending key order (key_range <= 65536)
 };
-size_t coalesce_temp_bytes(int64_t n);
-// sort rows by index; unique rows + segment starts
+constexpr int kCoalescePiece = 32;  // row-update piece: longer segments are summed in two levels
+size_t coalesce_scratch_ints(int64_t key_range);  // per-row scratch (3 arrays)
+// scratch: the cnt / first / fill arrays carved from a zeroed buffer of coalesce_scratch_ints ints
+void coalesce_bind_scratch(CoalesceWs& ws, int32_t* scratch, int64_t key_range);
+// group rows by index: unique rows + segment starts.  Two halves: the count (after it,
+// ws.first marks every row's first position) and the grouping; launch_coalesce runs both.
+int launch_coalesce_count(const int64_t* idx, int64_t n, int64_t table_rows, CoalesceWs& ws, hipStream_t s);
+int launch_coalesce_group(const int64_t* idx, int64_t n, int64_t table_rows, CoalesceWs& ws, hipStream_t s);
 int launch_coalesce(const int64_t* idx, int64_t n, int64_t table_rows, CoalesceWs& ws, hipStream_t s);
 
 // ------------------------------------------------------------------------------------
@@ -311,8 +326,6 @@ struct CalArgs {
     int nseg_max;               // min(R, num_categories)
     int32_t* pcount;            // [nseg_max] pieces per category segment
     int32_t* pstart;            // [nseg_max] exclusive scan
-    void* scan_temp;
-    size_t scan_temp_bytes;
     float* psum;                // [pieces, D]
     float* mean;                // [nseg_max, D]
     float* pslab;               // [pieces, D, D]
@@ -327,7 +340,8 @@ struct CalArgs {
     int64_t dA_rows;
 };
 int cal_max_pieces(int64_t R, int64_t nseg_max);
-size_t cal_scan_temp_bytes(int64_t nseg_max);
+// exclusive prefix sum of n ints by one block (n up to ~1M; used for small arrays)
+int launch_block_exclusive_scan(const int32_t* in, int32_t* out, int64_t n, hipStream_t s);
 int launch_category_alignment(const CalArgs& a, hipStream_t s);
 
 
@@ -357,8 +371,9 @@ struct RowUpdateArgs {
     int dim;
     const int32_t* n_unique;
     const int32_t* seg_start;
-    const int32_t* keys;    // sorted keys
-    const int32_t* rows;    // sorted tower row ids
+    const int32_t* keys;    // keys grouped by row (CoalesceWs keys_out)
+    const int32_t* rows;    // tower row ids, grouped by table row (CoalesceWs vals_out)
+    const int32_t* seglong; // CoalesceWs seglong: the slot's row has > kCoalescePiece contributions
     // ID table gradient source: dE[row] (ld)
     const float* dE;
     int64_t ld_dE;
@@ -404,6 +419,10 @@ struct ReplaySeg {
     const int32_t* keys;
     const int32_t* seg_start;
     const int32_t* n_unique;
+    // ... or the rows lead_idx[p] of batch positions p in [row_lo, row_hi) that are their row's
+    // first occurrence (lead_first[row] == INT_MAX - p: CoalesceWs.first after the count pass)
+    const int64_t* lead_idx;
+    const int32_t* lead_first;
 };
 constexpr int kMaxReplaySegs = 4;
 struct ReplayArgs {
@@ -468,6 +487,7 @@ SparseConsts make_sparse_consts(double lr, double beta1, double beta2, double ep
 // slot_base: global index of this batch's first slot (row_base * num_neg) — the Philox stream key
 int launch_sample_negatives(const int64_t* users, int64_t batch, int num_neg, int64_t num_items,
                             const int64_t* pos_offsets, const int64_t* pos_values, uint64_t seed,
-                            uint64_t counter, int64_t slot_base, int64_t* out, uint32_t* status, hipStream_t s);
+                            uint64_t counter, int64_t slot_base, int64_t* out, int64_t* out2, uint32_t* status,
+                            hipStream_t s);  // out2: optional second copy
 
 }  // namespace ttamm

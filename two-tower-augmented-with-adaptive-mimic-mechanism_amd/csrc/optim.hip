@@ -2,8 +2,9 @@
 // fused SparseAdam / AdamW updates.
 //
 // Row tables receive per-row gradient contributions from the batch (duplicates allowed).
-// They are coalesced by a stable radix sort of the int32 row keys, so duplicate rows are
-// summed in batch order — the order torch's CPU index_add / coalesce use
+// They are grouped by row (launch_coalesce: counts and first occurrences through per-row
+// scratch, a one-block scan, a scatter, then each row's positions put back in ascending order),
+// so duplicate rows are summed in batch order — the order torch's CPU index_add / coalesce use
 // (training.py:822 backward; _functional.py:44 grad.coalesce()).
 //
 // Tables in the dense group (the adaptive-mimic tables, adaptive_mimic.py:35-36, put in the
@@ -12,8 +13,8 @@
 // (2) a pure streaming AdamW(g = 0) pass over the whole table — the dominant HBM kernel of
 // the step, 24 bytes per element — and (3) a scatter of the side rows over the swept table.
 // The result equals one dense AdamW step over the full dense gradient.
-#include <hipcub/hipcub.hpp>
-
+#include <algorithm>
+#include <climits>
 #include <cmath>
 
 #include "kernels.h"
@@ -73,29 +74,215 @@ __device__ __forceinline__ void sparse_adam_elem(float& p, float& m, float& v, f
     p = p + c.neg_step * (numer / denom);
 }
 
-__global__ void keys_init_kernel(const int64_t* __restrict__ idx, int64_t n, int32_t* __restrict__ keys,
-                                 int32_t* __restrict__ vals) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        keys[i] = (int32_t)idx[i];
-        vals[i] = (int32_t)i;
+// ---- grouping of a batch's row ids (launch_coalesce) ----------------------------------------
+// first[key] holds INT_MAX - (first position): 0 = untouched, and atomicMax keeps the earliest.
+__global__ void co_count_kernel(const int64_t* __restrict__ idx, int64_t n, int32_t* __restrict__ cnt,
+                                int32_t* __restrict__ first) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const int64_t key = idx[p];
+    atomicAdd(&cnt[key], 1);
+    atomicMax(&first[key], (int32_t)(INT_MAX - p));
+}
+
+// Entry i of the segment scan: (flag, count) — a position's leader flag and its row's count,
+// or (sorted mode, entries = the key range) whether key i occurs and its count.
+__device__ __forceinline__ void co_entry(int by_key, int64_t i, const int64_t* __restrict__ idx,
+                                         const int32_t* __restrict__ cnt, const int32_t* __restrict__ first,
+                                         int32_t& f, int32_t& c) {
+    if (by_key) {
+        c = cnt[i];
+        f = c > 0;
+    } else {
+        const int64_t key = idx[i];
+        f = first[key] == (int32_t)(INT_MAX - i);
+        c = f ? cnt[key] : 0;
     }
 }
 
-__global__ void seg_flags_kernel(const int32_t* __restrict__ keys, int64_t n, int32_t* __restrict__ flags) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
+// block-wide inclusive scan of (f, c) over 256 threads
+__device__ __forceinline__ void block_scan2(int32_t& f, int32_t& c, int32_t* sf, int32_t* sc) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t a = __shfl_up(f, o, 64), b = __shfl_up(c, o, 64);
+        if (lane >= o) {
+            f += a;
+            c += b;
+        }
+    }
+    if (lane == 63) {
+        sf[w] = f;
+        sc[w] = c;
+    }
+    __syncthreads();
+    int32_t pf = 0, pc = 0;
+    for (int i = 0; i < w; ++i) {
+        pf += sf[i];
+        pc += sc[i];
+    }
+    f += pf;
+    c += pc;
 }
 
-__global__ void seg_start_kernel(const int32_t* __restrict__ flags, const int32_t* __restrict__ uid, int64_t n,
-                                 int32_t* __restrict__ seg_start, int32_t* __restrict__ n_unique) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        if (flags[i]) seg_start[uid[i] - 1] = (int32_t)i;
-        if (i == n - 1) {
-            n_unique[0] = uid[i];
-            seg_start[uid[i]] = (int32_t)n;
+// pass 1 of the segment scan: each 256-entry tile's totals
+__global__ __launch_bounds__(256) void co_tile_sum_kernel(int64_t n, int by_key, const int64_t* __restrict__ idx,
+                                                          const int32_t* __restrict__ cnt,
+                                                          const int32_t* __restrict__ first,
+                                                          int32_t* __restrict__ tile_f, int32_t* __restrict__ tile_c) {
+    __shared__ int32_t sf[4], sc[4];
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    int32_t f = 0, c = 0;
+    if (i < n) co_entry(by_key, i, idx, cnt, first, f, c);
+    block_scan2(f, c, sf, sc);
+    if (threadIdx.x == 255) {
+        tile_f[blockIdx.x] = f;
+        tile_c[blockIdx.x] = c;
+    }
+}
+
+// pass 2: exclusive scan of the tile totals (one block; tiles are few), n_unique, total
+__global__ __launch_bounds__(1024) void co_tile_scan_kernel(int64_t tiles, int32_t* __restrict__ tile_f,
+                                                            int32_t* __restrict__ tile_c, int32_t* __restrict__ seg_start,
+                                                            int32_t* __restrict__ n_unique) {
+    __shared__ int32_t sf[1024], sc[1024];
+    const int t = threadIdx.x;
+    const int64_t chunk = (tiles + 1023) / 1024;
+    const int64_t lo = min(tiles, t * chunk), hi = min(tiles, lo + chunk);
+    int32_t f_sum = 0, c_sum = 0;
+    for (int64_t i = lo; i < hi; ++i) {
+        f_sum += tile_f[i];
+        c_sum += tile_c[i];
+    }
+    sf[t] = f_sum;
+    sc[t] = c_sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int32_t a = t >= o ? sf[t - o] : 0, b = t >= o ? sc[t - o] : 0;
+        __syncthreads();
+        sf[t] += a;
+        sc[t] += b;
+        __syncthreads();
+    }
+    int32_t rf = sf[t] - f_sum, rc = sc[t] - c_sum;
+    for (int64_t i = lo; i < hi; ++i) {
+        const int32_t a = tile_f[i], b = tile_c[i];
+        tile_f[i] = rf;
+        tile_c[i] = rc;
+        rf += a;
+        rc += b;
+    }
+    if (t == 1023) {
+        n_unique[0] = sf[t];
+        seg_start[sf[t]] = sc[t];
+    }
+}
+
+// pass 3: every flagged entry's segment index and start; the index goes to lead[position]
+// (first-occurrence order) or first[key] (sorted mode)
+__global__ __launch_bounds__(256) void co_tile_write_kernel(int64_t n, int by_key, const int64_t* __restrict__ idx,
+                                                            const int32_t* __restrict__ cnt, int32_t* __restrict__ first,
+                                                            const int32_t* __restrict__ tile_f,
+                                                            const int32_t* __restrict__ tile_c,
+                                                            int32_t* __restrict__ lead, int32_t* __restrict__ seg_start) {
+    __shared__ int32_t sf[4], sc[4];
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    int32_t f = 0, c = 0;
+    if (i < n) co_entry(by_key, i, idx, cnt, first, f, c);
+    int32_t fi = f, ci = c;
+    block_scan2(fi, ci, sf, sc);
+    if (f) {
+        const int32_t u = tile_f[blockIdx.x] + fi - 1;
+        seg_start[u] = tile_c[blockIdx.x] + ci - c;
+        if (by_key) first[i] = u;
+        else lead[i] = u;
+    }
+}
+
+// every position into its row's segment (order within a segment: arbitrary, fixed next)
+__global__ void co_fill_kernel(const int64_t* __restrict__ idx, int64_t n, int by_key,
+                               const int32_t* __restrict__ lead, const int32_t* __restrict__ first,
+                               int32_t* __restrict__ fill, const int32_t* __restrict__ seg_start,
+                               int32_t* __restrict__ vals_tmp, int32_t* __restrict__ keys_out,
+                               int32_t* __restrict__ n_big) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p == 0) n_big[0] = 0;  // the long-segment list of the ordering pass
+    if (p >= n) return;
+    const int64_t key = idx[p];
+    const int32_t u = by_key ? first[key] : lead[INT_MAX - first[key]];  // the leader's segment
+    const int32_t slot = seg_start[u] + atomicAdd(&fill[key], 1);
+    vals_tmp[slot] = (int32_t)p;
+    keys_out[slot] = (int32_t)key;
+}
+
+// Segment ordering: every segment's positions in ascending order (so duplicate rows sum in
+// batch order), the long-segment flags, and the row's scratch back to zero.  One thread per
+// segment sorts up to kOrderSmall positions in registers (nearly every row of a batch occurs
+// once or a few times); longer segments (hot rows) are listed in `big` and ranked by whole
+// blocks, through LDS up to kOrderLds positions.
+constexpr int kOrderSmall = 16;
+constexpr int kOrderLds = 4096;
+
+__device__ __forceinline__ void co_reset(const CoalesceWs& W, int32_t key) {
+    W.cnt[key] = 0;
+    W.first[key] = 0;
+    W.fill[key] = 0;
+}
+
+__global__ __launch_bounds__(256) void co_order_small_kernel(CoalesceWs W, int32_t* __restrict__ big,
+                                                             int32_t* __restrict__ n_big) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= W.n_unique[0]) return;
+    const int32_t k0 = W.seg_start[u], L = W.seg_start[u + 1] - k0;
+    if (L > kOrderSmall) {
+        big[atomicAdd(n_big, 1)] = (int32_t)u;
+        return;
+    }
+    int32_t v[kOrderSmall];
+#pragma unroll
+    for (int i = 0; i < kOrderSmall; ++i) v[i] = i < L ? W.vals_tmp[k0 + i] : INT_MAX;
+#pragma unroll
+    for (int i = 1; i < kOrderSmall; ++i)  // insertion sort, fully unrolled (registers only)
+#pragma unroll
+        for (int j = i; j > 0; --j) {
+            const int32_t a = v[j - 1], b = v[j];
+            v[j - 1] = min(a, b);
+            v[j] = max(a, b);
         }
+    const int32_t longseg = L > kCoalescePiece ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < kOrderSmall; ++i)
+        if (i < L) {
+            W.vals_out[k0 + i] = v[i];
+            W.seglong[k0 + i] = longseg;
+        }
+    co_reset(W, W.keys_out[k0]);
+}
+
+__global__ __launch_bounds__(256) void co_order_big_kernel(CoalesceWs W, const int32_t* __restrict__ big,
+                                                           const int32_t* __restrict__ n_big) {
+    __shared__ int32_t sv[kOrderLds];
+    const int nb = n_big[0];
+    for (int b = blockIdx.x; b < nb; b += gridDim.x) {
+        const int32_t u = big[b];
+        const int32_t k0 = W.seg_start[u], k1 = W.seg_start[u + 1], L = k1 - k0;
+        const int32_t longseg = L > kCoalescePiece ? 1 : 0;
+        const bool in_lds = L <= kOrderLds;
+        __syncthreads();
+        if (in_lds)
+            for (int32_t j = threadIdx.x; j < L; j += blockDim.x) sv[j] = W.vals_tmp[k0 + j];
+        __syncthreads();
+        for (int32_t j = threadIdx.x; j < L; j += blockDim.x) {
+            const int32_t v = in_lds ? sv[j] : W.vals_tmp[k0 + j];
+            int32_t rank = 0;
+            if (in_lds)
+                for (int32_t i = 0; i < L; ++i) rank += sv[i] < v ? 1 : 0;
+            else
+                for (int32_t i = k0; i < k1; ++i) rank += W.vals_tmp[i] < v ? 1 : 0;
+            W.vals_out[k0 + rank] = v;
+            W.seglong[k0 + j] = longseg;
+        }
+        if (threadIdx.x == 0) co_reset(W, W.keys_out[k0]);
     }
 }
 
@@ -105,7 +292,7 @@ __global__ void seg_start_kernel(const int32_t* __restrict__ flags, const int32_
 //              inside its chunk ("piece") and stores it at the run's first position;
 //   row_update: one wave per unique row adds its pieces in position order, then applies
 //              the optimizer.  Both orders are fixed, so results are deterministic.
-constexpr int kPiece = 32;
+constexpr int kPiece = kCoalescePiece;
 constexpr int kRowWaves = 4;
 
 __device__ __forceinline__ const float* dA_row(const RowUpdateArgs& A, int64_t r) {
@@ -119,6 +306,8 @@ __global__ __launch_bounds__(64 * kRowWaves) void piece_sum_kernel(RowUpdateArgs
     const int64_t k0 = chunk * kPiece;
     if (k0 >= A.n) return;
     const int cnt = (int)min((int64_t)kPiece, A.n - k0);
+    // only segments longer than a piece are summed in two levels (row_update sums the rest)
+    if (__ballot(lane < cnt && A.seglong[k0 + lane] != 0) == 0ull) return;
     // positions of the chunk: lane p holds row / key / "last of a run" for position k0 + p
     int64_t my_row = 0;
     int my_key = 0, my_last = 1;
@@ -167,47 +356,63 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArg
     const int64_t key = A.keys[k0];
     const int D = A.dim;
     const bool mimic = A.mimic.weight != nullptr;
+    const bool direct = k1 - k0 <= kPiece;
     for (int d = lane; d < D; d += 64) {
-        float ge = A.piece_e[k0 * D + d];
-        float ga = mimic ? A.piece_a[k0 * D + d] : 0.f;
-        for (int64_t k = (k0 / kPiece + 1) * kPiece; k < k1; k += kPiece) {
-            ge += A.piece_e[k * D + d];
-            if (mimic) ga += A.piece_a[k * D + d];
+        // the table rows first: they do not depend on the gradient sums below
+        const int64_t o = key * D + d;
+        float ip = A.id.weight[o], im = A.id.exp_avg[o], iv = A.id.exp_avg_sq[o];
+        float mp = 0.f, mm = 0.f, mv = 0.f;
+        if (mimic) {
+            mp = A.mimic.weight[o];
+            mm = A.mimic.exp_avg[o];
+            mv = A.mimic.exp_avg_sq[o];
         }
-        {
-            const int64_t o = key * D + d;
-            float p = A.id.weight[o], m = A.id.exp_avg[o], v = A.id.exp_avg_sq[o];
-            if (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM) {
-                sparse_adam_elem(p, m, v, ge, A.sp);
-                A.id.weight[o] = p;
-                A.id.exp_avg[o] = m;
-                A.id.exp_avg_sq[o] = v;
-            } else if (A.id.last_step) {  // deferred mode: the row was caught up before the forward
-                adam_elem(p, m, v, ge, A.ad);
-                A.id.weight[o] = p;
-                A.id.exp_avg[o] = m;
-                A.id.exp_avg_sq[o] = v;
-            } else {
-                adam_elem(p, m, v, ge, A.ad);
-                float* sd = A.side_id + u * 3 * D;
-                sd[d] = p;
-                sd[D + d] = m;
-                sd[2 * D + d] = v;
+        float ge, ga = 0.f;
+        if (direct) {  // the row's contributions in batch order
+            const int64_t r0 = A.rows[k0];
+            ge = A.dE[r0 * A.ld_dE + d];
+            if (mimic) ga = dA_row(A, r0)[d];
+            for (int64_t k = k0 + 1; k < k1; ++k) {
+                const int64_t r = A.rows[k];
+                ge += A.dE[r * A.ld_dE + d];
+                if (mimic) ga += dA_row(A, r)[d];
+            }
+        } else {  // pieces (piece_sum_kernel), then the pieces in order
+            ge = A.piece_e[k0 * D + d];
+            ga = mimic ? A.piece_a[k0 * D + d] : 0.f;
+            for (int64_t k = (k0 / kPiece + 1) * kPiece; k < k1; k += kPiece) {
+                ge += A.piece_e[k * D + d];
+                if (mimic) ga += A.piece_a[k * D + d];
             }
         }
+        if (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM) {
+            sparse_adam_elem(ip, im, iv, ge, A.sp);
+            A.id.weight[o] = ip;
+            A.id.exp_avg[o] = im;
+            A.id.exp_avg_sq[o] = iv;
+        } else if (A.id.last_step) {  // deferred mode: the row was caught up before the forward
+            adam_elem(ip, im, iv, ge, A.ad);
+            A.id.weight[o] = ip;
+            A.id.exp_avg[o] = im;
+            A.id.exp_avg_sq[o] = iv;
+        } else {
+            adam_elem(ip, im, iv, ge, A.ad);
+            float* sd = A.side_id + u * 3 * D;
+            sd[d] = ip;
+            sd[D + d] = im;
+            sd[2 * D + d] = iv;
+        }
         if (mimic) {
-            const int64_t o = key * D + d;
-            float p = A.mimic.weight[o], m = A.mimic.exp_avg[o], v = A.mimic.exp_avg_sq[o];
-            adam_elem(p, m, v, ga, A.ad);
+            adam_elem(mp, mm, mv, ga, A.ad);
             if (A.mimic.last_step) {
-                A.mimic.weight[o] = p;
-                A.mimic.exp_avg[o] = m;
-                A.mimic.exp_avg_sq[o] = v;
+                A.mimic.weight[o] = mp;
+                A.mimic.exp_avg[o] = mm;
+                A.mimic.exp_avg_sq[o] = mv;
             } else {
                 float* sd = A.side_mimic + u * 3 * D;
-                sd[d] = p;
-                sd[D + d] = m;
-                sd[2 * D + d] = v;
+                sd[d] = mp;
+                sd[D + d] = mm;
+                sd[2 * D + d] = mv;
             }
         }
     }
@@ -273,13 +478,21 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
     __syncthreads();
     const int dim = S.dim, dim4 = dim >> 2;
     const int32_t target = ka->target;
-    const bool by_key = S.keys != nullptr;
+    const bool by_key = S.keys != nullptr, by_lead = S.lead_idx != nullptr;
     const int64_t nrows = by_key ? (int64_t)S.n_unique[0] : S.row_hi - S.row_lo;
     const int64_t total = nrows * dim4;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = e / dim4;
         const int q = (int)(e - r * dim4);
-        const int64_t row = by_key ? (int64_t)S.keys[S.seg_start[r]] : S.row_lo + r;
+        int64_t row;
+        if (by_key) {
+            row = S.keys[S.seg_start[r]];
+        } else if (by_lead) {  // batch position r: its row, replayed once (by its first occurrence)
+            row = S.lead_idx[S.row_lo + r];
+            if (S.lead_first[row] != (int32_t)(INT_MAX - (S.row_lo + r))) continue;
+        } else {
+            row = S.row_lo + r;
+        }
         const int32_t l = S.last[row];
         if (l >= target) continue;
         const int64_t o = row * dim + 4 * q;
@@ -373,11 +586,6 @@ inline unsigned grid_for(int64_t work, int threads = 256, int64_t cap = 65536) {
     return (unsigned)g;
 }
 
-inline int end_bit_for(int64_t rows) {
-    int b = 1;
-    while (b < 31 && (int64_t(1) << b) < rows) ++b;
-    return b;
-}
 
 }  // namespace
 
@@ -427,33 +635,93 @@ SparseConsts make_sparse_consts(double lr, double beta1, double beta2, double ep
     return c;
 }
 
-size_t coalesce_temp_bytes(int64_t n) {
-    size_t sort_bytes = 0, scan_bytes = 0;
-    const int nn = (int)(n > 0 ? n : 1);
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr,
-                                       (int32_t*)nullptr, nn, 0, 31, (hipStream_t)0);
-    (void)hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, (int32_t*)nullptr, (int32_t*)nullptr, nn, (hipStream_t)0);
-    return (sort_bytes > scan_bytes ? sort_bytes : scan_bytes) + 256;
+size_t coalesce_scratch_ints(int64_t key_range) { return (size_t)3 * (size_t)(key_range > 0 ? key_range : 1); }
+
+void coalesce_bind_scratch(CoalesceWs& ws, int32_t* scratch, int64_t key_range) {
+    const int64_t r = key_range > 0 ? key_range : 1;
+    ws.cnt = scratch;
+    ws.first = scratch ? scratch + r : nullptr;
+    ws.fill = scratch ? scratch + 2 * r : nullptr;
+    ws.key_range = key_range;
 }
 
-int launch_coalesce(const int64_t* idx, int64_t n, int64_t table_rows, CoalesceWs& ws, hipStream_t s) {
-    TTAMM_REQUIRE(table_rows < (int64_t(1) << 31), "coalesce: table too large for int32 keys");
+int launch_coalesce_count(const int64_t* idx, int64_t n, int64_t table_rows, CoalesceWs& ws, hipStream_t s) {
+    TTAMM_REQUIRE(table_rows < (int64_t(1) << 31) && n < (int64_t(1) << 31) - 1, "coalesce: table or batch too large");
+    TTAMM_REQUIRE(ws.key_range >= table_rows && ws.cnt && ws.first && ws.fill, "coalesce: per-row scratch missing");
+    TTAMM_REQUIRE(!ws.sorted || table_rows <= 65536, "coalesce: sorted grouping needs <= 65536 keys");
+    if (n <= 0) return TTAMM_OK;
+    hipLaunchKernelGGL(co_count_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, idx, n, ws.cnt, ws.first);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_coalesce_group(const int64_t* idx, int64_t n, int64_t table_rows, CoalesceWs& ws, hipStream_t s) {
     if (n <= 0) {
         TTAMM_HIP(hipMemsetAsync(ws.n_unique, 0, sizeof(int32_t), s));
         return TTAMM_OK;
     }
-    hipLaunchKernelGGL(keys_init_kernel, dim3(grid_for(n, 256, 1 << 30)), dim3(256), 0, s, idx, n, ws.keys_in,
-                       ws.vals_in);
+    const unsigned g = (unsigned)ceil_div(n, 256);
+    // segment scan over positions (first-occurrence order) or over the key range (sorted)
+    const int64_t entries = ws.sorted ? table_rows : n;
+    const int64_t tiles = ceil_div(entries, 256);
+    TTAMM_REQUIRE(tiles <= std::max<int64_t>(n, 257), "coalesce: tile scratch too small");
+    hipLaunchKernelGGL(co_tile_sum_kernel, dim3((unsigned)tiles), dim3(256), 0, s, entries, ws.sorted, idx, ws.cnt,
+                       ws.first, ws.lead_cnt, ws.seglong);
     TTAMM_LAUNCH_CHECK();
-    size_t bytes = ws.temp_bytes;
-    TTAMM_HIP(hipcub::DeviceRadixSort::SortPairs(ws.temp, bytes, ws.keys_in, ws.keys_out, ws.vals_in, ws.vals_out,
-                                                 (int)n, 0, end_bit_for(table_rows), s));
-    hipLaunchKernelGGL(seg_flags_kernel, dim3(grid_for(n, 256, 1 << 30)), dim3(256), 0, s, ws.keys_out, n, ws.flags);
+    hipLaunchKernelGGL(co_tile_scan_kernel, dim3(1), dim3(1024), 0, s, tiles, ws.lead_cnt, ws.seglong, ws.seg_start,
+                       ws.n_unique);
     TTAMM_LAUNCH_CHECK();
-    bytes = ws.temp_bytes;
-    TTAMM_HIP(hipcub::DeviceScan::InclusiveSum(ws.temp, bytes, ws.flags, ws.uid, (int)n, s));
-    hipLaunchKernelGGL(seg_start_kernel, dim3(grid_for(n, 256, 1 << 30)), dim3(256), 0, s, ws.flags, ws.uid, n,
-                       ws.seg_start, ws.n_unique);
+    hipLaunchKernelGGL(co_tile_write_kernel, dim3((unsigned)tiles), dim3(256), 0, s, entries, ws.sorted, idx, ws.cnt,
+                       ws.first, ws.lead_cnt, ws.seglong, ws.lead, ws.seg_start);
+    TTAMM_LAUNCH_CHECK();
+    hipLaunchKernelGGL(co_fill_kernel, dim3(g), dim3(256), 0, s, idx, n, ws.sorted, ws.lead, ws.first, ws.fill,
+                       ws.seg_start, ws.vals_tmp, ws.keys_out, ws.lead_cnt);
+    TTAMM_LAUNCH_CHECK();
+    // segments longer than kOrderSmall: their ids in `lead` (free again), their count in
+    // lead_cnt[0] (zeroed by co_fill)
+    hipLaunchKernelGGL(co_order_small_kernel, dim3(g), dim3(256), 0, s, ws, ws.lead, ws.lead_cnt);
+    TTAMM_LAUNCH_CHECK();
+    hipLaunchKernelGGL(co_order_big_kernel, dim3(256), dim3(256), 0, s, ws, ws.lead, ws.lead_cnt);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_coalesce(const int64_t* idx, int64_t n, int64_t table_rows, CoalesceWs& ws, hipStream_t s) {
+    int rc;
+    if ((rc = launch_coalesce_count(idx, n, table_rows, ws, s))) return rc;
+    return launch_coalesce_group(idx, n, table_rows, ws, s);
+}
+
+namespace {
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void block_exclusive_scan_kernel(const int32_t* __restrict__ in,
+                                                                            int32_t* __restrict__ out, int64_t n) {
+    __shared__ int32_t sc[kScanThreads];
+    const int t = threadIdx.x;
+    const int64_t chunk = (n + kScanThreads - 1) / kScanThreads;
+    const int64_t lo = min(n, t * chunk), hi = min(n, lo + chunk);
+    int32_t sum = 0;
+    for (int64_t i = lo; i < hi; ++i) sum += in[i];
+    sc[t] = sum;
+    __syncthreads();
+    for (int o = 1; o < kScanThreads; o <<= 1) {
+        const int32_t a = t >= o ? sc[t - o] : 0;
+        __syncthreads();
+        sc[t] += a;
+        __syncthreads();
+    }
+    int32_t run = sc[t] - sum;
+    for (int64_t i = lo; i < hi; ++i) {
+        const int32_t v = in[i];
+        out[i] = run;
+        run += v;
+    }
+}
+}  // namespace
+
+int launch_block_exclusive_scan(const int32_t* in, int32_t* out, int64_t n, hipStream_t s) {
+    if (n <= 0) return TTAMM_OK;
+    hipLaunchKernelGGL(block_exclusive_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, in, out, n);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

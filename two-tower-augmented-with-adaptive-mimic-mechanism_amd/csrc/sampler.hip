@@ -31,7 +31,7 @@ __global__ void sample_negatives_kernel(const int64_t* __restrict__ users, int64
                                         uint64_t num_items, const int64_t* __restrict__ pos_offsets,
                                         const int64_t* __restrict__ pos_values, uint32_t k0, uint32_t k1,
                                         uint64_t counter, int64_t slot_base, int64_t* __restrict__ out,
-                                        uint32_t* __restrict__ status) {
+                                        int64_t* __restrict__ out2, uint32_t* __restrict__ status) {
     const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (slot >= batch * num_neg) return;
     const int64_t b = slot / num_neg;
@@ -54,6 +54,7 @@ __global__ void sample_negatives_kernel(const int64_t* __restrict__ users, int64
         ok = (hi == lo) || !is_positive(pos_values, lo, hi, cand);
     }
     out[slot] = cand;
+    if (out2) out2[slot] = cand;
     if (!ok) atomicOr(status, TTAMM_STATUS_SAMPLER_EXHAUSTED);
 }
 
@@ -61,14 +62,14 @@ __global__ void sample_negatives_kernel(const int64_t* __restrict__ users, int64
 
 int launch_sample_negatives(const int64_t* users, int64_t batch, int num_neg, int64_t num_items,
                             const int64_t* pos_offsets, const int64_t* pos_values, uint64_t seed, uint64_t counter,
-                            int64_t slot_base, int64_t* out, uint32_t* status, hipStream_t s) {
+                            int64_t slot_base, int64_t* out, int64_t* out2, uint32_t* status, hipStream_t s) {
     TTAMM_REQUIRE(num_neg > 0, "num_negatives must be greater than zero.");
     TTAMM_REQUIRE(num_items > 1, "num_items must be greater than one.");
     const int64_t slots = batch * num_neg;
     if (slots <= 0) return TTAMM_OK;
     hipLaunchKernelGGL(sample_negatives_kernel, dim3((unsigned)ceil_div(slots, 256)), dim3(256), 0, s, users, batch,
                        num_neg, (uint64_t)num_items, pos_offsets, pos_values, (uint32_t)seed, (uint32_t)(seed >> 32),
-                       counter, slot_base, out, status);
+                       counter, slot_base, out, out2, status);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

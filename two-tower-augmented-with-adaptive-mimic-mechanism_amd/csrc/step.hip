@@ -188,12 +188,38 @@ int wgrad_shapes(const ttamm_tower& T, int64_t R, WgradShape* out) {
     return n;
 }
 
+// Per-row scratch of the row grouping (CoalesceWs cnt / first / fill) comes first in the
+// workspace: its offsets depend only on the table sizes, so it stays in place (and zero between
+// calls, as launch_coalesce leaves it) whatever the batch size.  The caller zeroes the
+// workspace once.
+void plan_scratch(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
+    coalesce_bind_scratch(ws.user.co, ar.take<int32_t>(coalesce_scratch_ints(A.user.id.rows)), A.user.id.rows);
+    coalesce_bind_scratch(ws.item.co, ar.take<int32_t>(coalesce_scratch_ints(A.item.id.rows)), A.item.id.rows);
+    if (cal_enabled(A) && !sharded(A)) {
+        const int64_t ncat = std::min<int64_t>(A.num_categories, 65535);
+        coalesce_bind_scratch(ws.cal.co, ar.take<int32_t>(coalesce_scratch_ints(ncat)), ncat);
+    }
+}
+
+void plan_coalesce(Arena& ar, CoalesceWs& co, int64_t R) {
+    co.keys_out = ar.take<int32_t>(R);
+    co.vals_out = ar.take<int32_t>(R);
+    co.vals_tmp = ar.take<int32_t>(R);
+    co.lead = ar.take<int32_t>(R);
+    // lead_cnt / seglong double as the segment scan's tile totals: ceil(entries / 256) of them
+    co.lead_cnt = ar.take<int32_t>(std::max<int64_t>(R, 257));
+    co.seglong = ar.take<int32_t>(std::max<int64_t>(R, 257));
+    co.seg_start = ar.take<int32_t>(R + 1);
+    co.n_unique = ar.take<int32_t>(1);
+}
+
 int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
     const int64_t B = A.b.batch;
     const int N = A.b.num_neg;
     const int D = A.user.id.dim;
     const bool mimic = A.mimic_enabled != 0;
     const bool shard = sharded(A);
+    plan_scratch(ar, A, ws);
     {
         WgradShape shapes[2 * (TTAMM_MAX_LINEAR + 2)];
         int n = wgrad_shapes(A.user, B, shapes);
@@ -246,16 +272,7 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
                     ar.take<float>(wgrad_slab_floats((int)R, L.out_features, L.in_features, w.wgrad_rps));
             }
         }
-        w.co.keys_in = ar.take<int32_t>(R);
-        w.co.vals_in = ar.take<int32_t>(R);
-        w.co.keys_out = ar.take<int32_t>(R);
-        w.co.vals_out = ar.take<int32_t>(R);
-        w.co.flags = ar.take<int32_t>(R);
-        w.co.uid = ar.take<int32_t>(R);
-        w.co.seg_start = ar.take<int32_t>(R + 1);
-        w.co.n_unique = ar.take<int32_t>(1);
-        w.co.temp_bytes = coalesce_temp_bytes(R);
-        w.co.temp = ar.take<char>(w.co.temp_bytes);
+        plan_coalesce(ar, w.co, R);
         if (needs_wpad(T)) w.wpad = ar.take<float>((size_t)T.linear[0].out_features * round4(T.linear[0].in_features));
         w.piece_e = ar.take<float>((size_t)R * D);
         if (mimic) w.piece_a = ar.take<float>((size_t)R * D);
@@ -292,20 +309,10 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         c.nseg_max = (int)std::min<int64_t>(R, std::max<int64_t>(1, std::min<int64_t>(A.num_categories, 65535)));
         const int pieces = cal_max_pieces(R, c.nseg_max);
         c.catrow = ar.take<int64_t>(R);
-        c.co.keys_in = ar.take<int32_t>(R);
-        c.co.vals_in = ar.take<int32_t>(R);
-        c.co.keys_out = ar.take<int32_t>(R);
-        c.co.vals_out = ar.take<int32_t>(R);
-        c.co.flags = ar.take<int32_t>(R);
-        c.co.uid = ar.take<int32_t>(R);
-        c.co.seg_start = ar.take<int32_t>(R + 1);
-        c.co.n_unique = ar.take<int32_t>(1);
-        c.co.temp_bytes = coalesce_temp_bytes(R);
-        c.co.temp = ar.take<char>(c.co.temp_bytes);
+        plan_coalesce(ar, c.co, R);
+        c.co.sorted = 1;  // categories ascending, as the reference's loop (training.py:567)
         c.pcount = ar.take<int32_t>(c.nseg_max);
         c.pstart = ar.take<int32_t>(c.nseg_max);
-        c.scan_temp_bytes = cal_scan_temp_bytes(c.nseg_max);
-        c.scan_temp = ar.take<char>(c.scan_temp_bytes);
         c.psum = ar.take<float>((size_t)pieces * D);
         c.mean = ar.take<float>((size_t)c.nseg_max * D);
         c.pslab = ar.take<float>((size_t)pieces * D * D);
@@ -753,11 +760,12 @@ ReplaySeg replay_seg(const ttamm_table& tb) {
     return g;
 }
 
-// Before a tower reads its rows: coalesce the batch's rows (also needed by the row updates)
-// and, deferred, bring the dense-group rows it touches current to step - 1.
-int tower_prepare(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred& df, hipStream_t s) {
+// Before a tower reads its rows (part A): count the batch's rows — which marks each row's first
+// position — and, deferred, bring the dense-group rows it touches current to step - 1 (each row
+// once, by its first position).  Part B groups the rows for the row updates at the step's end.
+int tower_prepare_a(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred& df, hipStream_t s) {
     int rc;
-    if ((rc = launch_coalesce(w.idx, w.R, t.id.rows, w.co, s))) return rc;
+    if ((rc = launch_coalesce_count(w.idx, w.R, t.id.rows, w.co, s))) return rc;
     if (!df.on || w.R == 0) return TTAMM_OK;
     ReplayArgs ra;
     std::memset(&ra, 0, sizeof(ra));
@@ -771,68 +779,92 @@ int tower_prepare(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred& 
     for (int i = 0; i < n; ++i) {
         ReplaySeg g = replay_seg(*tabs[i]);
         g.row_lo = 0;
-        g.row_hi = w.R;  // bound of the unique count
-        g.keys = w.co.keys_out;
-        g.seg_start = w.co.seg_start;
-        g.n_unique = w.co.n_unique;
+        g.row_hi = w.R;
+        g.lead_idx = w.idx;
+        g.lead_first = w.co.first;
         ra.seg[ra.count++] = g;
     }
     return launch_replay(ra, s);
 }
 
-// Fork / join events of the aux stream, one pair per host thread and device (reused across
-// steps: a wait binds to the record that precedes it).
-int aux_events(hipEvent_t* fork, hipEvent_t* join) {
-    struct Pair {
+int tower_prepare_b(const ttamm_tower& t, TowerWs& w, hipStream_t s) {
+    return launch_coalesce_group(w.idx, w.R, t.id.rows, w.co, s);
+}
+
+int tower_prepare(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred& df, hipStream_t s) {
+    int rc;
+    if ((rc = tower_prepare_a(t, w, mimic, df, s))) return rc;
+    return tower_prepare_b(t, w, s);
+}
+
+// Fork / join events of the aux stream, one set per host thread and device (reused across
+// steps: a wait binds to the record that precedes it).  [0] fork, [1] rows current (before the
+// fusion), [2] rows grouped (before the table updates).
+int aux_events(hipEvent_t ev[3]) {
+    struct Set {
         int dev;
-        hipEvent_t f, j;
+        hipEvent_t e[3];
     };
-    thread_local std::vector<Pair> cache;
+    thread_local std::vector<Set> cache;
     int dev = 0;
     TTAMM_HIP(hipGetDevice(&dev));
-    for (const Pair& p : cache)
+    for (const Set& p : cache)
         if (p.dev == dev) {
-            *fork = p.f;
-            *join = p.j;
+            for (int i = 0; i < 3; ++i) ev[i] = p.e[i];
             return TTAMM_OK;
         }
-    Pair p{dev, nullptr, nullptr};
-    TTAMM_HIP(hipEventCreateWithFlags(&p.f, hipEventDisableTiming));
-    TTAMM_HIP(hipEventCreateWithFlags(&p.j, hipEventDisableTiming));
+    Set p{dev, {nullptr, nullptr, nullptr}};
+    for (int i = 0; i < 3; ++i) TTAMM_HIP(hipEventCreateWithFlags(&p.e[i], hipEventDisableTiming));
     cache.push_back(p);
-    *fork = p.f;
-    *join = p.j;
+    for (int i = 0; i < 3; ++i) ev[i] = p.e[i];
     return TTAMM_OK;
 }
 
-// tower_prepare of `n` towers, then their forward.  With an aux stream the prepare work (sort
-// + deferred catch-up: index-only inputs) runs there while `s` gathers ID rows and runs the
-// feature MLP; `s` joins before the fusion, whose epilogue reads the mimic rows.  A deferred
-// dense ID table is read by the first gather, so that case stays serial.
-int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_batch& bt, int D, bool mimic,
-                    const Deferred& df, hipStream_t s, hipStream_t aux, void* const* l0_events) {
-    int rc;
+bool overlapped(const ttamm_tower* const* T, int n, const Deferred& df, hipStream_t s, hipStream_t aux) {
     bool overlap = aux != nullptr && aux != s;
     for (int k = 0; k < n; ++k)
         if (df.on && T[k]->id.optimizer == TTAMM_OPT_DENSE) overlap = false;
-    if (!overlap) {
+    return overlap;
+}
+
+// tower_prepare of `n` towers, then their forward.  With an aux stream the index-only prologue
+// runs there while `s` gathers ID rows and runs the feature MLP: part A (count + deferred
+// catch-up) first, joined before the fusion, whose epilogue reads the mimic rows; then part B
+// (grouping), joined by table_updates.  A deferred dense ID table is read by the first gather,
+// so that case stays serial.
+int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_batch& bt, int D, bool mimic,
+                    const Deferred& df, hipStream_t s, hipStream_t aux, void* const* l0_events) {
+    int rc;
+    if (!overlapped(T, n, df, s, aux)) {
         for (int k = 0; k < n; ++k)
             if ((rc = tower_prepare(*T[k], *W[k], mimic, df, s))) return rc;
         return tower_forward(T, W, bt, D, mimic, s, n, l0_events, FWD_ALL);
     }
-    // The MLP launches are enqueued first: the prologue is ~25 small launches (radix sort,
-    // scan, catch-up) whose host-side enqueue alone outlasts their GPU time, so issuing them
-    // first would hold the GEMMs back behind the host.
-    hipEvent_t fork, join;
-    if ((rc = aux_events(&fork, &join))) return rc;
-    TTAMM_HIP(hipEventRecord(fork, s));
+    // The MLP launches are enqueued first: the prologue is a dozen small launches whose
+    // host-side enqueue would otherwise hold the GEMMs back behind the host.
+    hipEvent_t ev[3];
+    if ((rc = aux_events(ev))) return rc;
+    TTAMM_HIP(hipEventRecord(ev[0], s));
     if ((rc = tower_forward(T, W, bt, D, mimic, s, n, l0_events, FWD_MLP))) return rc;
-    TTAMM_HIP(hipStreamWaitEvent(aux, fork, 0));
+    TTAMM_HIP(hipStreamWaitEvent(aux, ev[0], 0));
     for (int k = 0; k < n; ++k)
-        if ((rc = tower_prepare(*T[k], *W[k], mimic, df, aux))) return rc;
-    TTAMM_HIP(hipEventRecord(join, aux));
-    TTAMM_HIP(hipStreamWaitEvent(s, join, 0));
+        if ((rc = tower_prepare_a(*T[k], *W[k], mimic, df, aux))) return rc;
+    TTAMM_HIP(hipEventRecord(ev[1], aux));
+    for (int k = 0; k < n; ++k)
+        if ((rc = tower_prepare_b(*T[k], *W[k], aux))) return rc;
+    TTAMM_HIP(hipEventRecord(ev[2], aux));
+    TTAMM_HIP(hipStreamWaitEvent(s, ev[1], 0));
     return tower_forward(T, W, bt, D, mimic, s, n, l0_events, FWD_FUSION);
+}
+
+// the row updates need the grouping (prepare part B), possibly still running on the aux stream
+int join_grouping(hipStream_t s, hipStream_t aux) {
+    if (aux == nullptr || aux == s) return TTAMM_OK;
+    hipEvent_t ev[3];
+    int rc;
+    if ((rc = aux_events(ev))) return rc;
+    TTAMM_HIP(hipStreamWaitEvent(s, ev[2], 0));
+    return TTAMM_OK;
 }
 
 int tower_optimizer_rows(const ttamm_tower& t, TowerWs& w, int D, bool mimic, const SparseConsts& sp,
@@ -845,6 +877,7 @@ int tower_optimizer_rows(const ttamm_tower& t, TowerWs& w, int D, bool mimic, co
     ru.seg_start = w.co.seg_start;
     ru.keys = w.co.keys_out;
     ru.rows = w.co.vals_out;
+    ru.seglong = w.co.seglong;
     if (t.fusion == TTAMM_FUSION_GATED) {
         ru.dE = w.dEF;
         ru.ld_dE = 2 * D;
@@ -882,8 +915,9 @@ void add_seg(SweepArgs& sw, const ttamm_table& tb) {
 // batch did not touch: eagerly, one sweep over the dense-group tables and a scatter of the
 // staged touched rows; deferred, the replay of this step's 1/slices of the rows to `step`.
 int table_updates(const ttamm_tower* T[2], TowerWs* W[2], int n, int D, bool mimic, const SparseConsts& sp,
-                  const AdamConsts& ad, const Deferred& df, void* const events[2], hipStream_t s) {
+                  const AdamConsts& ad, const Deferred& df, void* const events[2], hipStream_t s, hipStream_t aux) {
     int rc;
+    if ((rc = join_grouping(s, aux))) return rc;
     for (int k = 0; k < n; ++k)
         if ((rc = tower_optimizer_rows(*T[k], *W[k], D, mimic, sp, ad, df, s))) return rc;
     if (df.on) {
@@ -1082,7 +1116,6 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         I.dA = A.item_bwd_in ? A.item_bwd_in + D : nullptr;
         I.dA_ld = 2 * D;
         I.dA_split = I.R;  // every row's mimic gradient is shipped in (dT | dA)
-        TTAMM_REQUIRE(coalesce_temp_bytes(I.R) <= I.co.temp_bytes, "coalesce workspace too small for n_item_rows");
         neg = A.b.neg_items;
     } else {
         I.idx = I.fidx = I.idx_own;
@@ -1126,11 +1159,12 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         TTAMM_REQUIRE(A.status != nullptr, "the training step needs a status word");
         if ((rc = launch_stage_rows(st, s))) return rc;
         if (A.b.sample_negatives && N > 0) {
+            // one process: into the item tower's rows and (when given) the caller's buffer
             if ((rc = launch_sample_negatives(U.idx_own, B, N, num_items, A.b.pos_offsets, A.b.pos_values, A.b.seed,
-                                              A.b.counter, A.row_base * N, neg, A.status, s)))
+                                              A.b.counter, A.row_base * N, neg,
+                                              (!shard && A.b.neg_items != neg) ? A.b.neg_items : nullptr, A.status,
+                                              s)))
                 return rc;
-            if (!shard && A.b.neg_items)
-                TTAMM_HIP(hipMemcpyAsync(A.b.neg_items, neg, B * N * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
         }
         // count the step and publish its AdamW constants, unless a status error stops it
         if ((rc = launch_step_begin(A.status, A.steps_applied, df.on ? df.hist : nullptr, df.cap, df.step, ad, s)))
@@ -1265,11 +1299,11 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         if (!shard) {
             // ---- the whole backward + optimizers in one process --------------------------------
             if ((rc = tower_backward(T, W, D, s, 2))) return rc;
-            if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, s))) return rc;
+            if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, s, aux))) return rc;
             return dense_update(T, W, ad, A.status, s);
         }
         if ((rc = tower_backward(T, W, D, s, 1))) return rc;
-        if ((rc = table_updates(T, W, 1, D, mimic, sp, ad, df, nullptr, s))) return rc;
+        if ((rc = table_updates(T, W, 1, D, mimic, sp, ad, df, nullptr, s, aux))) return rc;
     }
     // ---- item-side backward on the owner ------------------------------------------------------
     if (ph & TTAMM_PHASE_ITEM_BWD) {
@@ -1282,7 +1316,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
             const size_t n = tower_grad_floats(A.item);
             if (n) TTAMM_HIP(hipMemsetAsync(I.gw[0] ? I.gw[0] : I.ggw[0], 0, n * sizeof(float), s));
         }
-        if ((rc = table_updates(Ti, Wi, 1, D, mimic, sp, ad, df, A.timing_events, s))) return rc;
+        if ((rc = table_updates(Ti, Wi, 1, D, mimic, sp, ad, df, A.timing_events, s, aux))) return rc;
     }
     if (ph & TTAMM_PHASE_DENSE)
         if ((rc = dense_update(T, W, ad, A.status, s))) return rc;

@@ -312,7 +312,8 @@ class FusedTrainStep:
         args.aux_stream = self.aux_stream.cuda_stream if self.aux_stream is not None else None
         self._configure(args)
         self.ws_bytes = int(self.lib.ttamm_train_step_workspace_size(ctypes.byref(args)))
-        self.workspace = torch.empty(self.ws_bytes, dtype=torch.uint8, device=self.device)
+        # zeroed once: the row-grouping scratch at its head must start (and stays) zero
+        self.workspace = torch.zeros(self.ws_bytes, dtype=torch.uint8, device=self.device)
         args.workspace = self.workspace.data_ptr()
         args.workspace_bytes = self.ws_bytes
         self.neg_buffer = torch.empty(self.max_batch * self.num_neg, dtype=torch.long, device=self.device)
