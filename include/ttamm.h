@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 12
+#define TTAMM_ABI_VERSION 13
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -141,6 +141,11 @@ typedef struct ttamm_tower {
                               gradients) rounds both operands to bf16 (RNE) and accumulates in
                               fp32; activations, losses, tables, weights and optimizer state stay
                               fp32.  Both towers of a step must agree.                      */
+    /* matmul_bf16 towers, optional: the feature rows already rounded to bf16 (ttamm_to_bf16),
+     * [id.rows, feat_bf16_ld] with feat_bf16_ld % 8 == 0.  The first feature layer's forward
+     * GEMM then streams bf16 operands (same values, half the bytes) on bf16 MFMA. */
+    const uint16_t* features_bf16;
+    int64_t feat_bf16_ld;
 } ttamm_tower;
 
 /* Optimizer hyper-parameters for one step, as the Python floats torch holds (double).
@@ -291,6 +296,11 @@ int ttamm_candidate_topk(const float* queries, int64_t n_queries, int64_t ldq, c
                          int64_t ldi, int32_t dim, const int64_t* cand_offsets, const int64_t* cand_rows,
                          int32_t max_candidates, int32_t cosine, int32_t k, float* out_scores, int64_t* out_positions,
                          void* stream);
+
+/* dst[r, c] = bf16(src[r, c]) rounded to nearest even for c < cols, 0 for cols <= c < ld_dst: the
+ * bf16 feature copy of a matmul_bf16 tower (ttamm_tower.features_bf16). */
+int ttamm_to_bf16(const float* src, int64_t rows, int32_t cols, int64_t ld_src, uint16_t* dst, int64_t ld_dst,
+                  void* stream);
 
 /* faiss.normalize_L2 on device rows, in place (training.py:670-672 on the item matrix and
  * :954-955 on the queries when the model's similarity is cosine): row r of the [n, dim] matrix

@@ -73,6 +73,12 @@ TTAMM_API int ttamm_candidate_topk(const float* queries, int64_t n_queries, int6
                                  max_candidates, cosine, k, out_scores, out_positions, (hipStream_t)stream);
 }
 
+TTAMM_API int ttamm_to_bf16(const float* src, int64_t rows, int32_t cols, int64_t ld_src, uint16_t* dst,
+                            int64_t ld_dst, void* stream) {
+    g_last_error.clear();
+    return launch_to_bf16(src, rows, cols, ld_src, dst, ld_dst, (hipStream_t)stream);
+}
+
 TTAMM_API int ttamm_normalize_rows(float* rows, int64_t n, int32_t dim, int64_t ld, void* stream) {
     g_last_error.clear();
     return launch_normalize_rows(rows, n, dim, ld, (hipStream_t)stream);

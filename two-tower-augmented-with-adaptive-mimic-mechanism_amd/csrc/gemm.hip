@@ -37,6 +37,9 @@
 #ifndef TTAMM_GEMM_ABLATE
 #define TTAMM_GEMM_ABLATE 0
 #endif
+#ifndef TTAMM_B16_ABLATE
+#define TTAMM_B16_ABLATE 0
+#endif
 
 namespace ttamm {
 
@@ -501,6 +504,184 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
     }
 }
 
+// ---- bf16-operand forward GEMM (C5 layer 1) --------------------------------------------------
+// C[M, N] = epilogue(A16[M, K] . B16[N, K]^T) with both operands bf16 in HBM (the feature matrix
+// converted once, the weight once per step; the same RNE-rounded values the fp32-staged
+// variant forms in registers), v_mfma_f32_32x32x16_bf16, fp32 accumulation.
+// 256 x 256 tiles, BK = 64, 512 threads = 8 waves as 2 (M) x 4 (N), each wave 128 x 64
+// (4 x 2 MFMA blocks).  Operands are register-staged into double-buffered LDS images with
+// 144-B rows (64 bf16 + 16 B pad: ds_read_b128 fragment reads hit distinct bank quads), one
+// barrier per k-tile, the next k-tile's loads in flight during the current MFMAs.  Tiles are
+// remapped so the N-tiles of one M-tile run on one XCD (shared A rows in its L2).
+constexpr int kB16M = 256, kB16N = 256, kB16K = 64, kB16Threads = 512;
+constexpr int kB16Ld = kB16K + 8;                               // LDS row stride, bf16 elements
+constexpr int kB16Stage = (kB16M + kB16N) * kB16Ld;             // bf16 per buffer
+constexpr int kB16EpiRows = 64;                                 // epilogue slice
+constexpr int kB16Cld = kB16N + 4;
+constexpr int kB16Lds = 2 * kB16Stage * 2 > kB16EpiRows * kB16Cld * 4 ? 2 * kB16Stage * 2 : kB16EpiRows * kB16Cld * 4;
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int xcd_remap(int b, int n) {  // bijective: consecutive tiles on one XCD
+    const int q = n / 8, r = n % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+template <int E>
+__global__ __launch_bounds__(kB16Threads) void gemm_bf16_kernel(GemmBatch batch) {
+    __shared__ __attribute__((aligned(16))) unsigned char lds_raw[kB16Lds];
+    uint16_t* lds = reinterpret_cast<uint16_t*>(lds_raw);
+    const KArg(GemmBatch)* kb = (const KArg(GemmBatch)*)(__builtin_amdgcn_kernarg_segment_ptr());
+    int tile = xcd_remap(blockIdx.x, kb->total_tiles);
+    int pi = 0;
+#pragma unroll 1
+    for (int q = 1; q < kb->count; ++q)
+        if (tile >= kb->p[q].tile_begin) pi = q;
+    const KArg(GemmProblem)& P = kb->p[pi];
+    tile -= P.tile_begin;
+    const int tm = tile / P.tiles_n, tn = tile - tm * P.tiles_n;
+    const int m0 = tm * kB16M, n0 = tn * kB16N;
+    const int M = P.M, N = P.N, K = P.K;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 2, wn = wave & 3, li = lane & 31, h = lane >> 5;
+
+    // staging: thread -> 4 A chunks and 4 B chunks of 16 B (row = c / 8, k chunk = c % 8)
+    const uint16_t* a_rp[4];
+    const uint16_t* b_rp[4];
+    bool a_ok[4], b_ok[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = tid + i * kB16Threads, row = c >> 3;
+        const int gm = m0 + row, gn = n0 + row;
+        a_ok[i] = gm < M;
+        b_ok[i] = gn < N;
+        const int gmc = min(gm, M - 1), gnc = min(gn, N - 1);
+        a_rp[i] = P.A16 + (P.a_idx ? P.a_idx[gmc] : (int64_t)gmc) * P.lda + (c & 7) * 8;
+        b_rp[i] = P.B16 + (int64_t)gnc * P.ldb + (c & 7) * 8;
+    }
+    u32x4v ra[4], rb[4];
+    const u32x4v zero4 = {0u, 0u, 0u, 0u};
+    // unconditional loads from clamped in-bounds addresses, masked afterwards: a load under a
+    // runtime condition makes hipcc branch around it and wait for it on the spot
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ch = ((tid + i * kB16Threads) & 7) * 8;
+            const int kc = min(k0, K - 8 - ch);  // k0 + ch <= K - 8
+            ra[i] = *reinterpret_cast<const u32x4v*>(a_rp[i] + kc);
+            rb[i] = *reinterpret_cast<const u32x4v*>(b_rp[i] + kc);
+        }
+    };
+    auto mask = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool in_k = k0 + ((tid + i * kB16Threads) & 7) * 8 < K;
+            ra[i] = (a_ok[i] && in_k) ? ra[i] : zero4;
+            rb[i] = (b_ok[i] && in_k) ? rb[i] : zero4;
+        }
+    };
+    auto store = [&](int buf) {
+        uint16_t* as = lds + buf * kB16Stage;
+        uint16_t* bs = as + kB16M * kB16Ld;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int c = tid + i * kB16Threads, row = c >> 3, ch = (c & 7) * 8;
+            *reinterpret_cast<u32x4v*>(as + row * kB16Ld + ch) = ra[i];
+            *reinterpret_cast<u32x4v*>(bs + row * kB16Ld + ch) = rb[i];
+        }
+    };
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int nk = (K + kB16K - 1) / kB16K;
+    load(0);
+    mask(0);
+    store(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+#if TTAMM_B16_ABLATE != 2  // developer ablation 2: no k-loop loads (MFMA + LDS only)
+        if (kt + 1 < nk) load((kt + 1) * kB16K);  // in flight during this k-tile's MFMAs
+#endif
+        const uint16_t* as = lds + buf * kB16Stage;
+        const uint16_t* bs = as + kB16M * kB16Ld;
+#pragma unroll
+        for (int ks = 0; ks < kB16K / 16; ++ks) {
+            bf16x8 af[4], bfr[2];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                af[i] = *reinterpret_cast<const bf16x8*>(as + (wm * 128 + i * 32 + li) * kB16Ld + ks * 16 + 8 * h);
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                bfr[j] = *reinterpret_cast<const bf16x8*>(bs + (wn * 64 + j * 32 + li) * kB16Ld + ks * 16 + 8 * h);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+        // the other buffer was last read in k-tile kt - 1, before that tile's barrier
+        if (kt + 1 < nk) {
+            mask((kt + 1) * kB16K);
+            store(buf ^ 1);
+        }
+        __syncthreads();
+    }
+
+    // ---- epilogue: 64-row slices through LDS (the fp32 kernel's fused tails) ------------------
+    float* Cs = reinterpret_cast<float*>(lds_raw);
+    for (int ph = 0; ph < kB16M / kB16EpiRows; ++ph) {
+        const int row_lo = ph * kB16EpiRows;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int br = wm * 128 + i * 32;
+            if (br < row_lo || br >= row_lo + kB16EpiRows) continue;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int rr = br - row_lo + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    Cs[rr * kB16Cld + wn * 64 + j * 32 + li] = acc[i][j][r];
+                }
+        }
+        __syncthreads();
+        constexpr int C4 = kB16N / 4;              // 64 column groups
+        constexpr int RSTEP = kB16Threads / C4;    // 8 rows per pass
+        const int c4 = tid % C4, r0 = tid / C4;
+        const int col = n0 + c4 * 4;
+        if (col < N) {
+            const bool has_bias = (E == EPI_STORE || E == EPI_HIDDEN || E == EPI_GATE_HIDDEN || E == EPI_GATE_OUT) &&
+                                  P.bias != nullptr;
+            const float4 bias4 = has_bias ? ld4(P.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 2
+            for (int rr = r0; rr < kB16EpiRows; rr += RSTEP) {
+                const int row = m0 + row_lo + rr;
+#if TTAMM_B16_ABLATE == 1  // developer ablation 1: plain store instead of the fused tail
+                if (row < M) st4(P.C + (int64_t)row * P.ldc + col, ld4(Cs + rr * kB16Cld + c4 * 4));
+#else
+                if (row < M) epilogue4<E>(P, ld4(Cs + rr * kB16Cld + c4 * 4), bias4, 0, row, col);
+#endif
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void to_bf16_kernel(const float* __restrict__ src, int64_t rows, int cols, int64_t ld_src,
+                               uint16_t* __restrict__ dst, int64_t ld_dst) {
+    const int64_t total = rows * ld_dst;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / ld_dst;
+        const int c = (int)(i - r * ld_dst);
+        const __bf16 v = (__bf16)(c < cols ? src[r * ld_src + c] : 0.f);  // RNE
+        dst[i] = __builtin_bit_cast(uint16_t, v);
+    }
+}
+
 // grad_w[m_out][n_in] = sum_s slab[s][n_in][m_out] ; grad_b[m_out] = sum_s slab[s][N_in][m_out]
 __global__ void wgrad_reduce_kernel(WgradBatch batch, int64_t total) {
     const KArg(WgradBatch)* kb = (const KArg(WgradBatch)*)(__builtin_amdgcn_kernarg_segment_ptr());
@@ -572,8 +753,47 @@ int dispatch_epi(GemmBatch& b, hipStream_t s) {
 
 }  // namespace
 
+int launch_gemm_bf16(GemmBatch& b, hipStream_t s) {
+    int tiles = 0;
+    for (int i = 0; i < b.count; ++i) {
+        GemmProblem& p = b.p[i];
+        TTAMM_REQUIRE(p.A16 && p.B16 && !p.b_kn && p.M >= 0 && p.N > 0 && p.K > 0 && p.epi == b.p[0].epi,
+                      "gemm bf16: grouped NT problems with bf16 operands required");
+        TTAMM_REQUIRE(p.lda % 8 == 0 && p.ldb % 8 == 0 && p.K % 8 == 0 && ((uintptr_t)p.A16 | (uintptr_t)p.B16) % 16 == 0,
+                      "gemm bf16: 16-byte aligned rows with leading dims and K % 8 == 0");
+        TTAMM_REQUIRE(p.N % 4 == 0 && p.ldc % 4 == 0 && (uintptr_t)p.C % 16 == 0, "gemm: output must be float4-aligned");
+        p.tiles_m = (int)ceil_div(p.M, kB16M);
+        p.tiles_n = (int)ceil_div(p.N, kB16N);
+        p.k_split = p.K;
+        p.slab_stride = 0;
+        p.tile_begin = tiles;
+        tiles += p.tiles_m * p.tiles_n;
+    }
+    b.total_tiles = tiles;
+    if (tiles == 0) return TTAMM_OK;
+    switch (b.p[0].epi) {
+        case EPI_STORE: hipLaunchKernelGGL(gemm_bf16_kernel<EPI_STORE>, dim3(tiles), dim3(kB16Threads), 0, s, b); break;
+        case EPI_HIDDEN: hipLaunchKernelGGL(gemm_bf16_kernel<EPI_HIDDEN>, dim3(tiles), dim3(kB16Threads), 0, s, b); break;
+        default: return fail(TTAMM_E_INVALID, "gemm bf16: epilogue not supported");
+    }
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_to_bf16(const float* src, int64_t rows, int cols, int64_t ld_src, uint16_t* dst, int64_t ld_dst,
+                   hipStream_t s) {
+    TTAMM_REQUIRE(rows >= 0 && cols >= 0 && ld_dst >= cols && ld_src >= cols, "to_bf16: bad shape");
+    if (rows == 0 || ld_dst == 0) return TTAMM_OK;
+    int64_t blocks = ceil_div(rows * ld_dst, 256);
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(to_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, rows, cols, ld_src, dst, ld_dst);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
 int launch_gemm(GemmBatch& b, hipStream_t s) {
     if (b.count == 0) return TTAMM_OK;
+    if (b.p[0].A16) return launch_gemm_bf16(b, s);
     int maxN = 0;
     const int bkn = b.p[0].b_kn;
     for (int i = 0; i < b.count; ++i) {

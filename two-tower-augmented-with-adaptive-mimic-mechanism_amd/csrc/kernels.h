@@ -65,6 +65,11 @@ struct GemmProblem {
     int tile_begin;     // filled by the launcher
     int tiles_m, tiles_n;
     int bf16;           // 1: operands rounded to bf16 (RNE), fp32 accumulation (grouped problems agree)
+    // bf16 operands already in memory (A16 / B16 non-null: the gemm_bf16 kernel, forward "NT"
+    // GEMMs only): A16 rows [M, K] (gathered by a_idx), B16 = W [N, K]; lda / ldb in elements
+    // (multiples of 8), K a multiple of 8.  Same epilogues as the fp32 kernel.
+    const uint16_t* A16;
+    const uint16_t* B16;
 };
 
 constexpr int kMaxGemmProblems = 8;
@@ -75,6 +80,9 @@ struct GemmBatch {
 };
 
 int launch_gemm(GemmBatch& batch, hipStream_t s);
+// fp32 -> bf16 (round to nearest even) rows, zero-filled from `cols` to ld_dst
+int launch_to_bf16(const float* src, int64_t rows, int cols, int64_t ld_src, uint16_t* dst, int64_t ld_dst,
+                   hipStream_t s);
 
 // Weight-gradient GEMM (split-K over rows) + fixed-order reduce.
 //   dW[m, n] = sum_r dY[r, m] * X[r, n] ;  db[m] = sum_r dY[r, m]

@@ -70,6 +70,7 @@ struct TowerWs {
     float* piece_e = nullptr;
     float* piece_a = nullptr;
     float* wpad = nullptr;  // first feature layer weight, in_features padded to a multiple of 4
+    uint16_t* w16 = nullptr;  // bf16 towers with bf16 feature rows: the weight rounded, padded to % 8
     int wgrad_rps = 512;    // split-K rows of the weight gradients (shared by the step's launches)
 };
 
@@ -95,6 +96,11 @@ bool cal_enabled(const ttamm_step_args& A) {
 
 int tower_in_dim(const ttamm_tower& T, int l) { return l == 0 ? T.feat_dim : T.linear[l - 1].out_features; }
 inline int round4(int x) { return (x + 3) / 4 * 4; }
+inline int round8(int x) { return (x + 7) / 8 * 8; }
+// the first feature layer's forward on bf16 operands in memory (ttamm_tower.features_bf16)
+bool uses_w16(const ttamm_tower& T) {
+    return T.matmul_bf16 && T.features_bf16 != nullptr && T.fusion != TTAMM_FUSION_IDENTITY && T.n_linear > 0;
+}
 bool needs_wpad(const ttamm_tower& T) {
     return T.fusion != TTAMM_FUSION_IDENTITY && T.n_linear > 0 && T.linear[0].in_features % 4 != 0;
 }
@@ -115,6 +121,10 @@ int validate_tower(const ttamm_tower& T, const char* name, int D, bool training)
         TTAMM_REQUIRE(T.feat_ld >= T.feat_dim, n + ": feature row stride too small");
         TTAMM_REQUIRE(T.feat_ld % 4 == 0 && (uintptr_t)T.features % 16 == 0,
                       n + ": feature rows must be 16-byte aligned (row stride % 4 == 0)");
+        if (T.features_bf16)
+            TTAMM_REQUIRE(T.matmul_bf16 && T.feat_bf16_ld % 8 == 0 && T.feat_bf16_ld >= round8(T.feat_dim) &&
+                              (uintptr_t)T.features_bf16 % 16 == 0,
+                          n + ": bf16 feature rows need matmul_bf16, 16-byte aligned rows of >= round8(F) elements");
         for (int l = 0; l < T.n_linear; ++l) {
             const ttamm_linear& L = T.linear[l];
             TTAMM_REQUIRE(L.weight && L.bias, n + ": linear parameters missing");
@@ -274,6 +284,7 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         }
         plan_coalesce(ar, w.co, R);
         if (needs_wpad(T)) w.wpad = ar.take<float>((size_t)T.linear[0].out_features * round4(T.linear[0].in_features));
+        if (uses_w16(T)) w.w16 = ar.take<uint16_t>((size_t)T.linear[0].out_features * round8(T.linear[0].in_features));
         w.piece_e = ar.take<float>((size_t)R * D);
         if (mimic) w.piece_a = ar.take<float>((size_t)R * D);
         if (T.id.optimizer == TTAMM_OPT_DENSE) w.side_id = ar.take<float>((size_t)R * 3 * D);
@@ -461,7 +472,15 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
                 }
                 p.B = L.weight;
                 p.ldb = L.in_features;
-                if (l == 0 && w.wpad) {
+                if (l == 0 && w.w16) {  // bf16 operands in memory (C5 layer 1)
+                    const int kp = round8(L.in_features);
+                    if ((rc = launch_to_bf16(L.weight, L.out_features, L.in_features, L.in_features, w.w16, kp, s)))
+                        return rc;
+                    p.A16 = t.features_bf16;
+                    p.lda = t.feat_bf16_ld;
+                    p.B16 = w.w16;
+                    p.ldb = kp;
+                } else if (l == 0 && w.wpad) {
                     if ((rc = launch_pad_rows(L.weight, L.out_features, L.in_features, L.in_features, w.wpad,
                                               round4(L.in_features), s)))
                         return rc;
@@ -475,6 +494,7 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
                 // the feature rows and the padded weight are zero beyond F: run K to the padded
                 // width so every k-tile is whole (fast GEMM path)
                 if (l == 0 && w.wpad && t.feat_ld >= round4(L.in_features)) p.K = round4(L.in_features);
+                if (l == 0 && w.w16) p.K = round8(L.in_features);  // both operands zero beyond F
                 p.bias = L.bias;
                 if (l + 1 < t.n_linear) {
                     p.epi = EPI_HIDDEN;

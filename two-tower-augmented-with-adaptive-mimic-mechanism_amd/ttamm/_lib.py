@@ -73,6 +73,8 @@ class Tower(ctypes.Structure):
         ("linear", Linear * MAX_LINEAR),
         ("gate", Linear * 2),
         ("matmul_bf16", c_i32),
+        ("features_bf16", c_vp),
+        ("feat_bf16_ld", c_i64),
     ]
 
 
@@ -157,7 +159,7 @@ class StepArgs(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 12  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 13  # ttamm.h TTAMM_ABI_VERSION
 
 # ttamm.h TTAMM_PHASE_*
 PHASE_ALL = 0
@@ -182,6 +184,7 @@ SIGNATURES = {
     "ttamm_adam_history_entry_bytes": (ctypes.c_size_t, []),
     "ttamm_retrieval_topk_workspace_size": (ctypes.c_size_t, [c_i64, c_i64, c_i32, c_i32]),
     "ttamm_normalize_rows": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i64, c_vp]),
+    "ttamm_to_bf16": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i64, c_vp, c_i64, c_vp]),
     "ttamm_candidate_topk": (
         ctypes.c_int,
         [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],

@@ -236,6 +236,12 @@ class FusedTrainStep:
                 state=state,
                 id_optimizer=id_opt,
             )
+            if feats is not None and getattr(tower, "matmul_dtype", "fp32") == "bf16":
+                # bf16 towers: the feature rows rounded to bf16 once (RNE, the values every bf16
+                # GEMM of the step rounds them to), so the first layer streams half the bytes
+                f16 = self._bf16_copy(feats)
+                desc.features_bf16 = f16.data_ptr()
+                desc.feat_bf16_ld = f16.stride(0)
             setattr(args, name, desc)
         args.mimic_enabled = 1 if mimic is not None else 0
         args.in_batch = 1 if self.in_batch else 0
@@ -321,6 +327,16 @@ class FusedTrainStep:
         self.steps_done = 0
 
     # ------------------------------------------------------------------------------------
+    def _bf16_copy(self, feats: torch.Tensor) -> torch.Tensor:
+        rows, width = feats.shape
+        ld = (width + 7) // 8 * 8
+        out = torch.empty((rows, ld), dtype=torch.bfloat16, device=feats.device)
+        lib = _lib.load()
+        _lib.check(lib.ttamm_to_bf16(feats.data_ptr(), rows, width, feats.stride(0), out.data_ptr(), ld,
+                                     _lib.stream_handle(feats.device)))
+        self._keep = getattr(self, "_keep", []) + [out]
+        return out
+
     def _configure(self, args: _lib.StepArgs) -> None:
         """Hook: descriptor fields that shape the workspace (set before it is sized)."""
 
