@@ -145,3 +145,20 @@ def test_gate_paths_match_oracle(shape, generic, monkeypatch):
     for name in og:
         err = rel_err(tg[name], og[name])
         assert err <= GRAD_TOL, f"{name}: rel err {err:.3e}"
+
+
+@pytest.mark.parametrize("rows", [1024, 768], ids=["rps1024", "rps768"])
+def test_long_wgrad_splits_match_oracle(rows, monkeypatch):
+    """Weight-gradient split-K chunks longer than 512 rows (the C2 step picks 576): every row
+    of a chunk must reach the gradient, including the gathered feature rows past row 512."""
+    from gpu_helpers import run_ttamm
+
+    monkeypatch.setenv("TTAMM_WGRAD_ROWS_PER_SPLIT", str(rows))
+    shape = Shape(U=400, I=3000, F=40, H=64, D=32, B=400, N=5, hidden_dims=(64,))
+    prob = make_problem(shape, steps=1)
+    om, oo, _ = run_oracle(prob, lr=0.0, betas=(0.0, 0.999))
+    tm, to, _ = run_ttamm(prob, lr=0.0, betas=(0.0, 0.999))
+    og, tg = _grads_by_name(om, oo), _grads_by_name(tm, to)
+    for name in og:
+        err = rel_err(tg[name], og[name])
+        assert err <= GRAD_TOL, f"{name}: rel err {err:.3e}"

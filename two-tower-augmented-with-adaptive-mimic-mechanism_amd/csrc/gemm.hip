@@ -55,6 +55,8 @@ namespace {
 constexpr int BK = 16;
 constexpr int SK = BK + 4;  // MN-major LDS row stride (floats): keeps ds_read_b128 conflict-free
 constexpr int kThreads = 256;
+// rows of one weight-gradient split: their gather indices are staged in LDS (Cfg::KIDX)
+constexpr int kWgradMaxRowsPerSplit = 1024;
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 __device__ __forceinline__ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -114,7 +116,7 @@ struct Cfg {
     static constexpr int EPI_ROWS = WAVES_M >= 2 ? BM / 2 : (I > 1 ? (I + 1) / 2 * MF : BM);
     static constexpr int EPI_PHASES = (BM + EPI_ROWS - 1) / EPI_ROWS;
     static constexpr int EPI = EPI_ROWS * CLD;
-    static constexpr int KIDX = A_KMAJ ? 2 * 512 : 0;              // int64 gather rows (floats)
+    static constexpr int KIDX = A_KMAJ ? 2 * kWgradMaxRowsPerSplit : 0;  // int64 gather rows (floats)
     static constexpr int LDS = (STAGE + KIDX) > EPI ? (STAGE + KIDX) : EPI;
     static_assert(WAVES_M * WAVES_N == 4, "4 waves per block");
     static_assert(MF == 32 || MF == 16, "MFMA block edge");
@@ -831,14 +833,19 @@ int wgrad_slots(bool wide) {
 }
 }  // namespace
 
-// Rows per split-K chunk for a step's weight gradients: a multiple of BK in [512, 2048]
+// Rows per split-K chunk for a step's weight gradients: a multiple of BK in [512, 1024]
 // minimising the launches' makespan, (rounds of resident blocks) x (rows per block), so the
 // tile count lands just under a multiple of the device's block slots instead of spilling a
 // nearly empty extra round.
 int wgrad_rows_per_split(const WgradShape* shapes, int n) {
+    // developer / test override (tests/test_step_parity_gpu.py covers splits past 512 rows)
+    if (const char* e = std::getenv("TTAMM_WGRAD_ROWS_PER_SPLIT")) {
+        const int v = std::atoi(e);
+        if (v >= BK && v <= kWgradMaxRowsPerSplit && v % BK == 0) return v;
+    }
     int best = 512;
     double best_cost = -1.0;
-    for (int rps = 512; rps <= 2048; rps += BK) {
+    for (int rps = 512; rps <= kWgradMaxRowsPerSplit; rps += BK) {
         int64_t tiles[2] = {0, 0};
         for (int i = 0; i < n; ++i) {
             if (shapes[i].R <= 0) continue;
@@ -883,7 +890,8 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s) {
     int64_t total = 0;
     for (int i = 0; i < wb.count; ++i) {
         WgradProblem& w = wb.p[i];
-        TTAMM_REQUIRE(w.rows_per_split > 0 && w.rows_per_split % BK == 0, "wgrad: rows_per_split must be a multiple of 16");
+        TTAMM_REQUIRE(w.rows_per_split > 0 && w.rows_per_split % BK == 0 && w.rows_per_split <= kWgradMaxRowsPerSplit,
+                      "wgrad: rows_per_split must be a multiple of 16 and at most 1024");
         TTAMM_REQUIRE(w.bf16 == wb.p[0].bf16, "wgrad: the batch must share one matmul precision");
         w.splits = w.R > 0 ? (int)ceil_div(w.R, w.rows_per_split) : 1;
         total += (int64_t)w.M * (w.N + 1);
