@@ -506,6 +506,352 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
     }
 }
 
+// ---- split-bf16 MFMA GEMM (fp32 products from three bf16 planes) ------------------------------
+// Same problems, staging and epilogues as gemm_kernel; the matrix core is
+// v_mfma_f32_32x32x16_bf16 (16x the rate of v_mfma_f32_32x32x2_f32).  Each staged fp32 value x
+// is split, once, when its k-tile is written to LDS:
+//     hi = bf16(x),  mid = bf16(x - hi),  lo = bf16(x - hi - mid)      (RNE; all differences exact)
+// hi + mid + lo == x exactly for normal x (8 + 8 + 8 significand bits), so with PL = 3 planes
+//     a.b = ah.bh + ah.bm + am.bh + ah.bl + al.bh + am.bm   (+ terms below 2^-24 relative)
+// six bf16 MFMAs reproduce each fp32 product to within fp32 rounding, accumulated in fp32:
+// 6/16 of the fp32 MFMA's cycles.  PL = 1 keeps only hi: the bf16 towers of config C5 (the
+// operands rounded RNE once, as before).
+// Pipeline: KT = 16 k per tile (one 32x32x16 step), LDS double buffered, two register sets —
+// the k-tile two ahead is loaded while the current one is multiplied and the next one split
+// into the other buffer; one barrier per k-tile; two workgroups per CU.
+// LDS image per plane:
+//   MN-major operand: [mn][16 k] bf16, 32-B rows, the two 16-B halves swapped on rows with
+//                     bit 3 set — a lane's 8 k values are one ds_read_b128, conflict-free over
+//                     the b128 lane groups;
+//   K-major operand:  [16 k][mn] bf16, row stride = 64 or 192 (mod 256) bytes — fragments are
+//                     two ds_read_b64_tr_b16 (hardware transpose: lane i of a 16-lane group gets
+//                     column i of a 4 x 16 block), conflict-free per 32-lane half.
+template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KMAJ_, bool B_KMAJ_>
+struct XCfg {
+    static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_;
+    static constexpr bool A_KMAJ = A_KMAJ_, B_KMAJ = B_KMAJ_;
+    static constexpr int KT = 16;
+    static constexpr int TM = BM / WAVES_M, TN = BN / WAVES_N, I = TM / 32, J = TN / 32;
+    static constexpr int A_F4 = BM * KT / 4, B_F4 = BN * KT / 4;
+    static constexpr int A_LOADS = (A_F4 + kThreads - 1) / kThreads;
+    static constexpr int B_LOADS = (B_F4 + kThreads - 1) / kThreads;
+    static constexpr int kmaj_stride(int mn) {
+        int s = mn * 2;
+        while (s % 256 != 64 && s % 256 != 192) s += 16;
+        return s;
+    }
+    static constexpr int SA = A_KMAJ ? kmaj_stride(BM) : 32;  // row stride, bytes
+    static constexpr int SB = B_KMAJ ? kmaj_stride(BN) : 32;
+    static constexpr int A_PLANE = A_KMAJ ? KT * SA : BM * 32;  // bytes
+    static constexpr int B_PLANE = B_KMAJ ? KT * SB : BN * 32;
+    static constexpr int CLD = BN + 4;
+    static constexpr int EPI_ROWS = WAVES_M >= 2 ? BM / 2 : (I > 1 ? (I + 1) / 2 * 32 : BM);
+    static constexpr int EPI_PHASES = (BM + EPI_ROWS - 1) / EPI_ROWS;
+    static constexpr int KIDX_BYTES = A_KMAJ ? 8 * kWgradMaxRowsPerSplit : 0;
+    static constexpr int buf_bytes(int pl) { return pl * (A_PLANE + B_PLANE); }
+    static constexpr int lds_bytes(int pl) {
+        const int st = 2 * buf_bytes(pl) + KIDX_BYTES, ep = EPI_ROWS * CLD * 4;
+        return st > ep ? st : ep;
+    }
+    static_assert(WAVES_M * WAVES_N == 4, "4 waves per block");
+    static_assert(TM % 32 == 0 && TN % 32 == 0, "wave tile must be a multiple of 32");
+    static_assert(A_F4 % kThreads == 0, "whole A staging rounds");
+    static_assert(WAVES_M == 1 || WAVES_M % EPI_PHASES == 0, "epilogue slices must hold whole wave rows");
+};
+
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4e __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+#ifndef TTAMM_X_ABLATE
+#define TTAMM_X_ABLATE 0
+#endif
+// x -> (hi, mid, lo) bf16 quadruples, 8 bytes each
+template <int PL>
+__device__ __forceinline__ void split_bf16(float4 v, uint2 out[PL]) {
+    const f32x4e x = {v.x, v.y, v.z, v.w};
+    const bf16x4 h = __builtin_convertvector(x, bf16x4);
+    out[0] = __builtin_bit_cast(uint2, h);
+    if constexpr (PL == 3) {
+        const f32x4e r = x - __builtin_convertvector(h, f32x4e);
+        const bf16x4 m = __builtin_convertvector(r, bf16x4);
+        const f32x4e r2 = r - __builtin_convertvector(m, f32x4e);
+        out[1] = __builtin_bit_cast(uint2, m);
+        out[2] = __builtin_bit_cast(uint2, __builtin_convertvector(r2, bf16x4));
+    }
+}
+
+// byte offset of k values [c, c + 4) of row `row` in an MN-major plane (32-B rows, halves
+// swapped on rows with bit 3 set)
+__device__ __forceinline__ int mn_off(int row, int c) { return row * 32 + (((c >> 3) ^ ((row >> 3) & 1)) << 4) + (c & 4) * 2; }
+
+// 32x32x16 operand fragment of MFMA block rows [r0, r0 + 32) (lane l: row r0 + (l & 31),
+// k = 8 (l >> 5) + j)
+template <bool KMAJ, int S>
+__device__ __forceinline__ bf16x8 frag16(const unsigned char* plane, int r0, int lane) {
+    if constexpr (!KMAJ) {
+        return *reinterpret_cast<const bf16x8*>(plane + mn_off(r0 + (lane & 31), 8 * (lane >> 5)));
+    } else {
+        // lane 4q+p of 16-lane group g: block row k = 8(g>>1) + q, columns r0 + 16(g&1) + 4p
+        const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+        const unsigned char* a = plane + (8 * (g >> 1) + q) * S + (r0 + 16 * (g & 1) + 4 * p) * 2;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + 4 * S));
+        const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, v);
+    }
+}
+
+template <class CX, int E, int PL>
+__global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
+    constexpr int BM = CX::BM, BN = CX::BN, TM = CX::TM, TN = CX::TN, I = CX::I, J = CX::J, KT = CX::KT;
+    constexpr bool AK = CX::A_KMAJ, BKM = CX::B_KMAJ;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[CX::lds_bytes(PL)];
+
+    const KArg(GemmBatch)* kb = (const KArg(GemmBatch)*)(__builtin_amdgcn_kernarg_segment_ptr());
+    int tile = blockIdx.x;
+    int pi = 0;
+#pragma unroll 1
+    for (int q = 1; q < kb->count; ++q)
+        if (tile >= kb->p[q].tile_begin) pi = q;
+    const KArg(GemmProblem)& P = kb->p[pi];
+    tile -= P.tile_begin;
+    const int tiles_mn = P.tiles_m * P.tiles_n;
+    const int split = tile / tiles_mn;
+    tile -= split * tiles_mn;
+    const int tm = tile / P.tiles_n, tn = tile - tm * P.tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int M = P.M, N = P.N;
+    const int k_begin = split * P.k_split;
+    const int k_end = min(P.K, k_begin + P.k_split);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / CX::WAVES_N, wn = wave % CX::WAVES_N;
+    const int li = lane & 31, h = lane >> 5;
+
+    // staging maps: MN-major thread -> (row lin / 4, k 4 * (lin % 4)); K-major -> (k row, 4 mn)
+    const float* a_rp[CX::A_LOADS];
+    bool a_ok[CX::A_LOADS];
+    int a_r[CX::A_LOADS], a_c[CX::A_LOADS];
+#pragma unroll
+    for (int it = 0; it < CX::A_LOADS; ++it) {
+        const int lin = tid + it * kThreads;
+        if (!AK) {
+            a_r[it] = lin >> 2;
+            a_c[it] = (lin & 3) * 4;
+            const int gm = m0 + a_r[it];
+            a_ok[it] = gm < M;
+            const int gmc = min(gm, M - 1);
+            a_rp[it] = P.A + (P.a_idx ? P.a_idx[gmc] : (int64_t)gmc) * P.lda;
+        } else {
+            a_r[it] = lin / (BM / 4);
+            a_c[it] = (lin % (BM / 4)) * 4;
+            a_ok[it] = true;
+            a_rp[it] = P.A;
+        }
+    }
+    int64_t* kidx = reinterpret_cast<int64_t*>(lds + 2 * CX::buf_bytes(PL));
+    if (AK) {
+        for (int k = tid; k < k_end - k_begin; k += kThreads)
+            kidx[k] = P.a_idx ? P.a_idx[k_begin + k] : (int64_t)(k_begin + k);
+        __syncthreads();
+    }
+    const float* b_rp[CX::B_LOADS];
+#pragma unroll
+    for (int it = 0; it < CX::B_LOADS; ++it) {
+        const int lin = tid + it * kThreads;
+        if (!BKM) b_rp[it] = P.B + (int64_t)min(n0 + (lin >> 2), N - 1) * P.ldb + (lin & 3) * 4;
+        else b_rp[it] = P.B + (int64_t)(lin / (BN / 4)) * P.ldb + n0 + (lin % (BN / 4)) * 4;
+    }
+    const bool fast = ((k_end - k_begin) % KT == 0) && (n0 + BN <= N) &&
+                      (AK ? (m0 + BM <= P.a_cols) : (m0 + BM <= M));
+
+    f32x16 acc[I][J];
+#pragma unroll
+    for (int i = 0; i < I; ++i)
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    float4 ra[2][CX::A_LOADS], rb[2][CX::B_LOADS];
+
+    auto mainloop = [&](auto fast_tag) {
+        constexpr bool FAST = decltype(fast_tag)::value;
+        auto load_tile = [&](auto S, int k0) {
+            constexpr int R = decltype(S)::value;
+#pragma unroll
+            for (int it = 0; it < CX::A_LOADS; ++it) {
+                if (!AK) {
+                    ra[R][it] = FAST ? *reinterpret_cast<const float4*>(a_rp[it] + k0 + a_c[it])
+                                     : raw4(a_rp[it], k0 + a_c[it], P.lda);
+                } else {
+                    const int k = FAST ? k0 + a_r[it] : min(k0 + a_r[it], k_end - 1);
+                    const float* rp = P.A + kidx[k - k_begin] * P.lda;
+                    ra[R][it] = FAST ? *reinterpret_cast<const float4*>(rp + m0 + a_c[it]) : raw4(rp, m0 + a_c[it], P.lda);
+                }
+            }
+#pragma unroll
+            for (int it = 0; it < CX::B_LOADS; ++it) {
+                const int lin = tid + it * kThreads;
+                if (CX::B_F4 % kThreads && lin >= CX::B_F4) continue;  // partial last round (BN = 96)
+                if (!BKM) {
+                    rb[R][it] = FAST ? *reinterpret_cast<const float4*>(b_rp[it] + k0)
+                                     : raw4(b_rp[it] - (lin & 3) * 4, k0 + (lin & 3) * 4, P.ldb);
+                } else if (FAST) {
+                    rb[R][it] = *reinterpret_cast<const float4*>(b_rp[it] + (int64_t)k0 * P.ldb);
+                } else {
+                    const int k = min(k0 + lin / (BN / 4), k_end - 1);
+                    rb[R][it] = raw4(P.B + (int64_t)k * P.ldb, n0 + (lin % (BN / 4)) * 4, P.ldb);
+                }
+            }
+        };
+        // staged item q (A loads first, then B loads) of register set S -> its planes in buffer Buf
+        auto store_item = [&](auto S, auto Buf, int q, int k0) {
+            constexpr int R = decltype(S)::value;
+            unsigned char* Ap = lds + decltype(Buf)::value * CX::buf_bytes(PL);
+            unsigned char* Bp = Ap + PL * CX::A_PLANE;
+            float4 v;
+            int off;
+            unsigned char* base;
+            int plane;
+            if (q < CX::A_LOADS) {
+                const int it = q;
+                if (!AK) {
+                    v = FAST ? ra[R][it] : mask4(ra[R][it], k0 + a_c[it], k_end, P.lda, -1, a_ok[it]);
+                    off = mn_off(a_r[it], a_c[it]);
+                } else {
+                    v = FAST ? ra[R][it]
+                             : mask4(ra[R][it], m0 + a_c[it], P.a_cols, P.lda, P.a_ones_col, k0 + a_r[it] < k_end);
+                    off = a_r[it] * CX::SA + a_c[it] * 2;
+                }
+                base = Ap;
+                plane = CX::A_PLANE;
+            } else {
+                const int it = q - CX::A_LOADS;
+                const int lin = tid + it * kThreads;
+                if (CX::B_F4 % kThreads && lin >= CX::B_F4) return;  // partial last round (BN = 96)
+                if (!BKM) {
+                    const int n = n0 + (lin >> 2), c = k0 + (lin & 3) * 4;
+                    v = FAST ? rb[R][it] : mask4(rb[R][it], c, k_end, P.ldb, -1, n < N);
+                    off = mn_off(lin >> 2, (lin & 3) * 4);
+                } else {
+                    const int kr = lin / (BN / 4), nc = (lin % (BN / 4)) * 4;
+                    v = FAST ? rb[R][it] : mask4(rb[R][it], n0 + nc, N, P.ldb, -1, k0 + kr < k_end);
+                    off = kr * CX::SB + nc * 2;
+                }
+                base = Bp;
+                plane = CX::B_PLANE;
+            }
+            uint2 w[PL];
+            split_bf16<PL>(v, w);
+#pragma unroll
+            for (int pl = 0; pl < PL; ++pl) *reinterpret_cast<uint2*>(base + pl * plane + off) = w[pl];
+        };
+        constexpr int NITEMS = CX::A_LOADS + CX::B_LOADS;
+        auto store_tile = [&](auto S, auto Buf, int k0) {
+#pragma unroll
+            for (int q = 0; q < NITEMS; ++q) store_item(S, Buf, q, k0);
+        };
+        // multiply the k-tile in buffer Buf; the split + LDS writes of the next k-tile (register
+        // set S -> buffer NB) are spread between the MFMA groups so the vector work issues in the
+        // matrix pipe's shadow
+        auto compute = [&](auto Buf, auto S, auto NB, int k0n) {
+            const unsigned char* Ap = lds + decltype(Buf)::value * CX::buf_bytes(PL);
+            const unsigned char* Bp = Ap + PL * CX::A_PLANE;
+            bf16x8 af[PL][I], bf[PL][J];
+#pragma unroll
+            for (int pl = 0; pl < PL; ++pl) {
+#pragma unroll
+                for (int i = 0; i < I; ++i) af[pl][i] = frag16<AK, CX::SA>(Ap + pl * CX::A_PLANE, wm * TM + i * 32, lane);
+#pragma unroll
+                for (int j = 0; j < J; ++j) bf[pl][j] = frag16<BKM, CX::SB>(Bp + pl * CX::B_PLANE, wn * TN + j * 32, lane);
+            }
+            constexpr int NP = I * J;
+#pragma unroll
+            for (int pq = 0; pq < NP; ++pq) {
+                const int i = pq / J, j = pq % J;
+                if constexpr (PL == 3 && TTAMM_X_ABLATE != 2) {  // small terms first (ablation 2: hh only)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][i], bf[1][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2][i], bf[0][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][i], bf[2][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][i], bf[0][j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][i], bf[1][j], acc[i][j], 0, 0, 0);
+                }
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][i], bf[0][j], acc[i][j], 0, 0, 0);
+#if TTAMM_X_ABLATE != 3
+#pragma unroll
+                for (int q = (pq * NITEMS) / NP; q < ((pq + 1) * NITEMS) / NP; ++q) store_item(S, NB, q, k0n);
+#endif
+            }
+        };
+        using S0 = std::integral_constant<int, 0>;
+        using S1 = std::integral_constant<int, 1>;
+        const int nk = k_end > k_begin ? (k_end - k_begin + KT - 1) / KT : 0;
+        if (nk == 0) return;
+        // tile index clamped to the last one: the loop body has no branches (the surplus loads and
+        // writes at the end go to the free buffer and are never read)
+        auto kof = [&](int kt) { return k_begin + min(kt, nk - 1) * KT; };
+        load_tile(S0{}, kof(0));
+        store_tile(S0{}, S0{}, kof(0));
+        load_tile(S1{}, kof(1));
+        __syncthreads();
+        // k-tile kt: register set kt & 1, LDS buffer kt & 1.  Prefetch kt + 2 into the set tile kt
+        // left (already in LDS), multiply kt while splitting kt + 1 into the other buffer (last
+        // read in k-tile kt - 1, before that tile's barrier).
+        auto step = [&](auto Bf, auto NB, int kt) {
+#if TTAMM_X_ABLATE != 3  // developer ablation 3: no k-loop traffic (MFMA + LDS reads only)
+            load_tile(Bf, kof(kt + 2));
+#endif
+            compute(Bf, NB, NB, kof(kt + 1));
+            __syncthreads();
+        };
+        int kt = 0;
+        for (; kt + 1 < nk; kt += 2) {
+            step(S0{}, S1{}, kt);
+            step(S1{}, S0{}, kt + 1);
+        }
+        if (kt < nk) step(S0{}, S1{}, kt);
+    };
+    if (fast) mainloop(std::true_type{});
+    else mainloop(std::false_type{});
+
+    // ---- epilogue through LDS, in row slices (as gemm_kernel) ---------------------------------
+    float* Cs = reinterpret_cast<float*>(lds);
+    for (int ph = 0; ph < CX::EPI_PHASES; ++ph) {
+        const int row_lo = ph * CX::EPI_ROWS;
+        const int rows_here = min(CX::EPI_ROWS, BM - row_lo);
+#pragma unroll
+        for (int i = 0; i < I; ++i) {
+            const int br = wm * TM + i * 32;
+            if (br < row_lo || br >= row_lo + CX::EPI_ROWS) continue;
+#pragma unroll
+            for (int j = 0; j < J; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int rr = br - row_lo + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    Cs[rr * CX::CLD + wn * TN + j * 32 + li] = acc[i][j][r];
+                }
+        }
+        __syncthreads();
+        constexpr int C4 = BN / 4;
+        constexpr int RSTEP = kThreads / C4;
+        const int c4 = tid % C4, r0 = tid / C4;
+        const int col = n0 + c4 * 4;
+        if (r0 < RSTEP && col < N) {
+            const bool has_bias = (E == EPI_STORE || E == EPI_HIDDEN || E == EPI_GATE_HIDDEN || E == EPI_GATE_OUT) &&
+                                  P.bias != nullptr;
+            const float4 bias4 = has_bias ? ld4(P.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 4
+            for (int rr = r0; rr < rows_here; rr += RSTEP) {
+                const int row = m0 + row_lo + rr;
+                if (row < M) epilogue4<E>(P, ld4(Cs + rr * CX::CLD + c4 * 4), bias4, split, row, col);
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // ---- bf16-operand forward GEMM (C5 layer 1) --------------------------------------------------
 // C[M, N] = epilogue(A16[M, K] . B16[N, K]^T) with both operands bf16 in HBM (the feature matrix
 // converted once, the weight once per step; the same RNE-rounded values the fp32-staged
@@ -734,6 +1080,49 @@ int launch_one(GemmBatch& b, hipStream_t s) {
     return TTAMM_OK;
 }
 
+template <class CX, int E, int PL>
+int launch_one_x(GemmBatch& b, hipStream_t s) {
+    int tiles = 0;
+    for (int i = 0; i < b.count; ++i) {
+        GemmProblem& p = b.p[i];
+        p.tiles_m = (int)ceil_div(p.M, CX::BM);
+        p.tiles_n = (int)ceil_div(p.N, CX::BN);
+        if (p.k_split <= 0) p.k_split = p.K;
+        p.tile_begin = tiles;
+        tiles += p.tiles_m * p.tiles_n * (int)ceil_div(p.K, p.k_split);
+    }
+    b.total_tiles = tiles;
+    if (tiles == 0) return TTAMM_OK;
+    hipLaunchKernelGGL((gemm_x_kernel<CX, E, PL>), dim3(tiles), dim3(kThreads), 0, s, b);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+template <class CX, int PL>
+int dispatch_epi_x(GemmBatch& b, hipStream_t s) {
+    switch (b.p[0].epi) {
+        case EPI_STORE: return launch_one_x<CX, EPI_STORE, PL>(b, s);
+        case EPI_HIDDEN: return launch_one_x<CX, EPI_HIDDEN, PL>(b, s);
+        case EPI_GATE_HIDDEN: return launch_one_x<CX, EPI_GATE_HIDDEN, PL>(b, s);
+        case EPI_GATE_OUT: return launch_one_x<CX, EPI_GATE_OUT, PL>(b, s);
+        case EPI_DGRAD_RELU: return launch_one_x<CX, EPI_DGRAD_RELU, PL>(b, s);
+        case EPI_DGRAD_GATE_EF: return launch_one_x<CX, EPI_DGRAD_GATE_EF, PL>(b, s);
+        case EPI_DGRAD_HIDDEN: return launch_one_x<CX, EPI_DGRAD_HIDDEN, PL>(b, s);
+        default: return fail(TTAMM_E_INVALID, "gemm: unknown epilogue");
+    }
+}
+template <class CX>
+int dispatch_x(GemmBatch& b, hipStream_t s) {
+    return b.p[0].bf16 ? dispatch_epi_x<CX, 1>(b, s) : dispatch_epi_x<CX, 3>(b, s);
+}
+
+// Matrix-core path of the fp32 / bf16 GEMMs: the split-bf16 kernel (default), or with
+// TTAMM_FP32_MFMA=exact the v_mfma_f32_32x32x2_f32 kernel (exact fp32 products; bf16 towers
+// round in registers) — a developer switch, read per launch so tests can compare the two.
+bool exact_mfma() {
+    const char* e = std::getenv("TTAMM_FP32_MFMA");
+    return e && std::strcmp(e, "exact") == 0;
+}
+
 template <class CF, bool BF>
 int dispatch_epi_t(GemmBatch& b, hipStream_t s) {
     switch (b.p[0].epi) {
@@ -810,6 +1199,14 @@ int launch_gemm(GemmBatch& b, hipStream_t s) {
         p.slab_stride = 0;
         maxN = p.N > maxN ? p.N : maxN;
     }
+    if (!exact_mfma()) {
+        if (maxN > 96) {
+            if (bkn) return dispatch_x<XCfg<128, 192, 2, 2, false, true>>(b, s);
+            return dispatch_x<XCfg<128, 192, 2, 2, false, false>>(b, s);
+        }
+        if (bkn) return dispatch_x<XCfg<128, 96, 4, 1, false, true>>(b, s);
+        return dispatch_x<XCfg<128, 96, 4, 1, false, false>>(b, s);
+    }
     if (maxN > 96) {
         if (bkn) return dispatch_epi<Cfg<128, 192, 2, 2, false, true>>(b, s);
         return dispatch_epi<Cfg<128, 192, 2, 2, false, false>>(b, s);
@@ -820,49 +1217,65 @@ int launch_gemm(GemmBatch& b, hipStream_t s) {
 
 namespace {
 // Resident blocks of a wgrad launch config on this device (CUs x occupancy), cached.
-int wgrad_slots(bool wide) {
-    static int cached[2] = {0, 0};
-    if (cached[wide]) return cached[wide];
+using WgradWide = Cfg<128, 192, 2, 2, true, true>;
+using WgradNarrow = Cfg<128, 96, 4, 1, true, true>;
+using WgradWideX = XCfg<128, 192, 2, 2, true, true>;
+using WgradNarrowX = XCfg<128, 96, 4, 1, true, true>;
+int wgrad_slots(bool wide, bool exact) {
+    static int cached[2][2] = {{0, 0}, {0, 0}};
+    if (cached[exact][wide]) return cached[exact][wide];
     int dev = 0, cus = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* k = wide ? (const void*)gemm_kernel<Cfg<128, 192, 2, 2, true, true>, EPI_STORE, false>
-                         : (const void*)gemm_kernel<Cfg<128, 96, 4, 1, true, true>, EPI_STORE, false>;
+    const void* k = exact ? (wide ? (const void*)gemm_kernel<WgradWide, EPI_STORE, false>
+                                  : (const void*)gemm_kernel<WgradNarrow, EPI_STORE, false>)
+                          : (wide ? (const void*)gemm_x_kernel<WgradWideX, EPI_STORE, 3>
+                                  : (const void*)gemm_x_kernel<WgradNarrowX, EPI_STORE, 3>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-    cached[wide] = cus * per_cu;
-    return cached[wide];
+    cached[exact][wide] = cus * per_cu;
+    return cached[exact][wide];
 }
 }  // namespace
 
-// Rows per split-K chunk for a step's weight gradients: a multiple of BK in [512, 1024]
-// minimising the launches' makespan, (rounds of resident blocks) x (rows per block), so the
-// tile count lands just under a multiple of the device's block slots instead of spilling a
-// nearly empty extra round.
-int wgrad_rows_per_split(const WgradShape* shapes, int n) {
+// Rows per split-K chunk of a step's weight gradients, chosen per tile class (the wide and the
+// narrow launch run one after the other): a multiple of 32 in [128, 1024] minimising the
+// launch's makespan, (rounds of resident blocks) x (rows per block) x (measured time per row of
+// a block), plus the fixed-order reduce over the slabs (splits x M x (N + 1) floats written and
+// read at HBM speed).  Narrow gradients (M <= 96) are latency-bound per k-tile, so they want
+// many short splits; wide ones fill the chip with few.
+void wgrad_rows_per_split(const WgradShape* shapes, int n, int rps[2]) {
     // developer / test override (tests/test_step_parity_gpu.py covers splits past 512 rows)
     if (const char* e = std::getenv("TTAMM_WGRAD_ROWS_PER_SPLIT")) {
         const int v = std::atoi(e);
-        if (v >= BK && v <= kWgradMaxRowsPerSplit && v % BK == 0) return v;
-    }
-    int best = 512;
-    double best_cost = -1.0;
-    for (int rps = 512; rps <= kWgradMaxRowsPerSplit; rps += BK) {
-        int64_t tiles[2] = {0, 0};
-        for (int i = 0; i < n; ++i) {
-            if (shapes[i].R <= 0) continue;
-            const bool wide = shapes[i].M > 96;
-            const int tm = (int)ceil_div(shapes[i].N + 1, 128);
-            const int tn = (int)ceil_div(shapes[i].M, wide ? 192 : 96);
-            tiles[wide] += (int64_t)tm * tn * ceil_div(shapes[i].R, rps);
-        }
-        double cost = 0.0;
-        for (int w = 0; w < 2; ++w)
-            if (tiles[w]) cost += (double)ceil_div(tiles[w], wgrad_slots(w == 1)) * rps;
-        if (best_cost < 0.0 || cost < best_cost) {
-            best_cost = cost;
-            best = rps;
+        if (v >= BK && v <= kWgradMaxRowsPerSplit && v % BK == 0) {
+            rps[0] = rps[1] = v;
+            return;
         }
     }
-    return best;
+    const bool exact = exact_mfma();
+    const double us_per_row[2] = {0.11, 0.14};  // block time per split row (MI355X, C2 shapes)
+    const double hbm_us_per_byte = 1.0 / 5.0e6;  // ~5 TB/s
+    for (int c = 0; c < 2; ++c) {
+        int best = 512;
+        double best_cost = -1.0;
+        for (int r = 128; r <= kWgradMaxRowsPerSplit; r += 32) {
+            int64_t tiles = 0;
+            double slab_bytes = 0.0;
+            for (int i = 0; i < n; ++i) {
+                if (shapes[i].R <= 0 || wgrad_class(shapes[i].M) != c) continue;
+                const int64_t splits = ceil_div(shapes[i].R, r);
+                tiles += ceil_div(shapes[i].N + 1, 128) * ceil_div(shapes[i].M, c ? 192 : 96) * splits;
+                slab_bytes += 2.0 * 4.0 * (double)splits * shapes[i].M * (shapes[i].N + 1);
+            }
+            if (tiles == 0) break;
+            const double cost = (double)ceil_div(tiles, wgrad_slots(c == 1, exact)) * r * us_per_row[c] +
+                                slab_bytes * hbm_us_per_byte;
+            if (best_cost < 0.0 || cost < best_cost) {
+                best_cost = cost;
+                best = r;
+            }
+        }
+        rps[c] = best;
+    }
 }
 
 size_t wgrad_slab_floats(int R, int M, int N, int rps) {
@@ -877,13 +1290,18 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s) {
     std::memset(&wide, 0, sizeof(wide));
     std::memset(&narrow, 0, sizeof(narrow));
     const bool bf = wb.count > 0 && wb.p[0].bf16;
+    const bool exact = exact_mfma();
     auto flush = [&](GemmBatch& g, bool is_wide) -> int {
         if (g.count == 0) return TTAMM_OK;
-        using Wide = Cfg<128, 192, 2, 2, true, true>;
-        using Narrow = Cfg<128, 96, 4, 1, true, true>;
-        const int rc = is_wide ? (bf ? launch_one<Wide, EPI_STORE, true>(g, s) : launch_one<Wide, EPI_STORE, false>(g, s))
-                               : (bf ? launch_one<Narrow, EPI_STORE, true>(g, s)
-                                     : launch_one<Narrow, EPI_STORE, false>(g, s));
+        int rc;
+        if (!exact)
+            rc = is_wide ? (bf ? launch_one_x<WgradWideX, EPI_STORE, 1>(g, s) : launch_one_x<WgradWideX, EPI_STORE, 3>(g, s))
+                         : (bf ? launch_one_x<WgradNarrowX, EPI_STORE, 1>(g, s)
+                               : launch_one_x<WgradNarrowX, EPI_STORE, 3>(g, s));
+        else
+            rc = is_wide ? (bf ? launch_one<WgradWide, EPI_STORE, true>(g, s) : launch_one<WgradWide, EPI_STORE, false>(g, s))
+                         : (bf ? launch_one<WgradNarrow, EPI_STORE, true>(g, s)
+                               : launch_one<WgradNarrow, EPI_STORE, false>(g, s));
         std::memset(&g, 0, sizeof(g));
         return rc;
     };
@@ -923,7 +1341,7 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s) {
         p.keep_prob = 1.f;
         p.inv_keep = 1.f;
         p.bf16 = w.bf16;
-        const bool is_wide = w.M > 96;
+        const bool is_wide = wgrad_class(w.M) == 1;
         GemmBatch& g = is_wide ? wide : narrow;
         if (g.count == kMaxGemmProblems) {
             const int rc = flush(g, is_wide);

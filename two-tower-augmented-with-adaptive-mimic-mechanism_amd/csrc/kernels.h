@@ -112,7 +112,10 @@ struct WgradShape {
     int64_t R;  // rows
     int M, N;   // out features, in features
 };
-int wgrad_rows_per_split(const WgradShape* shapes, int n);
+// tile class of a weight gradient: m_out > 96 runs on the wide tile configuration
+inline int wgrad_class(int m_out) { return m_out > 96 ? 1 : 0; }
+// rows per split-K chunk for each class ([0] narrow, [1] wide) of a step's weight gradients
+void wgrad_rows_per_split(const WgradShape* shapes, int n, int rps[2]);
 size_t wgrad_slab_floats(int R, int M, int N, int rows_per_split);
 int launch_wgrad(WgradBatch& batch, hipStream_t s);
 

@@ -71,7 +71,7 @@ struct TowerWs {
     float* piece_a = nullptr;
     float* wpad = nullptr;  // first feature layer weight, in_features padded to a multiple of 4
     uint16_t* w16 = nullptr;  // bf16 towers with bf16 feature rows: the weight rounded, padded to % 8
-    int wgrad_rps = 512;    // split-K rows of the weight gradients (shared by the step's launches)
+    int wgrad_rps[2] = {512, 512};  // split-K rows of the weight gradients, per tile class (wgrad_class)
 };
 
 struct StepWs {
@@ -234,7 +234,9 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         WgradShape shapes[2 * (TTAMM_MAX_LINEAR + 2)];
         int n = wgrad_shapes(A.user, B, shapes);
         n += wgrad_shapes(A.item, shard ? A.item_rows_capacity : B * (1 + N), shapes + n);
-        ws.user.wgrad_rps = ws.item.wgrad_rps = wgrad_rows_per_split(shapes, n);
+        int rps[2];
+        wgrad_rows_per_split(shapes, n, rps);
+        for (int c = 0; c < 2; ++c) ws.user.wgrad_rps[c] = ws.item.wgrad_rps[c] = rps[c];
     }
     // ext_io: the item tower's t / a / dT / dA live in the caller's exchange buffers
     auto tower = [&](const ttamm_tower& T, TowerWs& w, int64_t R, bool ext_io, int64_t dA_rows) {
@@ -272,14 +274,16 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         if (T.fusion != TTAMM_FUSION_IDENTITY) {
             for (int l = 0; l < T.n_linear; ++l) {
                 const ttamm_linear& L = T.linear[l];
-                w.slab[l] = ar.take<float>(wgrad_slab_floats((int)R, L.out_features, L.in_features, w.wgrad_rps));
+                w.slab[l] = ar.take<float>(
+                    wgrad_slab_floats((int)R, L.out_features, L.in_features, w.wgrad_rps[wgrad_class(L.out_features)]));
             }
         }
         if (T.fusion == TTAMM_FUSION_GATED) {
             for (int q = 0; q < 2; ++q) {
                 const ttamm_linear& L = T.gate[q];
                 w.slab[TTAMM_MAX_LINEAR + q] =
-                    ar.take<float>(wgrad_slab_floats((int)R, L.out_features, L.in_features, w.wgrad_rps));
+                    ar.take<float>(wgrad_slab_floats((int)R, L.out_features, L.in_features,
+                                                     w.wgrad_rps[wgrad_class(L.out_features)]));
             }
         }
         plan_coalesce(ar, w.co, R);
@@ -700,7 +704,7 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
             g2.grad_w = w.ggw[1];
             g2.grad_b = w.ggb[1];
             g2.slab = w.slab[TTAMM_MAX_LINEAR + 1];
-            g2.rows_per_split = w.wgrad_rps;
+            g2.rows_per_split = w.wgrad_rps[wgrad_class(g2.M)];
             wb.p[wb.count++] = g2;
             WgradProblem g1{};
             g1.bf16 = t.matmul_bf16;
@@ -714,7 +718,7 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
             g1.grad_w = w.ggw[0];
             g1.grad_b = w.ggb[0];
             g1.slab = w.slab[TTAMM_MAX_LINEAR];
-            g1.rows_per_split = w.wgrad_rps;
+            g1.rows_per_split = w.wgrad_rps[wgrad_class(g1.M)];
             wb.p[wb.count++] = g1;
         }
         for (int l = t.n_linear - 1; l >= 0; --l) {
@@ -742,7 +746,7 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
             p.grad_w = w.gw[l];
             p.grad_b = w.gb[l];
             p.slab = w.slab[l];
-            p.rows_per_split = w.wgrad_rps;
+            p.rows_per_split = w.wgrad_rps[wgrad_class(p.M)];
             wb.p[wb.count++] = p;
         }
     }

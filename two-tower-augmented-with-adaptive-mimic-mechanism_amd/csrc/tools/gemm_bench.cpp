@@ -1,8 +1,13 @@
 // Developer micro-benchmark of the step's GEMM shapes (C2: R = 57344 tower rows).
 // Build: make -C csrc tools ; run on the GPU box: ./build/gemm_bench
+// Each case runs on the split-bf16 kernel and on the exact fp32 MFMA kernel
+// (TTAMM_FP32_MFMA=exact) and prints both times and their max output difference relative to
+// the output's max magnitude.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 #include <vector>
@@ -63,21 +68,39 @@ int main() {
         p.a_ones_col = -1;
         return p;
     };
-    auto time_it = [&](const char* name, double flop, auto fn) -> int {
+    auto time_one = [&](auto fn) -> double {
         for (int i = 0; i < 3; ++i) fn();
-        CK(hipEventRecord(e0, 0));
+        if (hipEventRecord(e0, 0) != hipSuccess) return -1;
         const int iters = 20;
         for (int i = 0; i < iters; ++i) fn();
-        CK(hipEventRecord(e1, 0));
-        CK(hipEventSynchronize(e1));
+        if (hipEventRecord(e1, 0) != hipSuccess || hipEventSynchronize(e1) != hipSuccess) return -1;
         float ms;
-        CK(hipEventElapsedTime(&ms, e0, e1));
-        const double us = ms * 1e3 / iters;
-        printf("%-34s %9.1f us  %7.1f TF/s  (%s)\n", name, us, flop / (us * 1e-6) / 1e12, ttamm_last_error());
+        if (hipEventElapsedTime(&ms, e0, e1) != hipSuccess) return -1;
+        return ms * 1e3 / iters;
+    };
+    // out: the tensor the case writes (n floats), compared between the two kernels
+    auto time_it = [&](const char* name, double flop, const float* out, size_t n, auto fn) -> int {
+        std::vector<float> ref(n), got(n);
+        setenv("TTAMM_FP32_MFMA", "exact", 1);
+        const double us_exact = time_one(fn);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(ref.data(), out, n * 4, hipMemcpyDeviceToHost));
+        unsetenv("TTAMM_FP32_MFMA");
+        const double us = time_one(fn);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(got.data(), out, n * 4, hipMemcpyDeviceToHost));
+        double mx = 0, md = 0;
+        for (size_t i = 0; i < n; ++i) {
+            mx = std::fmax(mx, std::fabs(ref[i]));
+            md = std::fmax(md, std::fabs((double)ref[i] - got[i]));
+        }
+        printf("%-36s split %8.1f us %6.1f TF/s | exact %8.1f us %6.1f TF/s | rel diff %.2e  (%s)\n", name, us,
+               flop / (us * 1e-6) / 1e12, us_exact, flop / (us_exact * 1e-6) / 1e12, mx > 0 ? md / mx : md,
+               ttamm_last_error());
         return 0;
     };
     // layer-1 forward: [R, F](gathered) x W1^T -> [R, H], bias+ReLU+dropout
-    time_it("fwd L1 R x 608 -> 192 (gather)", 2.0 * R * F * H, [&] {
+    time_it("fwd L1 R x 608 -> 192 (gather)", 2.0 * R * F * H, C, (size_t)R * H, [&] {
         GemmBatch b;
         std::memset(&b, 0, sizeof(b));
         GemmProblem p = base();
@@ -86,7 +109,7 @@ int main() {
         b.p[0] = p, b.count = 1;
         launch_gemm(b, 0);
     });
-    time_it("fwd L1 (no dropout)", 2.0 * R * F * H, [&] {
+    time_it("fwd L1 (no dropout)", 2.0 * R * F * H, C, (size_t)R * H, [&] {
         GemmBatch b;
         std::memset(&b, 0, sizeof(b));
         GemmProblem p = base();
@@ -95,7 +118,7 @@ int main() {
         b.p[0] = p, b.count = 1;
         launch_gemm(b, 0);
     });
-    time_it("fwd L1 (no gather, no dropout)", 2.0 * R * F * H, [&] {
+    time_it("fwd L1 (no gather, no dropout)", 2.0 * R * F * H, C, (size_t)R * H, [&] {
         GemmBatch b;
         std::memset(&b, 0, sizeof(b));
         GemmProblem p = base();
@@ -104,7 +127,7 @@ int main() {
         b.p[0] = p, b.count = 1;
         launch_gemm(b, 0);
     });
-    time_it("fwd L2 R x 192 -> 96", 2.0 * R * H * D, [&] {
+    time_it("fwd L2 R x 192 -> 96", 2.0 * R * H * D, C, (size_t)R * D, [&] {
         GemmBatch b;
         std::memset(&b, 0, sizeof(b));
         GemmProblem p = base();
@@ -113,7 +136,7 @@ int main() {
         b.p[0] = p, b.count = 1;
         launch_gemm(b, 0);
     });
-    time_it("dgrad R x 96 -> 192 (W KN)", 2.0 * R * H * D, [&] {
+    time_it("dgrad R x 96 -> 192 (W KN)", 2.0 * R * H * D, C, (size_t)R * H, [&] {
         GemmBatch b;
         std::memset(&b, 0, sizeof(b));
         GemmProblem p = base();
@@ -122,25 +145,29 @@ int main() {
         b.p[0] = p, b.count = 1;
         launch_gemm(b, 0);
     });
-    time_it("wgrad W1 192 x 608 over R (gather)", 2.0 * R * (F + 1) * H, [&] {
+    time_it("wgrad W1 192 x 608 over R (gather)", 2.0 * R * (F + 1) * H, gw, (size_t)H * (F - 3), [&] {
         WgradBatch wb;
         std::memset(&wb, 0, sizeof(wb));
         WgradProblem w{};
         w.dY = dY, w.ld_dy = H, w.X = X, w.x_idx = idx, w.ld_x = F, w.R = R, w.M = H, w.N = F - 3;
         w.grad_w = gw, w.grad_b = gb, w.slab = slab;
         const WgradShape sh{w.R, w.M, w.N};
-        w.rows_per_split = wgrad_rows_per_split(&sh, 1);
+        int rps[2];
+        wgrad_rows_per_split(&sh, 1, rps);
+        w.rows_per_split = rps[wgrad_class(w.M)];
         wb.p[0] = w, wb.count = 1;
         launch_wgrad(wb, 0);
     });
-    time_it("wgrad W2 96 x 192 over R", 2.0 * R * (H + 1) * D, [&] {
+    time_it("wgrad W2 96 x 192 over R", 2.0 * R * (H + 1) * D, gw, (size_t)D * H, [&] {
         WgradBatch wb;
         std::memset(&wb, 0, sizeof(wb));
         WgradProblem w{};
         w.dY = dF, w.ld_dy = D, w.X = Hb, w.ld_x = H, w.R = R, w.M = D, w.N = H;
         w.grad_w = gw, w.grad_b = gb, w.slab = slab;
         const WgradShape sh{w.R, w.M, w.N};
-        w.rows_per_split = wgrad_rows_per_split(&sh, 1);
+        int rps[2];
+        wgrad_rows_per_split(&sh, 1, rps);
+        w.rows_per_split = rps[wgrad_class(w.M)];
         wb.p[0] = w, wb.count = 1;
         launch_wgrad(wb, 0);
     });
