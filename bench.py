@@ -16,7 +16,11 @@ users (6.25M x 25K), D = 128, MLP 605 -> 256 -> 128, in-batch negatives (all-gat
 ranks); at --gpus 8 the global model is the full C4.
 
 One step = one call of ttamm_train_step on one batch (sampling, forward, loss, backward,
-both optimizers).  `value` = interactions (positives) per second over all ranks.
+both optimizers).  `value` = interactions (positives) per second over all ranks.  The timed
+region is K steps plus the closing flush of the deferred table AdamW (every row brought
+current, as `finish()` does at the end of an epoch); K defaults to one epoch of the config
+(C2: ceil(200K users x 20 positives / 8192) = 489 steps), so the flush is priced as the
+reference's per-epoch work, not per 20 steps.
 Multi-GPU (weak scaling): one process per GPU (torch.distributed.run, RCCL).  Rank r owns
 users and items with id % N == r — C2-sized shards, so the global model is N x C2 — and runs
 the row-sharded step of ttamm/sharded.py on a C2 batch of its own users: item requests and
@@ -113,7 +117,7 @@ class Workload:
     """C2 data + model on one GPU, or rank `rank`'s C2-sized shard of an N x C2 model."""
 
     def __init__(self, c: dict, device, seed: int, world: int = 1, rank: int = 0, step_seed: int | None = None,
-                 deferred: bool = True, overlap: bool = True, in_batch: bool = False):
+                 deferred: bool = True, overlap: bool = True, in_batch: bool = False, table_math: str = "fast"):
         import ttamm
         from ttamm.samplers import PositivesCSR
 
@@ -158,7 +162,8 @@ class Workload:
         self.opts = [torch.optim.AdamW(dense, lr=1e-3, weight_decay=0.01), torch.optim.SparseAdam(sparse, lr=1e-3)]
         kw = dict(negatives_per_positive=c["N"], positives=self.csr, user_features=self.user_features,
                   item_features=self.item_features, loss_weights={"mimic_user": 0.15, "mimic_item": 0.15},
-                  max_batch=c["B"], deferred_adamw=deferred, overlap=overlap, in_batch_negatives=in_batch)
+                  max_batch=c["B"], deferred_adamw=deferred, overlap=overlap, in_batch_negatives=in_batch,
+                  table_adamw_math=table_math)
         if world == 1:
             self.engine = ttamm.FusedTrainStep(self.model, self.opts, seed=seed, **kw)
         else:
@@ -238,7 +243,8 @@ def load_traffic(config: str) -> dict | None:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: one epoch of the config, ceil(U x positives per user / B))")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=1234)
@@ -248,6 +254,9 @@ def main() -> None:
                     help="gloo stages the exchanges through host memory (several ranks on one GPU, tests only)")
     ap.add_argument("--eager-adamw", action="store_true",
                     help="sweep AdamW(g=0) over the whole mimic tables every step instead of the deferred exact replay")
+    ap.add_argument("--exact-table-math", action="store_true",
+                    help="IEEE sqrt / division for the g = 0 table AdamW updates (bit-identical to torch) "
+                         "instead of v_sqrt / v_rcp")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the step's index-only prologue on the main stream (no aux stream)")
     ap.add_argument("--negatives", choices=["sampled", "in-batch"], default=None,
@@ -279,8 +288,11 @@ def main() -> None:
     elif in_batch and args.negatives == "in-batch" and "negatives" not in c:
         c["N"] = 0
 
+    if args.steps is None:  # one epoch: the deferred-AdamW flush closes it, as at the reference's epoch end
+        args.steps = max(1, math.ceil(c["U"] * c["pos_per_user"] / c["B"]))
     w = Workload(c, device, args.seed + rank, world=world, rank=rank, step_seed=args.seed,
-                 deferred=not args.eager_adamw, overlap=not args.no_overlap, in_batch=in_batch)
+                 deferred=not args.eager_adamw, overlap=not args.no_overlap, in_batch=in_batch,
+                 table_math="exact" if args.exact_table_math else "fast")
     eng = w.engine
     for _ in range(args.warmup):
         u, p = w.batch()
@@ -405,7 +417,8 @@ def main() -> None:
             "negatives_per_positive": N,
             "parallelism": f"row-sharded tables x{world} (all-to-all) + replicated MLP (all-reduce)"
                            if world > 1 else "single",
-            "adamw_tables": "deferred exact replay" if deferred else "eager sweep",
+            "adamw_tables": ("deferred replay" if deferred else "eager sweep")
+                            + (", IEEE g=0 arithmetic" if args.exact_table_math else ", v_sqrt/v_rcp g=0 arithmetic"),
         },
         "final_loss": round(loss, 6),
         "roofline": roof,

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 13
+#define TTAMM_ABI_VERSION 14
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -254,7 +254,17 @@ typedef struct ttamm_step_args {
     const float* inbatch_items;   /* sharded: [global_batch, dim] all ranks' (all-gathered)       */
     float* inbatch_dp_all;        /* sharded: [global_batch, dim] this rank's share of dP         */
     const float* inbatch_dp;      /* sharded: [batch, dim] summed dP of this rank's positives     */
+    /* ---- arithmetic of the g = 0 AdamW updates of untouched dense-group table rows (deferred
+     * replay, eager sweep, ttamm_flush_tables; rows with a gradient always use IEEE ops) --------
+     * TTAMM_G0_EXACT: IEEE sqrt and division — bit-identical to torch's AdamW step;
+     * TTAMM_G0_FAST:  v_sqrt_f32 / v_rcp_f32 (<= 1 ulp each) and a multiply by RN(1/sqrt(bc2)):
+     *                 each g = 0 update term within a few ulp of torch's, a third of the VALU work.
+     * Deferred and eager stay bit-identical to each other in either mode. */
+    int32_t table_g0_math;
 } ttamm_step_args;
+
+#define TTAMM_G0_EXACT 0
+#define TTAMM_G0_FAST 1
 
 /* ---------------------------------------------------------------------------------- */
 /* Entry points                                                                        */

@@ -369,6 +369,7 @@ struct AdamConsts {
     float inv_bc2_sqrt;  // RN(1 / bc2_sqrt): the correctly rounded reciprocal (div_by_const)
     float wd;        // weight_decay (Adam L2 form)
     int decoupled;
+    int fast_g0;     // g = 0 updates with v_sqrt / v_rcp (ttamm.h TTAMM_G0_FAST)
 };
 struct SparseConsts {
     float w1;        // 1 - beta1
@@ -444,6 +445,7 @@ struct ReplayArgs {
     int32_t target;   // replay every row up to this dense step
     int stamp;        // write last = target afterwards (row ranges only)
     int decoupled;    // AdamW (decoupled weight decay) vs Adam (L2): the optimizer's, every step
+    int fast_g0;      // TTAMM_G0_FAST arithmetic
     const uint32_t* status;  // poisoned: no write (null for the flush)
 };
 int launch_replay(const ReplayArgs& a, hipStream_t s);

@@ -30,7 +30,9 @@ namespace {
 //   p += -step * m / (sqrt(v)/sqrt(bc2) + eps)
 // G0: the gradient is the literal 0 (an untouched dense-table row): lerp(m, 0, w) =
 // m + w*(0 - m) == fma(w, -m, m) and v*b2 + (1-b2)*0*0 == v*b2 (v >= +0), bit for bit.
-template <bool DECOUPLED, bool G0 = false>
+// FAST (g = 0 rows only, ttamm.h TTAMM_G0_FAST): sqrt and 1/denom from v_sqrt_f32 / v_rcp_f32
+// (<= 1 ulp each) and a multiply by RN(1 / sqrt(bc2)) — a third of the IEEE sequences' VALU work.
+template <bool DECOUPLED, bool G0 = false, bool FAST = false>
 __device__ __forceinline__ void adam_elem_t(float& p, float& m, float& v, float g, const AdamConsts& c) {
     if (DECOUPLED) {
         p = p * c.decay;
@@ -45,8 +47,14 @@ __device__ __forceinline__ void adam_elem_t(float& p, float& m, float& v, float 
         v = v * c.b2;
         v = v + c.w2 * g * g;
     }
-    const float denom = div_by_const(sqrtf(v), c.bc2_sqrt, c.inv_bc2_sqrt) + c.eps;
-    p = p + c.neg_step * (m / denom);
+    if constexpr (FAST) {
+        static_assert(G0, "fast arithmetic is for the g = 0 updates only");
+        const float denom = __builtin_amdgcn_sqrtf(v) * c.inv_bc2_sqrt + c.eps;
+        p = p + c.neg_step * (m * __builtin_amdgcn_rcpf(denom));
+    } else {
+        const float denom = div_by_const(sqrtf(v), c.bc2_sqrt, c.inv_bc2_sqrt) + c.eps;
+        p = p + c.neg_step * (m / denom);
+    }
 }
 
 __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, const AdamConsts& c) {
@@ -56,10 +64,16 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
         adam_elem_t<false>(p, m, v, g, c);
 }
 __device__ __forceinline__ void adam_elem_g0(float& p, float& m, float& v, const AdamConsts& c) {
-    if (c.decoupled)
+    if (c.fast_g0) {
+        if (c.decoupled)
+            adam_elem_t<true, true, true>(p, m, v, 0.f, c);
+        else
+            adam_elem_t<false, true, true>(p, m, v, 0.f, c);
+    } else if (c.decoupled) {
         adam_elem_t<true, true>(p, m, v, 0.f, c);
-    else
+    } else {
         adam_elem_t<false, true>(p, m, v, 0.f, c);
+    }
 }
 
 // torch SparseAdam on one coalesced element (_functional.py:61-84).
@@ -467,7 +481,7 @@ __global__ void step_begin_kernel(const uint32_t* status, int64_t* applied, Adam
 // chains per thread sharing each step's constants); blockIdx.y = segment.  A row current to
 // step l is brought to A.target by replaying adam_elem(g = 0) with the constants of steps
 // l+1 .. target — the operations the eager sweep applies, so the bits agree.
-template <bool DECOUPLED>
+template <bool DECOUPLED, bool FAST>
 __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
     const KArg(ReplayArgs)* ka = (const KArg(ReplayArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
     const KArg(ReplaySeg)& S = ka->seg[blockIdx.y];
@@ -502,10 +516,10 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
         int j = (int)((l + 1) % cap);
         for (int32_t t = l + 1; t <= target; ++t) {
             const AdamConsts c = H[j];
-            adam_elem_t<DECOUPLED, true>(p.x, m.x, v.x, 0.f, c);
-            adam_elem_t<DECOUPLED, true>(p.y, m.y, v.y, 0.f, c);
-            adam_elem_t<DECOUPLED, true>(p.z, m.z, v.z, 0.f, c);
-            adam_elem_t<DECOUPLED, true>(p.w, m.w, v.w, 0.f, c);
+            adam_elem_t<DECOUPLED, true, FAST>(p.x, m.x, v.x, 0.f, c);
+            adam_elem_t<DECOUPLED, true, FAST>(p.y, m.y, v.y, 0.f, c);
+            adam_elem_t<DECOUPLED, true, FAST>(p.z, m.z, v.z, 0.f, c);
+            adam_elem_t<DECOUPLED, true, FAST>(p.w, m.w, v.w, 0.f, c);
             j = j + 1 == cap ? 0 : j + 1;
         }
         *reinterpret_cast<float4*>(S.p + o) = p;
@@ -621,6 +635,7 @@ AdamConsts make_adam_consts(double lr, double beta1, double beta2, double eps, d
     c.inv_bc2_sqrt = correctly_rounded_reciprocal(c.bc2_sqrt);
     c.wd = (float)wd;
     c.decoupled = decoupled;
+    c.fast_g0 = 0;
     return c;
 }
 
@@ -773,10 +788,15 @@ int launch_replay(const ReplayArgs& a, hipStream_t s) {
         most = n * (g.dim / 4) > most ? n * (g.dim / 4) : most;
     }
     if (most == 0) return TTAMM_OK;
-    if (a.decoupled)
-        hipLaunchKernelGGL(replay_kernel<true>, dim3(grid_for(most, 256, 16384), a.count), dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL(replay_kernel<false>, dim3(grid_for(most, 256, 16384), a.count), dim3(256), 0, s, a);
+    const dim3 grid(grid_for(most, 256, 16384), a.count);
+    if (a.fast_g0) {
+        if (a.decoupled) hipLaunchKernelGGL((replay_kernel<true, true>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((replay_kernel<false, true>), grid, dim3(256), 0, s, a);
+    } else if (a.decoupled) {
+        hipLaunchKernelGGL((replay_kernel<true, false>), grid, dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((replay_kernel<false, false>), grid, dim3(256), 0, s, a);
+    }
     TTAMM_LAUNCH_CHECK();
     if (a.stamp) {
         int64_t rows = 0;

@@ -762,6 +762,7 @@ struct Deferred {
     int slices = 1;
     int32_t step = 0;  // the dense step this call executes
     int decoupled = 1;
+    int fast = 0;  // TTAMM_G0_FAST arithmetic for the g = 0 updates
     const uint32_t* status = nullptr;  // poisoned: the step writes nothing
 };
 
@@ -796,6 +797,7 @@ int tower_prepare_a(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred
     ra.hist = df.hist;
     ra.cap = df.cap;
     ra.decoupled = df.decoupled;
+    ra.fast_g0 = df.fast;
     ra.status = df.status;
     ra.target = df.step - 1;
     const ttamm_table* tabs[2];
@@ -950,6 +952,7 @@ int table_updates(const ttamm_tower* T[2], TowerWs* W[2], int n, int D, bool mim
         ra.hist = df.hist;
         ra.cap = df.cap;
         ra.decoupled = df.decoupled;
+        ra.fast_g0 = df.fast;
         ra.status = df.status;
         ra.target = df.step;
         ra.stamp = 1;
@@ -1049,12 +1052,15 @@ int deferred_of(const ttamm_step_args& A, Deferred& df) {
     df.slices = A.replay_slices;
     df.step = (int32_t)A.hp.dense_step;
     df.decoupled = A.hp.decoupled_weight_decay ? 1 : 0;
+    df.fast = A.table_g0_math == TTAMM_G0_FAST ? 1 : 0;
     return TTAMM_OK;
 }
 
 int validate_step(const ttamm_step_args& A) {
     const int D = A.user.id.dim;
     int rc;
+    TTAMM_REQUIRE(A.table_g0_math == TTAMM_G0_EXACT || A.table_g0_math == TTAMM_G0_FAST,
+                  "table_g0_math must be TTAMM_G0_EXACT or TTAMM_G0_FAST");
     if ((rc = validate_tower(A.user, "user_encoder", D, true))) return rc;
     if ((rc = validate_tower(A.item, "item_encoder", D, true))) return rc;
     TTAMM_REQUIRE(A.user.matmul_bf16 == A.item.matmul_bf16, "user and item towers must share one matmul precision");
@@ -1152,8 +1158,9 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     const ttamm_tower* T[2] = {&A.user, &A.item};
     TowerWs* W[2] = {&U, &I};
     const ttamm_hparams& hp = A.hp;
-    const AdamConsts ad = make_adam_consts(hp.lr, hp.beta1, hp.beta2, hp.eps, hp.weight_decay,
-                                           hp.decoupled_weight_decay, hp.dense_step);
+    AdamConsts ad = make_adam_consts(hp.lr, hp.beta1, hp.beta2, hp.eps, hp.weight_decay,
+                                     hp.decoupled_weight_decay, hp.dense_step);
+    ad.fast_g0 = A.table_g0_math == TTAMM_G0_FAST ? 1 : 0;
     const SparseConsts sp = make_sparse_consts(hp.sparse_lr, hp.sparse_beta1, hp.sparse_beta2, hp.sparse_eps,
                                                hp.sparse_step);
     Deferred df;
@@ -1372,6 +1379,7 @@ int flush_tables(const ttamm_step_args& A, hipStream_t s) {
     ra.hist = df.hist;
     ra.cap = df.cap;
     ra.decoupled = df.decoupled;
+    ra.fast_g0 = df.fast;
     ra.target = df.step;
     ra.stamp = 1;
     for (const ttamm_tower* t : {&A.user, &A.item}) {

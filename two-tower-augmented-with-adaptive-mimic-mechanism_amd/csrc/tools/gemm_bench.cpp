@@ -79,6 +79,33 @@ int main() {
         return ms * 1e3 / iters;
     };
     // out: the tensor the case writes (n floats), compared between the two kernels
+    // fp64 reference of C = A B^T (+ bias) on sampled outputs: max |err| / max |C| of both kernels
+    auto fp64_check = [&](const char* name, const float* dA, int lda, const float* dB, int ldb, int Mr, int Nc, int K,
+                          const float* dbias, auto fn) -> int {
+        std::vector<float> a((size_t)Mr * lda), b((size_t)Nc * ldb), bias(Nc), out((size_t)Mr * Nc);
+        CK(hipMemcpy(a.data(), dA, a.size() * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(b.data(), dB, b.size() * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(bias.data(), dbias, Nc * 4, hipMemcpyDeviceToHost));
+        double errs[2];
+        for (int mode = 0; mode < 2; ++mode) {
+            if (mode == 0) setenv("TTAMM_FP32_MFMA", "exact", 1);
+            else unsetenv("TTAMM_FP32_MFMA");
+            fn();
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(out.data(), C, out.size() * 4, hipMemcpyDeviceToHost));
+            double mx = 0, md = 0;
+            for (int r = 0; r < Mr; r += 97)
+                for (int c = 0; c < Nc; ++c) {
+                    double acc = bias[c];
+                    for (int k = 0; k < K; ++k) acc += (double)a[(size_t)r * lda + k] * b[(size_t)c * ldb + k];
+                    mx = std::fmax(mx, std::fabs(acc));
+                    md = std::fmax(md, std::fabs(acc - out[(size_t)r * Nc + c]));
+                }
+            errs[mode] = md / mx;
+        }
+        printf("%-36s fp64 check: exact %.2e  split %.2e (max |err| / max |C|)\n", name, errs[0], errs[1]);
+        return 0;
+    };
     auto time_it = [&](const char* name, double flop, const float* out, size_t n, auto fn) -> int {
         std::vector<float> ref(n), got(n);
         setenv("TTAMM_FP32_MFMA", "exact", 1);
@@ -124,6 +151,24 @@ int main() {
         GemmProblem p = base();
         p.A = X, p.lda = F, p.B = W1, p.ldb = F, p.M = R, p.N = H, p.K = F;
         p.epi = EPI_HIDDEN, p.C = C, p.ldc = H, p.bias = b1;
+        b.p[0] = p, b.count = 1;
+        launch_gemm(b, 0);
+    });
+    fp64_check("fwd L2 R x 192 -> 96", Hb, H, W2, H, R, D, H, b1, [&] {
+        GemmBatch b;
+        std::memset(&b, 0, sizeof(b));
+        GemmProblem p = base();
+        p.A = Hb, p.lda = H, p.B = W2, p.ldb = H, p.M = R, p.N = D, p.K = H;
+        p.epi = EPI_STORE, p.C = C, p.ldc = D, p.bias = b1;
+        b.p[0] = p, b.count = 1;
+        launch_gemm(b, 0);
+    });
+    fp64_check("fwd L1 R x 608 -> 192 (no gather)", X, F, W1, F, R, H, F, b1, [&] {
+        GemmBatch b;
+        std::memset(&b, 0, sizeof(b));
+        GemmProblem p = base();
+        p.A = X, p.lda = F, p.B = W1, p.ldb = F, p.M = R, p.N = H, p.K = F;
+        p.epi = EPI_STORE, p.C = C, p.ldc = H, p.bias = b1;
         b.p[0] = p, b.count = 1;
         launch_gemm(b, 0);
     });

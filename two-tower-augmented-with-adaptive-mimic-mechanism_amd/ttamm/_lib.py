@@ -156,10 +156,13 @@ class StepArgs(ctypes.Structure):
         ("inbatch_items", c_vp),
         ("inbatch_dp_all", c_vp),
         ("inbatch_dp", c_vp),
+        ("table_g0_math", c_i32),
     ]
 
 
-ABI_VERSION = 13  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 14
+G0_EXACT = 0  # ttamm.h TTAMM_G0_EXACT
+G0_FAST = 1  # ttamm.h TTAMM_G0_FAST  # ttamm.h TTAMM_ABI_VERSION
 
 # ttamm.h TTAMM_PHASE_*
 PHASE_ALL = 0

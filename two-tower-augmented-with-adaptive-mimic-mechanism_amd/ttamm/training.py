@@ -122,6 +122,7 @@ class FusedTrainStep:
         num_items: int | None = None,
         deferred_adamw: bool = True,
         replay_slices: int = 64,
+        table_adamw_math: str = "fast",
         overlap: bool = True,
         item_category_tensor: torch.Tensor | None = None,
         major_category_id: int | None = None,
@@ -288,6 +289,11 @@ class FusedTrainStep:
         self.lib = _lib.load()
         self.dense_step0 = int(self._adam_steps[0]["step"].item()) if self._adam_steps else 0
         self.sparse_step0 = int(self._sparse_steps[0]["step"]) if self._sparse_steps else 0
+        # arithmetic of the g = 0 AdamW updates of untouched table rows (ttamm.h table_g0_math):
+        # "exact" = IEEE sqrt / division, bit-identical to torch; "fast" = v_sqrt / v_rcp
+        if table_adamw_math not in ("exact", "fast"):
+            raise ValueError("ttamm: table_adamw_math must be 'exact' or 'fast'")
+        args.table_g0_math = _lib.G0_FAST if table_adamw_math == "fast" else _lib.G0_EXACT
         # deferred exact AdamW(g = 0) on the dense-group tables (ttamm.h ttamm_table.last_step):
         # the rows are current to dense_step0 now
         self._deferred: list[torch.Tensor] = []
