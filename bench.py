@@ -355,10 +355,13 @@ def main() -> None:
     traffic = load_traffic(args.config)
     deferred = not args.eager_adamw
     if deferred:
-        maint = {"kernel": "replay_kernel (deferred exact AdamW g=0, this step's 1/64 slice of the mimic tables)",
+        maint = {"kernel": "replay_kernel (deferred AdamW g=0, this step's 1/64 slice of the mimic tables)",
                  "bound": "valu", "avg_launch_ms": round(maint_ms, 4),
-                 "note": "per-step share only; catch-up of touched rows and the closing flush are further "
-                         "replay_kernel launches (see profiles/)"}
+                 "note": "avg_launch_ms: the per-step slice only, live; the catch-up of touched rows (aux stream) "
+                         "and the flushes are further replay_kernel launches.  valu_roofline: all of them, from "
+                         "the committed rocprofv3 passes (SQ_INSTS_VALU per element-step x element-steps per "
+                         "step / replay time per step vs the chip's VALU issue rate)",
+                 "valu_roofline": (traffic or {}).get("replay_valu_roofline")}
     else:
         sweep_bytes = 24 * (U + I) * D if world == 1 else 24 * I * D
         gbs = sweep_bytes / (maint_ms * 1e-3) / 1e9
@@ -366,18 +369,32 @@ def main() -> None:
                  "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                  "traffic": (traffic or {}).get("dense_sweep_kernel_bytes_per_launch"),
                  "algorithmic_bytes_per_launch": sweep_bytes, "avg_launch_ms": round(maint_ms, 4)}
-    kernels = [{
+    exact_mfma = os.environ.get("TTAMM_FP32_MFMA") == "exact"
+    if bf16:
+        impl = "bf16 operands, v_mfma_f32_32x32x16_bf16"
+    elif exact_mfma:
+        impl = "fp32 v_mfma_f32_32x32x2_f32"
+    else:
+        impl = "fp32 as split-bf16 (hi/mid/lo planes, 6 x v_mfma_f32_32x32x16_bf16 per product)"
+    l1 = {
         "bound": "mfma",
-        "kernel": f"gemm_kernel first feature layer forward (Linear {F}->{H} + ReLU + dropout, user and item "
-                  f"rows grouped), {'bf16 MFMA 32x32x16' if bf16 else 'fp32 MFMA 32x32x2'}",
+        "kernel": f"first feature layer forward GEMM (Linear {F}->{H} + ReLU + dropout, user and item rows "
+                  f"grouped), {impl}",
         "achieved": round(tflops, 2),
         "peak": mfma_peak,
         "unit": "TFLOP/s",
         "frac": round(tflops / mfma_peak, 4),
         "traffic": (traffic or {}).get("l1_forward_gemm_bytes_per_launch"),
         "algorithmic_flops_per_launch": l1_flops,
+        "algorithmic_bytes_per_launch": l1_rows * (F * 4 + H * 4),
         "avg_launch_ms": round(gemm_ms, 4),
-    }]
+    }
+    if not bf16 and not exact_mfma:
+        # the split kernel's own ceiling: six bf16 MFMAs per fp32 product
+        ceil = MFMA_BF16_PEAK_TFLOPS / 6.0
+        l1["kernel_ceiling_tflops"] = round(ceil, 1)
+        l1["frac_of_kernel_ceiling"] = round(tflops / ceil, 4)
+    kernels = [l1]
     if in_batch:
         Bg = B * world
         ib_flops = 6.0 * B * Bg * D  # S = U P^T, dU = dS P, dP = dS^T U (S recomputed: not counted)
