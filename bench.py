@@ -15,8 +15,9 @@ default 0).  --config c4 is BASELINE configs[3] per GPU: a 1/8 shard of 50M item
 users (6.25M x 25K), D = 128, MLP 605 -> 256 -> 128, in-batch negatives (all-gathered across
 ranks); at --gpus 8 the global model is the full C4.
 
-One step = one call of ttamm_train_step on one batch (sampling, forward, loss, backward,
-both optimizers).  `value` = interactions (positives) per second over all ranks.  The timed
+One step = the loader's next batch (ttamm.DeviceInteractionLoader: the epoch order evaluated on
+the device, pairs resident in HBM) + one call of ttamm_train_step on it (sampling, forward,
+loss, backward, both optimizers).  `value` = interactions (positives) per second over all ranks.  The timed
 region is K steps plus the closing flush of the deferred table AdamW (every row brought
 current, as `finish()` does at the end of an epoch); K defaults to one epoch of the config
 (C2: ceil(200K users x 20 positives / 8192) = 489 steps), so the flush is priced as the
@@ -146,12 +147,14 @@ class Workload:
             rows = torch.div(items[lo:hi].reshape(-1), world, rounding_mode="floor")
             uf[lo:hi] = full[rows].view(hi - lo, per, Fp).mean(dim=1)
         self.user_features = uf[:, :F]
-        # interactions: every (user, positive) pair, shuffled once (DataLoader shuffle=True)
+        # interactions: every (user, positive) pair, HBM-resident; batches come from the on-device
+        # loader (ttamm.DeviceInteractionLoader = DataLoader(shuffle=True), a new order per epoch;
+        # drop_last keeps every step at B)
         self.users_all = torch.arange(U, device=device).repeat_interleave(per)
-        self.items_all = items.reshape(-1)
-        order = torch.randperm(U * per, device=device, generator=gen)
-        self.users_all = self.users_all[order].contiguous()
-        self.items_all = self.items_all[order].contiguous()
+        self.items_all = items.reshape(-1).contiguous()
+        self.loader = ttamm.DeviceInteractionLoader(self.users_all, self.items_all, c["B"], shuffle=True,
+                                                    drop_last=True, seed=seed)
+        self._it = iter(self.loader)
         # model + optimizers (training.py:1266-1350)
         cfg = tower_cfg(c)
         ue = ttamm.build_tower_encoder(cfg, num_embeddings=U, feature_dim=F, device=device)
@@ -172,16 +175,14 @@ class Workload:
             # step_seed: the same on every rank (the Philox streams are keyed by global position)
             self.engine = ShardedTrainStep(self.model, self.opts, world_size=world, rank=rank, num_items=Ig,
                                            comm=TorchComm(), seed=step_seed, **kw)
-        self.cursor = 0
 
     def batch(self):
-        B = self.c["B"]
-        n = self.users_all.numel()
-        if self.cursor + B > n:
-            self.cursor = 0
-        sl = slice(self.cursor, self.cursor + B)
-        self.cursor += B
-        return self.users_all[sl], self.items_all[sl]
+        """The next batch of the on-device loader (epochs run back to back)."""
+        try:
+            return next(self._it)
+        except StopIteration:
+            self._it = iter(self.loader)
+            return next(self._it)
 
 
 # ---------------------------------------------------------------------------------------
@@ -307,7 +308,6 @@ def main() -> None:
         for e in quad:
             e.record()
     torch.cuda.synchronize()
-    batches = [w.batch() for _ in range(args.steps)]
     rows0 = getattr(eng, "item_rows_seen", 0)
 
     if dist is not None:
@@ -317,7 +317,7 @@ def main() -> None:
     t0 = time.perf_counter()
     marks[0].record()
     for k in range(args.steps):
-        u, p = batches[k]
+        u, p = w.batch()  # ttamm_epoch_batch: the loader's gather runs inside the timed region
         eng.step(u, p, timing_events=[e.cuda_event for e in evs[k]])
     marks[1].record()
     # deferred AdamW: the g = 0 updates still owed to untouched rows are part of the K steps' work

@@ -312,6 +312,18 @@ int ttamm_candidate_topk(const float* queries, int64_t n_queries, int64_t ldq, c
 int ttamm_to_bf16(const float* src, int64_t rows, int32_t cols, int64_t ld_src, uint16_t* dst, int64_t ld_dst,
                   void* stream);
 
+/* DataLoader(InteractionDataset(train_df), batch_size, shuffle, drop_last=False)
+ * (datasets.py:12-45, training.py:260-264) over pairs resident in HBM: writes positions
+ * [start, start + count) of epoch `epoch`'s order of the n pairs (users[i], items[i]) — the
+ * batch of a loader is start = b * batch_size, count = min(batch_size, n - start).  shuffle = 0:
+ * the stored order; otherwise pair perm(p) at position p, perm a seeded bijection of [0, n)
+ * (4-round Feistel network on 2h-bit words, 4^h >= n, with cycle-walking; round keys from
+ * splitmix64 of (seed, epoch), restated in oracle/data_perm.py).  Replaces the host-side
+ * torch.randperm + collation of torch.utils.data. */
+int ttamm_epoch_batch(const int64_t* users, const int64_t* items, int64_t n, uint64_t seed, int64_t epoch,
+                      int32_t shuffle, int64_t start, int64_t count, int64_t* out_users, int64_t* out_items,
+                      void* stream);
+
 /* faiss.normalize_L2 on device rows, in place (training.py:670-672 on the item matrix and
  * :954-955 on the queries when the model's similarity is cosine): row r of the [n, dim] matrix
  * with leading dim ld is scaled by 1 / sqrt(sum of its squares); rows of norm 0 are left as

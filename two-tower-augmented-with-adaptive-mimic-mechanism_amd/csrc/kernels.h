@@ -80,6 +80,13 @@ struct GemmBatch {
 };
 
 int launch_gemm(GemmBatch& batch, hipStream_t s);
+
+// on-device epoch order of the interaction pairs (data.hip)
+int epoch_half_bits(int64_t n);
+void epoch_round_keys(uint64_t seed, int64_t epoch, uint32_t keys[4]);
+int launch_epoch_batch(const int64_t* users, const int64_t* items, int64_t n, uint64_t seed, int64_t epoch,
+                       int shuffle, int64_t start, int64_t count, int64_t* out_users, int64_t* out_items,
+                       hipStream_t s);
 // fp32 -> bf16 (round to nearest even) rows, zero-filled from `cols` to ld_dst
 int launch_to_bf16(const float* src, int64_t rows, int cols, int64_t ld_src, uint16_t* dst, int64_t ld_dst,
                    hipStream_t s);

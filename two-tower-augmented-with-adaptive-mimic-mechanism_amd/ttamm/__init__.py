@@ -4,6 +4,7 @@ models + training hot loop).  Compute runs in libttamm.so (gfx950 HIP kernels); 
 include/ttamm.h for the C ABI and DESIGN.md for the design."""
 
 from .adaptive_mimic import AdaptiveMimicMechanism
+from .data import DeviceInteractionLoader, load_features, load_interactions, save_features, save_interactions
 from .encoders import (
     FeatureEncoderConfig,
     FeatureEncoderWrapper,
@@ -20,6 +21,7 @@ from .two_tower import TwoTowerModel
 
 __all__ = [
     "AdaptiveMimicMechanism",
+    "DeviceInteractionLoader",
     "DotProductSimilarity",
     "FeatureEncoderConfig",
     "FeatureEncoderWrapper",
@@ -33,7 +35,11 @@ __all__ = [
     "build_tower_encoder",
     "encode_item_embeddings",
     "evaluate_model",
+    "load_features",
+    "load_interactions",
     "prepare_faiss_resources",
     "sample_negative_items",
+    "save_features",
+    "save_interactions",
     "train_one_epoch",
 ]
