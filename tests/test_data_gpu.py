@@ -23,8 +23,9 @@ def test_epoch_batch_matches_oracle(n, bs):
     for seed, epoch in ((0, 0), (1234, 3), (2**63 + 5, 11)):
         ld = ttamm.DeviceInteractionLoader(u, v, bs, seed=seed)
         ld.set_epoch(epoch)
-        got_u = torch.cat([b[0] for b in ld]).cpu().numpy()
-        got_v = torch.cat([b[1] for b in ld]).cpu().numpy()
+        bl = list(ld)  # one epoch
+        got_u = torch.cat([b[0] for b in bl]).cpu().numpy()
+        got_v = torch.cat([b[1] for b in bl]).cpu().numpy()
         order = data_perm.epoch_order(n, seed, epoch)
         assert np.array_equal(got_u, order * 3)
         assert np.array_equal(got_v, order * 5 + 1)
