@@ -1,0 +1,7 @@
+# GPU tests, then the C2 and C5 bench lines (developer script)
+set -e
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gt.log 2>&1
+timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/b_c2.json 2> gpurun_out/b_c2.err
+timeout -k 10 300 python bench.py --no-cpu-baseline --config c5 > gpurun_out/b_c5.json 2> gpurun_out/b_c5.err

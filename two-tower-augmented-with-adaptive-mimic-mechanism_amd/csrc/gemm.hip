@@ -249,8 +249,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
     for (int it = 0; it < CF::A_LOADS; ++it) {
         const int lin = tid + it * kThreads;
         if (!AK) {
-            a_r[it] = lin >> 2;
-            a_c[it] = (lin & 3) * 4;
+            a_r[it] = lin / (BK / 4);
+            a_c[it] = (lin % (BK / 4)) * 4;
             const int gm = m0 + a_r[it];
             a_ok[it] = lin < CF::A_F4 && gm < M;
             const int gmc = min(gm, M - 1);
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
                 const int lin = tid + it * kThreads;
                 if (!BKM) {
                     rb[R][it] = FAST ? *reinterpret_cast<const float4*>(b_rp[it] + k0)
-                                     : raw4(b_rp[it] - (lin & 3) * 4, k0 + (lin & 3) * 4, P.ldb);
+                                     : raw4(b_rp[it] - (lin % (BK / 4)) * 4, k0 + (lin % (BK / 4)) * 4, P.ldb);
                 } else if (FAST) {
                     rb[R][it] = *reinterpret_cast<const float4*>(b_rp[it] + (int64_t)k0 * P.ldb);
                 } else {
@@ -526,11 +526,12 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
 //   K-major operand:  [16 k][mn] bf16, row stride = 64 or 192 (mod 256) bytes — fragments are
 //                     two ds_read_b64_tr_b16 (hardware transpose: lane i of a 16-lane group gets
 //                     column i of a 4 x 16 block), conflict-free per 32-lane half.
-template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KMAJ_, bool B_KMAJ_>
+template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KMAJ_, bool B_KMAJ_, int KT_ = 16>
 struct XCfg {
     static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_;
     static constexpr bool A_KMAJ = A_KMAJ_, B_KMAJ = B_KMAJ_;
-    static constexpr int KT = 16;
+    static constexpr int KT = KT_;     // k per tile: 16 (three planes) or 32 (bf16, one plane)
+    static constexpr int RB = KT * 2;  // MN-major row bytes
     static constexpr int TM = BM / WAVES_M, TN = BN / WAVES_N, I = TM / 32, J = TN / 32;
     static constexpr int A_F4 = BM * KT / 4, B_F4 = BN * KT / 4;
     static constexpr int A_LOADS = (A_F4 + kThreads - 1) / kThreads;
@@ -540,10 +541,11 @@ struct XCfg {
         while (s % 256 != 64 && s % 256 != 192) s += 16;
         return s;
     }
-    static constexpr int SA = A_KMAJ ? kmaj_stride(BM) : 32;  // row stride, bytes
-    static constexpr int SB = B_KMAJ ? kmaj_stride(BN) : 32;
-    static constexpr int A_PLANE = A_KMAJ ? KT * SA : BM * 32;  // bytes
-    static constexpr int B_PLANE = B_KMAJ ? KT * SB : BN * 32;
+    static constexpr int SA = A_KMAJ ? kmaj_stride(BM) : RB;  // row stride, bytes
+    static constexpr int SB = B_KMAJ ? kmaj_stride(BN) : RB;
+    static constexpr int A_PLANE = A_KMAJ ? KT * SA : BM * RB;  // bytes
+    static constexpr int B_PLANE = B_KMAJ ? KT * SB : BN * RB;
+    static_assert(KT == 16 || KT == 32, "k tile of 16 or 32");
     static constexpr int CLD = BN + 4;
     static constexpr int EPI_ROWS = WAVES_M >= 2 ? BM / 2 : (I > 1 ? (I + 1) / 2 * 32 : BM);
     static constexpr int EPI_PHASES = (BM + EPI_ROWS - 1) / EPI_ROWS;
@@ -583,20 +585,26 @@ __device__ __forceinline__ void split_bf16(float4 v, uint2 out[PL]) {
     }
 }
 
-// byte offset of k values [c, c + 4) of row `row` in an MN-major plane (32-B rows, halves
-// swapped on rows with bit 3 set)
-__device__ __forceinline__ int mn_off(int row, int c) { return row * 32 + (((c >> 3) ^ ((row >> 3) & 1)) << 4) + (c & 4) * 2; }
+// byte offset of k values [c, c + 4) of row `row` in an MN-major plane of RB-byte rows: the
+// row's 16-B chunks are XOR-permuted by the row's index among the rows that share a 256-B bank
+// window (32-B rows: halves swapped on rows with bit 3 set; 64-B rows: chunk ^ (row >> 2) & 3),
+// so the 16 rows of every ds_read_b128 lane group hit 16 distinct bank quads
+template <int RB>
+__device__ __forceinline__ int mn_off(int row, int c) {
+    constexpr int CH = RB / 16, PER = 256 / RB;  // chunks per row, rows per bank window
+    return row * RB + (((c >> 3) ^ ((row / PER) & (CH - 1))) << 4) + (c & 4) * 2;
+}
 
 // 32x32x16 operand fragment of MFMA block rows [r0, r0 + 32) (lane l: row r0 + (l & 31),
 // k = 8 (l >> 5) + j)
 template <bool KMAJ, int S>
-__device__ __forceinline__ bf16x8 frag16(const unsigned char* plane, int r0, int lane) {
+__device__ __forceinline__ bf16x8 frag16(const unsigned char* plane, int r0, int kk, int lane) {
     if constexpr (!KMAJ) {
-        return *reinterpret_cast<const bf16x8*>(plane + mn_off(r0 + (lane & 31), 8 * (lane >> 5)));
+        return *reinterpret_cast<const bf16x8*>(plane + mn_off<S>(r0 + (lane & 31), kk + 8 * (lane >> 5)));
     } else {
-        // lane 4q+p of 16-lane group g: block row k = 8(g>>1) + q, columns r0 + 16(g&1) + 4p
+        // lane 4q+p of 16-lane group g: block row k = kk + 8(g>>1) + q, columns r0 + 16(g&1) + 4p
         const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-        const unsigned char* a = plane + (8 * (g >> 1) + q) * S + (r0 + 16 * (g & 1) + 4 * p) * 2;
+        const unsigned char* a = plane + (kk + 8 * (g >> 1) + q) * S + (r0 + 16 * (g & 1) + 4 * p) * 2;
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a));
         const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a + 4 * S));
         const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -638,8 +646,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
     for (int it = 0; it < CX::A_LOADS; ++it) {
         const int lin = tid + it * kThreads;
         if (!AK) {
-            a_r[it] = lin >> 2;
-            a_c[it] = (lin & 3) * 4;
+            a_r[it] = lin / (KT / 4);
+            a_c[it] = (lin % (KT / 4)) * 4;
             const int gm = m0 + a_r[it];
             a_ok[it] = gm < M;
             const int gmc = min(gm, M - 1);
@@ -661,7 +669,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
 #pragma unroll
     for (int it = 0; it < CX::B_LOADS; ++it) {
         const int lin = tid + it * kThreads;
-        if (!BKM) b_rp[it] = P.B + (int64_t)min(n0 + (lin >> 2), N - 1) * P.ldb + (lin & 3) * 4;
+        if (!BKM) b_rp[it] = P.B + (int64_t)min(n0 + lin / (KT / 4), N - 1) * P.ldb + (lin % (KT / 4)) * 4;
         else b_rp[it] = P.B + (int64_t)(lin / (BN / 4)) * P.ldb + n0 + (lin % (BN / 4)) * 4;
     }
     const bool fast = ((k_end - k_begin) % KT == 0) && (n0 + BN <= N) &&
@@ -674,7 +682,10 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
         for (int j = 0; j < J; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    float4 ra[2][CX::A_LOADS], rb[2][CX::B_LOADS];
+    // 16-k tiles: two register sets (the tile two ahead in flight); 32-k tiles (bf16): one set
+    // (the register budget), loaded at a step's start and written after its MFMAs
+    constexpr bool XDEEP = KT == 16;
+    float4 ra[XDEEP ? 2 : 1][CX::A_LOADS], rb[XDEEP ? 2 : 1][CX::B_LOADS];
 
     auto mainloop = [&](auto fast_tag) {
         constexpr bool FAST = decltype(fast_tag)::value;
@@ -697,7 +708,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
                 if (CX::B_F4 % kThreads && lin >= CX::B_F4) continue;  // partial last round (BN = 96)
                 if (!BKM) {
                     rb[R][it] = FAST ? *reinterpret_cast<const float4*>(b_rp[it] + k0)
-                                     : raw4(b_rp[it] - (lin & 3) * 4, k0 + (lin & 3) * 4, P.ldb);
+                                     : raw4(b_rp[it] - (lin % (KT / 4)) * 4, k0 + (lin % (KT / 4)) * 4, P.ldb);
                 } else if (FAST) {
                     rb[R][it] = *reinterpret_cast<const float4*>(b_rp[it] + (int64_t)k0 * P.ldb);
                 } else {
@@ -719,7 +730,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
                 const int it = q;
                 if (!AK) {
                     v = FAST ? ra[R][it] : mask4(ra[R][it], k0 + a_c[it], k_end, P.lda, -1, a_ok[it]);
-                    off = mn_off(a_r[it], a_c[it]);
+                    off = mn_off<CX::RB>(a_r[it], a_c[it]);
                 } else {
                     v = FAST ? ra[R][it]
                              : mask4(ra[R][it], m0 + a_c[it], P.a_cols, P.lda, P.a_ones_col, k0 + a_r[it] < k_end);
@@ -732,9 +743,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
                 const int lin = tid + it * kThreads;
                 if (CX::B_F4 % kThreads && lin >= CX::B_F4) return;  // partial last round (BN = 96)
                 if (!BKM) {
-                    const int n = n0 + (lin >> 2), c = k0 + (lin & 3) * 4;
+                    const int n = n0 + lin / (KT / 4), c = k0 + (lin % (KT / 4)) * 4;
                     v = FAST ? rb[R][it] : mask4(rb[R][it], c, k_end, P.ldb, -1, n < N);
-                    off = mn_off(lin >> 2, (lin & 3) * 4);
+                    off = mn_off<CX::RB>(lin / (KT / 4), (lin % (KT / 4)) * 4);
                 } else {
                     const int kr = lin / (BN / 4), nc = (lin % (BN / 4)) * 4;
                     v = FAST ? rb[R][it] : mask4(rb[R][it], n0 + nc, N, P.ldb, -1, k0 + kr < k_end);
@@ -759,30 +770,39 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
         auto compute = [&](auto Buf, auto S, auto NB, int k0n) {
             const unsigned char* Ap = lds + decltype(Buf)::value * CX::buf_bytes(PL);
             const unsigned char* Bp = Ap + PL * CX::A_PLANE;
-            bf16x8 af[PL][I], bf[PL][J];
+            constexpr int NP = I * J, KS = KT / 16, NSLOT = KS * NP;
 #pragma unroll
-            for (int pl = 0; pl < PL; ++pl) {
+            for (int ks = 0; ks < KS; ++ks) {
+                bf16x8 af[PL][I], bf[PL][J];
 #pragma unroll
-                for (int i = 0; i < I; ++i) af[pl][i] = frag16<AK, CX::SA>(Ap + pl * CX::A_PLANE, wm * TM + i * 32, lane);
+                for (int pl = 0; pl < PL; ++pl) {
 #pragma unroll
-                for (int j = 0; j < J; ++j) bf[pl][j] = frag16<BKM, CX::SB>(Bp + pl * CX::B_PLANE, wn * TN + j * 32, lane);
-            }
-            constexpr int NP = I * J;
+                    for (int i = 0; i < I; ++i)
+                        af[pl][i] = frag16<AK, CX::SA>(Ap + pl * CX::A_PLANE, wm * TM + i * 32, ks * 16, lane);
 #pragma unroll
-            for (int pq = 0; pq < NP; ++pq) {
-                const int i = pq / J, j = pq % J;
-                if constexpr (PL == 3 && TTAMM_X_ABLATE != 2) {  // small terms first (ablation 2: hh only)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][i], bf[1][j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2][i], bf[0][j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][i], bf[2][j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][i], bf[0][j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][i], bf[1][j], acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < J; ++j)
+                        bf[pl][j] = frag16<BKM, CX::SB>(Bp + pl * CX::B_PLANE, wn * TN + j * 32, ks * 16, lane);
                 }
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][i], bf[0][j], acc[i][j], 0, 0, 0);
-#if TTAMM_X_ABLATE != 3
 #pragma unroll
-                for (int q = (pq * NITEMS) / NP; q < ((pq + 1) * NITEMS) / NP; ++q) store_item(S, NB, q, k0n);
+                for (int pq = 0; pq < NP; ++pq) {
+                    const int i = pq / J, j = pq % J;
+                    if constexpr (PL == 3 && TTAMM_X_ABLATE != 2) {  // small terms first (ablation 2: hh only)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][i], bf[1][j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2][i], bf[0][j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][i], bf[2][j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][i], bf[0][j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][i], bf[1][j], acc[i][j], 0, 0, 0);
+                    }
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][i], bf[0][j], acc[i][j], 0, 0, 0);
+#if TTAMM_X_ABLATE != 3
+                    if constexpr (XDEEP) {
+                        const int slot = ks * NP + pq;
+#pragma unroll
+                        for (int q = (slot * NITEMS) / NSLOT; q < ((slot + 1) * NITEMS) / NSLOT; ++q)
+                            store_item(S, NB, q, k0n);
+                    }
 #endif
+                }
             }
         };
         using S0 = std::integral_constant<int, 0>;
@@ -792,26 +812,48 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
         // tile index clamped to the last one: the loop body has no branches (the surplus loads and
         // writes at the end go to the free buffer and are never read)
         auto kof = [&](int kt) { return k_begin + min(kt, nk - 1) * KT; };
-        load_tile(S0{}, kof(0));
-        store_tile(S0{}, S0{}, kof(0));
-        load_tile(S1{}, kof(1));
-        __syncthreads();
-        // k-tile kt: register set kt & 1, LDS buffer kt & 1.  Prefetch kt + 2 into the set tile kt
-        // left (already in LDS), multiply kt while splitting kt + 1 into the other buffer (last
-        // read in k-tile kt - 1, before that tile's barrier).
-        auto step = [&](auto Bf, auto NB, int kt) {
-#if TTAMM_X_ABLATE != 3  // developer ablation 3: no k-loop traffic (MFMA + LDS reads only)
-            load_tile(Bf, kof(kt + 2));
-#endif
-            compute(Bf, NB, NB, kof(kt + 1));
+        if constexpr (!XDEEP) {
+            load_tile(S0{}, kof(0));
+            store_tile(S0{}, S0{}, kof(0));
             __syncthreads();
-        };
-        int kt = 0;
-        for (; kt + 1 < nk; kt += 2) {
-            step(S0{}, S1{}, kt);
-            step(S1{}, S0{}, kt + 1);
+            auto sstep = [&](auto Buf, auto NB, int kt) {
+#if TTAMM_X_ABLATE != 3
+                load_tile(S0{}, kof(kt + 1));
+#endif
+                compute(Buf, S0{}, NB, kof(kt + 1));
+#if TTAMM_X_ABLATE != 3
+                store_tile(S0{}, NB, kof(kt + 1));
+#endif
+                __syncthreads();
+            };
+            int kt = 0;
+            for (; kt + 1 < nk; kt += 2) {
+                sstep(S0{}, S1{}, kt);
+                sstep(S1{}, S0{}, kt + 1);
+            }
+            if (kt < nk) sstep(S0{}, S1{}, kt);
+        } else {
+            load_tile(S0{}, kof(0));
+            store_tile(S0{}, S0{}, kof(0));
+            load_tile(S1{}, kof(1));
+            __syncthreads();
+            // k-tile kt: register set kt & 1, LDS buffer kt & 1.  Prefetch kt + 2 into the set tile
+            // kt left (already in LDS), multiply kt while splitting kt + 1 into the other buffer
+            // (last read in k-tile kt - 1, before that tile's barrier).
+            auto step = [&](auto Bf, auto NB, int kt) {
+#if TTAMM_X_ABLATE != 3  // developer ablation 3: no k-loop traffic (MFMA + LDS reads only)
+                load_tile(Bf, kof(kt + 2));
+#endif
+                compute(Bf, NB, NB, kof(kt + 1));
+                __syncthreads();
+            };
+            int kt = 0;
+            for (; kt + 1 < nk; kt += 2) {
+                step(S0{}, S1{}, kt);
+                step(S1{}, S0{}, kt + 1);
+            }
+            if (kt < nk) step(S0{}, S1{}, kt);
         }
-        if (kt < nk) step(S0{}, S1{}, kt);
     };
     if (fast) mainloop(std::true_type{});
     else mainloop(std::false_type{});
@@ -1110,9 +1152,12 @@ int dispatch_epi_x(GemmBatch& b, hipStream_t s) {
         default: return fail(TTAMM_E_INVALID, "gemm: unknown epilogue");
     }
 }
-template <class CX>
+// three planes on 16-k tiles (fp32 towers), or one plane on 32-k tiles (bf16 towers: twice the
+// MFMAs per barrier, the same LDS footprint)
+template <int BM, int BN, int WM, int WN, bool AK, bool BK>
 int dispatch_x(GemmBatch& b, hipStream_t s) {
-    return b.p[0].bf16 ? dispatch_epi_x<CX, 1>(b, s) : dispatch_epi_x<CX, 3>(b, s);
+    return b.p[0].bf16 ? dispatch_epi_x<XCfg<BM, BN, WM, WN, AK, BK, 32>, 1>(b, s)
+                       : dispatch_epi_x<XCfg<BM, BN, WM, WN, AK, BK, 16>, 3>(b, s);
 }
 
 // Matrix-core path of the fp32 / bf16 GEMMs: the split-bf16 kernel (default), or with
@@ -1201,11 +1246,11 @@ int launch_gemm(GemmBatch& b, hipStream_t s) {
     }
     if (!exact_mfma()) {
         if (maxN > 96) {
-            if (bkn) return dispatch_x<XCfg<128, 192, 2, 2, false, true>>(b, s);
-            return dispatch_x<XCfg<128, 192, 2, 2, false, false>>(b, s);
+            if (bkn) return dispatch_x<128, 192, 2, 2, false, true>(b, s);
+            return dispatch_x<128, 192, 2, 2, false, false>(b, s);
         }
-        if (bkn) return dispatch_x<XCfg<128, 96, 4, 1, false, true>>(b, s);
-        return dispatch_x<XCfg<128, 96, 4, 1, false, false>>(b, s);
+        if (bkn) return dispatch_x<128, 96, 4, 1, false, true>(b, s);
+        return dispatch_x<128, 96, 4, 1, false, false>(b, s);
     }
     if (maxN > 96) {
         if (bkn) return dispatch_epi<Cfg<128, 192, 2, 2, false, true>>(b, s);
@@ -1221,6 +1266,8 @@ using WgradWide = Cfg<128, 192, 2, 2, true, true>;
 using WgradNarrow = Cfg<128, 96, 4, 1, true, true>;
 using WgradWideX = XCfg<128, 192, 2, 2, true, true>;
 using WgradNarrowX = XCfg<128, 96, 4, 1, true, true>;
+using WgradWideX32 = XCfg<128, 192, 2, 2, true, true, 32>;
+using WgradNarrowX32 = XCfg<128, 96, 4, 1, true, true, 32>;
 int wgrad_slots(bool wide, bool exact) {
     static int cached[2][2] = {{0, 0}, {0, 0}};
     if (cached[exact][wide]) return cached[exact][wide];
@@ -1295,8 +1342,8 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s) {
         if (g.count == 0) return TTAMM_OK;
         int rc;
         if (!exact)
-            rc = is_wide ? (bf ? launch_one_x<WgradWideX, EPI_STORE, 1>(g, s) : launch_one_x<WgradWideX, EPI_STORE, 3>(g, s))
-                         : (bf ? launch_one_x<WgradNarrowX, EPI_STORE, 1>(g, s)
+            rc = is_wide ? (bf ? launch_one_x<WgradWideX32, EPI_STORE, 1>(g, s) : launch_one_x<WgradWideX, EPI_STORE, 3>(g, s))
+                         : (bf ? launch_one_x<WgradNarrowX32, EPI_STORE, 1>(g, s)
                                : launch_one_x<WgradNarrowX, EPI_STORE, 3>(g, s));
         else
             rc = is_wide ? (bf ? launch_one<WgradWide, EPI_STORE, true>(g, s) : launch_one<WgradWide, EPI_STORE, false>(g, s))
