@@ -108,6 +108,10 @@ def _run(batches, g, ranks, W):
     # in-batch negatives: all-gather of the positives + reduce-scatter of dP (ttamm.h INBATCH phases)
     (2, Shape(N=2), True),
     (3, Shape(U=300, I=900, N=0, B=70), True),
+    # C4 widths (D = 128, MLP 40 -> 64 -> 128: the generic gate path), in-batch, 2 ranks
+    (2, Shape(U=200, I=900, F=40, H=64, D=128, B=48, N=0, hidden_dims=(64,)), True),
+    # C5 arithmetic (bf16 tower GEMMs, D = 64, H = 128) through the sharded phases
+    (2, Shape(U=200, I=900, F=37, H=128, D=64, B=40, N=3, hidden_dims=(128,), matmul_dtype="bf16"), False),
 ])
 def test_sharded_gradients_match_global_step(W, shape, in_batch):
     prob, batches, g, ranks = _setup(shape, W, lr=0.0, betas=(0.0, 0.999), steps=1, in_batch=in_batch)
