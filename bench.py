@@ -118,7 +118,8 @@ class Workload:
     """C2 data + model on one GPU, or rank `rank`'s C2-sized shard of an N x C2 model."""
 
     def __init__(self, c: dict, device, seed: int, world: int = 1, rank: int = 0, step_seed: int | None = None,
-                 deferred: bool = True, overlap: bool = True, in_batch: bool = False, table_math: str = "fast"):
+                 deferred: bool = True, overlap: bool = True, in_batch: bool = False, table_math: str = "fast",
+                 replay_slices: int = 64):
         import ttamm
         from ttamm.samplers import PositivesCSR
 
@@ -166,7 +167,7 @@ class Workload:
         kw = dict(negatives_per_positive=c["N"], positives=self.csr, user_features=self.user_features,
                   item_features=self.item_features, loss_weights={"mimic_user": 0.15, "mimic_item": 0.15},
                   max_batch=c["B"], deferred_adamw=deferred, overlap=overlap, in_batch_negatives=in_batch,
-                  table_adamw_math=table_math)
+                  table_adamw_math=table_math, replay_slices=replay_slices)
         if world == 1:
             self.engine = ttamm.FusedTrainStep(self.model, self.opts, seed=seed, **kw)
         else:
@@ -255,6 +256,8 @@ def main() -> None:
                     help="gloo stages the exchanges through host memory (several ranks on one GPU, tests only)")
     ap.add_argument("--eager-adamw", action="store_true",
                     help="sweep AdamW(g=0) over the whole mimic tables every step instead of the deferred exact replay")
+    ap.add_argument("--replay-slices", type=int, default=64,
+                    help="deferred table AdamW: every row is replayed at least once per this many steps")
     ap.add_argument("--exact-table-math", action="store_true",
                     help="IEEE sqrt / division for the g = 0 table AdamW updates (bit-identical to torch) "
                          "instead of v_sqrt / v_rcp")
@@ -293,7 +296,7 @@ def main() -> None:
         args.steps = max(1, math.ceil(c["U"] * c["pos_per_user"] / c["B"]))
     w = Workload(c, device, args.seed + rank, world=world, rank=rank, step_seed=args.seed,
                  deferred=not args.eager_adamw, overlap=not args.no_overlap, in_batch=in_batch,
-                 table_math="exact" if args.exact_table_math else "fast")
+                 table_math="exact" if args.exact_table_math else "fast", replay_slices=args.replay_slices)
     eng = w.engine
     for _ in range(args.warmup):
         u, p = w.batch()

@@ -414,6 +414,7 @@ struct RowUpdateArgs {
     int32_t dense_step;     // deferred mode (table.last_step): rows are updated in place and
                             // stamped current to this step
     const uint32_t* status; // step_poisoned(status): no write (ttamm.h TTAMM_STATUS_*)
+    int lanes_per_row;      // set by the launcher
 };
 int launch_row_update(const RowUpdateArgs& a, hipStream_t s);
 

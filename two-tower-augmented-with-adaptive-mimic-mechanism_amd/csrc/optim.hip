@@ -362,75 +362,90 @@ __global__ __launch_bounds__(64 * kRowWaves) void piece_sum_kernel(RowUpdateArgs
     }
 }
 
+// float4 views of table / gradient rows (dim % 4 == 0, 16-byte aligned rows: checked by the
+// launcher)
+__device__ __forceinline__ float4 ldf4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void stf4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float4 addf4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+
+// One unique row per `lanes_per_row` lanes (a power of two >= dim / 4, at most 64: two rows per
+// wave at D = 96 / 128), four consecutive elements per lane with 16-byte loads and stores.
 __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArgs A) {
     const int lane = threadIdx.x & 63;
-    const int64_t u = (int64_t)blockIdx.x * kRowWaves + (threadIdx.x >> 6);
+    const int lpr = A.lanes_per_row, rpw = 64 / lpr;
+    const int64_t u = ((int64_t)blockIdx.x * kRowWaves + (threadIdx.x >> 6)) * rpw + lane / lpr;
+    const int sub = lane % lpr;
     if (u >= A.n || u >= (int64_t)A.n_unique[0] || step_poisoned(A.status)) return;
     const int64_t k0 = A.seg_start[u], k1 = A.seg_start[u + 1];
     const int64_t key = A.keys[k0];
     const int D = A.dim;
     const bool mimic = A.mimic.weight != nullptr;
     const bool direct = k1 - k0 <= kPiece;
-    for (int d = lane; d < D; d += 64) {
+    auto each = [](float4& p, float4& m, float4& v, float4 g, auto&& f) {
+        f(p.x, m.x, v.x, g.x);
+        f(p.y, m.y, v.y, g.y);
+        f(p.z, m.z, v.z, g.z);
+        f(p.w, m.w, v.w, g.w);
+    };
+    for (int d = 4 * sub; d < D; d += 4 * lpr) {
         // the table rows first: they do not depend on the gradient sums below
         const int64_t o = key * D + d;
-        float ip = A.id.weight[o], im = A.id.exp_avg[o], iv = A.id.exp_avg_sq[o];
-        float mp = 0.f, mm = 0.f, mv = 0.f;
+        float4 ip = ldf4(A.id.weight + o), im = ldf4(A.id.exp_avg + o), iv = ldf4(A.id.exp_avg_sq + o);
+        float4 mp = make_float4(0.f, 0.f, 0.f, 0.f), mm = mp, mv = mp;
         if (mimic) {
-            mp = A.mimic.weight[o];
-            mm = A.mimic.exp_avg[o];
-            mv = A.mimic.exp_avg_sq[o];
+            mp = ldf4(A.mimic.weight + o);
+            mm = ldf4(A.mimic.exp_avg + o);
+            mv = ldf4(A.mimic.exp_avg_sq + o);
         }
-        float ge, ga = 0.f;
+        float4 ge, ga = make_float4(0.f, 0.f, 0.f, 0.f);
         if (direct) {  // the row's contributions in batch order
             const int64_t r0 = A.rows[k0];
-            ge = A.dE[r0 * A.ld_dE + d];
-            if (mimic) ga = dA_row(A, r0)[d];
+            ge = ldf4(A.dE + r0 * A.ld_dE + d);
+            if (mimic) ga = ldf4(dA_row(A, r0) + d);
             for (int64_t k = k0 + 1; k < k1; ++k) {
                 const int64_t r = A.rows[k];
-                ge += A.dE[r * A.ld_dE + d];
-                if (mimic) ga += dA_row(A, r)[d];
+                ge = addf4(ge, ldf4(A.dE + r * A.ld_dE + d));
+                if (mimic) ga = addf4(ga, ldf4(dA_row(A, r) + d));
             }
         } else {  // pieces (piece_sum_kernel), then the pieces in order
-            ge = A.piece_e[k0 * D + d];
-            ga = mimic ? A.piece_a[k0 * D + d] : 0.f;
+            ge = ldf4(A.piece_e + k0 * D + d);
+            if (mimic) ga = ldf4(A.piece_a + k0 * D + d);
             for (int64_t k = (k0 / kPiece + 1) * kPiece; k < k1; k += kPiece) {
-                ge += A.piece_e[k * D + d];
-                if (mimic) ga += A.piece_a[k * D + d];
+                ge = addf4(ge, ldf4(A.piece_e + k * D + d));
+                if (mimic) ga = addf4(ga, ldf4(A.piece_a + k * D + d));
             }
         }
         if (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM) {
-            sparse_adam_elem(ip, im, iv, ge, A.sp);
-            A.id.weight[o] = ip;
-            A.id.exp_avg[o] = im;
-            A.id.exp_avg_sq[o] = iv;
-        } else if (A.id.last_step) {  // deferred mode: the row was caught up before the forward
-            adam_elem(ip, im, iv, ge, A.ad);
-            A.id.weight[o] = ip;
-            A.id.exp_avg[o] = im;
-            A.id.exp_avg_sq[o] = iv;
+            each(ip, im, iv, ge, [&](float& p, float& m, float& v, float g) { sparse_adam_elem(p, m, v, g, A.sp); });
         } else {
-            adam_elem(ip, im, iv, ge, A.ad);
+            each(ip, im, iv, ge, [&](float& p, float& m, float& v, float g) { adam_elem(p, m, v, g, A.ad); });
+        }
+        if (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM || A.id.last_step) {
+            // SparseAdam, or deferred mode: the row was caught up before the forward
+            stf4(A.id.weight + o, ip);
+            stf4(A.id.exp_avg + o, im);
+            stf4(A.id.exp_avg_sq + o, iv);
+        } else {
             float* sd = A.side_id + u * 3 * D;
-            sd[d] = ip;
-            sd[D + d] = im;
-            sd[2 * D + d] = iv;
+            stf4(sd + d, ip);
+            stf4(sd + D + d, im);
+            stf4(sd + 2 * D + d, iv);
         }
         if (mimic) {
-            adam_elem(mp, mm, mv, ga, A.ad);
+            each(mp, mm, mv, ga, [&](float& p, float& m, float& v, float g) { adam_elem(p, m, v, g, A.ad); });
             if (A.mimic.last_step) {
-                A.mimic.weight[o] = mp;
-                A.mimic.exp_avg[o] = mm;
-                A.mimic.exp_avg_sq[o] = mv;
+                stf4(A.mimic.weight + o, mp);
+                stf4(A.mimic.exp_avg + o, mm);
+                stf4(A.mimic.exp_avg_sq + o, mv);
             } else {
                 float* sd = A.side_mimic + u * 3 * D;
-                sd[d] = mp;
-                sd[D + d] = mm;
-                sd[2 * D + d] = mv;
+                stf4(sd + d, mp);
+                stf4(sd + D + d, mm);
+                stf4(sd + 2 * D + d, mv);
             }
         }
     }
-    if (lane == 0) {
+    if (sub == 0) {
         if (A.id.optimizer != TTAMM_OPT_SPARSE_ADAM && A.id.last_step) A.id.last_step[key] = A.dense_step;
         if (mimic && A.mimic.last_step) A.mimic.last_step[key] = A.dense_step;
     }
@@ -741,12 +756,19 @@ int launch_block_exclusive_scan(const int32_t* in, int32_t* out, int64_t n, hipS
     return TTAMM_OK;
 }
 
-int launch_row_update(const RowUpdateArgs& a, hipStream_t s) {
-    if (a.n <= 0) return TTAMM_OK;
+int launch_row_update(const RowUpdateArgs& args, hipStream_t s) {
+    if (args.n <= 0) return TTAMM_OK;
+    RowUpdateArgs a = args;
+    TTAMM_REQUIRE(a.dim % 4 == 0 && a.ld_dE % 4 == 0 && (!a.mimic.weight || a.ld_dA % 4 == 0),
+                  "row update: dim and gradient leading dims must be multiples of 4");
+    a.lanes_per_row = 1;
+    while (a.lanes_per_row < a.dim / 4 && a.lanes_per_row < 64) a.lanes_per_row *= 2;
     hipLaunchKernelGGL(piece_sum_kernel, dim3((unsigned)ceil_div(ceil_div(a.n, kPiece), kRowWaves)),
                        dim3(64 * kRowWaves), 0, s, a);
     TTAMM_LAUNCH_CHECK();
-    hipLaunchKernelGGL(row_update_kernel, dim3((unsigned)ceil_div(a.n, kRowWaves)), dim3(64 * kRowWaves), 0, s, a);
+    const int64_t rows_per_block = (int64_t)kRowWaves * (64 / a.lanes_per_row);
+    hipLaunchKernelGGL(row_update_kernel, dim3((unsigned)ceil_div(a.n, rows_per_block)), dim3(64 * kRowWaves), 0, s,
+                       a);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }
