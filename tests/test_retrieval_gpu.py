@@ -39,7 +39,9 @@ def _oracle_topk(items, queries, k, blocked):
 
 
 @pytest.mark.parametrize("nq,ni,D,k", [(300, 5000, 96, 20), (65, 4097, 128, 80), (7, 70, 8, 192),
-                                        (130, 1000, 256, 1), (64, 10, 16, 20)])
+                                        (130, 1000, 256, 1), (64, 10, 16, 20),
+                                        # D % 8 != 0 (trainable: D % 4 == 0): zero-padded columns
+                                        (50, 700, 12, 10), (33, 500, 20, 7)])
 def test_topk_bit_exact_on_exact_scores(nq, ni, D, k):
     g = torch.Generator().manual_seed(nq * 7 + ni)
     items = torch.randint(-3, 4, (ni, D), generator=g).float()

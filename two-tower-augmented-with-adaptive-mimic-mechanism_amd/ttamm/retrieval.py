@@ -126,6 +126,12 @@ def retrieve_topk(queries: torch.Tensor, items: torch.Tensor, k: int, *,
         raise ValueError("ttamm retrieval: float32 embeddings required")
     if queries.dim() != 2 or items.dim() != 2 or queries.shape[1] != items.shape[1]:
         raise ValueError("ttamm retrieval: queries [nq, D] and items [ni, D] with the same D")
+    if queries.shape[1] % 8:
+        # the kernel takes D % 8 == 0: zero columns leave every inner product unchanged (any D
+        # trains, and FAISS IndexFlatIP takes any D)
+        D8 = (queries.shape[1] + 7) // 8 * 8
+        queries = torch.nn.functional.pad(queries, (0, D8 - queries.shape[1]))
+        items = torch.nn.functional.pad(items, (0, D8 - items.shape[1]))
     q = _pad_features(queries) if queries.numel() else queries
     x = _pad_features(items) if items.numel() else items
     nq, D = queries.shape
