@@ -13,8 +13,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from ttamm.sharded import (AllGather, AllReduce, AllToAll, ReduceScatter, RowOwnership, TorchComm, Wait, route_requests,
-                           run_loopback)
+from ttamm.sharded import (AllGather, AllReduce, AllToAll, ReduceScatter, RowOwnership, TorchComm, Wait, route_pairs,
+                           route_requests, run_loopback)
 
 
 def test_row_ownership():
@@ -144,3 +144,24 @@ def test_exchange_gloo_world2(case):
     ref = run_loopback([_exchange_program(W, r, case) for r in range(W)])
     for a, b in zip(outs, ref):
         assert torch.equal(a["fwd"], b["fwd"]) and torch.equal(a["to_owner"], b["to_owner"])
+
+
+@pytest.mark.parametrize("W", [1, 2, 3])
+def test_route_pairs_to_user_owners(W):
+    """The sharded epoch's pair routing: rank r ends up with exactly the pairs whose user it
+    owns, source rank by source rank, each source's pairs in their original order."""
+    streams = []
+    for r in range(W):
+        g = torch.Generator().manual_seed(40 + r)
+        u = torch.randint(0, 50, (17,), generator=g)
+        streams.append((u, u * 100 + torch.arange(17) + 10000 * r))
+
+    def prog(r):
+        got = yield from route_pairs(RowOwnership(W, r), *streams[r])
+        return got
+
+    outs = run_loopback([prog(r) for r in range(W)])
+    for r, (u, i) in enumerate(outs):
+        want_u = torch.cat([su[su % W == r] for su, _ in streams])
+        want_i = torch.cat([si[su % W == r] for su, si in streams])
+        assert torch.equal(u, want_u) and torch.equal(i, want_i)

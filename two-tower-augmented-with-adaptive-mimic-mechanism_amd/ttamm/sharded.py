@@ -325,17 +325,23 @@ class ShardedTrainStep(FusedTrainStep):
 
     def program(self, users: torch.Tensor, pos_items: torch.Tensor, neg_items: torch.Tensor | None = None, *,
                 keep_masks: Mapping[str, Sequence[torch.Tensor]] | None = None,
-                timing_events: Sequence[Any] | None = None) -> Program:
+                timing_events: Sequence[Any] | None = None, row_base: int | None = None,
+                global_batch: int | None = None) -> Program:
         """One step as an SPMD program (yields collective requests).  ``timing_events``
         (hipEvent_t handles, pairs as in ttamm.h) bracket the owner's item-table maintenance
-        and its item-tower first-layer GEMM."""
+        and its item-tower first-layer GEMM.  By default every rank holds B interactions and
+        rank r's are global positions [r B, (r + 1) B); ranks with different batch sizes pass
+        ``row_base`` (the sizes of the ranks before this one) and ``global_batch`` (the sum)."""
         if not self._bind_batch(users, pos_items, neg_items, keep_masks):
             raise ValueError("ttamm: empty batch in a sharded step (every rank must step)")
         a = self.args
         W, rank = self.own.world_size, self.own.rank
         B, N, D = users.numel(), self.num_neg, self.D
-        Bg = W * B
-        a.row_base = rank * B
+        Bg = W * B if global_batch is None else int(global_batch)
+        base = rank * B if row_base is None else int(row_base)
+        if self.in_batch and Bg != W * B:
+            raise ValueError("ttamm: in-batch negatives need the same batch size on every rank")
+        a.row_base = base
         a.global_batch = Bg
         ev = list(timing_events or []) + [None] * 6
         for i in range(6):
@@ -346,8 +352,8 @@ class ShardedTrainStep(FusedTrainStep):
         # ---- route the item requests [positives; negatives] to their owners -----------------
         req = torch.cat([pos_items.reshape(-1), negs])
         dev = req.device
-        keys = torch.cat([torch.arange(B, device=dev) + rank * B,
-                          torch.arange(B * N, device=dev) + (Bg + rank * B * N)])
+        keys = torch.cat([torch.arange(B, device=dev) + base,
+                          torch.arange(B * N, device=dev) + (Bg + base * N)])
         route = yield from route_requests(self.own, req, keys)
         n = route.rows.numel()
         self.item_rows_seen += n
@@ -421,3 +427,51 @@ class ShardedTrainStep(FusedTrainStep):
     def last_losses(self) -> dict[str, float]:
         """Global losses of the last step (the all-reduced shares)."""
         return super().last_losses()
+
+
+# ---------------------------------------------------------------------------------------
+# the sharded epoch (training.py:1475-1490 over W ranks)
+# ---------------------------------------------------------------------------------------
+def route_pairs(own: RowOwnership, users: torch.Tensor, items: torch.Tensor) -> Program:
+    """Program: send every (user, item) pair to its user's owner (the all-to-all of SURVEY §8 e
+    (a)).  Returns (users, items) this rank owns: the pairs from rank 0, then rank 1, ..., each
+    source's pairs in their order."""
+    W = own.world_size
+    owner = own.owner(users)
+    order = torch.argsort(owner, stable=True)
+    counts = torch.bincount(owner, minlength=W)
+    recv = yield AllToAll(counts, [1] * W, [1] * W)
+    packed = torch.stack([users[order], items[order]], dim=1)
+    got = yield AllToAll(packed, counts.tolist(), recv.tolist())
+    return got[:, 0].contiguous(), got[:, 1].contiguous()
+
+
+def epoch_program(engine: ShardedTrainStep, batches: Any) -> Program:
+    """One epoch as an SPMD program: each rank iterates over its own part of the interaction
+    stream (any users — e.g. a DeviceInteractionLoader over the rank's slice of the pairs, or a
+    DistributedSampler); each batch's pairs are routed to their users' owners and the W routed
+    batches form one global step (the reference step over their rank-major concatenation).
+    Every rank must yield the same number of batches.  Returns the epoch's mean loss
+    (training.py:829-833)."""
+    own = engine.own
+    W, rank = own.world_size, own.rank
+    for users, items in batches:
+        u, i = yield from route_pairs(own, users, items)
+        sizes = yield AllGather(torch.tensor([u.numel()], dtype=torch.long, device=u.device))
+        sizes = sizes.tolist()
+        if min(sizes) == 0:
+            raise ValueError("ttamm: a rank received no interactions for this step")
+        yield from engine.program(own.local(u), i, row_base=sum(sizes[:rank]), global_batch=sum(sizes))
+    return (yield from engine.finish_program())
+
+
+def train_one_epoch_sharded(engine: ShardedTrainStep, batches: Any, comm: Callable[[Program], Any] | None = None
+                            ) -> float:
+    """``train_one_epoch`` for one rank of a W-rank job: ``batches`` is this rank's part of the
+    epoch's interactions; ``engine`` its ShardedTrainStep (sized with ``max_batch`` >= the largest
+    routed batch).  Collective: every rank calls it with the same number of batches."""
+    comm = comm or engine.comm
+    if comm is None:
+        raise RuntimeError("ttamm: train_one_epoch_sharded needs comm= (e.g. TorchComm())")
+    runner = comm.run if hasattr(comm, "run") else comm
+    return runner(epoch_program(engine, batches))
