@@ -86,8 +86,8 @@ def test_topk_edge_cases():
     assert s.shape == (0, 5)
     with pytest.raises(ValueError, match="k must be"):
         retrieve_topk(q, torch.randn((10, 8)).cuda(), 193)
-    with pytest.raises(ValueError, match="multiple of 8"):
-        retrieve_topk(torch.randn((3, 12)).cuda(), torch.randn((10, 12)).cuda(), 5)
+    with pytest.raises(ValueError, match="same D"):
+        retrieve_topk(torch.randn((3, 12)).cuda(), torch.randn((10, 16)).cuda(), 5)
 
 
 def test_topk_c3_properties():
