@@ -119,7 +119,7 @@ class Workload:
 
     def __init__(self, c: dict, device, seed: int, world: int = 1, rank: int = 0, step_seed: int | None = None,
                  deferred: bool = True, overlap: bool = True, in_batch: bool = False, table_math: str = "fast",
-                 replay_slices: int = 64):
+                 replay_slices: int = 64, aux_cus: int = 0):
         import ttamm
         from ttamm.samplers import PositivesCSR
 
@@ -167,7 +167,7 @@ class Workload:
         kw = dict(negatives_per_positive=c["N"], positives=self.csr, user_features=self.user_features,
                   item_features=self.item_features, loss_weights={"mimic_user": 0.15, "mimic_item": 0.15},
                   max_batch=c["B"], deferred_adamw=deferred, overlap=overlap, in_batch_negatives=in_batch,
-                  table_adamw_math=table_math, replay_slices=replay_slices)
+                  table_adamw_math=table_math, replay_slices=replay_slices, aux_cus=aux_cus or None)
         if world == 1:
             self.engine = ttamm.FusedTrainStep(self.model, self.opts, seed=seed, **kw)
         else:
@@ -256,6 +256,8 @@ def main() -> None:
                     help="gloo stages the exchanges through host memory (several ranks on one GPU, tests only)")
     ap.add_argument("--eager-adamw", action="store_true",
                     help="sweep AdamW(g=0) over the whole mimic tables every step instead of the deferred exact replay")
+    ap.add_argument("--aux-cus", type=int, default=0,
+                    help="run the step's aux-stream prologue on this many CUs only (0 = all)")
     ap.add_argument("--replay-slices", type=int, default=64,
                     help="deferred table AdamW: every row is replayed at least once per this many steps")
     ap.add_argument("--exact-table-math", action="store_true",
@@ -296,7 +298,8 @@ def main() -> None:
         args.steps = max(1, math.ceil(c["U"] * c["pos_per_user"] / c["B"]))
     w = Workload(c, device, args.seed + rank, world=world, rank=rank, step_seed=args.seed,
                  deferred=not args.eager_adamw, overlap=not args.no_overlap, in_batch=in_batch,
-                 table_math="exact" if args.exact_table_math else "fast", replay_slices=args.replay_slices)
+                 table_math="exact" if args.exact_table_math else "fast", replay_slices=args.replay_slices,
+                 aux_cus=args.aux_cus)
     eng = w.engine
     for _ in range(args.warmup):
         u, p = w.batch()

@@ -324,6 +324,14 @@ int ttamm_epoch_batch(const int64_t* users, const int64_t* items, int64_t n, uin
                       int32_t shuffle, int64_t start, int64_t count, int64_t* out_users, int64_t* out_items,
                       void* stream);
 
+/* A HIP stream whose kernels run on `num_cus` compute units only, spread evenly over the device
+ * (every (CUs / num_cus)-th CU, so every XCD keeps some): a ttamm_step_args.aux_stream for the
+ * index-only prologue that overlaps the feature GEMMs without co-residing on every CU they use.
+ * num_cus <= 0 or >= the device's CUs gives an unrestricted stream.  Release with
+ * ttamm_stream_destroy. */
+int ttamm_stream_create_cu_limited(int32_t num_cus, void** stream);
+int ttamm_stream_destroy(void* stream);
+
 /* faiss.normalize_L2 on device rows, in place (training.py:670-672 on the item matrix and
  * :954-955 on the queries when the model's similarity is cosine): row r of the [n, dim] matrix
  * with leading dim ld is scaled by 1 / sqrt(sum of its squares); rows of norm 0 are left as

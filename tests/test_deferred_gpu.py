@@ -21,7 +21,8 @@ pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parents[1]
 
 
-def _engine(prob, *, deferred: bool, slices: int, sparse: bool = True, overlap: bool = True, math: str = "fast"):
+def _engine(prob, *, deferred: bool, slices: int, sparse: bool = True, overlap: bool = True, math: str = "fast",
+            aux_cus=None):
     from gpu_helpers import ttamm_model_from
 
     model = ttamm_model_from(prob)
@@ -35,7 +36,7 @@ def _engine(prob, *, deferred: bool, slices: int, sparse: bool = True, overlap: 
                                user_features=prob.user_features.cuda(), item_features=prob.item_features.cuda(),
                                loss_weights=LOSS_WEIGHTS, max_batch=prob.shape.B, seed=11,
                                deferred_adamw=deferred, replay_slices=slices, overlap=overlap,
-                               table_adamw_math=math)
+                               table_adamw_math=math, aux_cus=aux_cus)
     return model, opts, eng
 
 
@@ -49,8 +50,10 @@ def _state(model, opts):
     return out
 
 
-def _run(prob, steps, *, deferred, slices, sparse=True, flush_at=None, lr_change_at=None, overlap=True, math="fast"):
-    model, opts, eng = _engine(prob, deferred=deferred, slices=slices, sparse=sparse, overlap=overlap, math=math)
+def _run(prob, steps, *, deferred, slices, sparse=True, flush_at=None, lr_change_at=None, overlap=True, math="fast",
+         aux_cus=None):
+    model, opts, eng = _engine(prob, deferred=deferred, slices=slices, sparse=sparse, overlap=overlap, math=math,
+                               aux_cus=aux_cus)
     gen = torch.Generator().manual_seed(3)
     losses = []
     for k in range(steps):
@@ -88,9 +91,12 @@ def test_aux_stream_overlap_bitwise(deferred, sparse):
     prob = make_problem(Shape(), seed=5)
     one, l1 = _run(prob, 9, deferred=deferred, slices=3, sparse=sparse, overlap=False)
     two, l2 = _run(prob, 9, deferred=deferred, slices=3, sparse=sparse, overlap=True)
-    assert l1 == l2
+    # the aux stream restricted to 16 CUs (ttamm_stream_create_cu_limited)
+    three, l3 = _run(prob, 9, deferred=deferred, slices=3, sparse=sparse, overlap=True, aux_cus=16)
+    assert l1 == l2 == l3
     for k in one:
         assert torch.equal(one[k], two[k]), k
+        assert torch.equal(one[k], three[k]), k
 
 
 def test_deferred_c2_equals_eager():

@@ -2,6 +2,8 @@
 #include <cstdio>
 #include <cstring>
 
+#include <vector>
+
 #include "kernels.h"
 
 namespace ttamm {
@@ -85,6 +87,33 @@ TTAMM_API int ttamm_epoch_batch(const int64_t* users, const int64_t* items, int6
     g_last_error.clear();
     return launch_epoch_batch(users, items, n, seed, epoch, shuffle, start, count, out_users, out_items,
                               (hipStream_t)stream);
+}
+
+TTAMM_API int ttamm_stream_create_cu_limited(int32_t num_cus, void** stream) {
+    g_last_error.clear();
+    if (!stream) return fail(TTAMM_E_INVALID, "stream: null output pointer");
+    int dev = 0, cus = 0;
+    TTAMM_HIP(hipGetDevice(&dev));
+    TTAMM_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    hipStream_t s = nullptr;
+    if (num_cus <= 0 || num_cus >= cus) {
+        TTAMM_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    } else {
+        std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+        for (int i = 0; i < num_cus; ++i) {
+            const int cu = (int)((int64_t)i * cus / num_cus);
+            mask[(size_t)cu / 32] |= 1u << (cu % 32);
+        }
+        TTAMM_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+    }
+    *stream = s;
+    return TTAMM_OK;
+}
+
+TTAMM_API int ttamm_stream_destroy(void* stream) {
+    g_last_error.clear();
+    if (stream) TTAMM_HIP(hipStreamDestroy((hipStream_t)stream));
+    return TTAMM_OK;
 }
 
 TTAMM_API int ttamm_normalize_rows(float* rows, int64_t n, int32_t dim, int64_t ld, void* stream) {

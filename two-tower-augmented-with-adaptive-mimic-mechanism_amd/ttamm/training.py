@@ -124,6 +124,7 @@ class FusedTrainStep:
         replay_slices: int = 64,
         table_adamw_math: str = "fast",
         overlap: bool = True,
+        aux_cus: int | None = None,
         item_category_tensor: torch.Tensor | None = None,
         major_category_id: int | None = None,
         in_batch_negatives: bool = False,
@@ -320,8 +321,18 @@ class FusedTrainStep:
                 args.replay_slices = replay_slices
         # second HIP stream for the index-only prologue (row sort + deferred catch-up),
         # overlapping the feature MLP (ttamm.h ttamm_step_args.aux_stream)
-        self.aux_stream = torch.cuda.Stream(device=self.device) if overlap else None
-        args.aux_stream = self.aux_stream.cuda_stream if self.aux_stream is not None else None
+        # (aux_cus: restrict it to that many CUs spread over the device, ttamm_stream_create_cu_limited,
+        # so it shares only part of the chip with the GEMMs it overlaps; None = every CU)
+        self._aux_handle = None
+        if overlap and aux_cus:
+            h = ctypes.c_void_p()
+            _lib.check(self.lib.ttamm_stream_create_cu_limited(int(aux_cus), ctypes.byref(h)))
+            self._aux_handle = h.value
+            self.aux_stream = None
+            args.aux_stream = self._aux_handle
+        else:
+            self.aux_stream = torch.cuda.Stream(device=self.device) if overlap else None
+            args.aux_stream = self.aux_stream.cuda_stream if self.aux_stream is not None else None
         self._configure(args)
         self.ws_bytes = int(self.lib.ttamm_train_step_workspace_size(ctypes.byref(args)))
         # zeroed once: the row-grouping scratch at its head must start (and stays) zero
@@ -418,6 +429,16 @@ class FusedTrainStep:
             for i in range(_lib.MAX_LINEAR):
                 field[i] = masks[i].data_ptr() if i < len(masks) and masks[i] is not None else None
         return True
+
+    def __del__(self) -> None:
+        h = getattr(self, "_aux_handle", None)
+        if h:
+            try:
+                torch.cuda.synchronize(self.device)
+                self.lib.ttamm_stream_destroy(ctypes.c_void_p(h))
+            except Exception:  # interpreter shutdown
+                pass
+            self._aux_handle = None
 
     def flush(self) -> None:
         """Bring every row of the deferred dense-group tables current (enqueued, no sync).
