@@ -119,7 +119,7 @@ class Workload:
 
     def __init__(self, c: dict, device, seed: int, world: int = 1, rank: int = 0, step_seed: int | None = None,
                  deferred: bool = True, overlap: bool = True, in_batch: bool = False, table_math: str = "fast",
-                 replay_slices: int = 64, aux_cus: int = 0):
+                 replay_slices: int = 64, aux_cus: int = 0, sharded_single: bool = False):
         import ttamm
         from ttamm.samplers import PositivesCSR
 
@@ -168,8 +168,18 @@ class Workload:
                   item_features=self.item_features, loss_weights={"mimic_user": 0.15, "mimic_item": 0.15},
                   max_batch=c["B"], deferred_adamw=deferred, overlap=overlap, in_batch_negatives=in_batch,
                   table_adamw_math=table_math, replay_slices=replay_slices, aux_cus=aux_cus or None)
-        if world == 1:
+        if world == 1 and not sharded_single:
             self.engine = ttamm.FusedTrainStep(self.model, self.opts, seed=seed, **kw)
+        elif world == 1:  # developer: the row-sharded phases at W = 1 (their overhead, no exchange cost)
+            from ttamm.sharded import ShardedTrainStep, run_loopback
+
+            class _One:
+                @staticmethod
+                def run(program):
+                    return run_loopback([program])[0]
+
+            self.engine = ShardedTrainStep(self.model, self.opts, world_size=1, rank=0, num_items=Ig, comm=_One(),
+                                           seed=seed, **kw)
         else:
             from ttamm.sharded import ShardedTrainStep, TorchComm
 
@@ -256,6 +266,8 @@ def main() -> None:
                     help="gloo stages the exchanges through host memory (several ranks on one GPU, tests only)")
     ap.add_argument("--eager-adamw", action="store_true",
                     help="sweep AdamW(g=0) over the whole mimic tables every step instead of the deferred exact replay")
+    ap.add_argument("--sharded-single", action="store_true",
+                    help="developer: run the row-sharded step's phases at one GPU (W = 1, in-process exchange)")
     ap.add_argument("--aux-cus", type=int, default=0,
                     help="run the step's aux-stream prologue on this many CUs only (0 = all)")
     ap.add_argument("--replay-slices", type=int, default=64,
@@ -299,7 +311,7 @@ def main() -> None:
     w = Workload(c, device, args.seed + rank, world=world, rank=rank, step_seed=args.seed,
                  deferred=not args.eager_adamw, overlap=not args.no_overlap, in_batch=in_batch,
                  table_math="exact" if args.exact_table_math else "fast", replay_slices=args.replay_slices,
-                 aux_cus=args.aux_cus)
+                 aux_cus=args.aux_cus, sharded_single=args.sharded_single)
     eng = w.engine
     for _ in range(args.warmup):
         u, p = w.batch()
@@ -350,7 +362,7 @@ def main() -> None:
     # first feature layer, grouped launch: rows x F x H multiply-adds (algorithmic F, not the
     # MFMA's zero-padded K).  One process: user rows B + item rows B(1+N); sharded: the
     # owner's item rows only (the events bracket its ITEM_FWD launch).
-    if world == 1:
+    if world == 1 and not args.sharded_single:
         l1_rows = B + B * (1 + N)
     else:
         l1_rows = (getattr(eng, "item_rows_seen", 0) - rows0) / args.steps
