@@ -119,7 +119,8 @@ class Workload:
 
     def __init__(self, c: dict, device, seed: int, world: int = 1, rank: int = 0, step_seed: int | None = None,
                  deferred: bool = True, overlap: bool = True, in_batch: bool = False, table_math: str = "fast",
-                 replay_slices: int = 64, aux_cus: int = 0, sharded_single: bool = False):
+                 replay_slices: int = 64, aux_cus: int = 0, sharded_single: bool = False,
+                 group_towers: bool = True):
         import ttamm
         from ttamm.samplers import PositivesCSR
 
@@ -179,13 +180,13 @@ class Workload:
                     return run_loopback([program])[0]
 
             self.engine = ShardedTrainStep(self.model, self.opts, world_size=1, rank=0, num_items=Ig, comm=_One(),
-                                           seed=seed, **kw)
+                                           seed=seed, group_towers=group_towers, **kw)
         else:
             from ttamm.sharded import ShardedTrainStep, TorchComm
 
             # step_seed: the same on every rank (the Philox streams are keyed by global position)
             self.engine = ShardedTrainStep(self.model, self.opts, world_size=world, rank=rank, num_items=Ig,
-                                           comm=TorchComm(), seed=step_seed, **kw)
+                                           comm=TorchComm(), seed=step_seed, group_towers=group_towers, **kw)
 
     def batch(self):
         """The next batch of the on-device loader (epochs run back to back)."""
@@ -266,6 +267,9 @@ def main() -> None:
                     help="gloo stages the exchanges through host memory (several ranks on one GPU, tests only)")
     ap.add_argument("--eager-adamw", action="store_true",
                     help="sweep AdamW(g=0) over the whole mimic tables every step instead of the deferred exact replay")
+    ap.add_argument("--overlap-exchange", action="store_true",
+                    help="row-sharded step: overlap the (t | a) all-to-all with a separate user-tower forward "
+                         "instead of grouping the two towers' launches (ShardedTrainStep(group_towers=False))")
     ap.add_argument("--sharded-single", action="store_true",
                     help="developer: run the row-sharded step's phases at one GPU (W = 1, in-process exchange)")
     ap.add_argument("--aux-cus", type=int, default=0,
@@ -311,7 +315,8 @@ def main() -> None:
     w = Workload(c, device, args.seed + rank, world=world, rank=rank, step_seed=args.seed,
                  deferred=not args.eager_adamw, overlap=not args.no_overlap, in_batch=in_batch,
                  table_math="exact" if args.exact_table_math else "fast", replay_slices=args.replay_slices,
-                 aux_cus=args.aux_cus, sharded_single=args.sharded_single)
+                 aux_cus=args.aux_cus, sharded_single=args.sharded_single,
+                 group_towers=not args.overlap_exchange)
     eng = w.engine
     for _ in range(args.warmup):
         u, p = w.batch()
@@ -361,11 +366,11 @@ def main() -> None:
     value = interactions / elapsed
     # first feature layer, grouped launch: rows x F x H multiply-adds (algorithmic F, not the
     # MFMA's zero-padded K).  One process: user rows B + item rows B(1+N); sharded: the
-    # owner's item rows only (the events bracket its ITEM_FWD launch).
+    # owner's item rows (+ its B user rows when the two towers' forward is grouped).
     if world == 1 and not args.sharded_single:
         l1_rows = B + B * (1 + N)
     else:
-        l1_rows = (getattr(eng, "item_rows_seen", 0) - rows0) / args.steps
+        l1_rows = (getattr(eng, "item_rows_seen", 0) - rows0) / args.steps + (B if eng.group_towers else 0)
     l1_flops = 2.0 * l1_rows * F * H
     tflops = l1_flops / (gemm_ms * 1e-3) / 1e12
     bf16 = c.get("matmul", "fp32") == "bf16"

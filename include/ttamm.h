@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 14
+#define TTAMM_ABI_VERSION 15
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -81,6 +81,14 @@ extern "C" {
  * then USER adds the sampled negatives (if any) and the mimic terms. */
 #define TTAMM_PHASE_INBATCH_SRC 64
 #define TTAMM_PHASE_INBATCH 128
+/* Grouped variant (ShardedTrainStep(group_towers=True)): ITEM_FWD | USER_FWD in one call run the
+ * two towers' forward as one set of grouped launches; USER splits into
+ *   SCORE      requester: scores + losses; (dT | dA) of its item requests -> item_bwd_out
+ *              [all-to-all: (dT | dA) rows -> owners]
+ *   TOWERS_BWD both towers' backward (user rows + owned item rows) grouped, both tables' updates
+ * so each tower-wide kernel is launched once per step, as in the one-process step. */
+#define TTAMM_PHASE_SCORE 256
+#define TTAMM_PHASE_TOWERS_BWD 512
 
 /* Device-side status word bits (written by kernels, read by the host at epoch end).  Once a
  * bit is set, every later step on that status word is skipped on the device (no parameter,
@@ -261,6 +269,12 @@ typedef struct ttamm_step_args {
      *                 each g = 0 update term within a few ulp of torch's, a third of the VALU work.
      * Deferred and eager stay bit-identical to each other in either mode. */
     int32_t table_g0_math;
+    /* ---- sharded requester: where each request's row sits in the exchange buffers ------------
+     * NULL: item_fwd_in / item_bwd_out row r is request r ([positives; negatives]).  Otherwise
+     * request r's (t | a) is read from, and its (dT | dA) written to, row item_slot[r] — the
+     * owner-grouped order ttamm_route_rows produced, so the all-to-alls move the buffers as
+     * they are (no permutation pass). */
+    const int64_t* item_slot;
 } ttamm_step_args;
 
 #define TTAMM_G0_EXACT 0
@@ -323,6 +337,22 @@ int ttamm_to_bf16(const float* src, int64_t rows, int32_t cols, int64_t ld_src, 
 int ttamm_epoch_batch(const int64_t* users, const int64_t* items, int64_t n, uint64_t seed, int64_t epoch,
                       int32_t shuffle, int64_t start, int64_t count, int64_t* out_users, int64_t* out_items,
                       void* stream);
+
+/* Owner routing of a row-sharded step (rows owned by rank id % world): the n = n0 + n1 ids
+ * id0[0..n0) then id1[0..n1) are grouped by owner, stably (positions in order within an owner).
+ * For every position j:  slot[j]              = its index in the grouped order,
+ *                         packed[slot[j]][0]  = id_j / world (the owner's local row),
+ *                         packed[slot[j]][1]  = payload ? payload[j] : (j < n0 ? key0 + j
+ *                                                                     : key1 + (j - n0));
+ * counts[o] = ids owned by rank o (int64[world]).  The requests of ShardedTrainStep (ids =
+ * [positives; negatives], keys = global request positions) and the pair routing of its epoch
+ * driver (ids = users, payload = items) — replaces a host argsort / bincount
+ * (torch.argsort(owner, stable=True), ttamm/sharded.py).  1 <= world <= 1024; every id >= 0;
+ * scratch: device memory of ttamm_route_scratch_bytes(n0 + n1, world) bytes. */
+size_t ttamm_route_scratch_bytes(int64_t n, int32_t world);
+int ttamm_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_t n1, const int64_t* payload,
+                     int64_t key0, int64_t key1, int32_t world, int64_t* packed, int64_t* slot, int64_t* counts,
+                     void* scratch, size_t scratch_bytes, void* stream);
 
 /* A HIP stream whose kernels run on `num_cus` compute units only, spread evenly over the device
  * (every (CUs / num_cus)-th CU, so every XCD keeps some): a ttamm_step_args.aux_stream for the

@@ -1,7 +1,9 @@
 """The sharded step's exchange layer on CPU: row ownership, request routing and the three
 all-to-alls + all-reduce of ttamm/sharded.py, served by torch.distributed (gloo, world_size 2,
 two processes) and by the in-process loopback — both must route every row to the right place
-in the right order, including a rank that receives no requests."""
+in the right order, including a rank that receives no requests.  The owner grouping itself is
+ttamm_route_rows on the GPU (tests/test_route_gpu.py); here its CPU restatement
+(oracle/route.py) stands in for it."""
 
 from __future__ import annotations
 
@@ -13,6 +15,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from oracle.route import route_rows  # the CPU router (ttamm_route_rows runs on the GPU)
 from ttamm.sharded import (AllGather, AllReduce, AllToAll, ReduceScatter, RowOwnership, TorchComm, Wait, route_pairs,
                            route_requests, run_loopback)
 
@@ -50,18 +53,21 @@ def _requests(W: int, rank: int, case: str):
 def _exchange_program(W: int, rank: int, case: str):
     own = RowOwnership(W, rank)
     items, keys = _requests(W, rank, case)
-    route = yield from route_requests(own, items, keys)
+    B, N = 5, 3
+    route = yield from route_requests(own, route_rows, items[:B], items[B:], rank * B, W * B + rank * B * N)
+    assert torch.equal(route.slot.sort().values, torch.arange(items.numel()))
     assert torch.equal(own.owner(own.global_ids(route.rows)), torch.full_like(route.rows, rank))
     # owner: payload rows (global id, request key, 7) for what it was asked
     payload = torch.stack([own.global_ids(route.rows).double(), route.keys.double(),
                            torch.full((route.rows.numel(),), 7.0, dtype=torch.float64)], dim=1)
     h = yield AllToAll(payload, route.recv_counts, route.send_counts, async_op=True)
     back = yield Wait(h)
-    fwd = torch.empty_like(back)
-    fwd.index_copy_(0, route.order, back)
-    # requester: gradient rows keyed by its request positions
+    fwd = back[route.slot]  # request j's row sits at slot[j] of the owner-grouped buffer
+    # requester: gradient rows keyed by its request positions, written at their slots
     grads = torch.stack([keys.double() * 3.0, items.double()], dim=1)
-    to_owner = yield AllToAll(grads.index_select(0, route.order), route.send_counts, route.recv_counts)
+    grouped = torch.empty_like(grads)
+    grouped[route.slot] = grads
+    to_owner = yield AllToAll(grouped, route.send_counts, route.recv_counts)
     acc = torch.tensor([float(rank + 1), 2.0 ** -rank])
     yield AllReduce(acc)
     # in-batch negatives: all-gather [2, 3] rows, reduce-scatter [2W, 3] rows
@@ -157,11 +163,12 @@ def test_route_pairs_to_user_owners(W):
         streams.append((u, u * 100 + torch.arange(17) + 10000 * r))
 
     def prog(r):
-        got = yield from route_pairs(RowOwnership(W, r), *streams[r])
+        got = yield from route_pairs(RowOwnership(W, r), route_rows, *streams[r])
         return got
 
     outs = run_loopback([prog(r) for r in range(W)])
-    for r, (u, i) in enumerate(outs):
+    for r, (u, i, sizes) in enumerate(outs):
         want_u = torch.cat([su[su % W == r] for su, _ in streams])
         want_i = torch.cat([si[su % W == r] for su, si in streams])
-        assert torch.equal(u, want_u) and torch.equal(i, want_i)
+        assert torch.equal(u, want_u // W) and torch.equal(i, want_i)  # local user rows
+        assert sizes == [sum(int((su % W == d).sum()) for su, _ in streams) for d in range(W)]

@@ -47,7 +47,7 @@ def _opts(model, lr, betas):
     return opts
 
 
-def _setup(shape: Shape, W: int, *, lr: float, betas, steps: int, in_batch: bool = False):
+def _setup(shape: Shape, W: int, *, lr: float, betas, steps: int, in_batch: bool = False, group: bool = True):
     prob = make_problem(shape, seed=77)
     state = prob.model.state_dict()
     gen = torch.Generator().manual_seed(5)
@@ -79,7 +79,7 @@ def _setup(shape: Shape, W: int, *, lr: float, betas, steps: int, in_batch: bool
         eng = ShardedTrainStep(m, opts, world_size=W, rank=r, num_items=shape.I, negatives_per_positive=shape.N,
                                positives=local_pos, user_features=own.shard(prob.user_features).cuda(),
                                item_features=own.shard(prob.item_features).cuda(), loss_weights=LOSS_WEIGHTS,
-                               max_batch=shape.B, seed=SEED, in_batch_negatives=in_batch)
+                               max_batch=shape.B, seed=SEED, in_batch_negatives=in_batch, group_towers=group)
         ranks.append((own, m, opts, eng))
     return prob, batches, (gm, gopts, geng), ranks
 
@@ -101,20 +101,26 @@ def _run(batches, g, ranks, W):
     return glosses, rlosses, negs, gavg, ravg
 
 
-@pytest.mark.parametrize("W,shape,in_batch", [
-    (2, Shape(), False),
-    (3, Shape(hidden_dims=(16, 12)), False),
-    (2, Shape(dropout=0.0, gate_hidden=20), False),
+@pytest.mark.parametrize("W,shape,in_batch,group", [
+    (2, Shape(), False, True),
+    # the overlapped schedule (ITEM_FWD, exchange under USER_FWD, USER, ITEM_BWD)
+    (2, Shape(), False, False),
+    (3, Shape(N=2), True, False),
+    # one rank: no exchange at all (the requester's buffers are the owner's)
+    (1, Shape(), False, True),
+    (1, Shape(N=2), True, True),
+    (3, Shape(hidden_dims=(16, 12)), False, True),
+    (2, Shape(dropout=0.0, gate_hidden=20), False, True),
     # in-batch negatives: all-gather of the positives + reduce-scatter of dP (ttamm.h INBATCH phases)
-    (2, Shape(N=2), True),
-    (3, Shape(U=300, I=900, N=0, B=70), True),
+    (2, Shape(N=2), True, True),
+    (3, Shape(U=300, I=900, N=0, B=70), True, True),
     # C4 widths (D = 128, MLP 40 -> 64 -> 128: the generic gate path), in-batch, 2 ranks
-    (2, Shape(U=200, I=900, F=40, H=64, D=128, B=48, N=0, hidden_dims=(64,)), True),
+    (2, Shape(U=200, I=900, F=40, H=64, D=128, B=48, N=0, hidden_dims=(64,)), True, True),
     # C5 arithmetic (bf16 tower GEMMs, D = 64, H = 128) through the sharded phases
-    (2, Shape(U=200, I=900, F=37, H=128, D=64, B=40, N=3, hidden_dims=(128,), matmul_dtype="bf16"), False),
+    (2, Shape(U=200, I=900, F=37, H=128, D=64, B=40, N=3, hidden_dims=(128,), matmul_dtype="bf16"), False, True),
 ])
-def test_sharded_gradients_match_global_step(W, shape, in_batch):
-    prob, batches, g, ranks = _setup(shape, W, lr=0.0, betas=(0.0, 0.999), steps=1, in_batch=in_batch)
+def test_sharded_gradients_match_global_step(W, shape, in_batch, group):
+    prob, batches, g, ranks = _setup(shape, W, lr=0.0, betas=(0.0, 0.999), steps=1, in_batch=in_batch, group=group)
     glosses, rlosses, negs, gavg, ravg = _run(batches, g, ranks, W)
     B, N = shape.B, shape.N
     gneg, rneg = negs[0]
@@ -136,10 +142,11 @@ def test_sharded_gradients_match_global_step(W, shape, in_batch):
             assert rel_err(st["exp_avg"], want) <= 1e-5, (own.rank, name)
 
 
+@pytest.mark.parametrize("group", [True, False], ids=["grouped", "overlapped"])
 @pytest.mark.parametrize("in_batch", [False, True], ids=["sampled", "in-batch"])
-def test_sharded_three_steps_match_global_step(in_batch):
+def test_sharded_three_steps_match_global_step(in_batch, group):
     W, shape = 2, Shape()
-    prob, batches, g, ranks = _setup(shape, W, lr=1e-3, betas=(0.9, 0.999), steps=3, in_batch=in_batch)
+    prob, batches, g, ranks = _setup(shape, W, lr=1e-3, betas=(0.9, 0.999), steps=3, in_batch=in_batch, group=group)
     glosses, rlosses, _, _, _ = _run(batches, g, ranks, W)
     for s in range(3):
         assert abs(rlosses[s][0]["total"] - glosses[s]["total"]) <= 1e-5 * abs(glosses[s]["total"])

@@ -83,6 +83,10 @@ int launch_gemm(GemmBatch& batch, hipStream_t s);
 
 // on-device epoch order of the interaction pairs (data.hip)
 int epoch_half_bits(int64_t n);
+size_t route_scratch_bytes(int64_t n, int world);
+int launch_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_t n1, const int64_t* payload,
+                      int64_t key0, int64_t key1, int world, int64_t* packed, int64_t* slot, int64_t* counts,
+                      void* scratch, size_t scratch_bytes, hipStream_t s);
 void epoch_round_keys(uint64_t seed, int64_t epoch, uint32_t keys[4]);
 int launch_epoch_batch(const int64_t* users, const int64_t* items, int64_t n, uint64_t seed, int64_t epoch,
                        int shuffle, int64_t start, int64_t count, int64_t* out_users, int64_t* out_items,
@@ -181,9 +185,10 @@ struct StageArgs {
     uint32_t* status;
 };
 int launch_stage_rows(const StageArgs& a, hipStream_t s);
-// out = x (+ y) over [n, dim] rows (y may be null): an augmented row t + a (adaptive_mimic.py:88-95)
+// out = x (+ y) over [n, dim] rows (y may be null): an augmented row t + a (adaptive_mimic.py:88-95);
+// with xrow, out row r reads row xrow[r] of x and y
 int launch_add_rows(const float* x, int64_t ldx, const float* y, int64_t ldy, int64_t n, int dim, float* out,
-                    int64_t ldo, hipStream_t s);
+                    int64_t ldo, hipStream_t s, const int64_t* xrow = nullptr);
 
 // Status bits that stop every later step (ttamm.h TTAMM_STATUS_*).
 constexpr uint32_t kStatusPoison = TTAMM_STATUS_SAMPLER_EXHAUSTED | TTAMM_STATUS_INDEX_OUT_OF_RANGE;
@@ -222,6 +227,7 @@ struct ScoreArgs {
     float* dA_item;   // (mimic) [B, ld_dti] positives only, or all B(1+N) rows when dA_all
     int dA_all;
     int64_t ld_dti;
+    const int64_t* item_slot;  // or null: item request r's rows (t_item .. dA_item) are at item_slot[r]
     float* partials;  // [blocks, 3]
     int blocks;
     float inv_numel;  // 1 / logits in the BCE mean: Bg (1 + N), or Bg (Bg + N) in-batch

@@ -1,0 +1,165 @@
+// Owner routing of a row-sharded step: group n ids by owner rank (id % world), stably, and
+// emit each position's slot in that order plus the (local row, key) rows the owners receive.
+// It replaces the host-side torch.argsort(owner, stable=True) / bincount / gathers of the
+// sharded step (ttamm/sharded.py route_requests, route_pairs) with three small launches:
+//   count    one block per 2048 positions: per-owner counts in LDS           -> blk[b][o]
+//   scan     one block: counts[o], then blk[b][o] := first slot of (b, o)   (owner-major,
+//            block-minor: the stable order)
+//   scatter  one block per 2048 positions, 256 at a time in position order: a position's rank
+//            among the equal-owner positions of its wave comes from ballots over the owner's
+//            bits, the waves before it from per-wave counts in LDS.
+// Integer-only, so the result is exactly the stable sort (oracle: tests/test_route_gpu.py).
+#include "kernels.h"
+
+namespace ttamm {
+
+namespace {
+
+constexpr int kRouteThreads = 256;
+constexpr int kRouteRounds = 8;
+constexpr int kRouteSpan = kRouteThreads * kRouteRounds;  // positions per block
+constexpr int kRouteWaves = kRouteThreads / 64;
+
+struct RouteIn {
+    const int64_t* id0;
+    int64_t n0;
+    const int64_t* id1;
+    int64_t n;  // n0 + n1
+    const int64_t* payload;
+    int64_t key0, key1;
+    uint64_t world;
+};
+
+__device__ __forceinline__ uint64_t id_at(const RouteIn& a, int64_t j) {
+    return (uint64_t)(j < a.n0 ? a.id0[j] : a.id1[j - a.n0]);
+}
+
+__global__ __launch_bounds__(kRouteThreads) void route_count_kernel(RouteIn a, int32_t* __restrict__ blk) {
+    extern __shared__ int32_t hist[];
+    const int W = (int)a.world;
+    for (int o = threadIdx.x; o < W; o += kRouteThreads) hist[o] = 0;
+    __syncthreads();
+    const int64_t lo = (int64_t)blockIdx.x * kRouteSpan;
+    for (int r = 0; r < kRouteRounds; ++r) {
+        const int64_t j = lo + r * kRouteThreads + threadIdx.x;
+        if (j < a.n) atomicAdd(&hist[id_at(a, j) % a.world], 1);
+    }
+    __syncthreads();
+    for (int o = threadIdx.x; o < W; o += kRouteThreads) blk[(int64_t)blockIdx.x * W + o] = hist[o];
+}
+
+__global__ __launch_bounds__(kRouteThreads) void route_scan_kernel(int32_t* __restrict__ blk, int nb, int W,
+                                                                   int64_t* __restrict__ counts) {
+    extern __shared__ int64_t tot[];
+    for (int o = threadIdx.x; o < W; o += kRouteThreads) {
+        int64_t t = 0;
+        for (int b = 0; b < nb; ++b) t += blk[(int64_t)b * W + o];
+        tot[o] = t;
+        counts[o] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // exclusive scan over owners (W <= 1024)
+        int64_t run = 0;
+        for (int o = 0; o < W; ++o) {
+            const int64_t t = tot[o];
+            tot[o] = run;
+            run += t;
+        }
+    }
+    __syncthreads();
+    for (int o = threadIdx.x; o < W; o += kRouteThreads) {
+        int64_t run = tot[o];
+        for (int b = 0; b < nb; ++b) {
+            const int64_t x = blk[(int64_t)b * W + o];
+            blk[(int64_t)b * W + o] = (int32_t)run;  // slots < n < 2^31 (checked by the launcher)
+            run += x;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(RouteIn a, const int32_t* __restrict__ blk,
+                                                                      int owner_bits, int64_t* __restrict__ packed,
+                                                                      int64_t* __restrict__ slot) {
+    extern __shared__ int32_t lds[];
+    const int W = (int)a.world;
+    int32_t* off = lds;       // [W] next slot of each owner in this block
+    int32_t* wc = lds + W;    // [kRouteWaves][W] this round's per-wave counts
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int o = threadIdx.x; o < W; o += kRouteThreads) off[o] = blk[(int64_t)blockIdx.x * W + o];
+    const int64_t lo = (int64_t)blockIdx.x * kRouteSpan;
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (int r = 0; r < kRouteRounds; ++r) {
+        for (int i = threadIdx.x; i < kRouteWaves * W; i += kRouteThreads) wc[i] = 0;
+        __syncthreads();
+        const int64_t j = lo + r * kRouteThreads + threadIdx.x;
+        const bool valid = j < a.n;
+        uint64_t id = 0;
+        int o = 0;
+        if (valid) {
+            id = id_at(a, j);
+            o = (int)(id % a.world);
+        }
+        uint64_t m = __ballot(valid);  // lanes with the same owner as this one
+        for (int k = 0; k < owner_bits; ++k) {
+            const bool bit = (o >> k) & 1;
+            const uint64_t bal = __ballot(valid && bit);
+            m &= bit ? bal : ~bal;
+        }
+        const int rank = __popcll(m & below);
+        if (valid && rank == 0) wc[w * W + o] = __popcll(m);
+        __syncthreads();
+        if (valid) {
+            int32_t s = off[o] + rank;
+            for (int q = 0; q < w; ++q) s += wc[q * W + o];
+            slot[j] = s;
+            packed[2 * (int64_t)s] = (int64_t)(id / a.world);
+            packed[2 * (int64_t)s + 1] = a.payload ? a.payload[j] : (j < a.n0 ? a.key0 + j : a.key1 + (j - a.n0));
+        }
+        __syncthreads();
+        for (int oo = threadIdx.x; oo < W; oo += kRouteThreads) {
+            int32_t t = 0;
+            for (int q = 0; q < kRouteWaves; ++q) t += wc[q * W + oo];
+            off[oo] += t;
+        }
+        // the next round's zeroing of wc is ordered after these reads by its own barrier below
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+size_t route_scratch_bytes(int64_t n, int world) {
+    const int64_t nb = n > 0 ? ceil_div(n, kRouteSpan) : 0;
+    return (size_t)(nb * (world > 0 ? world : 0)) * sizeof(int32_t);
+}
+
+int launch_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_t n1, const int64_t* payload,
+                      int64_t key0, int64_t key1, int world, int64_t* packed, int64_t* slot, int64_t* counts,
+                      void* scratch, size_t scratch_bytes, hipStream_t s) {
+    TTAMM_REQUIRE(world >= 1 && world <= 1024, "route: world must be in [1, 1024]");
+    TTAMM_REQUIRE(n0 >= 0 && n1 >= 0 && n0 + n1 < (int64_t(1) << 31), "route: bad sizes");
+    TTAMM_REQUIRE(counts != nullptr, "route: counts missing");
+    const int64_t n = n0 + n1;
+    if (n == 0) {
+        TTAMM_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * world, s));
+        return TTAMM_OK;
+    }
+    TTAMM_REQUIRE((n0 == 0 || id0) && (n1 == 0 || id1) && packed && slot, "route: null pointer");
+    TTAMM_REQUIRE(scratch && scratch_bytes >= route_scratch_bytes(n, world), "route: scratch too small");
+    RouteIn a{id0, n0, id1, n, payload, key0, key1, (uint64_t)world};
+    const int nb = (int)ceil_div(n, kRouteSpan);
+    int bits = 0;
+    while ((1 << bits) < world) ++bits;
+    int32_t* blk = static_cast<int32_t*>(scratch);
+    hipLaunchKernelGGL(route_count_kernel, dim3(nb), dim3(kRouteThreads), sizeof(int32_t) * world, s, a, blk);
+    TTAMM_LAUNCH_CHECK();
+    hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(kRouteThreads), sizeof(int64_t) * world, s, blk, nb, world,
+                       counts);
+    TTAMM_LAUNCH_CHECK();
+    hipLaunchKernelGGL(route_scatter_kernel, dim3(nb), dim3(kRouteThreads),
+                       sizeof(int32_t) * world * (1 + kRouteWaves), s, a, blk, bits, packed, slot);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+}  // namespace ttamm

@@ -171,6 +171,7 @@ constexpr int kScoreWaves = 4;
 constexpr int kMaxDChunks = 8;  // D <= 512
 constexpr int kMaxNeg = 64;
 
+// r: the row in the item buffers (item_slot already applied)
 __device__ __forceinline__ float item_aug_at(const ScoreArgs& A, int64_t r, int d) {
     if (A.item_aug) return A.item_aug[r * A.ld_item + d];
     const float t = A.t_item[r * A.ld_item + d];
@@ -188,6 +189,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
     const bool ib = A.ib_du != nullptr;
     float bce = 0.f, mse_u = 0.f, mse_i = 0.f;
     if (b < B) {
+        const int64_t pb = A.item_slot ? A.item_slot[b] : b;  // the positive's item row
         const int nch = (D + 63) / 64;
         float u[kMaxDChunks], p[kMaxDChunks], du[kMaxDChunks];
         float dot = 0.f;
@@ -197,7 +199,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
             const int d = c * 64 + lane;
             if (c < nch && d < D) {
                 u[c] = A.user_aug[b * D + d];
-                p[c] = item_aug_at(A, b, d);
+                p[c] = item_aug_at(A, pb, d);
                 dot += u[c] * p[c];
             }
         }
@@ -215,12 +217,12 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
             dpos[c] = 0.f;
             if (c < nch && d < D) {
                 dpos[c] = ib ? A.ib_dp[b * A.ib_ld + d] : dsp * u[c];
-                A.dT_item[b * ldi + d] = dpos[c];
+                A.dT_item[pb * ldi + d] = dpos[c];
                 du[c] = ib ? A.ib_du[b * D + d] : dsp * p[c];
             }
         }
         for (int j = 0; j < N; ++j) {
-            const int64_t nr = B + b * N + j;
+            const int64_t nr = A.item_slot ? A.item_slot[B + b * N + j] : B + b * N + j;
             float nv[kMaxDChunks];
             float dn = 0.f;
 #pragma unroll
@@ -253,13 +255,13 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
             if (c < nch && d < D) {
                 A.dT_user[b * D + d] = du[c];
                 if (A.mimic) {
-                    const float au = A.a_user[b * D + d], tp = A.t_item[b * A.ld_item + d];
-                    const float ap = A.a_item[b * A.ld_item + d], tu = A.t_user[b * D + d];
+                    const float au = A.a_user[b * D + d], tp = A.t_item[pb * A.ld_item + d];
+                    const float ap = A.a_item[pb * A.ld_item + d], tu = A.t_user[b * D + d];
                     const float xu = au - tp, xi = ap - tu;
                     mse_u += xu * xu;
                     mse_i += xi * xi;
                     A.dA_user[b * D + d] = du[c] + norm * xu * A.lambda_u;
-                    A.dA_item[b * ldi + d] = dpos[c] + norm * xi * A.lambda_i;
+                    A.dA_item[pb * ldi + d] = dpos[c] + norm * xi * A.lambda_i;
                 }
             }
         }
@@ -445,21 +447,24 @@ namespace ttamm {
 namespace {
 // out = x (+ y), row-wise over [n, dim]
 __global__ void add_rows_kernel(const float* __restrict__ x, int64_t ldx, const float* __restrict__ y, int64_t ldy,
-                                int64_t n, int dim, float* __restrict__ out, int64_t ldo) {
+                                int64_t n, int dim, float* __restrict__ out, int64_t ldo,
+                                const int64_t* __restrict__ xrow) {
     const int64_t total = n * dim;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = i / dim;
         const int c = (int)(i - r * dim);
-        const float v = x[r * ldx + c];
-        out[r * ldo + c] = y ? v + y[r * ldy + c] : v;
+        const int64_t q = xrow ? xrow[r] : r;
+        const float v = x[q * ldx + c];
+        out[r * ldo + c] = y ? v + y[q * ldy + c] : v;
     }
 }
 }  // namespace
 
 int launch_add_rows(const float* x, int64_t ldx, const float* y, int64_t ldy, int64_t n, int dim, float* out,
-                    int64_t ldo, hipStream_t s) {
+                    int64_t ldo, hipStream_t s, const int64_t* xrow) {
     if (n <= 0) return TTAMM_OK;
-    hipLaunchKernelGGL(add_rows_kernel, dim3(grid_for(n * dim)), dim3(256), 0, s, x, ldx, y, ldy, n, dim, out, ldo);
+    hipLaunchKernelGGL(add_rows_kernel, dim3(grid_for(n * dim)), dim3(256), 0, s, x, ldx, y, ldy, n, dim, out, ldo,
+                       xrow);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

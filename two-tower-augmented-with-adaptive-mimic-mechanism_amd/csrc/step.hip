@@ -1092,7 +1092,9 @@ int validate_step(const ttamm_step_args& A) {
                   "row_base / global_batch out of range");
     if (!sharded(A)) return TTAMM_OK;
     const int ph = A.phase;
-    TTAMM_REQUIRE((ph & ~255) == 0, "unknown phase bits");
+    TTAMM_REQUIRE((ph & ~1023) == 0, "unknown phase bits");
+    TTAMM_REQUIRE(!((ph & TTAMM_PHASE_USER) && (ph & (TTAMM_PHASE_SCORE | TTAMM_PHASE_TOWERS_BWD))),
+                  "USER and SCORE / TOWERS_BWD are alternatives");
     TTAMM_REQUIRE(A.in_batch || (ph & (TTAMM_PHASE_INBATCH_SRC | TTAMM_PHASE_INBATCH)) == 0,
                   "INBATCH phases need in_batch");
     TTAMM_REQUIRE(A.item_rows_capacity >= 0 && A.n_item_rows >= 0 && A.n_item_rows <= A.item_rows_capacity,
@@ -1102,9 +1104,12 @@ int validate_step(const ttamm_step_args& A) {
     if ((ph & (TTAMM_PHASE_ITEM_FWD | TTAMM_PHASE_ITEM_BWD)) && A.n_item_rows > 0)
         TTAMM_REQUIRE(A.item_rows && A.item_row_keys, "item_rows / item_row_keys missing");
     if (ph & TTAMM_PHASE_ITEM_FWD) TTAMM_REQUIRE(A.item_fwd_out || A.n_item_rows == 0, "item_fwd_out missing");
-    if (ph & TTAMM_PHASE_USER) TTAMM_REQUIRE(A.item_fwd_in && A.item_bwd_out, "item_fwd_in / item_bwd_out missing");
-    if (ph & TTAMM_PHASE_ITEM_BWD) TTAMM_REQUIRE(A.item_bwd_in || A.n_item_rows == 0, "item_bwd_in missing");
-    if (ph & (TTAMM_PHASE_USER | TTAMM_PHASE_ITEM_BWD | TTAMM_PHASE_DENSE))
+    if (ph & (TTAMM_PHASE_USER | TTAMM_PHASE_SCORE))
+        TTAMM_REQUIRE(A.item_fwd_in && A.item_bwd_out, "item_fwd_in / item_bwd_out missing");
+    if (ph & (TTAMM_PHASE_ITEM_BWD | TTAMM_PHASE_TOWERS_BWD))
+        TTAMM_REQUIRE(A.item_bwd_in || A.n_item_rows == 0, "item_bwd_in missing");
+    if (ph & (TTAMM_PHASE_USER | TTAMM_PHASE_SCORE | TTAMM_PHASE_ITEM_BWD | TTAMM_PHASE_TOWERS_BWD |
+              TTAMM_PHASE_DENSE))
         TTAMM_REQUIRE(A.dense_grads != nullptr, "dense_grads missing");
     return TTAMM_OK;
 }
@@ -1215,14 +1220,17 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     } else {
         const ttamm_tower* Ti[2] = {&A.item, nullptr};
         TowerWs* Wi[2] = {&I, nullptr};
-        if (ph & TTAMM_PHASE_ITEM_FWD) {
+        const int both = TTAMM_PHASE_ITEM_FWD | TTAMM_PHASE_USER_FWD;
+        if ((ph & both) == both && I.R > 0) {  // grouped: both towers' launches at once
+            if ((rc = prepare_forward(T, W, 2, A.b, D, mimic, df, s, aux, A.timing_events + 2))) return rc;
+        } else if (ph & TTAMM_PHASE_ITEM_FWD) {
             if (I.R > 0) {
                 if ((rc = prepare_forward(Ti, Wi, 1, A.b, D, mimic, df, s, aux, A.timing_events + 2))) return rc;
             } else if ((rc = tower_prepare(A.item, I, mimic, df, s))) {
                 return rc;
             }
         }
-        if (ph & TTAMM_PHASE_USER_FWD)
+        if ((ph & TTAMM_PHASE_USER_FWD) && !((ph & both) == both && I.R > 0))
             if ((rc = prepare_forward(T, W, 1, A.b, D, mimic, df, s, aux, nullptr))) return rc;
     }
     // ---- in-batch negatives: S = U P^T, its BCE, dU and dP ------------------------------------
@@ -1230,7 +1238,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     if (ws.ib_on && shard && (ph & TTAMM_PHASE_INBATCH_SRC)) {
         TTAMM_REQUIRE(A.item_fwd_in && A.inbatch_local, "INBATCH_SRC needs item_fwd_in and inbatch_local");
         if ((rc = launch_add_rows(A.item_fwd_in, 2 * D, mimic ? A.item_fwd_in + D : nullptr, 2 * D, B, D,
-                                  A.inbatch_local, D, s)))
+                                  A.inbatch_local, D, s, A.item_slot)))
             return rc;
     }
     if (ws.ib_on && (ph & (shard ? TTAMM_PHASE_INBATCH : TTAMM_PHASE_USER))) {
@@ -1260,7 +1268,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         if (ev[0] && ev[1]) TTAMM_HIP(hipEventRecord((hipEvent_t)ev[1], s));
     }
     // ---- score + loss (fwd + bwd seeds), user-side backward ---------------------------------
-    if (ph & TTAMM_PHASE_USER) {
+    if (ph & (TTAMM_PHASE_USER | TTAMM_PHASE_SCORE)) {
         ScoreArgs sa;
         std::memset(&sa, 0, sizeof(sa));
         sa.B = B;
@@ -1284,6 +1292,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
             sa.dA_item = mimic ? A.item_bwd_out + D : nullptr;
             sa.dA_all = 1;
             sa.ld_dti = 2 * D;
+            sa.item_slot = A.item_slot;
         } else {
             sa.item_aug = I.aug;
             sa.t_item = I.t;
@@ -1333,8 +1342,21 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
             if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, s, aux))) return rc;
             return dense_update(T, W, ad, A.status, s);
         }
-        if ((rc = tower_backward(T, W, D, s, 1))) return rc;
-        if ((rc = table_updates(T, W, 1, D, mimic, sp, ad, df, nullptr, s, aux))) return rc;
+        if (ph & TTAMM_PHASE_USER) {
+            if ((rc = tower_backward(T, W, D, s, 1))) return rc;
+            if ((rc = table_updates(T, W, 1, D, mimic, sp, ad, df, nullptr, s, aux))) return rc;
+        }
+    }
+    // ---- grouped: both towers' backward and table updates ------------------------------------
+    if (ph & TTAMM_PHASE_TOWERS_BWD) {
+        if (I.R > 0) {
+            if ((rc = tower_backward(T, W, D, s, 2))) return rc;
+        } else {
+            if ((rc = tower_backward(T, W, D, s, 1))) return rc;
+            const size_t n = tower_grad_floats(A.item);
+            if (n) TTAMM_HIP(hipMemsetAsync(I.gw[0] ? I.gw[0] : I.ggw[0], 0, n * sizeof(float), s));
+        }
+        if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, s, aux))) return rc;
     }
     // ---- item-side backward on the owner ------------------------------------------------------
     if (ph & TTAMM_PHASE_ITEM_BWD) {

@@ -157,12 +157,13 @@ class StepArgs(ctypes.Structure):
         ("inbatch_dp_all", c_vp),
         ("inbatch_dp", c_vp),
         ("table_g0_math", c_i32),
+        ("item_slot", c_vp),
     ]
 
 
-ABI_VERSION = 14
+ABI_VERSION = 15  # ttamm.h TTAMM_ABI_VERSION
 G0_EXACT = 0  # ttamm.h TTAMM_G0_EXACT
-G0_FAST = 1  # ttamm.h TTAMM_G0_FAST  # ttamm.h TTAMM_ABI_VERSION
+G0_FAST = 1  # ttamm.h TTAMM_G0_FAST
 
 # ttamm.h TTAMM_PHASE_*
 PHASE_ALL = 0
@@ -174,6 +175,8 @@ PHASE_ITEM_BWD = 16
 PHASE_DENSE = 32
 PHASE_INBATCH_SRC = 64
 PHASE_INBATCH = 128
+PHASE_SCORE = 256
+PHASE_TOWERS_BWD = 512
 
 
 # Symbol table: name -> (restype, argtypes).  tests/ check every one is exported and that this
@@ -190,6 +193,9 @@ SIGNATURES = {
     "ttamm_to_bf16": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i64, c_vp, c_i64, c_vp]),
     "ttamm_stream_create_cu_limited": (ctypes.c_int, [c_i32, ctypes.POINTER(c_vp)]),
     "ttamm_stream_destroy": (ctypes.c_int, [c_vp]),
+    "ttamm_route_scratch_bytes": (ctypes.c_size_t, [c_i64, c_i32]),
+    "ttamm_route_rows": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp,
+                                        ctypes.c_size_t, c_vp]),
     "ttamm_epoch_batch": (ctypes.c_int, [c_vp, c_vp, c_i64, ctypes.c_uint64, c_i64, c_i32, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "ttamm_candidate_topk": (
         ctypes.c_int,

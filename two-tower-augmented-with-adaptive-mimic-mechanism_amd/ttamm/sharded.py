@@ -37,6 +37,7 @@ The step is written as an SPMD program that yields a request at each collective.
 from __future__ import annotations
 
 import ctypes
+import functools
 from dataclasses import dataclass
 from typing import Any, Callable, Generator, Mapping, Sequence
 
@@ -89,6 +90,7 @@ class AllToAll:
     send_splits: list[int]
     recv_splits: list[int]
     async_op: bool = False
+    out: torch.Tensor | None = None  # receive buffer (sum(recv_splits) rows); None = a new tensor
 
 
 @dataclass
@@ -142,8 +144,10 @@ class TorchComm:
             out = send.new_empty((sum(req.recv_splits),) + tuple(send.shape[1:]))
             if self.staged:
                 dist.all_to_all_single(out, send, req.recv_splits, req.send_splits, group=self.group)
-                out = out.to(dev)
+                out = out.to(dev) if req.out is None else req.out.copy_(out)
                 return (None, out) if req.async_op else out
+            if req.out is not None:
+                out = req.out
             work = dist.all_to_all_single(out, send, req.recv_splits, req.send_splits,
                                           group=self.group, async_op=req.async_op)
             return (work, out) if req.async_op else out
@@ -222,6 +226,8 @@ def run_loopback(programs: Sequence[Program]) -> list[Any]:
                 got = torch.cat([chunks[s][d] for s in range(W)])
                 if got.shape[0] != sum(reqs[d].recv_splits):
                     raise RuntimeError("loopback: recv splits do not match the senders")
+                if reqs[d].out is not None:
+                    got = reqs[d].out.copy_(got)
                 results[d] = ("done", got) if reqs[d].async_op else got
         elif kind is Wait:
             for r in range(W):
@@ -253,25 +259,51 @@ def run_loopback(programs: Sequence[Program]) -> list[Any]:
 # ---------------------------------------------------------------------------------------
 @dataclass
 class Route:
-    order: torch.Tensor  # request positions grouped by owner rank (stable)
+    slot: torch.Tensor  # request position -> its row in the owner-grouped exchange buffers
     send_counts: list[int]  # requests to each owner
     recv_counts: list[int]  # requests from each requester
     rows: torch.Tensor  # owner side: local rows requested [n_recv]
     keys: torch.Tensor  # owner side: global request positions [n_recv]
 
 
-def route_requests(own: RowOwnership, items: torch.Tensor, keys: torch.Tensor) -> Program:
-    """Program: send (local row, key) of every requested item to its owner.  Returns a Route."""
+def device_route(lib: Any, world: int, id0: torch.Tensor, id1: torch.Tensor | None = None,
+                 payload: torch.Tensor | None = None, key0: int = 0, key1: int = 0,
+                 counts_out: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """ttamm_route_rows: ids [id0; id1] grouped by owner (id % world), stably.  Returns (packed
+    [n, 2] = (id // world, payload or key) in the grouped order, slot [n], counts [world])."""
+    dev = id0.device
+    n0 = id0.numel()
+    n1 = id1.numel() if id1 is not None else 0
+    n = n0 + n1
+    packed = torch.empty((n, 2), dtype=torch.long, device=dev)
+    slot = torch.empty(n, dtype=torch.long, device=dev)
+    counts = counts_out if counts_out is not None else torch.empty(world, dtype=torch.long, device=dev)
+    scratch = torch.empty(max(1, int(lib.ttamm_route_scratch_bytes(n, world))), dtype=torch.uint8, device=dev)
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None and t.numel() else None  # noqa: E731
+    _lib.check(lib.ttamm_route_rows(ptr(id0), n0, ptr(id1), n1, ptr(payload), key0, key1, world, ptr(packed),
+                                    ptr(slot), ctypes.c_void_p(counts.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
+                                    scratch.numel(), _lib.stream_handle(dev)))
+    return packed, slot, counts
+
+
+Router = Callable[..., "tuple[torch.Tensor, torch.Tensor, torch.Tensor]"]  # device_route minus lib
+
+
+def route_requests(own: RowOwnership, router: Router, pos: torch.Tensor, negs: torch.Tensor, key0: int,
+                   key1: int) -> Program:
+    """Program: send (local row, key) of every requested item ([pos; negs], keys key0 + j for
+    positives, key1 + j for negatives) to its owner.  Returns a Route.  One host sync (the
+    counts, which size the variable all-to-all); none at world size 1."""
     W = own.world_size
-    owner = own.owner(items)
-    order = torch.argsort(owner, stable=True)
-    counts = torch.bincount(owner, minlength=W)
-    recv = yield AllToAll(counts, [1] * W, [1] * W)
-    send_counts = counts.tolist()
-    recv_counts = recv.tolist()
-    packed = torch.stack([own.local(items)[order], keys[order]], dim=1)
-    got = yield AllToAll(packed, send_counts, recv_counts)
-    return Route(order, send_counts, recv_counts, got[:, 0].contiguous(), got[:, 1].contiguous())
+    n = pos.numel() + negs.numel()
+    cnt = torch.empty(2 * W, dtype=torch.long, device=pos.device)
+    packed, slot, _ = router(W, pos, negs, None, key0, key1, counts_out=cnt[:W])
+    if W == 1:
+        return Route(slot, [n], [n], packed[:, 0].contiguous(), packed[:, 1].contiguous())
+    yield AllToAll(cnt[:W], [1] * W, [1] * W, out=cnt[W:])
+    c = cnt.tolist()
+    got = yield AllToAll(packed, c[:W], c[W:])
+    return Route(slot, c[:W], c[W:], got[:, 0].contiguous(), got[:, 1].contiguous())
 
 
 # ---------------------------------------------------------------------------------------
@@ -288,11 +320,17 @@ class ShardedTrainStep(FusedTrainStep):
     """
 
     def __init__(self, model, optimizers, *, world_size: int, rank: int, num_items: int,
-                 comm: Callable[[Program], Any] | None = None, **kw: Any) -> None:
+                 comm: Callable[[Program], Any] | None = None, group_towers: bool = True, **kw: Any) -> None:
         self.own = RowOwnership(world_size, rank)
         self.comm = comm
+        # True: both towers' forward in one set of grouped launches, then the (t | a) exchange;
+        # False: the item forward, the exchange overlapping the user forward, then the rest
+        # (backward: score, exchange, then both towers' backward grouped / the user backward
+        # first).  The grouped schedule launches each tower-wide kernel once per step.
+        self.group_towers = bool(group_towers)
         self.item_rows_seen = 0  # item-tower rows this owner ran (bench roofline)
         super().__init__(model, optimizers, num_items=num_items, **kw)
+        self.router: Router = functools.partial(device_route, self.lib)
 
     def _configure(self, args: _lib.StepArgs) -> None:
         W = self.own.world_size
@@ -350,11 +388,7 @@ class ShardedTrainStep(FusedTrainStep):
         negs = neg_items.reshape(-1) if neg_items is not None else self.neg_buffer[: B * N]
         self._phase(_lib.PHASE_SAMPLE)
         # ---- route the item requests [positives; negatives] to their owners -----------------
-        req = torch.cat([pos_items.reshape(-1), negs])
-        dev = req.device
-        keys = torch.cat([torch.arange(B, device=dev) + base,
-                          torch.arange(B * N, device=dev) + (Bg + base * N)])
-        route = yield from route_requests(self.own, req, keys)
+        route = yield from route_requests(self.own, self.router, pos_items.reshape(-1), negs, base, Bg + base * N)
         n = route.rows.numel()
         self.item_rows_seen += n
         if n > self.capacity:
@@ -362,18 +396,26 @@ class ShardedTrainStep(FusedTrainStep):
         a.item_rows = route.rows.data_ptr()
         a.item_row_keys = route.keys.data_ptr()
         a.n_item_rows = n
+        a.item_slot = route.slot.data_ptr()  # exchange buffers stay in owner-grouped order
         a.item_fwd_out = self.fwd_out.data_ptr()
-        a.timing_events[2], a.timing_events[3] = ev[2], ev[3]
-        self._phase(_lib.PHASE_ITEM_FWD)
-        a.timing_events[2] = a.timing_events[3] = None
-        # ---- (t | a) back to the requesters, user tower meanwhile ----------------------------
-        h = yield AllToAll(self.fwd_out[:n], route.recv_counts, route.send_counts, async_op=True)
-        self._phase(_lib.PHASE_USER_FWD)
-        back = yield Wait(h)
         R = B * (1 + N)
-        fwd_in = self.fwd_in[:R]
-        fwd_in.index_copy_(0, route.order, back)
-        a.item_fwd_in = fwd_in.data_ptr()
+        a.timing_events[2], a.timing_events[3] = ev[2], ev[3]
+        if W == 1:  # no exchange: the requester's buffers are the owner's
+            self._phase(_lib.PHASE_ITEM_FWD | _lib.PHASE_USER_FWD if self.group_towers else _lib.PHASE_ITEM_FWD)
+            if not self.group_towers:
+                self._phase(_lib.PHASE_USER_FWD)
+            back = self.fwd_out[:n]
+        elif self.group_towers:
+            self._phase(_lib.PHASE_ITEM_FWD | _lib.PHASE_USER_FWD)
+            back = yield AllToAll(self.fwd_out[:n], route.recv_counts, route.send_counts, out=self.fwd_in[:R])
+        else:  # (t | a) back to the requesters, the user tower meanwhile
+            self._phase(_lib.PHASE_ITEM_FWD)
+            h = yield AllToAll(self.fwd_out[:n], route.recv_counts, route.send_counts, async_op=True,
+                               out=self.fwd_in[:R])
+            self._phase(_lib.PHASE_USER_FWD)
+            back = yield Wait(h)
+        a.timing_events[2] = a.timing_events[3] = None
+        a.item_fwd_in = back.data_ptr()
         a.item_bwd_out = self.bwd_out.data_ptr()
         ib = ()
         if self.in_batch:
@@ -389,19 +431,22 @@ class ShardedTrainStep(FusedTrainStep):
             dp = yield ReduceScatter(self.ib_dp_all[: W * B])
             a.inbatch_dp = dp.data_ptr()
             ib = (gathered, dp)
-        self._phase(_lib.PHASE_USER)
-        # ---- (dT | dA) to the owners -----------------------------------------------------------
-        bwd_in = yield AllToAll(self.bwd_out[:R].index_select(0, route.order), route.send_counts,
-                                route.recv_counts)
+        # ---- scores; (dT | dA) to the owners; backward -------------------------------------------
+        self._phase(_lib.PHASE_SCORE if self.group_towers else _lib.PHASE_USER)
+        if W == 1:
+            bwd_in = self.bwd_out[:R]
+        else:
+            bwd_in = yield AllToAll(self.bwd_out[:R], route.send_counts, route.recv_counts)
         a.item_bwd_in = bwd_in.data_ptr()
         a.timing_events[0], a.timing_events[1] = ev[0], ev[1]
-        self._phase(_lib.PHASE_ITEM_BWD)
+        self._phase(_lib.PHASE_TOWERS_BWD if self.group_towers else _lib.PHASE_ITEM_BWD)
         a.timing_events[0] = a.timing_events[1] = None
-        yield AllReduce(self.arena)
+        if W > 1:
+            yield AllReduce(self.arena)
         self._phase(_lib.PHASE_DENSE)
         self.steps_done += 1
         # keep the step's device buffers alive until the stream has consumed them
-        self._live = (route, back, bwd_in, req, keys) + ib
+        self._live = (route, back, bwd_in) + ib
 
     def step(self, users, pos_items, neg_items=None, *, keep_masks=None, timing_events=None) -> None:
         if self.comm is None:
@@ -432,18 +477,21 @@ class ShardedTrainStep(FusedTrainStep):
 # ---------------------------------------------------------------------------------------
 # the sharded epoch (training.py:1475-1490 over W ranks)
 # ---------------------------------------------------------------------------------------
-def route_pairs(own: RowOwnership, users: torch.Tensor, items: torch.Tensor) -> Program:
+def route_pairs(own: RowOwnership, router: Router, users: torch.Tensor, items: torch.Tensor) -> Program:
     """Program: send every (user, item) pair to its user's owner (the all-to-all of SURVEY §8 e
-    (a)).  Returns (users, items) this rank owns: the pairs from rank 0, then rank 1, ..., each
-    source's pairs in their order."""
+    (a)).  Returns (local users, items, sizes): the pairs this rank owns — from rank 0, then
+    rank 1, ..., each source's pairs in their order — and every rank's routed batch size.  The
+    W x W count matrix is all-gathered once (one host sync) and gives the splits and sizes."""
     W = own.world_size
-    owner = own.owner(users)
-    order = torch.argsort(owner, stable=True)
-    counts = torch.bincount(owner, minlength=W)
-    recv = yield AllToAll(counts, [1] * W, [1] * W)
-    packed = torch.stack([users[order], items[order]], dim=1)
-    got = yield AllToAll(packed, counts.tolist(), recv.tolist())
-    return got[:, 0].contiguous(), got[:, 1].contiguous()
+    packed, _, counts = router(W, users, None, items)
+    if W == 1:
+        return packed[:, 0].contiguous(), packed[:, 1].contiguous(), [users.numel()]
+    m = yield AllGather(counts)
+    m = m.reshape(W, W).tolist()  # m[src][dst]
+    rank = own.rank
+    got = yield AllToAll(packed, m[rank], [m[src][rank] for src in range(W)])
+    sizes = [sum(m[src][dst] for src in range(W)) for dst in range(W)]
+    return got[:, 0].contiguous(), got[:, 1].contiguous(), sizes
 
 
 def epoch_program(engine: ShardedTrainStep, batches: Any) -> Program:
@@ -454,14 +502,12 @@ def epoch_program(engine: ShardedTrainStep, batches: Any) -> Program:
     Every rank must yield the same number of batches.  Returns the epoch's mean loss
     (training.py:829-833)."""
     own = engine.own
-    W, rank = own.world_size, own.rank
+    rank = own.rank
     for users, items in batches:
-        u, i = yield from route_pairs(own, users, items)
-        sizes = yield AllGather(torch.tensor([u.numel()], dtype=torch.long, device=u.device))
-        sizes = sizes.tolist()
+        u, i, sizes = yield from route_pairs(own, engine.router, users, items)
         if min(sizes) == 0:
             raise ValueError("ttamm: a rank received no interactions for this step")
-        yield from engine.program(own.local(u), i, row_base=sum(sizes[:rank]), global_batch=sum(sizes))
+        yield from engine.program(u, i, row_base=sum(sizes[:rank]), global_batch=sum(sizes))
     return (yield from engine.finish_program())
 
 
