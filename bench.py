@@ -424,12 +424,19 @@ def main() -> None:
         ib_tf = ib_flops / (ib_ms * 1e-3) / 1e12
         kernels.append({
             "bound": "mfma",
-            "kernel": f"inbatch_kernel (S = U P^T [{B} x {Bg}] + BCE + dU + dP, fp32 MFMA 32x32x2) + ib_reduce",
+            "kernel": f"inbatch_x_kernel (S = U P^T [{B} x {Bg}] + BCE + dU + dP, fp32 as split-bf16: "
+                      f"6 x v_mfma_f32_32x32x16_bf16 per product) + ib_reduce"
+                      if not exact_mfma else
+                      f"inbatch_kernel (S = U P^T [{B} x {Bg}] + BCE + dU + dP, fp32 MFMA 32x32x2) + ib_reduce",
             "achieved": round(ib_tf, 2), "peak": MFMA_FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ib_tf / MFMA_FP32_PEAK_TFLOPS, 4),
             "traffic": (traffic or {}).get("inbatch_bytes_per_launch"),
             "algorithmic_flops_per_launch": ib_flops, "avg_launch_ms": round(ib_ms, 4),
         })
+        if not exact_mfma:  # S is formed twice (user and item roles): 8 B Bg D executed flops
+            ceil = MFMA_BF16_PEAK_TFLOPS / 6.0 * 6.0 / 8.0
+            kernels[-1]["kernel_ceiling_tflops"] = round(ceil, 1)
+            kernels[-1]["frac_of_kernel_ceiling"] = round(ib_tf / ceil, 4)
     roof = max(kernels, key=lambda k: k["avg_launch_ms"])
     neg_desc = (f"in-batch negatives (all {B * world} positives of the global batch)"
                 + (f" + {N} sampled" if N else "")) if in_batch else f"N={N} sampled negatives"

@@ -2,7 +2,7 @@
 // oracle/cpu_reference.py train_step(in_batch=True) — not reference behaviour, which scores
 // sampled negatives only, training.py:770-798):
 //
-//   S  = U P^T              [B, Bc]  users x every positive of the (global) batch, fp32 MFMA
+//   S  = U P^T              [B, Bc]  users x every positive of the (global) batch, fp32-accurate MFMA
 //   dS = (sigmoid(S) - Y) / T        Y(b, j) = (j == row_base + b), T = logits in the BCE mean
 //   dU = dS P   [B, D]               dP = dS^T U   [Bc, D]        + the BCE sum of S
 //
@@ -13,8 +13,11 @@
 // operand streams through LDS in 64-row tiles (double buffered).  Per tile a wave computes its
 // 32 x 64 score block (v_mfma_f32_32x32x2_f32, K = D), turns it into dS in registers, parks dS in
 // its LDS slice and multiplies it back against the same LDS tile (K = 64).  Blocks write
-// partial rows to slabs that ib_reduce_kernel sums in split order (deterministic).
+// partial rows to slabs that ib_reduce_kernel sums in split order (deterministic).  This fp32-MFMA
+// kernel runs with TTAMM_FP32_MFMA=exact; the default is the split-bf16 inbatch_x_kernel below.
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 #include "kernels.h"
 
@@ -182,6 +185,242 @@ __global__ __launch_bounds__(256) void inbatch_kernel(InBatchArgs A) {
     }
 }
 
+// ---- split-bf16 variant (default) ---------------------------------------------------------------
+// The same roles, splits and slabs, on v_mfma_f32_32x32x16_bf16: every fp32 operand x is split
+// into bf16 planes hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid) (RNE, exact
+// differences) and a product is formed by six MFMAs (hh, hm, mh, hl, lh, mm; the dropped terms
+// are below 2^-24 relative), as in gemm.hip's split kernel: fp32-accurate at 6/16 of the fp32
+// MFMA's cycles.
+//   Product 1 (per wave, per 64-column tile): S^T[c][u] = C_tile[c][:] . R[u][:]  — the tile as
+//     the A operand (row reads), the wave's 32 rows as the B operand (register fragments).  S^T
+//     lands with the row u on the lane and the tile column c in registers.
+//   dS^T = (sigmoid(S^T) - Y) / T in registers.
+//   Product 2: dR[u][:] += sum_c dS^T[c][u] . C_tile[c][:] — dS^T is the A operand straight from
+//     its accumulator registers (a 32x32x16 MFMA summing over the accumulator's row index takes
+//     it with no lane movement; k order 16s + 8(j>>2) + 4h + (j&3)), the tile the B operand read
+//     column-wise with ds_read_b64_tr_b16 in that k order.
+// The tile's three planes share one LDS image that serves both the row reads (ds_read_b128) and
+// the transposed reads: 256-B rows (128 bf16, columns past D zero and never multiplied) with the
+// 16-B chunks XOR-permuted by the row, conflict-free for both.  Single LDS buffer, the next tile
+// in flight in registers; two blocks per CU.
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4e_t __attribute__((ext_vector_type(4)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x8_t __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+
+constexpr int kIbxRowBytes = 256;                  // LDS image row: 128 bf16
+constexpr int kIbxPlane = kIbTile * kIbxRowBytes;  // one plane of a 64-row tile
+
+__device__ __forceinline__ int ibx_off(int row, int ch) {  // byte offset of 16-B chunk ch of row
+    return row * kIbxRowBytes + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
+}
+// x -> hi, mid, lo (4 bf16 each)
+__device__ __forceinline__ void ibx_split(float4 v, uint2 out[3]) {
+    const f32x4e_t x = {v.x, v.y, v.z, v.w};
+    const bf16x4_t h = __builtin_convertvector(x, bf16x4_t);
+    const f32x4e_t r = x - __builtin_convertvector(h, f32x4e_t);
+    const bf16x4_t m = __builtin_convertvector(r, bf16x4_t);
+    const f32x4e_t r2 = r - __builtin_convertvector(m, f32x4e_t);
+    out[0] = __builtin_bit_cast(uint2, h);
+    out[1] = __builtin_bit_cast(uint2, m);
+    out[2] = __builtin_bit_cast(uint2, __builtin_convertvector(r2, bf16x4_t));
+}
+__device__ __forceinline__ bf16x8_t ibx_cat(uint2 a, uint2 b) {
+    return __builtin_bit_cast(bf16x8_t, uint4{a.x, a.y, b.x, b.y});
+}
+__device__ __forceinline__ f32x16 ibx_mfma6(const bf16x8_t a[3], const bf16x8_t b[3], f32x16 c) {
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
+    return c;
+}
+
+// MINB blocks per CU
+template <int DP, int MINB>
+__global__ __launch_bounds__(256, MINB) void inbatch_x_kernel(InBatchArgs A) {
+    constexpr int NB = DP / 32;                      // 32-wide output column blocks
+    constexpr int KS = DP / 16;                      // k steps of product 1
+    constexpr int TF4 = kIbTile * DP / 4;            // float4 per column tile
+    constexpr int LOADS = TF4 / 256;
+    static_assert(TF4 % 256 == 0, "whole staging rounds");
+    __shared__ __attribute__((aligned(16))) unsigned char tile[3 * kIbxPlane];
+    __shared__ float red[4];
+
+    int blk = blockIdx.x;
+    const int nu = A.rblk_u * A.splits_u;
+    const bool role_u = blk < nu;
+    if (!role_u) blk -= nu;
+    const int splits = role_u ? A.splits_u : A.splits_p;
+    const int rb = blk / splits, sp = blk - (blk / splits) * splits;
+    const float* R = role_u ? A.U : A.P;
+    const int64_t ldr = role_u ? A.ldu : A.ldp, nr = role_u ? A.B : A.Bc;
+    const float* C = role_u ? A.P : A.U;
+    const int64_t ldc = role_u ? A.ldp : A.ldu, nc = role_u ? A.Bc : A.B;
+    const int64_t per = role_u ? A.cols_u : A.cols_p;
+    const int64_t c_begin = min(nc, (int64_t)sp * per), c_end = min(nc, c_begin + per);
+    const int D = A.D;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, h = lane >> 5;
+    const int64_t r0 = (int64_t)rb * kIbRows + 32 * w;
+
+    // this lane's row fragments (B operand of product 1): R[r0 + li][16 s + 8 h + j], zero past D / nr
+    bf16x8_t rf[KS][3];
+    {
+        const int64_t row = r0 + li;
+        const bool rok = row < nr;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int col = 16 * s + 8 * h;
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 a = (rok && col < D) ? *reinterpret_cast<const float4*>(R + row * ldr + col) : z;
+            const float4 b = (rok && col + 4 < D) ? *reinterpret_cast<const float4*>(R + row * ldr + col + 4) : z;
+            uint2 pa[3], pb[3];
+            ibx_split(a, pa);
+            ibx_split(b, pb);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) rf[s][q] = ibx_cat(pa[q], pb[q]);
+        }
+    }
+    f32x16 acc[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[n][r] = 0.f;
+    float bce = 0.f;
+
+    // column tile -> registers (zero past c_end / D, so masked rows contribute exact zeros)
+    float4 st[LOADS];
+    auto load = [&](int64_t c0) {
+#pragma unroll
+        for (int it = 0; it < LOADS; ++it) {
+            const int lin = tid + it * 256;
+            const int row = lin / (DP / 4), col = (lin - row * (DP / 4)) * 4;
+            const int64_t gc = c0 + row;
+            st[it] = (gc < c_end && col < D) ? *reinterpret_cast<const float4*>(C + gc * ldc + col)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int it = 0; it < LOADS; ++it) {
+            const int lin = tid + it * 256;
+            const int row = lin / (DP / 4), c4 = lin - row * (DP / 4);
+            const int o = ibx_off(row, c4 >> 1) + 8 * (c4 & 1);
+            uint2 pl[3];
+            ibx_split(st[it], pl);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) *reinterpret_cast<uint2*>(tile + q * kIbxPlane + o) = pl[q];
+        }
+    };
+
+    const int ntiles = c_end > c_begin ? (int)((c_end - c_begin + kIbTile - 1) / kIbTile) : 0;
+    // the next tile in flight in registers while this one is multiplied (narrow D); at D > 64 the
+    // registers go to the operands and the second block of the CU hides the load instead
+    constexpr bool PREFETCH = DP <= 64 || MINB == 1;
+    if (PREFETCH && ntiles > 0) load(c_begin);
+    // tr-read lane roles: 16-lane group g, lane 4q + p of the group
+    const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+    const int64_t gr = r0 + li;
+    for (int t = 0; t < ntiles; ++t) {
+        const int64_t c0 = c_begin + (int64_t)t * kIbTile;
+        if (!PREFETCH) load(c0);
+        __syncthreads();  // every wave is done with the previous tile
+        store();
+        __syncthreads();
+        if (PREFETCH && t + 1 < ntiles) load(c0 + kIbTile);  // in flight during this tile's MFMAs
+        // the label Y = 1 sits at tile column diag of this lane's row: user u's own positive is
+        // column row_base + u (user role), positive i's user is row i - row_base (item role)
+        const int64_t dl = role_u ? A.row_base + gr - c0 : gr - A.row_base - c0;
+        const int diag = (dl >= 0 && dl < kIbTile) ? (int)dl : -1;
+        const int cols_here = (int)min((int64_t)kIbTile, c_end - c0);
+        const bool row_ok = gr < nr;
+#pragma unroll
+        for (int jc = 0; jc < 2; ++jc) {  // tile rows 32 jc .. 32 jc + 31
+            // ---- product 1: S^T block [32 c x 32 u] --------------------------------------------------
+            f32x16 s2;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s2[r] = 0.f;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const int o = ibx_off(32 * jc + li, 2 * s + h);
+                bf16x8_t a[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) a[q] = *reinterpret_cast<const bf16x8_t*>(tile + q * kIbxPlane + o);
+                s2 = ibx_mfma6(a, rf[s], s2);
+            }
+            // ---- dS^T in registers (lane: row u = r0 + li; register r: tile column c) -----------
+            // hardware exp2 / log2 / rcp (<= 1-2 ulp): this elementwise pass, not the MFMAs, bounds
+            // the kernel with IEEE expf / logf / division
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int lc = 32 * jc + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const bool ok = row_ok && lc < cols_here;
+                const float y = lc == diag ? 1.0f : 0.0f;
+                const float x = s2[r];
+                // sigmoid and the ATen BCE term from one exp: t = exp(-|x|); for x >= 0
+                // exp(-max(-x,0)) = 1 and exp(-x-max(-x,0)) = t, for x < 0 the reverse
+                const float tx = __builtin_amdgcn_exp2f(-fabsf(x) * 1.4426950408889634f);
+                const float inv = __builtin_amdgcn_rcpf(1.0f + tx);
+                const float sg = x >= 0.f ? inv : tx * inv;
+                if (role_u && ok) bce += (1.0f - y) * x + fmaxf(-x, 0.f) + __builtin_amdgcn_logf(1.0f + tx) * 0.6931471805599453f;
+                s2[r] = ok ? (sg - y) * A.inv_T : 0.f;
+            }
+            // ---- product 2: acc[n] (rows u, columns 32 n ..) += dS . tile ---------------------------
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                bf16x8_t a[3];
+                {
+                    const float4 x0 = make_float4(s2[8 * s + 0], s2[8 * s + 1], s2[8 * s + 2], s2[8 * s + 3]);
+                    const float4 x1 = make_float4(s2[8 * s + 4], s2[8 * s + 5], s2[8 * s + 6], s2[8 * s + 7]);
+                    uint2 pa[3], pb[3];
+                    ibx_split(x0, pa);
+                    ibx_split(x1, pb);
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) a[q] = ibx_cat(pa[q], pb[q]);
+                }
+                // B: tile rows 32 jc + 16 s + 4 h + q (elements 0..3) and + 8 (elements 4..7)
+                const int brow = 32 * jc + 16 * s + 4 * h + q4;
+#pragma unroll
+                for (int n = 0; n < NB; ++n) {
+                    const int ch = 4 * n + 2 * (g & 1) + (p4 >> 1);
+                    const int o0 = ibx_off(brow, ch) + 8 * (p4 & 1), o1 = ibx_off(brow + 8, ch) + 8 * (p4 & 1);
+                    bf16x8_t b[3];
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(tile + q * kIbxPlane + o0));
+                        const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(tile + q * kIbxPlane + o1));
+                        const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                        b[q] = __builtin_bit_cast(bf16x8_t, v);
+                    }
+                    acc[n] = ibx_mfma6(a, b, acc[n]);
+                }
+            }
+        }
+    }
+    // ---- partial rows -> this split's slab ------------------------------------------------------
+    float* slab = role_u ? A.slab_u + (int64_t)sp * A.B * D : A.slab_p + (int64_t)sp * A.Bc * D;
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int lr = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int64_t gr = r0 + lr;
+            const int col = 32 * n + li;
+            if (gr < nr && col < D) slab[gr * D + col] = acc[n][r];
+        }
+    if (role_u) {
+        bce = wave_sum(bce);
+        if (lane == 0) red[w] = bce;
+        __syncthreads();
+        if (tid == 0) A.loss_part[blk] = (red[0] + red[1]) + (red[2] + red[3]);
+    }
+}
+
 // dU = sum of the user slabs, dP = sum of the item slabs, in split order.
 __global__ void ib_reduce_kernel(InBatchArgs A) {
     const int64_t nu = A.B * A.D, total = nu + A.Bc * A.D;
@@ -232,11 +471,24 @@ int launch_inbatch(InBatchArgs& a, hipStream_t s) {
     inbatch_plan(a.B, a.Bc, a);
     const unsigned blocks = (unsigned)(a.rblk_u * a.splits_u + a.rblk_p * a.splits_p);
     const int dp = (a.D + 31) / 32 * 32;
-    switch (dp) {
-        case 32: hipLaunchKernelGGL(inbatch_kernel<32>, dim3(blocks), dim3(256), 0, s, a); break;
-        case 64: hipLaunchKernelGGL(inbatch_kernel<64>, dim3(blocks), dim3(256), 0, s, a); break;
-        case 96: hipLaunchKernelGGL(inbatch_kernel<96>, dim3(blocks), dim3(256), 0, s, a); break;
-        default: hipLaunchKernelGGL(inbatch_kernel<128>, dim3(blocks), dim3(256), 0, s, a); break;
+    // TTAMM_FP32_MFMA=exact: the v_mfma_f32_32x32x2_f32 kernel (as gemm.hip's developer switch)
+    const char* env = std::getenv("TTAMM_FP32_MFMA");
+    if (env && std::strcmp(env, "exact") == 0) {
+        switch (dp) {
+            case 32: hipLaunchKernelGGL(inbatch_kernel<32>, dim3(blocks), dim3(256), 0, s, a); break;
+            case 64: hipLaunchKernelGGL(inbatch_kernel<64>, dim3(blocks), dim3(256), 0, s, a); break;
+            case 96: hipLaunchKernelGGL(inbatch_kernel<96>, dim3(blocks), dim3(256), 0, s, a); break;
+            default: hipLaunchKernelGGL(inbatch_kernel<128>, dim3(blocks), dim3(256), 0, s, a); break;
+        }
+    } else {
+        switch (dp) {
+            case 32: hipLaunchKernelGGL((inbatch_x_kernel<32, 2>), dim3(blocks), dim3(256), 0, s, a); break;
+            case 64: hipLaunchKernelGGL((inbatch_x_kernel<64, 2>), dim3(blocks), dim3(256), 0, s, a); break;
+            case 96: hipLaunchKernelGGL((inbatch_x_kernel<96, 2>), dim3(blocks), dim3(256), 0, s, a); break;
+            // D = 128 at two blocks per CU spills ~20 registers and still beats one block per CU
+            // (C4: 0.41 vs 0.50 ms per launch)
+            default: hipLaunchKernelGGL((inbatch_x_kernel<128, 2>), dim3(blocks), dim3(256), 0, s, a); break;
+        }
     }
     TTAMM_LAUNCH_CHECK();
     const int64_t total = (a.B + a.Bc) * a.D;
