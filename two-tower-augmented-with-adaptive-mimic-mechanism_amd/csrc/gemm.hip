@@ -89,11 +89,6 @@ __device__ __forceinline__ float4 mask4(float4 v, int c, int lim, int ld, int on
     return make_float4(t[0], t[1], t[2], t[3]);
 }
 
-__device__ __forceinline__ uint32_t keep_threshold(float keep_prob) {
-    const double t = (double)keep_prob * 4294967296.0;
-    return t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
-}
-
 // MF: MFMA block edge — 32 (v_mfma_f32_32x32x2_f32 / 32x32x16_bf16) or 16
 // (v_mfma_f32_16x16x4_f32, fp32 only): the 16-row granularity lets a tile height divide the
 // step's row count into exactly two tiles per CU (C2: 57344 = 512 x 112).
@@ -137,28 +132,8 @@ __device__ __forceinline__ void epilogue4(const KArg(GemmProblem) & P, float4 v,
                                           int col) {
     const int N = P.N;
     float x[4] = {v.x + bias4.x, v.y + bias4.y, v.z + bias4.z, v.w + bias4.w};
-    if (E == EPI_HIDDEN) {
-        u32x4 rnd = {0u, 0u, 0u, 0u};
-        const bool drop = P.keep_prob < 1.0f;
-        if (drop && P.keep_mask == nullptr) {
-            const int64_t key = P.row_key ? P.row_key[row]
-                                          : (row < P.key_split ? P.key_base0 + row : P.key_base1 + (row - P.key_split));
-            rnd = philox4x32(u32x4{(uint32_t)key, (uint32_t)col, P.rng_c2, P.rng_c3}, P.rng_k0, P.rng_k1);
-        }
-        uint32_t km = 0xFFFFFFFFu;
-        if (drop && P.keep_mask) km = *reinterpret_cast<const uint32_t*>(P.keep_mask + (int64_t)row * N + col);
-        const uint32_t thresh = keep_threshold(P.keep_prob);
-        const uint32_t w[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            float hv = x[e] > 0.f ? x[e] : 0.f;
-            if (drop) {
-                const bool keep = P.keep_mask ? ((km >> (8 * e)) & 0xFFu) != 0 : w[e] < thresh;
-                hv = hv * (keep ? P.inv_keep : 0.f);
-            }
-            x[e] = hv;
-        }
-    } else if (E == EPI_GATE_HIDDEN) {
+    static_assert(E != EPI_HIDDEN, "EPI_HIDDEN runs through epilogue8_hidden");
+    if (E == EPI_GATE_HIDDEN) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) x[e] = x[e] > 0.f ? x[e] : 0.f;
     } else if (E == EPI_GATE_OUT) {
@@ -204,6 +179,96 @@ __device__ __forceinline__ void epilogue4(const KArg(GemmProblem) & P, float4 v,
     }
     if (E == EPI_GATE_OUT && P.C == nullptr) return;  // sharded item owner: aug is formed by the requester
     st4(P.C + (int64_t)split * P.slab_stride + (int64_t)row * P.ldc + col, make_float4(x[0], x[1], x[2], x[3]));
+}
+
+// EPI_HIDDEN: bias, ReLU, dropout.  Dropout stream: the keep decision of column c of row r is
+// 16-bit uniform (c & 1 ? high : low half) of word (c & 7) >> 1 of ONE Philox4x32-10 draw keyed
+// by (row key, c / 8); keep iff u < round_down(keep_prob * 2^16) (resolution 2^-16).  Eight
+// decisions per draw instead of four halve the tail's integer-multiply work (v_mul_hi is quarter
+// rate), which bounded the first layer's epilogue.  A thread stores 4 columns of two rows
+// (ra, rb = ra + row step), so a wave's stores stay contiguous; the lane pair (l, l ^ 1) holds the
+// two halves of one 8-column group, each lane draws one of the two rows' words and they swap the
+// halves the other needs.  An injected mask (uint8 per element, the parity tests) replaces the
+// draw.  Both lanes of a pair must reach this call (a lane past N still draws; it stores nothing).
+__device__ __forceinline__ uint32_t keep_threshold16(float keep_prob) {
+    const float t = keep_prob * 65536.0f;  // exact (power-of-two scale)
+    return t >= 65536.0f ? 65536u : (uint32_t)t;
+}
+__device__ __forceinline__ int64_t dropout_key(const KArg(GemmProblem) & P, int row) {
+    return P.row_key ? P.row_key[row] : (row < P.key_split ? P.key_base0 + row : P.key_base1 + (row - P.key_split));
+}
+__device__ __forceinline__ void epilogue_hidden_pair(const KArg(GemmProblem) & P, float4 va, float4 vb, float4 bias4,
+                                                     int split, int ra, int rb, bool oka, bool okb, int col) {
+    const bool drop = P.keep_prob < 1.0f;
+    uint32_t wa[2] = {0u, 0u}, wb[2] = {0u, 0u};
+    if (drop && P.keep_mask == nullptr) {
+        const int half = (col >> 2) & 1;
+        const int M = P.M;
+        const int my = min(half ? rb : ra, M - 1);  // half 0 draws row ra's group, half 1 row rb's
+        const u32x4 d = philox4x32(u32x4{(uint32_t)dropout_key(P, my), (uint32_t)(col >> 3), P.rng_c2, P.rng_c3},
+                                   P.rng_k0, P.rng_k1);
+        // half 0 needs words 0, 1 of both rows; half 1 words 2, 3: send the partner its pair
+        const uint32_t s0 = half ? d.x : d.z, s1 = half ? d.y : d.w;
+        const uint32_t r0 = (uint32_t)__shfl_xor((int)s0, 1), r1 = (uint32_t)__shfl_xor((int)s1, 1);
+        wa[0] = half ? r0 : d.x, wa[1] = half ? r1 : d.y;
+        wb[0] = half ? d.z : r0, wb[1] = half ? d.w : r1;
+    }
+    const uint32_t thresh = keep_threshold16(P.keep_prob);
+    auto tail = [&](float4 v, const uint32_t w[2], int row) {
+        float x[4] = {v.x + bias4.x, v.y + bias4.y, v.z + bias4.z, v.w + bias4.w};
+        uint32_t km = 0xFFFFFFFFu;
+        if (drop && P.keep_mask) km = *reinterpret_cast<const uint32_t*>(P.keep_mask + (int64_t)row * P.N + col);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float hv = x[e] > 0.f ? x[e] : 0.f;
+            if (drop) {
+                const bool keep = P.keep_mask ? ((km >> (8 * e)) & 0xFFu) != 0
+                                              : ((w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu) < thresh;
+                hv = hv * (keep ? P.inv_keep : 0.f);
+            }
+            x[e] = hv;
+        }
+        st4(P.C + (int64_t)split * P.slab_stride + (int64_t)row * P.ldc + col, make_float4(x[0], x[1], x[2], x[3]));
+    };
+    if (oka) tail(va, wa, ra);
+    if (okb) tail(vb, wb, rb);
+}
+
+// The same stream, one thread per 8 consecutive columns of a row (one draw each): the split
+// kernel's epilogue measured faster this way (its stores are 32-B strided per instruction but its
+// loop half as long); the bf16-operand kernel's faster with the lane pairs above.
+__device__ __forceinline__ void epilogue8_hidden(const KArg(GemmProblem) & P, float4 v0, float4 v1, float4 b0,
+                                                 float4 b1, int split, int row, int col) {
+    const int N = P.N;
+    float x[8] = {v0.x + b0.x, v0.y + b0.y, v0.z + b0.z, v0.w + b0.w,
+                  v1.x + b1.x, v1.y + b1.y, v1.z + b1.z, v1.w + b1.w};
+    const bool hi_ok = col + 4 < N;
+    const bool drop = P.keep_prob < 1.0f;
+    u32x4 rnd = {0u, 0u, 0u, 0u};
+    if (drop && P.keep_mask == nullptr)
+        rnd = philox4x32(u32x4{(uint32_t)dropout_key(P, row), (uint32_t)(col >> 3), P.rng_c2, P.rng_c3}, P.rng_k0,
+                         P.rng_k1);
+    uint32_t km[2] = {0xFFFFFFFFu, 0xFFFFFFFFu};
+    if (drop && P.keep_mask) {
+        const uint8_t* mrow = P.keep_mask + (int64_t)row * N + col;
+        km[0] = *reinterpret_cast<const uint32_t*>(mrow);
+        if (hi_ok) km[1] = *reinterpret_cast<const uint32_t*>(mrow + 4);
+    }
+    const uint32_t thresh = keep_threshold16(P.keep_prob);
+    const uint32_t w[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        float hv = x[e] > 0.f ? x[e] : 0.f;
+        if (drop) {
+            const bool keep = P.keep_mask ? ((km[e >> 2] >> (8 * (e & 3))) & 0xFFu) != 0
+                                          : ((w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu) < thresh;
+            hv = hv * (keep ? P.inv_keep : 0.f);
+        }
+        x[e] = hv;
+    }
+    float* out = P.C + (int64_t)split * P.slab_stride + (int64_t)row * P.ldc + col;
+    st4(out, make_float4(x[0], x[1], x[2], x[3]));
+    if (hi_ok) st4(out + 4, make_float4(x[4], x[5], x[6], x[7]));
 }
 
 template <class CF, int E, bool BF>
@@ -488,18 +553,39 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
         }
         __syncthreads();
         // each thread owns one 4-column group (bias loaded once) and walks rows
-        constexpr int C4 = BN / 4;
-        constexpr int RSTEP = kThreads / C4;
-        const int c4 = tid % C4, r0 = tid / C4;
-        const int col = n0 + c4 * 4;
-        if (r0 < RSTEP && col < N) {
-            const bool has_bias = (E == EPI_STORE || E == EPI_HIDDEN || E == EPI_GATE_HIDDEN || E == EPI_GATE_OUT) &&
-                                  P.bias != nullptr;
-            const float4 bias4 = has_bias ? ld4(P.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (E == EPI_HIDDEN) {
+            // two rows per pass; lane pairs share the dropout draws (epilogue_hidden_pair)
+            constexpr int C4 = BN / 4;
+            constexpr int RSTEP = kThreads / C4;
+            static_assert(C4 % 2 == 0, "lane pairs hold 8-column groups");
+            const int c4 = tid % C4, r0 = tid / C4;
+            const int col = n0 + c4 * 4;
+            if (r0 < RSTEP && col < ((N + 7) & ~7)) {
+                const float4 bias4 = (P.bias && col < N) ? ld4(P.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 2
+                for (int rr = r0; rr < rows_here; rr += 2 * RSTEP) {
+                    const int rb_ = rr + RSTEP;
+                    const int ra = m0 + row_lo + rr, rb = m0 + row_lo + rb_;
+                    const bool in_b = rb_ < rows_here;
+                    epilogue_hidden_pair(P, ld4(Cs + rr * CF::CLD + c4 * 4), in_b ? ld4(Cs + rb_ * CF::CLD + c4 * 4) : z4, bias4,
+                                         split, ra, rb, ra < M && col < N, in_b && rb < M && col < N, col);
+                }
+            }
+        } else {
+            constexpr int C4 = BN / 4;
+            constexpr int RSTEP = kThreads / C4;
+            const int c4 = tid % C4, r0 = tid / C4;
+            const int col = n0 + c4 * 4;
+            if (r0 < RSTEP && col < N) {
+                const bool has_bias = (E == EPI_STORE || E == EPI_HIDDEN || E == EPI_GATE_HIDDEN || E == EPI_GATE_OUT) &&
+                                      P.bias != nullptr;
+                const float4 bias4 = has_bias ? ld4(P.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 4
-            for (int rr = r0; rr < rows_here; rr += RSTEP) {
-                const int row = m0 + row_lo + rr;
-                if (row < M) epilogue4<E>(P, ld4(Cs + rr * CF::CLD + c4 * 4), bias4, split, row, col);
+                for (int rr = r0; rr < rows_here; rr += RSTEP) {
+                    const int row = m0 + row_lo + rr;
+                    if (row < M) epilogue4<E>(P, ld4(Cs + rr * CF::CLD + c4 * 4), bias4, split, row, col);
+                }
             }
         }
         __syncthreads();
@@ -876,18 +962,38 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
                 }
         }
         __syncthreads();
-        constexpr int C4 = BN / 4;
-        constexpr int RSTEP = kThreads / C4;
-        const int c4 = tid % C4, r0 = tid / C4;
-        const int col = n0 + c4 * 4;
-        if (r0 < RSTEP && col < N) {
-            const bool has_bias = (E == EPI_STORE || E == EPI_HIDDEN || E == EPI_GATE_HIDDEN || E == EPI_GATE_OUT) &&
-                                  P.bias != nullptr;
-            const float4 bias4 = has_bias ? ld4(P.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (E == EPI_HIDDEN) {
+            // 8 columns per thread: one dropout draw each (epilogue8_hidden)
+            constexpr int C8 = BN / 8;
+            constexpr int RSTEP8 = kThreads / C8;
+            const int c8 = tid % C8, r8 = tid / C8;
+            const int col = n0 + c8 * 8;
+            if (r8 < RSTEP8 && col < N) {
+                const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 b0 = P.bias ? ld4(P.bias + col) : z4;
+                const float4 b1 = (P.bias && col + 4 < N) ? ld4(P.bias + col + 4) : z4;
+#pragma unroll 2
+                for (int rr = r8; rr < rows_here; rr += RSTEP8) {
+                    const int row = m0 + row_lo + rr;
+                    if (row < M)
+                        epilogue8_hidden(P, ld4(Cs + rr * CX::CLD + c8 * 8), ld4(Cs + rr * CX::CLD + c8 * 8 + 4), b0, b1,
+                                         split, row, col);
+                }
+            }
+        } else {
+            constexpr int C4 = BN / 4;
+            constexpr int RSTEP = kThreads / C4;
+            const int c4 = tid % C4, r0 = tid / C4;
+            const int col = n0 + c4 * 4;
+            if (r0 < RSTEP && col < N) {
+                const bool has_bias = (E == EPI_STORE || E == EPI_HIDDEN || E == EPI_GATE_HIDDEN || E == EPI_GATE_OUT) &&
+                                      P.bias != nullptr;
+                const float4 bias4 = has_bias ? ld4(P.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 4
-            for (int rr = r0; rr < rows_here; rr += RSTEP) {
-                const int row = m0 + row_lo + rr;
-                if (row < M) epilogue4<E>(P, ld4(Cs + rr * CX::CLD + c4 * 4), bias4, split, row, col);
+                for (int rr = r0; rr < rows_here; rr += RSTEP) {
+                    const int row = m0 + row_lo + rr;
+                    if (row < M) epilogue4<E>(P, ld4(Cs + rr * CX::CLD + c4 * 4), bias4, split, row, col);
+                }
             }
         }
         __syncthreads();
@@ -1039,22 +1145,43 @@ __global__ __launch_bounds__(kB16Threads) void gemm_bf16_kernel(GemmBatch batch)
                 }
         }
         __syncthreads();
-        constexpr int C4 = kB16N / 4;              // 64 column groups
-        constexpr int RSTEP = kB16Threads / C4;    // 8 rows per pass
-        const int c4 = tid % C4, r0 = tid / C4;
-        const int col = n0 + c4 * 4;
-        if (col < N) {
-            const bool has_bias = (E == EPI_STORE || E == EPI_HIDDEN || E == EPI_GATE_HIDDEN || E == EPI_GATE_OUT) &&
-                                  P.bias != nullptr;
-            const float4 bias4 = has_bias ? ld4(P.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (E == EPI_HIDDEN) {
+            // two rows per pass; lane pairs share the dropout draws (epilogue_hidden_pair)
+            constexpr int C4 = kB16N / 4;
+            constexpr int RSTEP = kB16Threads / C4;
+            static_assert(C4 % 2 == 0, "lane pairs hold 8-column groups");
+            const int c4 = tid % C4, r0 = tid / C4;
+            const int col = n0 + c4 * 4;
+            if (r0 < RSTEP && col < ((N + 7) & ~7)) {
+                const float4 bias4 = (P.bias && col < N) ? ld4(P.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 2
-            for (int rr = r0; rr < kB16EpiRows; rr += RSTEP) {
-                const int row = m0 + row_lo + rr;
-#if TTAMM_B16_ABLATE == 1  // developer ablation 1: plain store instead of the fused tail
-                if (row < M) st4(P.C + (int64_t)row * P.ldc + col, ld4(Cs + rr * kB16Cld + c4 * 4));
-#else
-                if (row < M) epilogue4<E>(P, ld4(Cs + rr * kB16Cld + c4 * 4), bias4, 0, row, col);
-#endif
+                for (int rr = r0; rr < kB16EpiRows; rr += 2 * RSTEP) {
+                    const int rb_ = rr + RSTEP;
+                    const int ra = m0 + row_lo + rr, rb = m0 + row_lo + rb_;
+                    const bool in_b = rb_ < kB16EpiRows;
+                    epilogue_hidden_pair(P, ld4(Cs + rr * kB16Cld + c4 * 4), in_b ? ld4(Cs + rb_ * kB16Cld + c4 * 4) : z4, bias4,
+                                         0, ra, rb, ra < M && col < N, in_b && rb < M && col < N, col);
+                }
+            }
+        } else {
+            constexpr int C4 = kB16N / 4;              // 64 column groups
+            constexpr int RSTEP = kB16Threads / C4;    // 8 rows per pass
+            const int c4 = tid % C4, r0 = tid / C4;
+            const int col = n0 + c4 * 4;
+            if (col < N) {
+                const bool has_bias = (E == EPI_STORE || E == EPI_HIDDEN || E == EPI_GATE_HIDDEN || E == EPI_GATE_OUT) &&
+                                      P.bias != nullptr;
+                const float4 bias4 = has_bias ? ld4(P.bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+    #pragma unroll 2
+                for (int rr = r0; rr < kB16EpiRows; rr += RSTEP) {
+                    const int row = m0 + row_lo + rr;
+    #if TTAMM_B16_ABLATE == 1  // developer ablation 1: plain store instead of the fused tail
+                    if (row < M) st4(P.C + (int64_t)row * P.ldc + col, ld4(Cs + rr * kB16Cld + c4 * 4));
+    #else
+                    if (row < M) epilogue4<E>(P, ld4(Cs + rr * kB16Cld + c4 * 4), bias4, 0, row, col);
+    #endif
+                }
             }
         }
         __syncthreads();

@@ -107,6 +107,21 @@ int main(int argc, char** argv) {
         launch_gemm(b, 0);
     };
     const double l1 = 2.0 * R * F * H;
+    {  // dropout keep rate of the GEMM epilogue: nonzeros with dropout / nonzeros without (ReLU only)
+        std::vector<float> h((size_t)R * H);
+        auto nonzero = [&]() -> double {
+            if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(h.data(), C, h.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+                return -1;
+            size_t nz = 0;
+            for (float v : h) nz += v != 0.f;
+            return (double)nz;
+        };
+        l1_mem(idx, EPI_HIDDEN, 1.f);
+        const double base = nonzero();
+        l1_mem(idx, EPI_HIDDEN, 0.85f);
+        const double kept = nonzero();
+        printf("dropout keep rate (p = 0.15): %.5f over %.0f ReLU-positive elements (expect 0.85)\n", kept / base, base);
+    }
     report("L1 fwd bf16-mem gather, ReLU+dropout", l1, time_one([&] { l1_mem(idx, EPI_HIDDEN, 0.85f); }));
     report("L1 fwd bf16-mem gather, ReLU", l1, time_one([&] { l1_mem(idx, EPI_HIDDEN, 1.f); }));
     report("L1 fwd bf16-mem gather, store", l1, time_one([&] { l1_mem(idx, EPI_STORE, 1.f); }));
