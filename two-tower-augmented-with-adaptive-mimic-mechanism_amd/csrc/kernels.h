@@ -457,7 +457,8 @@ struct ReplayArgs {
     const AdamConsts* hist;
     int cap;
     int32_t target;   // replay every row up to this dense step
-    int stamp;        // write last = target afterwards (row ranges only)
+    int stamp;        // write last = target afterwards (row ranges, lead positions); 2: atomicMax (a concurrent
+                      // row update may have moved a row past target)
     int decoupled;    // AdamW (decoupled weight decay) vs Adam (L2): the optimizer's, every step
     int fast_g0;      // TTAMM_G0_FAST arithmetic
     const uint32_t* status;  // poisoned: no write (null for the flush)

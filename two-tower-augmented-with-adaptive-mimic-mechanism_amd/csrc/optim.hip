@@ -547,9 +547,17 @@ __global__ void stamp_kernel(ReplayArgs) {
     const KArg(ReplayArgs)* ka = (const KArg(ReplayArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
     const KArg(ReplaySeg)& S = ka->seg[blockIdx.y];
     if (step_poisoned(ka->status)) return;
+    const bool at_least = ka->stamp == 2;
     for (int64_t r = S.row_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < S.row_hi;
-         r += (int64_t)gridDim.x * blockDim.x)
-        S.last[r] = ka->target;
+         r += (int64_t)gridDim.x * blockDim.x) {
+        int64_t row = r;
+        if (S.lead_idx) {  // batch positions: the row of each first occurrence
+            row = S.lead_idx[r];
+            if (S.lead_first[row] != (int32_t)(INT_MAX - r)) continue;
+        }
+        if (at_least) atomicMax(&S.last[row], ka->target);
+        else S.last[row] = ka->target;
+    }
 }
 
 __global__ void side_scatter_kernel(const int32_t* __restrict__ n_unique, const int32_t* __restrict__ keys,

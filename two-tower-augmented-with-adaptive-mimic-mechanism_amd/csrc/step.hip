@@ -764,6 +764,9 @@ struct Deferred {
     int decoupled = 1;
     int fast = 0;  // TTAMM_G0_FAST arithmetic for the g = 0 updates
     const uint32_t* status = nullptr;  // poisoned: the step writes nothing
+    // one-process step with the aux stream: the rolling slice runs there (replay_slice_aux)
+    // instead of at the end of the main stream's step
+    bool slice_on_aux = false;
 };
 
 // The tables of a tower that belong to the dense (AdamW) group.
@@ -785,6 +788,38 @@ ReplaySeg replay_seg(const ttamm_table& tb) {
     return g;
 }
 
+// The rolling slice of the deferred AdamW(g = 0): this step's 1/slices of every dense-group
+// table's rows brought to `target` (every row's lag stays below the history ring).
+int replay_slice(const ttamm_tower* const* T, int n, bool mimic, const Deferred& df, int32_t target, int stamp,
+                 void* const* events, hipStream_t s) {
+    int rc;
+    ReplayArgs ra;
+    std::memset(&ra, 0, sizeof(ra));
+    ra.hist = df.hist;
+    ra.cap = df.cap;
+    ra.decoupled = df.decoupled;
+    ra.fast_g0 = df.fast;
+    ra.status = df.status;
+    ra.target = target;
+    ra.stamp = stamp;
+    const int slice = (int)(((int64_t)target % df.slices + df.slices) % df.slices);
+    for (int k = 0; k < n; ++k) {
+        const ttamm_table* tabs[2];
+        const int nt = dense_tables(*T[k], mimic, tabs);
+        for (int i = 0; i < nt; ++i) {
+            ReplaySeg g = replay_seg(*tabs[i]);
+            const int64_t per = (tabs[i]->rows + df.slices - 1) / df.slices;
+            g.row_lo = std::min<int64_t>(tabs[i]->rows, slice * per);
+            g.row_hi = std::min<int64_t>(tabs[i]->rows, g.row_lo + per);
+            ra.seg[ra.count++] = g;
+        }
+    }
+    if (events && events[0]) TTAMM_HIP(hipEventRecord((hipEvent_t)events[0], s));
+    if ((rc = launch_replay(ra, s))) return rc;
+    if (events && events[1]) TTAMM_HIP(hipEventRecord((hipEvent_t)events[1], s));
+    return TTAMM_OK;
+}
+
 // Before a tower reads its rows (part A): count the batch's rows — which marks each row's first
 // position — and, deferred, bring the dense-group rows it touches current to step - 1 (each row
 // once, by its first position).  Part B groups the rows for the row updates at the step's end.
@@ -800,6 +835,9 @@ int tower_prepare_a(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred
     ra.fast_g0 = df.fast;
     ra.status = df.status;
     ra.target = df.step - 1;
+    // stamp the caught-up rows: a replay that runs before this step's row updates (the aux
+    // stream's slice, a flush after a poisoned step) must see them current to step - 1
+    ra.stamp = 1;
     const ttamm_table* tabs[2];
     const int n = dense_tables(t, mimic, tabs);
     for (int i = 0; i < n; ++i) {
@@ -859,7 +897,8 @@ bool overlapped(const ttamm_tower* const* T, int n, const Deferred& df, hipStrea
 // (grouping), joined by table_updates.  A deferred dense ID table is read by the first gather,
 // so that case stays serial.
 int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_batch& bt, int D, bool mimic,
-                    const Deferred& df, hipStream_t s, hipStream_t aux, void* const* l0_events) {
+                    const Deferred& df, hipStream_t s, hipStream_t aux, void* const* l0_events,
+                    void* const* maint_events = nullptr) {
     int rc;
     if (!overlapped(T, n, df, s, aux)) {
         for (int k = 0; k < n; ++k)
@@ -879,6 +918,14 @@ int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_b
     for (int k = 0; k < n; ++k)
         if ((rc = tower_prepare_b(*T[k], *W[k], aux))) return rc;
     TTAMM_HIP(hipEventRecord(ev[2], aux));
+    if (df.slice_on_aux) {
+        // The previous step's slice (target step - 1), behind this step's catch-up on the aux
+        // stream, overlapping the main stream's GEMMs instead of closing the step.  The rows this
+        // batch touches are current to step - 1 after the catch-up, so the slice skips them and
+        // never races the row updates; its stamp is an atomicMax (a row update may have moved a
+        // row to `step` meanwhile).  The next step's catch-up and the flush are ordered after it.
+        if ((rc = replay_slice(T, n, mimic, df, df.step - 1, 2, maint_events, aux))) return rc;
+    }
     TTAMM_HIP(hipStreamWaitEvent(s, ev[1], 0));
     return tower_forward(T, W, bt, D, mimic, s, n, l0_events, FWD_FUSION);
 }
@@ -947,31 +994,8 @@ int table_updates(const ttamm_tower* T[2], TowerWs* W[2], int n, int D, bool mim
     for (int k = 0; k < n; ++k)
         if ((rc = tower_optimizer_rows(*T[k], *W[k], D, mimic, sp, ad, df, s))) return rc;
     if (df.on) {
-        ReplayArgs ra;
-        std::memset(&ra, 0, sizeof(ra));
-        ra.hist = df.hist;
-        ra.cap = df.cap;
-        ra.decoupled = df.decoupled;
-        ra.fast_g0 = df.fast;
-        ra.status = df.status;
-        ra.target = df.step;
-        ra.stamp = 1;
-        const int slice = df.step % df.slices;
-        for (int k = 0; k < n; ++k) {
-            const ttamm_table* tabs[2];
-            const int nt = dense_tables(*T[k], mimic, tabs);
-            for (int i = 0; i < nt; ++i) {
-                ReplaySeg g = replay_seg(*tabs[i]);
-                const int64_t per = (tabs[i]->rows + df.slices - 1) / df.slices;
-                g.row_lo = std::min<int64_t>(tabs[i]->rows, slice * per);
-                g.row_hi = std::min<int64_t>(tabs[i]->rows, g.row_lo + per);
-                ra.seg[ra.count++] = g;
-            }
-        }
-        if (events && events[0]) TTAMM_HIP(hipEventRecord((hipEvent_t)events[0], s));
-        if ((rc = launch_replay(ra, s))) return rc;
-        if (events && events[1]) TTAMM_HIP(hipEventRecord((hipEvent_t)events[1], s));
-        return TTAMM_OK;
+        if (df.slice_on_aux) return TTAMM_OK;  // replayed on the aux stream (replay_slice_aux)
+        return replay_slice(T, n, mimic, df, df.step, 1, events, s);
     }
     SweepArgs sw;
     std::memset(&sw, 0, sizeof(sw));
@@ -1216,7 +1240,8 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     // ---- forward ----------------------------------------------------------------------------
     hipStream_t aux = static_cast<hipStream_t>(A.aux_stream);
     if (!shard) {
-        if ((rc = prepare_forward(T, W, 2, A.b, D, mimic, df, s, aux, A.timing_events + 2))) return rc;
+        df.slice_on_aux = df.on && overlapped(T, 2, df, s, aux) && !std::getenv("TTAMM_SLICE_MAIN");
+        if ((rc = prepare_forward(T, W, 2, A.b, D, mimic, df, s, aux, A.timing_events + 2, A.timing_events))) return rc;
     } else {
         const ttamm_tower* Ti[2] = {&A.item, nullptr};
         TowerWs* Wi[2] = {&I, nullptr};
@@ -1396,6 +1421,14 @@ int flush_tables(const ttamm_step_args& A, hipStream_t s) {
     int rc;
     if ((rc = deferred_of(A, df))) return rc;
     if (!df.on) return TTAMM_OK;
+    hipStream_t aux = static_cast<hipStream_t>(A.aux_stream);
+    if (aux != nullptr && aux != s) {  // the last steps' slices may still run on the aux stream
+        hipEvent_t e;
+        TTAMM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        TTAMM_HIP(hipEventRecord(e, aux));
+        TTAMM_HIP(hipStreamWaitEvent(s, e, 0));
+        TTAMM_HIP(hipEventDestroy(e));
+    }
     ReplayArgs ra;
     std::memset(&ra, 0, sizeof(ra));
     ra.hist = df.hist;
