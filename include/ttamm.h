@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 15
+#define TTAMM_ABI_VERSION 16
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -129,6 +129,11 @@ typedef struct ttamm_table {
      * (same fp32 operations, same per-step constants from adam_history) before the row is
      * read, on a rolling 1/replay_slices of the rows each step, and by ttamm_flush_tables. */
     int32_t* last_step;
+    /* nn.Embedding(padding_idx=...) (encoders.py:47,55-57): has_padding_idx != 0 makes row
+     * padding_idx receive no gradient — SparseAdam leaves it untouched (torch drops the row from
+     * the sparse gradient), AdamW updates it with g = 0.  The lookup itself is unchanged. */
+    int32_t has_padding_idx;
+    int64_t padding_idx;
 } ttamm_table;
 
 /* One tower: TowerEncoder (encoders.py:171-255) + its half of AdaptiveMimicMechanism
@@ -170,6 +175,11 @@ typedef struct ttamm_hparams {
     double lambda_mimic_item; /* loss_weights.mimic_item (training.py:723,802-803)    */
     double lambda_category_alignment; /* loss_weights.category_alignment (training.py:724,805-820);
                                          used when ttamm_step_args.item_categories is set */
+    double grad_clip_norm; /* gradient_clip_norm (training.py:712,824-825): > 0 scales every
+                              gradient of the step by min(clip / (||g||_2 + 1e-6), 1) before the
+                              optimizers, ||g|| over all parameters (clip_grad_norm_).  One-process
+                              step with dense ID tables only (torch raises on the sparse
+                              gradients of sparse ID tables); 0 = off */
 } ttamm_hparams;
 
 /* One batch of the training loop (training.py:726-736). */

@@ -74,7 +74,8 @@ def build_tower(cfg: Mapping[str, Any], *, num_embeddings: int, feature_dim: int
     """encoders.py:258-331 with the same parameter construction / init order."""
     id_cfg = cfg.get("id_embedding", {}) or {}
     params = id_cfg.get("params", {}) or {}
-    emb = nn.Embedding(num_embeddings, int(params.get("embedding_dim", 64)), sparse=bool(params.get("sparse", False)))
+    emb = nn.Embedding(num_embeddings, int(params.get("embedding_dim", 64)), padding_idx=params.get("padding_idx"),
+                       sparse=bool(params.get("sparse", False)))
     init = id_cfg.get("init") or {"type": "normal", "std": 0.02}
     nn.init.normal_(emb.weight, mean=0.0, std=float(init.get("std", 0.02)))  # encoders.py:25-27
     fusion = str(cfg.get("fusion", "gated" if feature_dim > 0 else "identity")).lower()
@@ -338,6 +339,7 @@ def train_step(
     item_category_tensor: torch.Tensor | None = None,
     major_category_id: int | None = None,
     in_batch: bool = False,
+    gradient_clip_norm: float | None = None,
 ) -> StepResult:
     """One iteration of _train_one_epoch's body.  item_keep_masks rows are ordered
     [positives; negatives] (the two item_encoder calls, training.py:750 and :776).
@@ -403,6 +405,8 @@ def train_step(
                                       category_tensor=item_category_tensor, major_category_id=major_category_id)
         total = total + lam_cal * cal
     total.backward()  # :822
+    if gradient_clip_norm is not None and gradient_clip_norm > 0:  # :824-825
+        torch.nn.utils.clip_grad_norm_(model.parameters(), gradient_clip_norm)
     for opt in optimizers:  # :826-827
         opt.step()
     return StepResult(
@@ -417,7 +421,8 @@ def train_one_epoch(model, batches: Iterable, optimizers, *, negatives_per_posit
                     positives: Mapping[int, set[int]], user_features, item_features,
                     loss_weights: Mapping[str, float] | None = None, max_steps: int | None = None,
                     item_category_tensor: torch.Tensor | None = None, major_category_id: int | None = None,
-                    batch_hook=None, step_losses: list | None = None, in_batch: bool = False) -> tuple[float, int, float]:
+                    batch_hook=None, step_losses: list | None = None, in_batch: bool = False,
+                    gradient_clip_norm: float | None = None) -> tuple[float, int, float]:
     """training.py:700-833 with the reference's per-row sampler; returns
     (mean loss, interactions, seconds).  ``batch_hook(step, users, pos) -> (negatives | None,
     {"user": masks, "item": masks} | None)`` injects the RNG streams (the same hook ttamm's
@@ -436,7 +441,7 @@ def train_one_epoch(model, batches: Iterable, optimizers, *, negatives_per_posit
                          item_features=item_features, loss_weights=loss_weights,
                          user_keep_masks=masks.get("user"), item_keep_masks=masks.get("item"),
                          item_category_tensor=item_category_tensor, major_category_id=major_category_id,
-                         in_batch=in_batch)
+                         in_batch=in_batch, gradient_clip_norm=gradient_clip_norm)
         if step_losses is not None:
             step_losses.append(res)
         running += res.total * users.shape[0]

@@ -30,13 +30,14 @@ def ttamm_optimizers(model, *, lr=1e-3, betas=(0.9, 0.999), weight_decay=0.01):
     return opts
 
 
-def run_ttamm(prob: Problem, *, lr=1e-3, betas=(0.9, 0.999), weight_decay=0.01, steps=None, device="cuda"):
+def run_ttamm(prob: Problem, *, lr=1e-3, betas=(0.9, 0.999), weight_decay=0.01, steps=None, device="cuda",
+              gradient_clip_norm=None):
     model = ttamm_model_from(prob, device)
     opts = ttamm_optimizers(model, lr=lr, betas=betas, weight_decay=weight_decay)
     eng = ttamm.FusedTrainStep(
         model, opts, negatives_per_positive=prob.shape.N, positives=prob.positives,
         user_features=prob.user_features.to(device), item_features=prob.item_features.to(device),
-        loss_weights=LOSS_WEIGHTS, max_batch=prob.shape.B,
+        loss_weights=LOSS_WEIGHTS, max_batch=prob.shape.B, gradient_clip_norm=gradient_clip_norm,
     )
     losses = []
     for (users, pos, neg, um, im) in prob.batches[: steps or len(prob.batches)]:

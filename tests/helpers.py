@@ -27,13 +27,16 @@ class Shape:
     sparse: bool = True
     hidden_dims: tuple = (16,)
     matmul_dtype: str = "fp32"
+    padding_idx: int | None = None  # nn.Embedding padding_idx of both ID tables (encoders.py:47)
 
     def tower_cfg(self) -> dict:
+        params = {"embedding_dim": self.D, "sparse": self.sparse}
+        if self.padding_idx is not None:
+            params["padding_idx"] = self.padding_idx
         return {
             "type": "tower",
             "matmul_dtype": self.matmul_dtype,
-            "id_embedding": {"params": {"embedding_dim": self.D, "sparse": self.sparse},
-                             "init": {"type": "normal", "std": 0.02}},
+            "id_embedding": {"params": params, "init": {"type": "normal", "std": 0.02}},
             "feature_encoder": {"type": "mlp", "hidden_dims": list(self.hidden_dims), "activation": "relu",
                                 "output_dim": self.D, "dropout": self.dropout},
             "fusion": "gated",
@@ -86,6 +89,10 @@ def make_problem(shape: Shape, *, seed: int = 1234, steps: int = 1, positives_pe
         users = torch.randint(0, shape.U, (shape.B,), generator=gen)
         pos = torch.tensor([sorted(positives[int(u)])[0] for u in users], dtype=torch.long)
         neg = torch.randint(0, shape.I, (shape.B, shape.N), generator=gen)
+        if shape.padding_idx is not None:  # the padding id occurs among users, positives and negatives
+            users[:3] = shape.padding_idx
+            pos[3] = shape.padding_idx
+            neg[:2, :2] = shape.padding_idx
         nh = len(shape.hidden_dims)
         um = [(torch.rand((shape.B, h), generator=gen) >= shape.dropout).to(torch.uint8) for h in shape.hidden_dims][:nh]
         im = [(torch.rand((shape.B * (1 + shape.N), h), generator=gen) >= shape.dropout).to(torch.uint8)
@@ -98,7 +105,8 @@ def clone_model(model):
     return copy.deepcopy(model)
 
 
-def run_oracle(prob: Problem, *, lr=1e-3, betas=(0.9, 0.999), weight_decay=0.01, steps=None, model=None):
+def run_oracle(prob: Problem, *, lr=1e-3, betas=(0.9, 0.999), weight_decay=0.01, steps=None, model=None,
+               gradient_clip_norm=None):
     model = model if model is not None else clone_model(prob.model)
     opts = ref.build_optimizers(model, lr=lr or 1e-3, betas=betas, weight_decay=weight_decay)
     set_lr(opts, lr)
@@ -106,7 +114,7 @@ def run_oracle(prob: Problem, *, lr=1e-3, betas=(0.9, 0.999), weight_decay=0.01,
     for (users, pos, neg, um, im) in prob.batches[: steps or len(prob.batches)]:
         results.append(ref.train_step(model, opts, users, pos, neg, user_features=prob.user_features,
                                       item_features=prob.item_features, loss_weights=LOSS_WEIGHTS,
-                                      user_keep_masks=um, item_keep_masks=im))
+                                      user_keep_masks=um, item_keep_masks=im, gradient_clip_norm=gradient_clip_norm))
     return model, opts, results
 
 

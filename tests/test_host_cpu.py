@@ -144,6 +144,20 @@ def test_train_one_epoch_rejects_unsupported_options():
               item_features=None, device=torch.device("cpu"))
     with pytest.raises(NotImplementedError, match="BCEWithLogitsLoss"):
         ttamm.train_one_epoch(model, [], criterion=torch.nn.BCEWithLogitsLoss(reduction="sum"), **kw)
-    with pytest.raises(NotImplementedError, match="clipping"):
-        ttamm.train_one_epoch(model, [], criterion=torch.nn.BCEWithLogitsLoss(), gradient_clip_norm=1.0, **kw)
     assert ttamm.train_one_epoch(model, [], criterion=torch.nn.BCEWithLogitsLoss(), **kw) == 0.0
+
+
+def test_reference_clipping_rejects_sparse_id_gradients():
+    """training.py:824-825 calls clip_grad_norm_(model.parameters(), ...): with the default sparse
+    ID tables (configs/default.yaml:30,47) torch raises NotImplementedError on their sparse
+    gradients — the fused step raises the same type there and clips dense-ID models."""
+    from helpers import make_problem
+    from oracle import cpu_reference as ref
+
+    prob = make_problem(Shape(), steps=1)
+    opts = ref.build_optimizers(prob.model, lr=1e-3)
+    users, pos, neg, um, im = prob.batches[0]
+    with pytest.raises(NotImplementedError):
+        ref.train_step(prob.model, opts, users, pos, neg, user_features=prob.user_features,
+                       item_features=prob.item_features, user_keep_masks=um, item_keep_masks=im,
+                       gradient_clip_norm=1.0)

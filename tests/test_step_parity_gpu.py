@@ -27,8 +27,10 @@ def _grads_by_name(model, opts):
         Shape(U=64, I=512, F=20, D=16, B=64, N=5, hidden_dims=(32, 24)),
         Shape(mimic=False),
         Shape(sparse=False),
+        Shape(padding_idx=5),
+        Shape(sparse=False, padding_idx=5),
     ],
-    ids=["tiny", "nodrop", "odd", "2hidden", "nomimic", "dense-id"],
+    ids=["tiny", "nodrop", "odd", "2hidden", "nomimic", "dense-id", "padding", "dense-id-padding"],
 )
 def test_step_gradients_match_oracle(shape):
     from gpu_helpers import run_ttamm
@@ -52,7 +54,8 @@ def test_step_gradients_match_oracle(shape):
         assert torch.equal(q.cpu(), p), n
 
 
-@pytest.mark.parametrize("shape", [Shape(), Shape(sparse=False)], ids=["tiny", "dense-id"])
+@pytest.mark.parametrize("shape", [Shape(), Shape(sparse=False), Shape(padding_idx=5), Shape(sparse=False, padding_idx=5)],
+                         ids=["tiny", "dense-id", "padding", "dense-id-padding"])
 def test_three_steps_match_oracle(shape):
     from gpu_helpers import run_ttamm
 
@@ -71,6 +74,12 @@ def test_three_steps_match_oracle(shape):
         assert rel_err(tst[n]["exp_avg"], ost[n]["exp_avg"]) <= 1e-4, n
         assert rel_err(tst[n]["exp_avg_sq"], ost[n]["exp_avg_sq"]) <= 1e-4, n
         assert float(tst[n]["step"]) == float(ost[n]["step"]), n
+    if shape.padding_idx is not None and shape.sparse:
+        # SparseAdam never sees the padding row (torch drops it from the sparse gradient)
+        init = prob.model.state_dict()
+        for n in ("user_encoder.embedding.weight", "item_encoder.embedding.weight"):
+            assert torch.equal(tsd[n][shape.padding_idx].cpu(), init[n][shape.padding_idx]), n
+            assert not tst[n]["exp_avg"][shape.padding_idx].any(), n
 
 
 # bf16 towers (ttamm.h ttamm_tower.matmul_bf16; BASELINE config C5): checked against the
@@ -162,3 +171,39 @@ def test_long_wgrad_splits_match_oracle(rows, monkeypatch):
     for name in og:
         err = rel_err(tg[name], og[name])
         assert err <= GRAD_TOL, f"{name}: rel err {err:.3e}"
+
+
+# gradient_clip_norm (training.py:824-825): clip_grad_norm_ over every parameter between backward
+# and the optimizers.  Dense ID tables (torch cannot clip the sparse ones: see
+# test_host_cpu.test_reference_clipping_rejects_sparse_id_gradients).  max_norm 0.05 clips every
+# step of this problem; 100 never does (coefficient 1).
+@pytest.mark.parametrize("max_norm", [0.05, 100.0], ids=["clipped", "unclipped"])
+def test_gradient_clipping_matches_oracle(max_norm):
+    from gpu_helpers import run_ttamm
+
+    shape = Shape(sparse=False)
+    prob = make_problem(shape, steps=3)
+    om, oo, ores = run_oracle(prob, gradient_clip_norm=max_norm)
+    tm, to, tres = run_ttamm(prob, gradient_clip_norm=max_norm)
+    for o, t in zip(ores, tres):
+        assert abs(t["total"] - o.total) <= 1e-5 * abs(o.total)
+    osd, tsd = om.state_dict(), tm.state_dict()
+    for n in osd:
+        d = (tsd[n].cpu() - osd[n]).abs().max().item()
+        assert d <= 1e-3 * 1e-3 * 50, f"{n}: max abs diff {d:.3e}"
+    ost, tst = named_optimizer_state(om, oo), named_optimizer_state(tm, to)
+    for n in ost:
+        assert rel_err(tst[n]["exp_avg"], ost[n]["exp_avg"]) <= 1e-4, n
+        assert rel_err(tst[n]["exp_avg_sq"], ost[n]["exp_avg_sq"]) <= 1e-4, n
+    if max_norm < 1:  # the clip was active: the moments differ from an unclipped run
+        om2, oo2, _ = run_oracle(prob)
+        ost2 = named_optimizer_state(om2, oo2)
+        assert any(rel_err(ost2[n]["exp_avg"], ost[n]["exp_avg"]) > 1e-2 for n in ost)
+
+
+def test_gradient_clipping_rejects_sparse_id_tables():
+    from gpu_helpers import run_ttamm
+
+    prob = make_problem(Shape(), steps=1)
+    with pytest.raises(NotImplementedError, match="sparse"):
+        run_ttamm(prob, gradient_clip_norm=1.0)

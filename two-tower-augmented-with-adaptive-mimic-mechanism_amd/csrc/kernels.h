@@ -420,9 +420,15 @@ struct RowUpdateArgs {
     int32_t dense_step;     // deferred mode (table.last_step): rows are updated in place and
                             // stamped current to this step
     const uint32_t* status; // step_poisoned(status): no write (ttamm.h TTAMM_STATUS_*)
+    const float* grad_scale; // clip_grad_norm_ coefficient on the device (null: 1)
     int lanes_per_row;      // set by the launcher
 };
 int launch_row_update(const RowUpdateArgs& a, hipStream_t s);
+// clip_grad_norm_ (training.py:824-825): sums of squares of the step's gradients into partials
+// (the tables' per-row gradient sums, and the dense tensors), then the clip coefficient
+// min(max_norm / (sqrt(sum) + 1e-6), 1) into *coef.  Fixed-order reductions.
+int rows_sumsq_blocks(int64_t n, int dim);
+int launch_rows_sumsq(const RowUpdateArgs& a, float* partials, hipStream_t s);
 
 // ---- deferred exact AdamW(g = 0) (ttamm.h ttamm_table.last_step) ------------------------
 // history[t % cap] holds the fp32 constants of dense step t; a row current to step l that is
@@ -498,8 +504,12 @@ struct DenseAdamArgs {
     int count;
     AdamConsts ad;
     const uint32_t* status;
+    const float* grad_scale;  // clip_grad_norm_ coefficient on the device (null: 1)
 };
 int launch_dense_adam(const DenseAdamArgs& a, hipStream_t s);
+constexpr int kDenseSumsqBlocks = 256;
+int launch_dense_sumsq(const DenseAdamArgs& a, float* partials, hipStream_t s);
+int launch_clip_coef(const float* partials, int n, float max_norm, float* coef, hipStream_t s);
 
 int launch_sparse_adam_rows(float* w, float* m, float* v, int dim, const int64_t* rows,
                             const float* grad, int64_t n, SparseConsts sp, hipStream_t s);

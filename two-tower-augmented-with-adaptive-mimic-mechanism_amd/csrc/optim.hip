@@ -415,12 +415,24 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArg
                 if (mimic) ga = addf4(ga, ldf4(A.piece_a + k * D + d));
             }
         }
+        if (A.grad_scale) {  // clip_grad_norm_: g *= coef (training.py:824-825)
+            const float c = *A.grad_scale;
+            ge = make_float4(ge.x * c, ge.y * c, ge.z * c, ge.w * c);
+            ga = make_float4(ga.x * c, ga.y * c, ga.z * c, ga.w * c);
+        }
+        // nn.Embedding padding_idx: no gradient into that row (SparseAdam: not in the sparse
+        // gradient at all, so the row is left as it is; AdamW: a zero gradient row)
+        const bool pad = A.id.has_padding_idx && key == A.id.padding_idx;
+        if (pad) ge = make_float4(0.f, 0.f, 0.f, 0.f);
         if (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM) {
-            each(ip, im, iv, ge, [&](float& p, float& m, float& v, float g) { sparse_adam_elem(p, m, v, g, A.sp); });
+            if (!pad)
+                each(ip, im, iv, ge, [&](float& p, float& m, float& v, float g) { sparse_adam_elem(p, m, v, g, A.sp); });
         } else {
             each(ip, im, iv, ge, [&](float& p, float& m, float& v, float g) { adam_elem(p, m, v, g, A.ad); });
         }
-        if (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM || A.id.last_step) {
+        if (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM && pad) {
+            // untouched
+        } else if (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM || A.id.last_step) {
             // SparseAdam, or deferred mode: the row was caught up before the forward
             stf4(A.id.weight + o, ip);
             stf4(A.id.exp_avg + o, im);
@@ -592,12 +604,82 @@ __global__ void dense_adam_kernel(DenseAdamArgs A, int64_t total) {
         }
         const DenseTensor& T = A.t[t];
         float p = T.p[off], m = T.m[off], v = T.v[off];
-        adam_elem(p, m, v, T.g[off], A.ad);
+        adam_elem(p, m, v, A.grad_scale ? T.g[off] * *A.grad_scale : T.g[off], A.ad);
         T.p[off] = p;
         T.m[off] = m;
         T.v[off] = v;
     }
 }
+
+// ---- clip_grad_norm_ (training.py:824-825; torch/nn/utils/clip_grad.py) ---------------------
+// sum over a tower table pair's touched rows of |sum of the row's gradient contributions|^2
+// (the dense gradient tensor's rows; the padding row's ID gradient is zero), one thread per
+// (row, 4 columns), the row's contributions summed in batch order
+__global__ void rows_sumsq_kernel(RowUpdateArgs A, float* __restrict__ partials) {
+    __shared__ float red[4];
+    const int dim4 = A.dim >> 2;
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t u = e / dim4;
+    float acc = 0.f;
+    if (u < A.n && u < (int64_t)A.n_unique[0]) {
+        const int d = (int)(e - u * dim4) * 4;
+        const int64_t k0 = A.seg_start[u], k1 = A.seg_start[u + 1];
+        const int64_t key = A.keys[k0];
+        const bool mimic = A.mimic.weight != nullptr;
+        float4 ge = make_float4(0.f, 0.f, 0.f, 0.f), ga = ge;
+        for (int64_t k = k0; k < k1; ++k) {
+            const int64_t r = A.rows[k];
+            ge = addf4(ge, ldf4(A.dE + r * A.ld_dE + d));
+            if (mimic) ga = addf4(ga, ldf4(dA_row(A, r) + d));
+        }
+        if (A.id.has_padding_idx && key == A.id.padding_idx) ge = make_float4(0.f, 0.f, 0.f, 0.f);
+        acc = (ge.x * ge.x + ge.y * ge.y) + (ge.z * ge.z + ge.w * ge.w) +
+              ((ga.x * ga.x + ga.y * ga.y) + (ga.z * ga.z + ga.w * ga.w));
+    }
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void dense_sumsq_kernel(DenseAdamArgs A, int64_t total, float* __restrict__ partials) {
+    __shared__ float red[4];
+    float acc = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t off = i;
+        int t = 0;
+        while (t < A.count - 1 && off >= A.t[t].n) {
+            off -= A.t[t].n;
+            ++t;
+        }
+        const float g = A.t[t].g[off];
+        acc += g * g;
+    }
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// one block: the partials summed in a fixed order (fp64), then torch's fp32 coefficient
+// clip_coef = max_norm / (total_norm + 1e-6), clamped to <= 1
+__global__ void clip_coef_kernel(const float* __restrict__ partials, int n, float max_norm, float* coef) {
+    __shared__ double red[256];
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) acc += (double)partials[i];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const float total = (float)sqrt(red[0]);
+        const float c = max_norm / (total + 1e-6f);
+        *coef = c < 1.0f ? c : 1.0f;
+    }
+}
+
 
 __global__ void sparse_adam_rows_kernel(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
                                         int dim, const int64_t* __restrict__ rows, const float* __restrict__ grad,
@@ -842,6 +924,34 @@ int launch_side_scatter(const int32_t* n_unique, const int32_t* keys, const int3
     if (n <= 0) return TTAMM_OK;
     hipLaunchKernelGGL(side_scatter_kernel, dim3(grid_for(n * dim)), dim3(256), 0, s, n_unique, keys, seg_start, side,
                        n, dim, t, status);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int rows_sumsq_blocks(int64_t n, int dim) { return (int)std::max<int64_t>(1, ceil_div(n * (dim / 4), 256)); }
+
+int launch_rows_sumsq(const RowUpdateArgs& a, float* partials, hipStream_t s) {
+    if (a.n <= 0) return TTAMM_OK;
+    TTAMM_REQUIRE(a.dim % 4 == 0, "clip: dim must be a multiple of 4");
+    hipLaunchKernelGGL(rows_sumsq_kernel, dim3((unsigned)rows_sumsq_blocks(a.n, a.dim)), dim3(256), 0, s, a, partials);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_dense_sumsq(const DenseAdamArgs& a, float* partials, hipStream_t s) {
+    int64_t total = 0;
+    for (int i = 0; i < a.count; ++i) total += a.t[i].n;
+    if (total == 0) {
+        TTAMM_HIP(hipMemsetAsync(partials, 0, kDenseSumsqBlocks * sizeof(float), s));
+        return TTAMM_OK;
+    }
+    hipLaunchKernelGGL(dense_sumsq_kernel, dim3(kDenseSumsqBlocks), dim3(256), 0, s, a, total, partials);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_clip_coef(const float* partials, int n, float max_norm, float* coef, hipStream_t s) {
+    hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(256), 0, s, partials, n, max_norm, coef);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

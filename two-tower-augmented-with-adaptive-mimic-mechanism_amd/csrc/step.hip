@@ -86,6 +86,11 @@ struct StepWs {
     int ib_parts = 0;
     bool cal_on = false;  // category-alignment loss this step
     CalArgs cal{};
+    // gradient clipping (ttamm_hparams.grad_clip_norm)
+    bool clip_on = false;
+    float* clip_partials = nullptr;
+    int clip_parts = 0;
+    float* clip_coef = nullptr;
 };
 
 // The category-alignment loss runs when categories are given and its weight is positive
@@ -303,6 +308,12 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         tower(A.item, ws.item, B * (1 + N), false, B);
     ws.score_blocks = score_blocks(B);
     ws.partials = ar.take<float>((size_t)ws.score_blocks * 3);
+    if (A.hp.grad_clip_norm > 0.0 && !shard) {
+        ws.clip_on = true;
+        ws.clip_parts = rows_sumsq_blocks(B, D) + rows_sumsq_blocks(B * (1 + N), D) + kDenseSumsqBlocks;
+        ws.clip_partials = ar.take<float>((size_t)ws.clip_parts);
+        ws.clip_coef = ar.take<float>(1);
+    }
     if (A.in_batch) {
         ws.ib_on = true;
         const int64_t Bc = shard ? global_batch(A) : B;
@@ -940,8 +951,8 @@ int join_grouping(hipStream_t s, hipStream_t aux) {
     return TTAMM_OK;
 }
 
-int tower_optimizer_rows(const ttamm_tower& t, TowerWs& w, int D, bool mimic, const SparseConsts& sp,
-                         const AdamConsts& ad, const Deferred& df, hipStream_t s) {
+RowUpdateArgs row_update_args(const ttamm_tower& t, TowerWs& w, int D, bool mimic, const SparseConsts& sp,
+                              const AdamConsts& ad, const Deferred& df, const float* grad_scale) {
     RowUpdateArgs ru;
     std::memset(&ru, 0, sizeof(ru));
     ru.n = w.R;
@@ -974,7 +985,12 @@ int tower_optimizer_rows(const ttamm_tower& t, TowerWs& w, int D, bool mimic, co
     ru.ad = ad;
     ru.dense_step = df.step;
     ru.status = df.status;
-    return launch_row_update(ru, s);
+    ru.grad_scale = grad_scale;
+    return ru;
+}
+int tower_optimizer_rows(const ttamm_tower& t, TowerWs& w, int D, bool mimic, const SparseConsts& sp,
+                         const AdamConsts& ad, const Deferred& df, hipStream_t s, const float* grad_scale) {
+    return launch_row_update(row_update_args(t, w, D, mimic, sp, ad, df, grad_scale), s);
 }
 void add_seg(SweepArgs& sw, const ttamm_table& tb) {
     sw.seg[sw.count].p = tb.weight;
@@ -988,11 +1004,12 @@ void add_seg(SweepArgs& sw, const ttamm_table& tb) {
 // batch did not touch: eagerly, one sweep over the dense-group tables and a scatter of the
 // staged touched rows; deferred, the replay of this step's 1/slices of the rows to `step`.
 int table_updates(const ttamm_tower* T[2], TowerWs* W[2], int n, int D, bool mimic, const SparseConsts& sp,
-                  const AdamConsts& ad, const Deferred& df, void* const events[2], hipStream_t s, hipStream_t aux) {
+                  const AdamConsts& ad, const Deferred& df, void* const events[2], hipStream_t s, hipStream_t aux,
+                  const float* grad_scale = nullptr) {
     int rc;
     if ((rc = join_grouping(s, aux))) return rc;
     for (int k = 0; k < n; ++k)
-        if ((rc = tower_optimizer_rows(*T[k], *W[k], D, mimic, sp, ad, df, s))) return rc;
+        if ((rc = tower_optimizer_rows(*T[k], *W[k], D, mimic, sp, ad, df, s, grad_scale))) return rc;
     if (df.on) {
         if (df.slice_on_aux) return TTAMM_OK;  // replayed on the aux stream (replay_slice_aux)
         return replay_slice(T, n, mimic, df, df.step, 1, events, s);
@@ -1023,11 +1040,13 @@ int table_updates(const ttamm_tower* T[2], TowerWs* W[2], int n, int D, bool mim
     return TTAMM_OK;
 }
 
-int dense_update(const ttamm_tower* T[2], TowerWs* W[2], const AdamConsts& ad, const uint32_t* status, hipStream_t s) {
+DenseAdamArgs dense_args(const ttamm_tower* T[2], TowerWs* W[2], const AdamConsts& ad, const uint32_t* status,
+                         const float* grad_scale) {
     DenseAdamArgs da;
     std::memset(&da, 0, sizeof(da));
     da.ad = ad;
     da.status = status;
+    da.grad_scale = grad_scale;
     auto add_dense = [&](float* p, float* m, float* v, const float* g, int64_t n) {
         da.t[da.count++] = DenseTensor{p, m, v, g, n};
     };
@@ -1049,7 +1068,30 @@ int dense_update(const ttamm_tower* T[2], TowerWs* W[2], const AdamConsts& ad, c
             }
         }
     }
-    return launch_dense_adam(da, s);
+    return da;
+}
+int dense_update(const ttamm_tower* T[2], TowerWs* W[2], const AdamConsts& ad, const uint32_t* status, hipStream_t s,
+                 const float* grad_scale = nullptr) {
+    return launch_dense_adam(dense_args(T, W, ad, status, grad_scale), s);
+}
+
+// clip_grad_norm_(model.parameters(), max_norm) (training.py:824-825): the global gradient norm
+// over both towers' table rows and dense tensors -> ws.clip_coef, read by the optimizer kernels
+int clip_coefficient(const ttamm_tower* T[2], TowerWs* W[2], int D, bool mimic, const SparseConsts& sp,
+                     const AdamConsts& ad, const Deferred& df, const ttamm_step_args& A, StepWs& ws, hipStream_t s,
+                     hipStream_t aux) {
+    int rc;
+    if ((rc = join_grouping(s, aux))) return rc;  // the row grouping
+    int off = 0;
+    for (int k = 0; k < 2; ++k) {
+        const RowUpdateArgs ru = row_update_args(*T[k], *W[k], D, mimic, sp, ad, df, nullptr);
+        if ((rc = launch_rows_sumsq(ru, ws.clip_partials + off, s))) return rc;
+        off += rows_sumsq_blocks(W[k]->R, D);
+    }
+    if ((rc = launch_dense_sumsq(dense_args(T, W, ad, A.status, nullptr), ws.clip_partials + off, s))) return rc;
+    off += kDenseSumsqBlocks;
+    TTAMM_REQUIRE(off <= ws.clip_parts, "clip: partials overflow");
+    return launch_clip_coef(ws.clip_partials, off, (float)A.hp.grad_clip_norm, ws.clip_coef, s);
 }
 
 // Deferred mode is all-or-nothing over the dense-group tables of both towers.
@@ -1112,6 +1154,12 @@ int validate_step(const ttamm_step_args& A) {
                       "Adaptive mimic requires user and item embedding dimensions to match.");
     }
     TTAMM_REQUIRE(A.hp.dense_step >= 1 && A.hp.sparse_step >= 1, "optimizer step counts must be >= 1");
+    if (A.hp.grad_clip_norm > 0.0) {
+        TTAMM_REQUIRE(!sharded(A), "gradient clipping is not implemented in the row-sharded step");
+        TTAMM_REQUIRE(A.user.id.optimizer == TTAMM_OPT_DENSE && A.item.id.optimizer == TTAMM_OPT_DENSE,
+                      "gradient clipping needs dense ID tables (clip_grad_norm_ cannot take the sparse gradients "
+                      "of sparse ID tables)");
+    }
     TTAMM_REQUIRE(A.row_base >= 0 && (A.global_batch == 0 || A.global_batch >= A.row_base + A.b.batch),
                   "row_base / global_batch out of range");
     if (!sharded(A)) return TTAMM_OK;
@@ -1364,8 +1412,9 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         if (!shard) {
             // ---- the whole backward + optimizers in one process --------------------------------
             if ((rc = tower_backward(T, W, D, s, 2))) return rc;
-            if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, s, aux))) return rc;
-            return dense_update(T, W, ad, A.status, s);
+            if (ws.clip_on && (rc = clip_coefficient(T, W, D, mimic, sp, ad, df, A, ws, s, aux))) return rc;
+            if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, s, aux, ws.clip_coef))) return rc;
+            return dense_update(T, W, ad, A.status, s, ws.clip_coef);
         }
         if (ph & TTAMM_PHASE_USER) {
             if ((rc = tower_backward(T, W, D, s, 1))) return rc;

@@ -57,6 +57,8 @@ class Table(ctypes.Structure):
         ("dim", c_i32),
         ("optimizer", c_i32),
         ("last_step", c_vp),
+        ("has_padding_idx", c_i32),
+        ("padding_idx", c_i64),
     ]
 
 
@@ -95,6 +97,7 @@ class HParams(ctypes.Structure):
         ("lambda_mimic_user", c_d),
         ("lambda_mimic_item", c_d),
         ("lambda_category_alignment", c_d),
+        ("grad_clip_norm", c_d),
     ]
 
 
@@ -161,7 +164,7 @@ class StepArgs(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 15  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 16  # ttamm.h TTAMM_ABI_VERSION
 G0_EXACT = 0  # ttamm.h TTAMM_G0_EXACT
 G0_FAST = 1  # ttamm.h TTAMM_G0_FAST
 

@@ -324,14 +324,17 @@ def describe_tower(
 ) -> _lib.Tower:
     if tower.fusion == "concat":
         raise NotImplementedError("ttamm: 'concat' fusion is not on the MI355X hot path")
-    if tower.embedding.padding_idx is not None or tower.embedding.max_norm is not None:
-        raise NotImplementedError("ttamm: padding_idx / max_norm embeddings are not implemented")
+    if tower.embedding.max_norm is not None:
+        raise NotImplementedError("ttamm: max_norm embeddings are not implemented")
     s = _lib.Tower()
     emb = tower.embedding.weight
     s.id.weight = emb.data_ptr()
     s.id.rows = emb.shape[0]
     s.id.dim = emb.shape[1]
     s.id.optimizer = id_optimizer
+    if tower.embedding.padding_idx is not None:  # nn.Embedding normalises it to [0, rows)
+        s.id.has_padding_idx = 1
+        s.id.padding_idx = int(tower.embedding.padding_idx)
     if state is not None:
         st = state[id(emb)]
         s.id.exp_avg = st["exp_avg"].data_ptr()

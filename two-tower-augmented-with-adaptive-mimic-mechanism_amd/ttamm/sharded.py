@@ -321,6 +321,10 @@ class ShardedTrainStep(FusedTrainStep):
 
     def __init__(self, model, optimizers, *, world_size: int, rank: int, num_items: int,
                  comm: Callable[[Program], Any] | None = None, group_towers: bool = True, **kw: Any) -> None:
+        for enc in (model.user_encoder, model.item_encoder):
+            if enc.embedding.padding_idx is not None:
+                # a global padding id lives on one owner as a local row: not mapped here
+                raise NotImplementedError("ttamm: padding_idx is not implemented in the row-sharded step")
         self.own = RowOwnership(world_size, rank)
         self.comm = comm
         # True: both towers' forward in one set of grouped launches, then the (t | a) exchange;

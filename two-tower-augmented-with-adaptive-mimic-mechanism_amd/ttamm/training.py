@@ -128,6 +128,7 @@ class FusedTrainStep:
         item_category_tensor: torch.Tensor | None = None,
         major_category_id: int | None = None,
         in_batch_negatives: bool = False,
+        gradient_clip_norm: float | None = None,
     ) -> None:
         # in_batch_negatives: ttamm's in-batch mode (ttamm.h ttamm_step_args.in_batch; not the
         # reference's behaviour): every user is also scored against every positive of the batch
@@ -253,6 +254,16 @@ class FusedTrainStep:
         # category-alignment loss (training.py:530-579, :805-820): the reference returns 0
         # without a category tensor / major id, so the fused step runs it only with both
         args.hp.lambda_category_alignment = float(lw.get("category_alignment", 0.0))
+        # clip_grad_norm_(model.parameters(), gradient_clip_norm) between backward and the
+        # optimizers (training.py:824-825).  torch's clip_grad_norm_ cannot take the sparse
+        # gradients of sparse ID tables (linalg_vector_norm has no sparse kernel: the reference
+        # raises NotImplementedError there), so the fused step clips dense-ID models only
+        if gradient_clip_norm is not None and gradient_clip_norm > 0:
+            if any(self.towers[n][2] == _lib.OPT_SPARSE_ADAM for n in ("user", "item")):
+                raise NotImplementedError(
+                    "gradient clipping with sparse ID embeddings: clip_grad_norm_ cannot take sparse gradients "
+                    "(torch: 'aten::linalg_vector_norm' has no SparseCPU/SparseCUDA kernel)")
+            args.hp.grad_clip_norm = float(gradient_clip_norm)
         self.item_categories = None
         if item_category_tensor is not None and major_category_id is not None and \
                 args.hp.lambda_category_alignment > 0:
@@ -529,8 +540,6 @@ def train_one_epoch(
     if not isinstance(criterion, nn.BCEWithLogitsLoss) or criterion.reduction != "mean" or \
             criterion.weight is not None or criterion.pos_weight is not None:
         raise NotImplementedError("ttamm: the step implements BCEWithLogitsLoss(reduction='mean')")
-    if gradient_clip_norm is not None and gradient_clip_norm > 0:
-        raise NotImplementedError("ttamm: gradient clipping is not implemented in the fused step")
     lw = dict(loss_weights or {})
     if num_items != model.item_encoder.num_embeddings:
         raise ValueError("num_items does not match the item embedding table")
@@ -548,7 +557,7 @@ def train_one_epoch(
                 user_features=user_features, item_features=item_features, loss_weights=lw,
                 max_batch=max(int(size), users.numel()),
                 item_category_tensor=item_category_tensor, major_category_id=major_category_id,
-                in_batch_negatives=in_batch_negatives,
+                in_batch_negatives=in_batch_negatives, gradient_clip_norm=gradient_clip_norm,
             )
         neg = masks = None
         if batch_hook is not None:
