@@ -266,9 +266,12 @@ __device__ __forceinline__ void epilogue8_hidden(const KArg(GemmProblem) & P, fl
         }
         x[e] = hv;
     }
+    // plain (write-back) stores: a wave's two store instructions each cover every other 16 B of
+    // its rows' span, and L2 merges the halves into whole lines; non-temporal stores of the halves
+    // doubled the HBM write bytes (PMC WRITE_SIZE 82 MB vs 44 MB of hidden rows at C2)
     float* out = P.C + (int64_t)split * P.slab_stride + (int64_t)row * P.ldc + col;
-    st4(out, make_float4(x[0], x[1], x[2], x[3]));
-    if (hi_ok) st4(out + 4, make_float4(x[4], x[5], x[6], x[7]));
+    *reinterpret_cast<float4*>(out) = make_float4(x[0], x[1], x[2], x[3]);
+    if (hi_ok) *reinterpret_cast<float4*>(out + 4) = make_float4(x[4], x[5], x[6], x[7]);
 }
 
 template <class CF, int E, bool BF>
