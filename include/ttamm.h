@@ -45,6 +45,9 @@ extern "C" {
 #define TTAMM_FUSION_IDENTITY 0
 #define TTAMM_FUSION_SUM 1
 #define TTAMM_FUSION_GATED 2
+/* concat (encoders.py:211-215,242-244): t = projection([e | f]); the projection (Linear 2D -> D,
+ * output_dim == embedding_dim) rides in ttamm_tower.gate[0] */
+#define TTAMM_FUSION_CONCAT 3
 
 /* Which optimizer owns a row table (training.py:276-309, :1311-1350). */
 #define TTAMM_OPT_SPARSE_ADAM 0 /* nn.Embedding(sparse=True) -> torch.optim.SparseAdam      */

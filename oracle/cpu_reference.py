@@ -36,7 +36,8 @@ class FeatureFusionGate(nn.Module):  # encoders.py:149-168
 
 
 class OracleTower(nn.Module):  # encoders.py:171-219 (constructor) — forward is tower_forward below
-    def __init__(self, embedding: nn.Embedding, feature_encoder, fusion: str, gate, matmul_dtype: str = "fp32") -> None:
+    def __init__(self, embedding: nn.Embedding, feature_encoder, fusion: str, gate, matmul_dtype: str = "fp32",
+                 output_dim: int | None = None) -> None:
         super().__init__()
         # not in the reference: the "bf16 towers" precision of BASELINE config C5 (see _bf16_linear)
         self.matmul_dtype = matmul_dtype
@@ -47,6 +48,11 @@ class OracleTower(nn.Module):  # encoders.py:171-219 (constructor) — forward i
         self.num_embeddings = embedding.num_embeddings
         self.id_dim = embedding.embedding_dim
         self.output_dim = self.id_dim
+        if self.fusion == "concat":  # encoders.py:211-216
+            joint = self.id_dim + feature_encoder.output_dim
+            self.projection = nn.Linear(joint, int(output_dim or joint))
+            nn.init.xavier_uniform_(self.projection.weight)
+            self.output_dim = self.projection.out_features
 
 
 class OracleMimic(nn.Module):  # adaptive_mimic.py:20-38
@@ -110,7 +116,8 @@ def build_tower(cfg: Mapping[str, Any], *, num_embeddings: int, feature_dim: int
         gate = FeatureFusionGate(emb.embedding_dim, (cfg.get("adaptive_mimic") or {}).get("hidden_dim"))
         fusion = "gated"
     mm = str(cfg.get("matmul_dtype", "fp32")).lower()
-    return OracleTower(emb, fe, fusion, gate, "bf16" if mm in ("bf16", "bfloat16") else "fp32")
+    return OracleTower(emb, fe, fusion, gate, "bf16" if mm in ("bf16", "bfloat16") else "fp32",
+                       output_dim=cfg.get("output_dim"))
 
 
 def build_model(
@@ -191,6 +198,8 @@ def tower_forward(tower: OracleTower, idx: torch.Tensor, feats: torch.Tensor | N
     f = feature_forward(tower.feature_encoder, feats, keep_masks, training, bf16)  # :233
     if tower.fusion == "sum":
         return e + f  # :240
+    if tower.fusion == "concat":
+        return _linear(tower.projection, torch.cat([e, f], dim=-1), bf16)  # :242-244
     g1, _, g2, _ = tower.adaptive_mimic.gate_network  # Linear, ReLU, Linear, Sigmoid (:157-162)
     gate = torch.sigmoid(_linear(g2, torch.relu(_linear(g1, torch.cat([e, f], dim=-1), bf16)), bf16))  # :164-168
     return gate * e + (1.0 - gate) * f

@@ -28,6 +28,7 @@ class Shape:
     hidden_dims: tuple = (16,)
     matmul_dtype: str = "fp32"
     padding_idx: int | None = None  # nn.Embedding padding_idx of both ID tables (encoders.py:47)
+    fusion: str = "gated"  # TowerEncoder fusion (encoders.py:203): gated / sum / concat
 
     def tower_cfg(self) -> dict:
         params = {"embedding_dim": self.D, "sparse": self.sparse}
@@ -39,7 +40,8 @@ class Shape:
             "id_embedding": {"params": params, "init": {"type": "normal", "std": 0.02}},
             "feature_encoder": {"type": "mlp", "hidden_dims": list(self.hidden_dims), "activation": "relu",
                                 "output_dim": self.D, "dropout": self.dropout},
-            "fusion": "gated",
+            "fusion": self.fusion,
+            "output_dim": self.D,  # the concat projection's width (encoders.py:211)
             "adaptive_mimic": {"hidden_dim": self.gate_hidden} if self.gate_hidden else {},
         }
 

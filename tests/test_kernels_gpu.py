@@ -52,8 +52,9 @@ def test_gather_rows_strided_output_bit_exact():
 
 
 @pytest.mark.parametrize("shape", [Shape(dropout=0.0), Shape(F=605, H=192, D=96, hidden_dims=(192,), dropout=0.0),
-                                   Shape(F=37, D=12, gate_hidden=20, hidden_dims=(24, 16), dropout=0.0)],
-                         ids=["tiny", "c2dims", "odd"])
+                                   Shape(F=37, D=12, gate_hidden=20, hidden_dims=(24, 16), dropout=0.0),
+                                   Shape(dropout=0.0, fusion="sum"), Shape(dropout=0.0, fusion="concat")],
+                         ids=["tiny", "c2dims", "odd", "sum", "concat"])
 def test_tower_forward_eval_matches_oracle(shape):
     from gpu_helpers import ttamm_model_from
 

@@ -29,8 +29,12 @@ def _grads_by_name(model, opts):
         Shape(sparse=False),
         Shape(padding_idx=5),
         Shape(sparse=False, padding_idx=5),
+        Shape(fusion="sum"),
+        Shape(fusion="concat"),
+        Shape(U=50, I=300, F=37, H=24, D=12, B=40, N=3, hidden_dims=(24, 16), fusion="concat"),
     ],
-    ids=["tiny", "nodrop", "odd", "2hidden", "nomimic", "dense-id", "padding", "dense-id-padding"],
+    ids=["tiny", "nodrop", "odd", "2hidden", "nomimic", "dense-id", "padding", "dense-id-padding", "sum", "concat",
+         "concat-odd"],
 )
 def test_step_gradients_match_oracle(shape):
     from gpu_helpers import run_ttamm
@@ -54,8 +58,9 @@ def test_step_gradients_match_oracle(shape):
         assert torch.equal(q.cpu(), p), n
 
 
-@pytest.mark.parametrize("shape", [Shape(), Shape(sparse=False), Shape(padding_idx=5), Shape(sparse=False, padding_idx=5)],
-                         ids=["tiny", "dense-id", "padding", "dense-id-padding"])
+@pytest.mark.parametrize("shape", [Shape(), Shape(sparse=False), Shape(padding_idx=5), Shape(sparse=False, padding_idx=5),
+                                   Shape(fusion="concat")],
+                         ids=["tiny", "dense-id", "padding", "dense-id-padding", "concat"])
 def test_three_steps_match_oracle(shape):
     from gpu_helpers import run_ttamm
 

@@ -106,6 +106,12 @@ inline int round8(int x) { return (x + 7) / 8 * 8; }
 bool uses_w16(const ttamm_tower& T) {
     return T.matmul_bf16 && T.features_bf16 != nullptr && T.fusion != TTAMM_FUSION_IDENTITY && T.n_linear > 0;
 }
+// gated and concat towers keep [e | f] rows (the gate's / projection's input) and their gradient
+bool uses_ef(const ttamm_tower& T) { return T.fusion == TTAMM_FUSION_GATED || T.fusion == TTAMM_FUSION_CONCAT; }
+// Linear layers after the feature encoder: the gate's two, or the concat projection
+int fusion_linears(const ttamm_tower& T) {
+    return T.fusion == TTAMM_FUSION_GATED ? 2 : T.fusion == TTAMM_FUSION_CONCAT ? 1 : 0;
+}
 bool needs_wpad(const ttamm_tower& T) {
     return T.fusion != TTAMM_FUSION_IDENTITY && T.n_linear > 0 && T.linear[0].in_features % 4 != 0;
 }
@@ -120,7 +126,7 @@ int validate_tower(const ttamm_tower& T, const char* name, int D, bool training)
     TTAMM_REQUIRE(T.id.rows > 0, n + ": empty embedding table");
     TTAMM_REQUIRE(T.id.rows < (int64_t(1) << 31), n + ": tables of 2^31 rows or more are not supported (int32 row keys)");
     TTAMM_REQUIRE(T.n_linear >= 0 && T.n_linear <= TTAMM_MAX_LINEAR, n + ": too many feature-encoder layers");
-    TTAMM_REQUIRE(T.fusion >= TTAMM_FUSION_IDENTITY && T.fusion <= TTAMM_FUSION_GATED, n + ": unsupported fusion");
+    TTAMM_REQUIRE(T.fusion >= TTAMM_FUSION_IDENTITY && T.fusion <= TTAMM_FUSION_CONCAT, n + ": unsupported fusion");
     if (T.fusion != TTAMM_FUSION_IDENTITY) {
         TTAMM_REQUIRE(T.features != nullptr && T.feat_dim > 0, n + ": fusion needs feature rows");
         TTAMM_REQUIRE(T.feat_ld >= T.feat_dim, n + ": feature row stride too small");
@@ -141,7 +147,8 @@ int validate_tower(const ttamm_tower& T, const char* name, int D, bool training)
         }
         const int fo = T.n_linear ? T.linear[T.n_linear - 1].out_features : T.feat_dim;
         TTAMM_REQUIRE(fo == D,
-                      n + ": Feature encoder output dimension must equal embedding dimension for 'sum' or 'gated' fusion.");
+                      n + ": Feature encoder output dimension must equal embedding dimension for 'sum', 'gated' or "
+                          "'concat' fusion.");
         TTAMM_REQUIRE(T.dropout >= 0.f && T.dropout < 1.f, n + ": dropout must be in [0, 1)");
     }
     if (T.fusion == TTAMM_FUSION_GATED) {
@@ -154,6 +161,15 @@ int validate_tower(const ttamm_tower& T, const char* name, int D, bool training)
         TTAMM_REQUIRE(G1.in_features == 2 * D && G2.out_features == D && G2.in_features == G1.out_features,
                       n + ": gate shapes do not match the embedding dimension");
         TTAMM_REQUIRE(G1.out_features % 4 == 0, n + ": ttamm requires the gate hidden width % 4 == 0");
+    }
+    if (T.fusion == TTAMM_FUSION_CONCAT) {
+        const ttamm_linear& P = T.gate[0];
+        TTAMM_REQUIRE(P.weight && P.bias, n + ": concat projection parameters missing");
+        if (training)
+            TTAMM_REQUIRE(P.weight_exp_avg && P.weight_exp_avg_sq && P.bias_exp_avg && P.bias_exp_avg_sq,
+                          n + ": concat projection optimizer state missing");
+        TTAMM_REQUIRE(P.in_features == 2 * D && P.out_features == D,
+                      n + ": concat projection must map [e | f] (2 x embedding dim) to the embedding dim");
     }
     return TTAMM_OK;
 }
@@ -169,9 +185,8 @@ size_t tower_grad_floats(const ttamm_tower& T) {
     if (T.fusion == TTAMM_FUSION_IDENTITY) return 0;
     for (int l = 0; l < T.n_linear; ++l)
         n += pad64((size_t)T.linear[l].out_features * T.linear[l].in_features) + pad64(T.linear[l].out_features);
-    if (T.fusion == TTAMM_FUSION_GATED)
-        for (int q = 0; q < 2; ++q)
-            n += pad64((size_t)T.gate[q].out_features * T.gate[q].in_features) + pad64(T.gate[q].out_features);
+    for (int q = 0; q < fusion_linears(T); ++q)
+        n += pad64((size_t)T.gate[q].out_features * T.gate[q].in_features) + pad64(T.gate[q].out_features);
     return n;
 }
 void carve_grads(const ttamm_tower& T, TowerWs& w, float*& cur) {
@@ -182,8 +197,7 @@ void carve_grads(const ttamm_tower& T, TowerWs& w, float*& cur) {
         w.gb[l] = cur;
         cur += pad64(T.linear[l].out_features);
     }
-    if (T.fusion == TTAMM_FUSION_GATED)
-        for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < fusion_linears(T); ++q) {
             w.ggw[q] = cur;
             cur += pad64((size_t)T.gate[q].out_features * T.gate[q].in_features);
             w.ggb[q] = cur;
@@ -198,8 +212,7 @@ int wgrad_shapes(const ttamm_tower& T, int64_t R, WgradShape* out) {
     int n = 0;
     if (T.fusion == TTAMM_FUSION_IDENTITY) return 0;
     for (int l = 0; l < T.n_linear; ++l) out[n++] = WgradShape{R, T.linear[l].out_features, T.linear[l].in_features};
-    if (T.fusion == TTAMM_FUSION_GATED)
-        for (int q = 0; q < 2; ++q) out[n++] = WgradShape{R, T.gate[q].out_features, T.gate[q].in_features};
+    for (int q = 0; q < fusion_linears(T); ++q) out[n++] = WgradShape{R, T.gate[q].out_features, T.gate[q].in_features};
     return n;
 }
 
@@ -252,14 +265,16 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
             w.dhid[l] = ar.take<float>((size_t)R * T.linear[l].out_features);
         }
         const int Hg = T.fusion == TTAMM_FUSION_GATED ? T.gate[0].out_features : 0;
-        if (T.fusion == TTAMM_FUSION_GATED) {
+        if (uses_ef(T)) {
             w.ef = ar.take<float>((size_t)R * 2 * D);
             w.dEF = ar.take<float>((size_t)R * 2 * D);
+        }
+        if (T.fusion == TTAMM_FUSION_GATED) {
             w.z = ar.take<float>((size_t)R * Hg);
             w.dz = ar.take<float>((size_t)R * Hg);
             w.g = ar.take<float>((size_t)R * D);
             w.dq = ar.take<float>((size_t)R * D);
-        } else {
+        } else if (!uses_ef(T)) {
             w.e = ar.take<float>((size_t)R * D);
             if (T.fusion == TTAMM_FUSION_SUM) w.f = ar.take<float>((size_t)R * D);
         }
@@ -283,8 +298,8 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
                     wgrad_slab_floats((int)R, L.out_features, L.in_features, w.wgrad_rps[wgrad_class(L.out_features)]));
             }
         }
-        if (T.fusion == TTAMM_FUSION_GATED) {
-            for (int q = 0; q < 2; ++q) {
+        {
+            for (int q = 0; q < fusion_linears(T); ++q) {
                 const ttamm_linear& L = T.gate[q];
                 w.slab[TTAMM_MAX_LINEAR + q] =
                     ar.take<float>(wgrad_slab_floats((int)R, L.out_features, L.in_features,
@@ -460,8 +475,8 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
         for (int k = 0; k < ntowers; ++k) {
             const ttamm_tower& t = *T[k];
             TowerWs& w = *W[k];
-            float* dst = t.fusion == TTAMM_FUSION_GATED ? w.ef : w.e;
-            const int64_t ld = t.fusion == TTAMM_FUSION_GATED ? 2 * D : D;
+            float* dst = uses_ef(t) ? w.ef : w.e;
+            const int64_t ld = uses_ef(t) ? 2 * D : D;
             if ((rc = launch_gather_rows(t.id.weight, t.id.rows, D, w.idx, w.R, dst, ld, s))) return rc;
         }
         // feature encoder layers
@@ -519,7 +534,7 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
                     set_keys(p, w);
                 } else {
                     p.epi = EPI_STORE;
-                    if (t.fusion == TTAMM_FUSION_GATED) {
+                    if (uses_ef(t)) {
                         p.C = w.ef + D;
                         p.ldc = 2 * D;
                     } else {
@@ -547,11 +562,28 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
     const bool fused_gate = gate_group(T, W, ntowers, D, mimic, ga);
     if (fused_gate && ga.count > 0)
         if ((rc = launch_gate(ga, false, s))) return rc;
-    Batcher g1, g2;
+    Batcher g1, g2, gc;
     for (int k = 0; k < ntowers; ++k) {
         const ttamm_tower& t = *T[k];
         TowerWs& w = *W[k];
         const float* table = mimic ? t.mimic.weight : nullptr;
+        if (t.fusion == TTAMM_FUSION_CONCAT) {  // t = [e | f] P^T + b (encoders.py:242-244)
+            GemmProblem p = gp_base();
+            p.bf16 = t.matmul_bf16;
+            p.A = w.ef;
+            p.lda = 2 * D;
+            p.B = t.gate[0].weight;
+            p.ldb = 2 * D;
+            p.M = (int)w.R;
+            p.N = D;
+            p.K = 2 * D;
+            p.bias = t.gate[0].bias;
+            p.epi = EPI_STORE;
+            p.C = w.t;
+            p.ldc = w.t_ld;
+            gc.add(p);
+            continue;
+        }
         if (t.fusion == TTAMM_FUSION_GATED) {
             if (fused_gate) continue;
             const int Hg = t.gate[0].out_features;
@@ -600,6 +632,15 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
     }
     if ((rc = g1.run(s))) return rc;
     if ((rc = g2.run(s))) return rc;
+    if ((rc = gc.run(s))) return rc;
+    for (int k = 0; k < ntowers; ++k) {  // concat: a = A[idx], aug = t + a (in place on t)
+        const ttamm_tower& t = *T[k];
+        TowerWs& w = *W[k];
+        if (t.fusion != TTAMM_FUSION_CONCAT) continue;
+        if ((rc = launch_combine(w.t, w.t_ld, nullptr, D, mimic ? t.mimic.weight : nullptr, t.mimic.rows, w.idx, w.R,
+                                 D, w.t, w.a, w.t_ld, w.aug, s)))
+            return rc;
+    }
     return TTAMM_OK;
 }
 
@@ -653,6 +694,25 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
         q.ld_aux2 = D;
         b2.add(q);
     }
+    for (int k = 0; k < ntowers; ++k) {  // concat: d[e | f] = dT P
+        const ttamm_tower& t = *T[k];
+        TowerWs& w = *W[k];
+        if (t.fusion != TTAMM_FUSION_CONCAT) continue;
+        GemmProblem q = gp_base();
+        q.bf16 = t.matmul_bf16;
+        q.A = w.dT;
+        q.lda = w.dT_ld;
+        q.B = t.gate[0].weight;  // [D, 2D] = [K, N]
+        q.ldb = 2 * D;
+        q.b_kn = 1;
+        q.M = (int)w.R;
+        q.N = 2 * D;
+        q.K = D;
+        q.epi = EPI_STORE;
+        q.C = w.dEF;
+        q.ldc = 2 * D;
+        b2.add(q);
+    }
     if ((rc = b1.run(s))) return rc;
     if ((rc = b2.run(s))) return rc;
     // MLP dgrad chain (layers L-1 .. 1)
@@ -671,8 +731,8 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
             GemmProblem p = gp_base();
             p.bf16 = t.matmul_bf16;
             if (l == t.n_linear - 1) {
-                p.A = t.fusion == TTAMM_FUSION_GATED ? w.dEF + D : w.dT;
-                p.lda = t.fusion == TTAMM_FUSION_GATED ? 2 * D : w.dT_ld;
+                p.A = uses_ef(t) ? w.dEF + D : w.dT;
+                p.lda = uses_ef(t) ? 2 * D : w.dT_ld;
             } else {
                 p.A = w.dhid[l];
                 p.lda = L.out_features;
@@ -732,13 +792,29 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
             g1.rows_per_split = w.wgrad_rps[wgrad_class(g1.M)];
             wb.p[wb.count++] = g1;
         }
+        if (t.fusion == TTAMM_FUSION_CONCAT) {  // dP = dT^T [e | f], db = sum dT
+            WgradProblem pp{};
+            pp.bf16 = t.matmul_bf16;
+            pp.dY = w.dT;
+            pp.ld_dy = w.dT_ld;
+            pp.X = w.ef;
+            pp.ld_x = 2 * D;
+            pp.R = (int)w.R;
+            pp.M = D;
+            pp.N = 2 * D;
+            pp.grad_w = w.ggw[0];
+            pp.grad_b = w.ggb[0];
+            pp.slab = w.slab[TTAMM_MAX_LINEAR];
+            pp.rows_per_split = w.wgrad_rps[wgrad_class(pp.M)];
+            wb.p[wb.count++] = pp;
+        }
         for (int l = t.n_linear - 1; l >= 0; --l) {
             const ttamm_linear& L = t.linear[l];
             WgradProblem p{};
             p.bf16 = t.matmul_bf16;
             if (l == t.n_linear - 1) {
-                p.dY = t.fusion == TTAMM_FUSION_GATED ? w.dEF + D : w.dT;
-                p.ld_dy = t.fusion == TTAMM_FUSION_GATED ? 2 * D : w.dT_ld;
+                p.dY = uses_ef(t) ? w.dEF + D : w.dT;
+                p.ld_dy = uses_ef(t) ? 2 * D : w.dT_ld;
             } else {
                 p.dY = w.dhid[l];
                 p.ld_dy = L.out_features;
@@ -962,7 +1038,7 @@ RowUpdateArgs row_update_args(const ttamm_tower& t, TowerWs& w, int D, bool mimi
     ru.keys = w.co.keys_out;
     ru.rows = w.co.vals_out;
     ru.seglong = w.co.seglong;
-    if (t.fusion == TTAMM_FUSION_GATED) {
+    if (uses_ef(t)) {
         ru.dE = w.dEF;
         ru.ld_dE = 2 * D;
     } else {
@@ -1059,8 +1135,8 @@ DenseAdamArgs dense_args(const ttamm_tower* T[2], TowerWs* W[2], const AdamConst
             add_dense(L.weight, L.weight_exp_avg, L.weight_exp_avg_sq, w.gw[l], (int64_t)L.out_features * L.in_features);
             add_dense(L.bias, L.bias_exp_avg, L.bias_exp_avg_sq, w.gb[l], L.out_features);
         }
-        if (t.fusion == TTAMM_FUSION_GATED) {
-            for (int q = 0; q < 2; ++q) {
+        {
+            for (int q = 0; q < fusion_linears(t); ++q) {
                 const ttamm_linear& L = t.gate[q];
                 add_dense(L.weight, L.weight_exp_avg, L.weight_exp_avg_sq, w.ggw[q],
                           (int64_t)L.out_features * L.in_features);
@@ -1546,7 +1622,7 @@ int tower_forward_eval(const ttamm_tower& T, const int64_t* idx, const int64_t* 
         w.idx = idx;
         w.fidx = fidx;
     }
-    if (T.fusion == TTAMM_FUSION_GATED) {
+    if (uses_ef(T)) {
         w.ef = efbuf;
         w.z = zbuf;
         w.g = gbuf;

@@ -19,7 +19,7 @@ TTAMM_E_RUNTIME = 2
 TTAMM_E_HIP = 3
 
 MAX_LINEAR = 4
-FUSION_IDENTITY, FUSION_SUM, FUSION_GATED = 0, 1, 2
+FUSION_IDENTITY, FUSION_SUM, FUSION_GATED, FUSION_CONCAT = 0, 1, 2, 3
 OPT_SPARSE_ADAM, OPT_DENSE = 0, 1
 STATUS_SAMPLER_EXHAUSTED = 1
 STATUS_INDEX_OUT_OF_RANGE = 2

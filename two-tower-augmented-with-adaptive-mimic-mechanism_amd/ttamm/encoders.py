@@ -262,7 +262,8 @@ def build_tower_encoder(
 # ---------------------------------------------------------------------------------------
 # Mapping of a TowerEncoder onto the libttamm tower descriptor
 # ---------------------------------------------------------------------------------------
-_FUSION_CODE = {"identity": _lib.FUSION_IDENTITY, "sum": _lib.FUSION_SUM, "gated": _lib.FUSION_GATED}
+_FUSION_CODE = {"identity": _lib.FUSION_IDENTITY, "sum": _lib.FUSION_SUM, "gated": _lib.FUSION_GATED,
+                "concat": _lib.FUSION_CONCAT}
 
 
 def _matmul_dtype(name: str) -> str:
@@ -322,8 +323,9 @@ def describe_tower(
     state: Mapping[int, Mapping[str, torch.Tensor]] | None = None,
     id_optimizer: int = _lib.OPT_SPARSE_ADAM,
 ) -> _lib.Tower:
-    if tower.fusion == "concat":
-        raise NotImplementedError("ttamm: 'concat' fusion is not on the MI355X hot path")
+    if tower.fusion == "concat" and tower.projection.out_features != tower.id_dim:
+        # the step's score / mimic rows are embedding-dim wide (AdaptiveMimicMechanism needs it)
+        raise NotImplementedError("ttamm: 'concat' fusion needs output_dim == embedding_dim")
     if tower.embedding.max_norm is not None:
         raise NotImplementedError("ttamm: max_norm embeddings are not implemented")
     s = _lib.Tower()
@@ -367,6 +369,8 @@ def describe_tower(
             g = tower.adaptive_mimic.gate_network
             s.gate[0] = _linear_struct(g[0], state)
             s.gate[1] = _linear_struct(g[2], state)
+        elif tower.fusion == "concat":  # the projection rides in gate[0] (ttamm.h TTAMM_FUSION_CONCAT)
+            s.gate[0] = _linear_struct(tower.projection, state)
     return s
 
 

@@ -208,6 +208,9 @@ class FusedTrainStep:
                     for i in (0, 2):
                         dense_param(tower.adaptive_mimic.gate_network[i].weight)
                         dense_param(tower.adaptive_mimic.gate_network[i].bias)
+                elif tower.fusion == "concat":
+                    dense_param(tower.projection.weight)
+                    dense_param(tower.projection.bias)
             elif tower.fusion != "identity":
                 # no feature rows: the reference's tower falls back to the ID embedding
                 # (encoders.py:228-231), so these parameters get no gradient and torch's
@@ -224,7 +227,7 @@ class FusedTrainStep:
         unhandled = [i for i in dense_ids | sparse_ids if i not in handled]
         if unhandled:
             raise NotImplementedError(
-                "ttamm: the optimizers hold parameters outside the fused step (e.g. concat projection)"
+                "ttamm: the optimizers hold parameters outside the fused step"
             )
         self.state = state
 
