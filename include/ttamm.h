@@ -137,6 +137,12 @@ typedef struct ttamm_table {
      * the sparse gradient), AdamW updates it with g = 0.  The lookup itself is unchanged. */
     int32_t has_padding_idx;
     int64_t padding_idx;
+    /* nn.Embedding(max_norm=...) (encoders.py:48,58; dense tables only, as the reference
+     * requires): > 0 renormalises every looked-up row whose L2 norm exceeds it, in place and
+     * before the lookup (torch embedding_renorm_: row *= max_norm / (norm + 1e-7)), once per
+     * forward call — the user rows, then the positives', then the negatives' (training.py:
+     * 748-775 calls the item encoder twice).  0 = off. */
+    double max_norm;
 } ttamm_table;
 
 /* One tower: TowerEncoder (encoders.py:171-255) + its half of AdaptiveMimicMechanism

@@ -80,8 +80,10 @@ def build_tower(cfg: Mapping[str, Any], *, num_embeddings: int, feature_dim: int
     """encoders.py:258-331 with the same parameter construction / init order."""
     id_cfg = cfg.get("id_embedding", {}) or {}
     params = id_cfg.get("params", {}) or {}
+    if bool(params.get("sparse", False)) and params.get("max_norm") is not None:  # encoders.py:51-52
+        raise ValueError("max_norm is not supported when using sparse embeddings.")
     emb = nn.Embedding(num_embeddings, int(params.get("embedding_dim", 64)), padding_idx=params.get("padding_idx"),
-                       sparse=bool(params.get("sparse", False)))
+                       max_norm=params.get("max_norm"), sparse=bool(params.get("sparse", False)))
     init = id_cfg.get("init") or {"type": "normal", "std": 0.02}
     nn.init.normal_(emb.weight, mean=0.0, std=float(init.get("std", 0.02)))  # encoders.py:25-27
     fusion = str(cfg.get("fusion", "gated" if feature_dim > 0 else "identity")).lower()

@@ -29,11 +29,14 @@ class Shape:
     matmul_dtype: str = "fp32"
     padding_idx: int | None = None  # nn.Embedding padding_idx of both ID tables (encoders.py:47)
     fusion: str = "gated"  # TowerEncoder fusion (encoders.py:203): gated / sum / concat
+    max_norm: float | None = None  # nn.Embedding max_norm of both ID tables (dense only, encoders.py:48-52)
 
     def tower_cfg(self) -> dict:
         params = {"embedding_dim": self.D, "sparse": self.sparse}
         if self.padding_idx is not None:
             params["padding_idx"] = self.padding_idx
+        if self.max_norm is not None:
+            params["max_norm"] = self.max_norm
         return {
             "type": "tower",
             "matmul_dtype": self.matmul_dtype,

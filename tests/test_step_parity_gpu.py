@@ -59,8 +59,8 @@ def test_step_gradients_match_oracle(shape):
 
 
 @pytest.mark.parametrize("shape", [Shape(), Shape(sparse=False), Shape(padding_idx=5), Shape(sparse=False, padding_idx=5),
-                                   Shape(fusion="concat")],
-                         ids=["tiny", "dense-id", "padding", "dense-id-padding", "concat"])
+                                   Shape(fusion="concat"), Shape(sparse=False, max_norm=0.05)],
+                         ids=["tiny", "dense-id", "padding", "dense-id-padding", "concat", "max-norm"])
 def test_three_steps_match_oracle(shape):
     from gpu_helpers import run_ttamm
 
@@ -212,3 +212,24 @@ def test_gradient_clipping_rejects_sparse_id_tables():
     prob = make_problem(Shape(), steps=1)
     with pytest.raises(NotImplementedError, match="sparse"):
         run_ttamm(prob, gradient_clip_norm=1.0)
+
+
+def test_max_norm_renormalises_looked_up_rows():
+    """nn.Embedding(max_norm) (encoders.py:48,58): the step renorms the rows it looks up in place,
+    as torch's embedding_renorm_ does in the reference's forward: after one step with lr = 0 the
+    looked-up rows of both ID tables equal the oracle's (the renorm is the only change), and
+    rows no batch touched keep their norm."""
+    from gpu_helpers import run_ttamm
+
+    shape = Shape(sparse=False, max_norm=0.05)
+    prob = make_problem(shape, steps=1)
+    init = {k: v.clone() for k, v in prob.model.state_dict().items()}
+    om, oo, ores = run_oracle(prob, lr=0.0, betas=(0.0, 0.999), weight_decay=0.0)
+    tm, to, tres = run_ttamm(prob, lr=0.0, betas=(0.0, 0.999), weight_decay=0.0)
+    assert abs(tres[0]["total"] - ores[0].total) <= GRAD_TOL * abs(ores[0].total)
+    osd, tsd = om.state_dict(), tm.state_dict()
+    for n in ("user_encoder.embedding.weight", "item_encoder.embedding.weight"):
+        changed = (osd[n] != init[n]).any(dim=1)
+        assert changed.any(), n  # the renorm did act
+        assert (tsd[n].cpu().norm(dim=1)[changed] <= 0.05 * (1 + 1e-6)).all(), n
+        assert rel_err(tsd[n].cpu(), osd[n]) <= 1e-6, n

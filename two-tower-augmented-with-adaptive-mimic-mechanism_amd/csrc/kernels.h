@@ -167,6 +167,11 @@ int launch_gate(GateArgs& a, bool backward, hipStream_t s);
 // Row kernels (rows.hip)
 // ------------------------------------------------------------------------------------
 // ids outside [0, table_rows) give zero rows (never an out-of-table read)
+// nn.Embedding max_norm (embedding_renorm_): each distinct row of idx[0, n) whose L2 norm exceeds
+// max_norm is scaled by max_norm / (norm + 1e-7) in place; one wave per position, the first
+// wave to claim a row through mark[row] = tag does it (tags unique per call, mark zeroed once)
+int launch_renorm_rows(float* table, int64_t table_rows, int dim, const int64_t* idx, int64_t n, double max_norm,
+                       int32_t* mark, int32_t tag, hipStream_t s);
 int launch_gather_rows(const float* table, int64_t table_rows, int dim, const int64_t* idx, int64_t n, float* out,
                        int64_t out_ld, hipStream_t s);
 

@@ -345,7 +345,41 @@ inline unsigned grid_for(int64_t work, int threads = 256) {
     return (unsigned)g;
 }
 
+// torch embedding_renorm_ on the rows a lookup touches (encoders.py:48,58 max_norm)
+__global__ void renorm_rows_kernel(float* __restrict__ table, int64_t table_rows, int dim,
+                                   const int64_t* __restrict__ idx, int64_t n, double max_norm,
+                                   int32_t* __restrict__ mark, int32_t tag) {
+    const int64_t p = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (p >= n) return;
+    const int64_t row = idx[p];
+    if (row < 0 || row >= table_rows) return;  // reported by the staging kernel
+    int claimed = 0;
+    if (lane == 0) claimed = atomicExch(&mark[row], tag) != tag;
+    claimed = __shfl(claimed, 0);
+    if (!claimed) return;
+    float* r = table + row * (int64_t)dim;
+    float ss = 0.f;
+    for (int c = lane; c < dim; c += 64) ss += r[c] * r[c];
+    ss = wave_sum(ss);
+    const float norm = sqrtf(ss);
+    if ((double)norm > max_norm) {  // torch: norm > max_norm, scale = max_norm / (norm + 1e-7) in double
+        const float scale = (float)(max_norm / ((double)norm + 1e-7));
+        for (int c = lane; c < dim; c += 64) r[c] = r[c] * scale;
+    }
+}
+
 }  // namespace
+
+int launch_renorm_rows(float* table, int64_t table_rows, int dim, const int64_t* idx, int64_t n, double max_norm,
+                       int32_t* mark, int32_t tag, hipStream_t s) {
+    if (n <= 0) return TTAMM_OK;
+    TTAMM_REQUIRE(mark != nullptr && max_norm > 0.0 && tag != 0, "renorm: bad arguments");
+    hipLaunchKernelGGL(renorm_rows_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, s, table, table_rows, dim, idx, n,
+                       max_norm, mark, tag);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
 
 int launch_gather_rows(const float* table, int64_t table_rows, int dim, const int64_t* idx, int64_t n, float* out,
                        int64_t out_ld, hipStream_t s) {

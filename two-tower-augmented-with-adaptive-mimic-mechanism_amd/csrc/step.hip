@@ -38,6 +38,10 @@ struct TowerWs {
     // dropout stream key of row r (see GemmProblem::row_key)
     const int64_t* row_key = nullptr;
     int64_t key_base0 = 0, key_base1 = 0, key_split = 0;
+    // ID-table max_norm: per-row claim marks (persistent, zero once) and this call's tag base
+    int32_t* renorm_mark = nullptr;
+    int32_t renorm_tag = 0;
+    int64_t renorm_split = 0;  // item tower: positives [0, split) are one lookup, negatives the next
     float* hid[TTAMM_MAX_LINEAR] = {};
     float* dhid[TTAMM_MAX_LINEAR] = {};
     float* ef = nullptr;    // gated: [R, 2D] = [e | f]
@@ -227,6 +231,8 @@ void plan_scratch(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         const int64_t ncat = std::min<int64_t>(A.num_categories, 65535);
         coalesce_bind_scratch(ws.cal.co, ar.take<int32_t>(coalesce_scratch_ints(ncat)), ncat);
     }
+    if (A.user.id.max_norm > 0.0) ws.user.renorm_mark = ar.take<int32_t>(A.user.id.rows);
+    if (A.item.id.max_norm > 0.0) ws.item.renorm_mark = ar.take<int32_t>(A.item.id.rows);
 }
 
 void plan_coalesce(Arena& ar, CoalesceWs& co, int64_t R) {
@@ -475,6 +481,16 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
         for (int k = 0; k < ntowers; ++k) {
             const ttamm_tower& t = *T[k];
             TowerWs& w = *W[k];
+            if (t.id.max_norm > 0.0 && w.R > 0) {  // nn.Embedding max_norm: renorm, then look up
+                const int64_t split = w.renorm_split > 0 && w.renorm_split < w.R ? w.renorm_split : w.R;
+                if ((rc = launch_renorm_rows(t.id.weight, t.id.rows, D, w.idx, split, t.id.max_norm, w.renorm_mark,
+                                             w.renorm_tag, s)))
+                    return rc;
+                if (split < w.R &&
+                    (rc = launch_renorm_rows(t.id.weight, t.id.rows, D, w.idx + split, w.R - split, t.id.max_norm,
+                                             w.renorm_mark, w.renorm_tag + 1, s)))
+                    return rc;
+            }
             float* dst = uses_ef(t) ? w.ef : w.e;
             const int64_t ld = uses_ef(t) ? 2 * D : D;
             if ((rc = launch_gather_rows(t.id.weight, t.id.rows, D, w.idx, w.R, dst, ld, s))) return rc;
@@ -1230,6 +1246,11 @@ int validate_step(const ttamm_step_args& A) {
                       "Adaptive mimic requires user and item embedding dimensions to match.");
     }
     TTAMM_REQUIRE(A.hp.dense_step >= 1 && A.hp.sparse_step >= 1, "optimizer step counts must be >= 1");
+    for (const ttamm_tower* t : {&A.user, &A.item})
+        if (t->id.max_norm > 0.0) {
+            TTAMM_REQUIRE(t->id.optimizer == TTAMM_OPT_DENSE, "max_norm is not supported when using sparse embeddings.");
+            TTAMM_REQUIRE(!sharded(A), "max_norm embeddings are not implemented in the row-sharded step");
+        }
     if (A.hp.grad_clip_norm > 0.0) {
         TTAMM_REQUIRE(!sharded(A), "gradient clipping is not implemented in the row-sharded step");
         TTAMM_REQUIRE(A.user.id.optimizer == TTAMM_OPT_DENSE && A.item.id.optimizer == TTAMM_OPT_DENSE,
@@ -1308,6 +1329,9 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         I.key_base1 = Bg + A.row_base * N;
         neg = I.idx_own + B;
     }
+    // max_norm claim tags: unique per lookup (users; positives, then negatives)
+    U.renorm_tag = I.renorm_tag = (int32_t)(2 * (A.hp.dense_step % (1 << 29)) + 1);
+    if (!shard) I.renorm_split = B;
     const ttamm_tower* T[2] = {&A.user, &A.item};
     TowerWs* W[2] = {&U, &I};
     const ttamm_hparams& hp = A.hp;
@@ -1586,6 +1610,7 @@ size_t tower_forward_workspace_size(const ttamm_tower& T, int64_t n) {
     for (int q = 0; q < 3; ++q) ar.take<float>((size_t)n * D);  // g, t, a
     ar.take<int64_t>(n);                                         // range-checked ids
     if (needs_wpad(T)) ar.take<float>((size_t)T.linear[0].out_features * round4(T.linear[0].in_features));
+    if (T.id.max_norm > 0.0) ar.take<int32_t>(T.id.rows);  // renorm claim marks
     return ar.off + 256;
 }
 
@@ -1611,7 +1636,12 @@ int tower_forward_eval(const ttamm_tower& T, const int64_t* idx, const int64_t* 
     float* abuf = ar.take<float>((size_t)n * D);
     int64_t* idxc = ar.take<int64_t>(n);
     if (needs_wpad(T)) w.wpad = ar.take<float>((size_t)T.linear[0].out_features * round4(T.linear[0].in_features));
+    if (T.id.max_norm > 0.0) {  // nn.Embedding max_norm renorms in eval mode too (one lookup)
+        w.renorm_mark = ar.take<int32_t>(T.id.rows);
+        w.renorm_tag = 1;
+    }
     TTAMM_REQUIRE(ar.ok(), "workspace too small for tower forward");
+    if (w.renorm_mark) TTAMM_HIP(hipMemsetAsync(w.renorm_mark, 0, (size_t)T.id.rows * sizeof(int32_t), s));
     {  // ids outside the tables read row 0 (the Python mirror raises IndexError before calling)
         StageArgs st;
         std::memset(&st, 0, sizeof(st));

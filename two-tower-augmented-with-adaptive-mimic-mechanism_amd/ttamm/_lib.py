@@ -59,6 +59,7 @@ class Table(ctypes.Structure):
         ("last_step", c_vp),
         ("has_padding_idx", c_i32),
         ("padding_idx", c_i64),
+        ("max_norm", c_d),
     ]
 
 

@@ -326,8 +326,8 @@ def describe_tower(
     if tower.fusion == "concat" and tower.projection.out_features != tower.id_dim:
         # the step's score / mimic rows are embedding-dim wide (AdaptiveMimicMechanism needs it)
         raise NotImplementedError("ttamm: 'concat' fusion needs output_dim == embedding_dim")
-    if tower.embedding.max_norm is not None:
-        raise NotImplementedError("ttamm: max_norm embeddings are not implemented")
+    if tower.embedding.max_norm is not None and float(tower.embedding.norm_type) != 2.0:
+        raise NotImplementedError("ttamm: max_norm embeddings with norm_type != 2")
     s = _lib.Tower()
     emb = tower.embedding.weight
     s.id.weight = emb.data_ptr()
@@ -337,6 +337,8 @@ def describe_tower(
     if tower.embedding.padding_idx is not None:  # nn.Embedding normalises it to [0, rows)
         s.id.has_padding_idx = 1
         s.id.padding_idx = int(tower.embedding.padding_idx)
+    if tower.embedding.max_norm is not None:  # renorm of looked-up rows (embedding_renorm_)
+        s.id.max_norm = float(tower.embedding.max_norm)
     if state is not None:
         st = state[id(emb)]
         s.id.exp_avg = st["exp_avg"].data_ptr()

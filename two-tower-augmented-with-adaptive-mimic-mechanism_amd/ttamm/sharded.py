@@ -325,6 +325,8 @@ class ShardedTrainStep(FusedTrainStep):
             if enc.embedding.padding_idx is not None:
                 # a global padding id lives on one owner as a local row: not mapped here
                 raise NotImplementedError("ttamm: padding_idx is not implemented in the row-sharded step")
+            if enc.embedding.max_norm is not None:
+                raise NotImplementedError("ttamm: max_norm embeddings are not implemented in the row-sharded step")
         self.own = RowOwnership(world_size, rank)
         self.comm = comm
         # True: both towers' forward in one set of grouped launches, then the (t | a) exchange;
