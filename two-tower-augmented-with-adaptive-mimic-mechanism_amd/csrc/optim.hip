@@ -513,7 +513,10 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
     const KArg(ReplayArgs)* ka = (const KArg(ReplayArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
     const KArg(ReplaySeg)& S = ka->seg[blockIdx.y];
     if (step_poisoned(ka->status)) return;
-    __shared__ AdamConsts H[kMaxHistory];
+    // the history ring, sized at launch to its capacity (replay_slices + 2 entries, ~3 KB by
+    // default): a static kMaxHistory array took 24 KB of LDS per block and kept the GEMMs that
+    // overlap the aux stream's catch-up (147 KB per bf16 tile) off the CUs it occupied
+    extern __shared__ AdamConsts H[];
     const int cap = ka->cap;
     for (int i = threadIdx.x; i < cap; i += blockDim.x) H[i] = ka->hist[i];
     __syncthreads();
@@ -901,13 +904,14 @@ int launch_replay(const ReplayArgs& a, hipStream_t s) {
     }
     if (most == 0) return TTAMM_OK;
     const dim3 grid(grid_for(most, 256, 16384), a.count);
+    const size_t lds = (size_t)a.cap * sizeof(AdamConsts);
     if (a.fast_g0) {
-        if (a.decoupled) hipLaunchKernelGGL((replay_kernel<true, true>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((replay_kernel<false, true>), grid, dim3(256), 0, s, a);
+        if (a.decoupled) hipLaunchKernelGGL((replay_kernel<true, true>), grid, dim3(256), lds, s, a);
+        else hipLaunchKernelGGL((replay_kernel<false, true>), grid, dim3(256), lds, s, a);
     } else if (a.decoupled) {
-        hipLaunchKernelGGL((replay_kernel<true, false>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((replay_kernel<true, false>), grid, dim3(256), lds, s, a);
     } else {
-        hipLaunchKernelGGL((replay_kernel<false, false>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((replay_kernel<false, false>), grid, dim3(256), lds, s, a);
     }
     TTAMM_LAUNCH_CHECK();
     if (a.stamp) {
