@@ -1018,6 +1018,10 @@ int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_b
     for (int k = 0; k < n; ++k)
         if ((rc = tower_prepare_a(*T[k], *W[k], mimic, df, aux))) return rc;
     TTAMM_HIP(hipEventRecord(ev[1], aux));
+    // the fusion is enqueued before the grouping's dozen launches: enqueued after them, the host
+    // still issued them when the GPU finished the MLP (~55 us idle per C2 step)
+    TTAMM_HIP(hipStreamWaitEvent(s, ev[1], 0));
+    if ((rc = tower_forward(T, W, bt, D, mimic, s, n, l0_events, FWD_FUSION))) return rc;
     for (int k = 0; k < n; ++k)
         if ((rc = tower_prepare_b(*T[k], *W[k], aux))) return rc;
     TTAMM_HIP(hipEventRecord(ev[2], aux));
@@ -1029,8 +1033,7 @@ int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_b
         // row to `step` meanwhile).  The next step's catch-up and the flush are ordered after it.
         if ((rc = replay_slice(T, n, mimic, df, df.step - 1, 2, maint_events, aux))) return rc;
     }
-    TTAMM_HIP(hipStreamWaitEvent(s, ev[1], 0));
-    return tower_forward(T, W, bt, D, mimic, s, n, l0_events, FWD_FUSION);
+    return TTAMM_OK;
 }
 
 // the row updates need the grouping (prepare part B), possibly still running on the aux stream
