@@ -5,7 +5,8 @@ element by element:
     the data path; fixed-order reductions);
   * untouched rows of the dense-group mimic tables follow torch's AdamW with g = 0 exactly;
   * sampled negatives are in range and never a user's positive;
-  * the loss goes down."""
+  * the loss goes down.
+and at the per-GPU C4 shard (6.25M items x 25K users, D = 128, H = 256, in-batch negatives)."""
 
 import sys
 from pathlib import Path
@@ -82,4 +83,61 @@ def test_c2_negatives_and_loss(c2):
         losses.append(w.engine.last_losses()["total"])
     w.engine.finish()
     assert all(torch.isfinite(torch.tensor(losses)))
+    assert sum(losses[-5:]) / 5 < sum(losses[:5]) / 5
+
+
+# ---- BASELINE C4 per-GPU shard: 6.25M items x 25K users, D = 128, H = 256, in-batch negatives ----
+@pytest.fixture(scope="module")
+def c4():
+    import bench
+
+    return bench.CONFIGS["c4"]
+
+
+def test_c4_deterministic_and_adamw_untouched_rows(c4):
+    """The C4 shard (the per-GPU table of the 8-way 50M x 128 model) through the in-batch step:
+    untouched mimic rows follow torch's AdamW(g = 0) exactly, two runs agree bit for bit."""
+    import bench
+
+    w1 = bench.Workload(c4, torch.device("cuda"), seed=11, in_batch=True)
+    table0 = w1.model.adaptive_mimic.item_augmented.weight.detach().clone()
+    batches = [w1.batch() for _ in range(2)]
+    w1.engine.step(*batches[0])
+    w1.engine.flush()
+    torch.cuda.synchronize()
+    mask = torch.ones(c4["I"], dtype=torch.bool, device="cuda")
+    mask[batches[0][1].unique()] = False  # in-batch: the positives are the only item rows
+    rows = mask.nonzero().squeeze(1)
+    rows = rows[torch.randperm(rows.numel(), device="cuda")[:4096]]
+    p = table0[rows].cpu()
+    opt_p = torch.nn.Parameter(p.clone())
+    opt = torch.optim.AdamW([opt_p], lr=1e-3, weight_decay=0.01)
+    opt_p.grad = torch.zeros_like(p)
+    opt.step()
+    got = w1.model.adaptive_mimic.item_augmented.weight[rows].detach().cpu()
+    assert torch.equal(got, opt_p.detach())
+    w1.engine.step(*batches[1])
+    w1.engine.finish()
+    sums1 = _checksum(w1.model)
+    del w1
+    torch.cuda.empty_cache()
+    w2 = bench.Workload(c4, torch.device("cuda"), seed=11, in_batch=True)
+    for b in [w2.batch() for _ in range(2)]:
+        w2.engine.step(*b)
+    w2.engine.finish()
+    assert _checksum(w2.model) == sums1
+
+
+def test_c4_inbatch_loss_decreases(c4):
+    import bench
+
+    w = bench.Workload(c4, torch.device("cuda"), seed=3, in_batch=True)
+    losses = []
+    for _ in range(30):
+        w.engine.step(*w.batch())
+        losses.append(w.engine.last_losses()["total"])
+    w.engine.finish()
+    assert all(torch.isfinite(torch.tensor(losses)))
+    # BCE over B x B logits with one positive per row starts near log 2
+    assert 0.5 < losses[0] < 0.8
     assert sum(losses[-5:]) / 5 < sum(losses[:5]) / 5
