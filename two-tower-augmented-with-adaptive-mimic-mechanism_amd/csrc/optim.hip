@@ -49,8 +49,11 @@ __device__ __forceinline__ void adam_elem_t(float& p, float& m, float& v, float 
     }
     if constexpr (FAST) {
         static_assert(G0, "fast arithmetic is for the g = 0 updates only");
-        const float denom = __builtin_amdgcn_sqrtf(v) * c.inv_bc2_sqrt + c.eps;
-        p = p + c.neg_step * (m * __builtin_amdgcn_rcpf(denom));
+        // two fmas instead of mul + add pairs (the compiler kept them separate): the replay is
+        // VALU-bound, and this is ~25 % of its instructions.  m and v stay bit-exact (torch's
+        // operations); p moves by the same update term within an ulp or two.
+        const float denom = fmaf(__builtin_amdgcn_sqrtf(v), c.inv_bc2_sqrt, c.eps);
+        p = fmaf(c.neg_step, m * __builtin_amdgcn_rcpf(denom), p);
     } else {
         const float denom = div_by_const(sqrtf(v), c.bc2_sqrt, c.inv_bc2_sqrt) + c.eps;
         p = p + c.neg_step * (m / denom);
@@ -508,17 +511,25 @@ __global__ void step_begin_kernel(const uint32_t* status, int64_t* applied, Adam
 // chains per thread sharing each step's constants); blockIdx.y = segment.  A row current to
 // step l is brought to A.target by replaying adam_elem(g = 0) with the constants of steps
 // l+1 .. target — the operations the eager sweep applies, so the bits agree.
+// The per-step constants a g = 0 replay reads (the AdamW path loads the first 24 B)
+struct ReplayConsts {
+    float decay, w1, b2, eps, neg_step, inv_bc2_sqrt, bc2_sqrt, wd, w2, pad0, pad1, pad2;
+};
+
 template <bool DECOUPLED, bool FAST>
 __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
     const KArg(ReplayArgs)* ka = (const KArg(ReplayArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
     const KArg(ReplaySeg)& S = ka->seg[blockIdx.y];
     if (step_poisoned(ka->status)) return;
-    // the history ring, sized at launch to its capacity (replay_slices + 2 entries, ~3 KB by
-    // default): a static kMaxHistory array took 24 KB of LDS per block and kept the GEMMs that
-    // overlap the aux stream's catch-up (147 KB per bf16 tile) off the CUs it occupied
-    extern __shared__ AdamConsts H[];
+    // the history ring unrolled twice in LDS (2 cap entries, sized at launch: ~4 KB by default),
+    // so a row's steps l+1 .. target are consecutive entries from (l + 1) % cap — no wrap test
+    // and no address arithmetic beyond a pointer increment in the VALU-bound loop
+    extern __shared__ ReplayConsts H2[];
     const int cap = ka->cap;
-    for (int i = threadIdx.x; i < cap; i += blockDim.x) H[i] = ka->hist[i];
+    for (int i = threadIdx.x; i < 2 * cap; i += blockDim.x) {
+        const AdamConsts& h = ka->hist[i < cap ? i : i - cap];
+        H2[i] = ReplayConsts{h.decay, h.w1, h.b2, h.eps, h.neg_step, h.inv_bc2_sqrt, h.bc2_sqrt, h.wd, h.w2, 0.f, 0.f, 0.f};
+    }
     __syncthreads();
     const int dim = S.dim, dim4 = dim >> 2;
     const int32_t target = ka->target;
@@ -543,14 +554,17 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
         float4 p = *reinterpret_cast<const float4*>(S.p + o);
         float4 m = *reinterpret_cast<const float4*>(S.m + o);
         float4 v = *reinterpret_cast<const float4*>(S.v + o);
-        int j = (int)((l + 1) % cap);
-        for (int32_t t = l + 1; t <= target; ++t) {
-            const AdamConsts c = H[j];
+        const ReplayConsts* hc = H2 + (l + 1) % cap;
+        const ReplayConsts* const hend = hc + (target - l);
+        for (; hc != hend; ++hc) {
+            AdamConsts c;
+            c.decay = hc->decay, c.w1 = hc->w1, c.b2 = hc->b2, c.eps = hc->eps, c.neg_step = hc->neg_step;
+            c.bc2_sqrt = hc->bc2_sqrt, c.inv_bc2_sqrt = hc->inv_bc2_sqrt, c.wd = hc->wd, c.w2 = hc->w2;
+            c.decoupled = DECOUPLED ? 1 : 0, c.fast_g0 = FAST ? 1 : 0;
             adam_elem_t<DECOUPLED, true, FAST>(p.x, m.x, v.x, 0.f, c);
             adam_elem_t<DECOUPLED, true, FAST>(p.y, m.y, v.y, 0.f, c);
             adam_elem_t<DECOUPLED, true, FAST>(p.z, m.z, v.z, 0.f, c);
             adam_elem_t<DECOUPLED, true, FAST>(p.w, m.w, v.w, 0.f, c);
-            j = j + 1 == cap ? 0 : j + 1;
         }
         *reinterpret_cast<float4*>(S.p + o) = p;
         *reinterpret_cast<float4*>(S.m + o) = m;
@@ -904,7 +918,7 @@ int launch_replay(const ReplayArgs& a, hipStream_t s) {
     }
     if (most == 0) return TTAMM_OK;
     const dim3 grid(grid_for(most, 256, 16384), a.count);
-    const size_t lds = (size_t)a.cap * sizeof(AdamConsts);
+    const size_t lds = (size_t)2 * a.cap * sizeof(ReplayConsts);
     if (a.fast_g0) {
         if (a.decoupled) hipLaunchKernelGGL((replay_kernel<true, true>), grid, dim3(256), lds, s, a);
         else hipLaunchKernelGGL((replay_kernel<false, true>), grid, dim3(256), lds, s, a);
