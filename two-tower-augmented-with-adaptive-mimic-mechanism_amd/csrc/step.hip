@@ -474,7 +474,7 @@ bool gate_group(const ttamm_tower* const* T, TowerWs* const* W, int ntowers, int
 // part FWD_MLP: ID-row gather + feature encoder; FWD_FUSION: gate / combine (reads the mimic rows)
 enum { FWD_MLP = 1, FWD_FUSION = 2, FWD_ALL = 3 };
 int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt, int D, bool mimic, hipStream_t s,
-                  int ntowers, void* const* l0_events = nullptr, int part = FWD_ALL) {
+                  int ntowers, void* const* l0_events = nullptr, int part = FWD_ALL, hipEvent_t after_l0 = nullptr) {
     int rc;
     if (part & FWD_MLP) {
         // ID rows -> e (ef[:, :D] when gated)
@@ -564,6 +564,7 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
             if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)l0_events[0], s));
             if ((rc = bb.run(s))) return rc;
             if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)l0_events[1], s));
+            if (l == 0 && after_l0) TTAMM_HIP(hipEventRecord(after_l0, s));
         }
     }
     if (!(part & FWD_FUSION)) return TTAMM_OK;
@@ -1012,8 +1013,11 @@ int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_b
     // host-side enqueue would otherwise hold the GEMMs back behind the host.
     hipEvent_t ev[3];
     if ((rc = aux_events(ev))) return rc;
-    TTAMM_HIP(hipEventRecord(ev[0], s));
-    if ((rc = tower_forward(T, W, bt, D, mimic, s, n, l0_events, FWD_MLP))) return rc;
+    // bf16 towers: the prologue starts after the first layer's GEMM (its one-block-per-CU tiles
+    // otherwise wait for CUs behind the catch-up replay); fp32 towers: at once
+    const bool late_fork = T[0]->matmul_bf16 && std::getenv("TTAMM_EARLY_FORK") == nullptr;
+    if (!late_fork) TTAMM_HIP(hipEventRecord(ev[0], s));
+    if ((rc = tower_forward(T, W, bt, D, mimic, s, n, l0_events, FWD_MLP, late_fork ? ev[0] : nullptr))) return rc;
     TTAMM_HIP(hipStreamWaitEvent(aux, ev[0], 0));
     for (int k = 0; k < n; ++k)
         if ((rc = tower_prepare_a(*T[k], *W[k], mimic, df, aux))) return rc;
