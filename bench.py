@@ -29,12 +29,18 @@ the row-sharded step of ttamm/sharded.py on a C2 batch of its own users: item re
 all-reduce.
 
 The JSON line also carries
-  roofline:     the dominant MFMA kernel — the first feature-layer forward GEMM (sampled mode),
-                or the in-batch scoring kernel when it takes longer — timed with HIP events on
-                the step's stream over the timed steps; algorithmic FLOPs per launch (2 R F H,
-                or 6 B Bg D for S = U P^T, dU = dS P, dP = dS^T U); `kernels` lists both.
+  kernels:      the step's largest kernels, each timed live with HIP events on the stream it
+                runs on, over the timed steps: the deferred table AdamW replay (rolling slice +
+                both towers' catch-up, + the closing flush's share; VALU-bound), the first
+                feature-layer forward GEMM, the wide weight-gradient GEMM launch, the in-batch
+                scoring kernel (MFMA-bound; algorithmic FLOPs 2 R F H, 2 R M N, 6 B Bg D);
+  roofline:     the one of them with the most time per step;
   cpu_baseline: the CPU oracle (oracle/cpu_reference.py, the reference's step restated on
                 PyTorch-CPU incl. its per-row sampler loop) timed on this host, rank 0, N=1.
+--emulate-world W (one GPU, developer): rank 0 of a W-rank row-sharded job whose other ranks
+mirror it (ttamm.sharded.MirrorComm: the per-rank work of the W-rank step — W x the item
+requests as owner, the W B all-gathered in-batch positives — without interconnect traffic);
+`value` is then this rank's own throughput.
 """
 
 from __future__ import annotations
@@ -57,6 +63,9 @@ METRIC = "training interactions/sec at 1/2/4/8 MI355X; Recall@20 parity vs CPU r
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: fp32 matrix (v_mfma_f32_32x32x2_f32), dense
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 MFMA ~2.5 PF dense (no sparsity)
+# VALU issue: 256 CUs x 4 SIMD-32, one wave64 instruction per 2 cycles at 2.4 GHz
+# (MI355X_MICROARCH.md "Wave scheduling" and the v_fma_f32 row of the cycle constants)
+VALU_WAVE_INSTR_PEAK = 1024 * 2.4e9 / 2
 
 CONFIGS = {
     "c2": dict(U=200_000, I=2_000_000, D=96, H=192, F=605, B=8192, N=5, dropout=0.15, pos_per_user=20),
@@ -122,7 +131,7 @@ class Workload:
     def __init__(self, c: dict, device, seed: int, world: int = 1, rank: int = 0, step_seed: int | None = None,
                  deferred: bool = True, overlap: bool = True, in_batch: bool = False, table_math: str = "fast",
                  replay_slices: int = 64, aux_cus: int = 0, sharded_single: bool = False,
-                 group_towers: bool = True):
+                 group_towers: bool = True, emulate: bool = False):
         import ttamm
         from ttamm.samplers import PositivesCSR
 
@@ -184,11 +193,12 @@ class Workload:
             self.engine = ShardedTrainStep(self.model, self.opts, world_size=1, rank=0, num_items=Ig, comm=_One(),
                                            seed=seed, group_towers=group_towers, **kw)
         else:
-            from ttamm.sharded import ShardedTrainStep, TorchComm
+            from ttamm.sharded import MirrorComm, ShardedTrainStep, TorchComm
 
             # step_seed: the same on every rank (the Philox streams are keyed by global position)
+            comm = MirrorComm(world, rank) if emulate else TorchComm()
             self.engine = ShardedTrainStep(self.model, self.opts, world_size=world, rank=rank, num_items=Ig,
-                                           comm=TorchComm(), seed=step_seed, group_towers=group_towers, **kw)
+                                           comm=comm, seed=step_seed, group_towers=group_towers, **kw)
 
     def batch(self):
         """The next batch of the on-device loader (epochs run back to back)."""
@@ -237,12 +247,23 @@ def cpu_baseline(c: dict, steps: int, warmup: int, seed: int, in_batch: bool = F
         "value": round(seen / secs, 1),
         "unit": "interactions/s",
         "cores": threads,
+        "cpu_model": cpu_model(),
         "kind": "port",
         "sample": f"{steps} timed steps (+{warmup} warm-up) of the same-shaped step, batch {B}, on "
                   f"{threads} host threads: oracle/cpu_reference.py (reference per-row sampler, AdamW over the "
                   f"full {U}x{c['D']} + {I}x{c['D']} mimic tables, SparseAdam"
-                  f"{', in-batch B x B logits' if in_batch else ''})",
+                  f"{', in-batch B x B logits' if in_batch else ''}); {secs:.1f} s timed",
     }
+
+
+def cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def load_traffic(config: str) -> dict | None:
@@ -255,6 +276,16 @@ def load_traffic(config: str) -> dict | None:
         return None
 
 
+def wgrad_problems(c: dict, rows: dict) -> list[tuple[int, int, int]]:
+    """(R, M, N) of the step's weight gradients (tower_backward): per tower the feature MLP's
+    layers, then the gate's two Linear (Hg = D)."""
+    F, H, D = c["F"], c["H"], c["D"]
+    out = []
+    for R in rows.values():
+        out += [(R, H, F), (R, D, H), (R, D, 2 * D), (R, D, D)]
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -263,7 +294,8 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=1234)
-    ap.add_argument("--cpu-steps", type=int, default=8)
+    ap.add_argument("--cpu-steps", type=int, default=20)
+    ap.add_argument("--cpu-warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo stages the exchanges through host memory (several ranks on one GPU, tests only)")
@@ -274,6 +306,9 @@ def main() -> None:
                          "instead of grouping the two towers' launches (ShardedTrainStep(group_towers=False))")
     ap.add_argument("--sharded-single", action="store_true",
                     help="developer: run the row-sharded step's phases at one GPU (W = 1, in-process exchange)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="developer: rank 0 of a W-rank sharded job on one GPU, the other ranks mirrored "
+                         "(ttamm.sharded.MirrorComm: per-rank work without interconnect traffic)")
     ap.add_argument("--aux-cus", type=int, default=0,
                     help="run the step's aux-stream prologue on this many CUs only (0 = all)")
     ap.add_argument("--replay-slices", type=int, default=None,
@@ -303,6 +338,8 @@ def main() -> None:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
+    emulate = args.emulate_world > 1 and world == 1
+    shard_world = args.emulate_world if emulate else world  # the W of the sharded step's shapes
     # more ranks than GPUs only with --dist-backend gloo (RCCL needs one GPU per rank)
     device = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(device)
@@ -317,11 +354,11 @@ def main() -> None:
         args.replay_slices = int(c.get("replay_slices", 64))
     if args.steps is None:  # one epoch: the deferred-AdamW flush closes it, as at the reference's epoch end
         args.steps = max(1, math.ceil(c["U"] * c["pos_per_user"] / c["B"]))
-    w = Workload(c, device, args.seed + rank, world=world, rank=rank, step_seed=args.seed,
+    w = Workload(c, device, args.seed + rank, world=shard_world, rank=rank, step_seed=args.seed,
                  deferred=not args.eager_adamw, overlap=not args.no_overlap, in_batch=in_batch,
                  table_math="exact" if args.exact_table_math else "fast", replay_slices=args.replay_slices,
                  aux_cus=args.aux_cus, sharded_single=args.sharded_single,
-                 group_towers=not args.overlap_exchange)
+                 group_towers=not args.overlap_exchange, emulate=emulate)
     eng = w.engine
     for _ in range(args.warmup):
         u, p = w.batch()
@@ -329,9 +366,12 @@ def main() -> None:
     eng.flush()  # the timed region starts with every table row current
     torch.cuda.synchronize()
 
-    # per-step HIP event pairs on the step's stream (ttamm.h ttamm_step_args.timing_events):
-    # [0,1] dense-group table maintenance, [2,3] the grouped first feature-layer forward GEMM
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(args.steps)]
+    # per-step HIP event pairs (ttamm.h ttamm_step_args.timing_events), each recorded on the
+    # stream its kernel runs on: [0,1] the deferred slice's replay kernel, [2,3] the grouped first
+    # feature-layer forward GEMM, [4,5] the in-batch kernel, [6,7] the wide weight-gradient GEMM
+    # launch, [8,9] / [10,11] the user / item catch-up replay kernels
+    NEV = 12
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(NEV)] for _ in range(args.steps)]
     for quad in evs:  # materialise the hipEvent_t handles
         for e in quad:
             e.record()
@@ -362,88 +402,115 @@ def main() -> None:
     loss = eng.finish()
     steps_only_ms = marks[0].elapsed_time(marks[1]) / args.steps
     flush_ms = marks[1].elapsed_time(marks[2])
-    maint_ms = sum(q[0].elapsed_time(q[1]) for q in evs) / args.steps
-    gemm_ms = sum(q[2].elapsed_time(q[3]) for q in evs) / args.steps
-    ib_ms = sum(q[4].elapsed_time(q[5]) for q in evs) / args.steps if in_batch else 0.0
+
+    def pair_ms(i: int) -> float:  # mean over the timed steps of event pair (i, i + 1); 0 if unused
+        tot = 0.0
+        for q in evs:
+            try:
+                tot += q[i].elapsed_time(q[i + 1])
+            except RuntimeError:  # not recorded this step
+                return 0.0
+        return tot / args.steps
 
     B, U, I, D, F, H, N = c["B"], c["U"], c["I"], c["D"], c["F"], c["H"], c["N"]
+    sharded = shard_world > 1 or args.sharded_single
     interactions = args.steps * B * world
     value = interactions / elapsed
-    # first feature layer, grouped launch: rows x F x H multiply-adds (algorithmic F, not the
-    # MFMA's zero-padded K).  One process: user rows B + item rows B(1+N); sharded: the
-    # owner's item rows (+ its B user rows when the two towers' forward is grouped).
-    if world == 1 and not args.sharded_single:
-        l1_rows = B + B * (1 + N)
-    else:
-        l1_rows = (getattr(eng, "item_rows_seen", 0) - rows0) / args.steps + (B if eng.group_towers else 0)
-    l1_flops = 2.0 * l1_rows * F * H
-    tflops = l1_flops / (gemm_ms * 1e-3) / 1e12
     bf16 = c.get("matmul", "fp32") == "bf16"
-    mfma_peak = MFMA_BF16_PEAK_TFLOPS if bf16 else MFMA_FP32_PEAK_TFLOPS
-    traffic = load_traffic(args.config)
-    deferred = not args.eager_adamw
-    if deferred:
-        maint = {"kernel": "replay_kernel (deferred AdamW g=0, this step's 1/64 slice of the mimic tables)",
-                 "bound": "valu", "avg_launch_ms": round(maint_ms, 4),
-                 "note": "avg_launch_ms: the per-step slice only, live; the catch-up of touched rows (aux stream) "
-                         "and the flushes are further replay_kernel launches.  valu_roofline: all of them, from "
-                         "the committed rocprofv3 passes (SQ_INSTS_VALU per element-step x element-steps per "
-                         "step / replay time per step vs the chip's VALU issue rate)",
-                 "valu_roofline": (traffic or {}).get("replay_valu_roofline")}
-    else:
-        sweep_bytes = 24 * (U + I) * D if world == 1 else 24 * I * D
-        gbs = sweep_bytes / (maint_ms * 1e-3) / 1e9
-        maint = {"kernel": "dense_sweep_kernel (eager AdamW g=0 over the mimic tables)", "bound": "hbm",
-                 "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
-                 "traffic": (traffic or {}).get("dense_sweep_kernel_bytes_per_launch"),
-                 "algorithmic_bytes_per_launch": sweep_bytes, "avg_launch_ms": round(maint_ms, 4)}
     exact_mfma = os.environ.get("TTAMM_FP32_MFMA") == "exact"
+    mfma_peak = MFMA_BF16_PEAK_TFLOPS if bf16 else MFMA_FP32_PEAK_TFLOPS
+    split_ceiling = None if (bf16 or exact_mfma) else MFMA_BF16_PEAK_TFLOPS / 6.0  # six bf16 MFMAs per product
+    traffic = load_traffic(args.config) or {}
+    # tower rows of one step: users B; items B (1 + N) (one process) or the owner's requested rows
+    if not sharded:
+        item_rows = B * (1 + N)
+    else:
+        item_rows = (getattr(eng, "item_rows_seen", 0) - rows0) / args.steps
+    rows = {"user": B, "item": item_rows}
     if bf16:
         impl = "bf16 operands, v_mfma_f32_32x32x16_bf16"
     elif exact_mfma:
         impl = "fp32 v_mfma_f32_32x32x2_f32"
     else:
         impl = "fp32 as split-bf16 (hi/mid/lo planes, 6 x v_mfma_f32_32x32x16_bf16 per product)"
-    l1 = {
-        "bound": "mfma",
-        "kernel": f"first feature layer forward GEMM (Linear {F}->{H} + ReLU + dropout, user and item rows "
-                  f"grouped), {impl}",
-        "achieved": round(tflops, 2),
-        "peak": mfma_peak,
-        "unit": "TFLOP/s",
-        "frac": round(tflops / mfma_peak, 4),
-        "traffic": (traffic or {}).get("l1_forward_gemm_bytes_per_launch"),
-        "algorithmic_flops_per_launch": l1_flops,
-        "algorithmic_bytes_per_launch": l1_rows * (F * 4 + H * 4),
-        "avg_launch_ms": round(gemm_ms, 4),
-    }
-    if not bf16 and not exact_mfma:
-        # the split kernel's own ceiling: six bf16 MFMAs per fp32 product
-        ceil = MFMA_BF16_PEAK_TFLOPS / 6.0
-        l1["kernel_ceiling_tflops"] = round(ceil, 1)
-        l1["frac_of_kernel_ceiling"] = round(tflops / ceil, 4)
-    kernels = [l1]
+
+    def mfma_entry(name: str, flops: float, ms: float, ceiling: float | None, traffic_key: str,
+                   alg_bytes: float | None = None) -> dict:
+        tf = flops / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+        e = {"bound": "mfma", "kernel": name, "achieved": round(tf, 2), "peak": mfma_peak, "unit": "TFLOP/s",
+             "frac": round(tf / mfma_peak, 4), "traffic": traffic.get(traffic_key),
+             "algorithmic_flops_per_launch": flops, "avg_launch_ms": round(ms, 4), "ms_per_step": round(ms, 4)}
+        if alg_bytes is not None:
+            e["algorithmic_bytes_per_launch"] = alg_bytes
+        if ceiling:
+            e["kernel_ceiling_tflops"] = round(ceiling, 1)
+            e["frac_of_kernel_ceiling"] = round(tf / ceiling, 4)
+        return e
+
+    kernels = []
+    # first feature layer, grouped launch: rows x F x H multiply-adds (algorithmic F, not the
+    # MFMA's zero-padded K); sharded + grouped towers: the owner's item rows + its B user rows
+    l1_rows = rows["item"] + (B if (not sharded or eng.group_towers) else 0)
+    kernels.append(mfma_entry(
+        f"first feature layer forward GEMM (Linear {F}->{H} + ReLU + dropout, user and item rows grouped), {impl}",
+        2.0 * l1_rows * F * H, pair_ms(2), split_ceiling, "l1_forward_gemm_bytes_per_launch",
+        alg_bytes=l1_rows * (F * 4 + H * 4)))
+    wide = [(R, M, Nn) for R, M, Nn in wgrad_problems(c, rows) if M > 96]
+    if wide:
+        kernels.append(mfma_entry(
+            "wide weight-gradient GEMM launch (dW = dY^T X, split-K slabs; "
+            + ", ".join(f"{M}x{Nn}" for _, M, Nn in wide[: len(wide) // 2]) + f" per tower), {impl}",
+            sum(2.0 * R * M * Nn for R, M, Nn in wide), pair_ms(6), split_ceiling, "wgrad_wide_bytes_per_launch"))
     if in_batch:
-        Bg = B * world
+        Bg = B * shard_world if sharded else B
         ib_flops = 6.0 * B * Bg * D  # S = U P^T, dU = dS P, dP = dS^T U (S recomputed: not counted)
-        ib_tf = ib_flops / (ib_ms * 1e-3) / 1e12
-        kernels.append({
-            "bound": "mfma",
-            "kernel": f"inbatch_x_kernel (S = U P^T [{B} x {Bg}] + BCE + dU + dP, fp32 as split-bf16: "
-                      f"6 x v_mfma_f32_32x32x16_bf16 per product) + ib_reduce"
-                      if not exact_mfma else
-                      f"inbatch_kernel (S = U P^T [{B} x {Bg}] + BCE + dU + dP, fp32 MFMA 32x32x2) + ib_reduce",
-            "achieved": round(ib_tf, 2), "peak": MFMA_FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(ib_tf / MFMA_FP32_PEAK_TFLOPS, 4),
-            "traffic": (traffic or {}).get("inbatch_bytes_per_launch"),
-            "algorithmic_flops_per_launch": ib_flops, "avg_launch_ms": round(ib_ms, 4),
-        })
-        if not exact_mfma:  # S is formed twice (user and item roles): 8 B Bg D executed flops
-            ceil = MFMA_BF16_PEAK_TFLOPS / 6.0 * 6.0 / 8.0
-            kernels[-1]["kernel_ceiling_tflops"] = round(ceil, 1)
-            kernels[-1]["frac_of_kernel_ceiling"] = round(ib_tf / ceil, 4)
-    roof = max(kernels, key=lambda k: k["avg_launch_ms"])
-    neg_desc = (f"in-batch negatives (all {B * world} positives of the global batch)"
+        # S is formed twice (user and item roles): 8 B Bg D executed flops
+        kernels.append(mfma_entry(
+            f"inbatch_x_kernel (S = U P^T [{B} x {Bg}] + BCE + dU + dP), {impl}" if not exact_mfma else
+            f"inbatch_kernel (S = U P^T [{B} x {Bg}] + BCE + dU + dP, fp32 MFMA 32x32x2)",
+            ib_flops, pair_ms(4), split_ceiling * 6.0 / 8.0 if split_ceiling else None, "inbatch_bytes_per_launch"))
+    deferred = not args.eager_adamw
+    slice_ms, cu_user_ms, cu_item_ms = pair_ms(0), pair_ms(8), pair_ms(10)
+    if deferred:
+        # every element of the dense-group tables moves one AdamW(g = 0) step per training step
+        # (the rows a step touches take their real update in row_update_kernel instead)
+        table_rows = (U + I) if not sharded else (U + I)  # this rank's shards
+        es_per_step = table_rows * D
+        flush_share = flush_ms / args.steps
+        rep_ms = slice_ms + cu_user_ms + cu_item_ms + flush_share
+        rv = traffic.get("replay_valu_roofline") or {}
+        per_es = rv.get("valu_lane_instr_per_element_step")
+        ent = {"bound": "valu",
+               "kernel": "replay_kernel (deferred AdamW g=0): rolling slice + user / item catch-up lists + the "
+                         "closing flush's share, per step",
+               "ms_per_step": round(rep_ms, 4),
+               "parts_ms_per_step": {"slice": round(slice_ms, 4), "catchup_user": round(cu_user_ms, 4),
+                                     "catchup_item": round(cu_item_ms, 4), "closing_flush_share": round(flush_share, 4)},
+               "element_steps_per_step": es_per_step, "unit": "wave-instr/s", "peak": VALU_WAVE_INSTR_PEAK,
+               "valu_lane_instr_per_element_step": per_es,
+               "note": "achieved = element-steps per step x VALU lane-instructions per element-step (SQ_INSTS_VALU "
+                       "from the committed rocprofv3 pass, profiles/pmc_traffic.json) / 64 / ms_per_step; peak = "
+                       "one wave64 VALU instruction per 2 cycles per SIMD (1024 SIMDs, 2.4 GHz)",
+               "traffic": rv.get("hbm_bytes_per_step")}
+        if per_es and rep_ms > 0:
+            ach = es_per_step * per_es / 64 / (rep_ms * 1e-3)
+            ent["achieved"] = round(ach, 0)
+            ent["frac"] = round(ach / VALU_WAVE_INSTR_PEAK, 4)
+        kernels.insert(0, ent)
+        maint = ent
+    else:
+        maint_ms = pair_ms(0)
+        sweep_bytes = 24 * (U + I) * D
+        gbs = sweep_bytes / (maint_ms * 1e-3) / 1e9 if maint_ms > 0 else 0.0
+        maint = {"kernel": "dense_sweep_kernel (eager AdamW g=0 over the mimic tables)", "bound": "hbm",
+                 "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                 "traffic": traffic.get("dense_sweep_kernel_bytes_per_launch"),
+                 "algorithmic_bytes_per_launch": sweep_bytes, "avg_launch_ms": round(maint_ms, 4),
+                 "ms_per_step": round(maint_ms, 4)}
+        kernels.insert(0, maint)
+    roof = max(kernels, key=lambda k: k.get("ms_per_step", 0.0))
+    Bg_desc = B * shard_world if sharded else B
+    neg_desc = (f"in-batch negatives (all {Bg_desc} positives of the global batch)"
                 + (f" + {N} sampled" if N else "")) if in_batch else f"N={N} sampled negatives"
     out = {
         "metric": METRIC,
@@ -460,7 +527,7 @@ def main() -> None:
         "data": f"synthetic: {args.config.upper()} shapes, Zipf(1.05) positives (20/user), features shaped like "
                 "features.py, random-init weights",
         "config": {
-            "workload": f"{args.config.upper()}: {I * world} items x {U * world} users, D={D}, "
+            "workload": f"{args.config.upper()}: {I * shard_world} items x {U * shard_world} users, D={D}, "
                         f"MLP {F}->{H}->{D} (ReLU, dropout {c['dropout']}), gated fusion, adaptive mimic, "
                         f"{'bf16' if bf16 else 'fp32'} tower GEMMs, "
                         f"B={B} per GPU, {neg_desc}, AdamW + SparseAdam",
@@ -482,9 +549,15 @@ def main() -> None:
                              "every deferred table row current (part of the K steps' work)"},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if emulate:
+        out["emulated_world"] = shard_world
+        out["config"]["parallelism"] = (f"EMULATED rank 0 of {shard_world}: row-sharded step with mirrored ranks "
+                                        "(ttamm.sharded.MirrorComm, no interconnect traffic)")
+        out["note"] = ("value = this rank's own interactions/s; a W-rank job's aggregate is at most W x value "
+                       "(collectives over xGMI not included)")
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not emulate:
         try:
-            out["cpu_baseline"] = cpu_baseline(c, args.cpu_steps, 1, args.seed, in_batch=in_batch)
+            out["cpu_baseline"] = cpu_baseline(c, args.cpu_steps, args.cpu_warmup, args.seed, in_batch=in_batch)
         except Exception as exc:  # reported, not fatal to the GPU measurement
             out["cpu_baseline"] = {"error": repr(exc)}
     if rank == 0:

@@ -32,14 +32,20 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 16
+#define TTAMM_ABI_VERSION 19
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
 #define TTAMM_E_RUNTIME 2 /* runtime condition          -> RuntimeError */
 #define TTAMM_E_HIP 3     /* HIP API failure            -> RuntimeError */
 
-#define TTAMM_MAX_LINEAR 4 /* feature-encoder Linear layers per tower (hidden + final) */
+#define TTAMM_MAX_LINEAR 6 /* feature-encoder Linear layers per tower (hidden + final) */
+
+/* Feature-MLP activations (encoders.py:68-78 _get_activation; ttamm_tower.activation). */
+#define TTAMM_ACT_RELU 0
+#define TTAMM_ACT_GELU 1 /* nn.GELU(approximate='none'): x / 2 (1 + erf(x / sqrt 2)) */
+#define TTAMM_ACT_TANH 2
+#define TTAMM_ACT_SELU 3
 
 /* Fusion strategies of TowerEncoder (encoders.py:194-219). "concat" is not on the hot path. */
 #define TTAMM_FUSION_IDENTITY 0
@@ -92,6 +98,12 @@ extern "C" {
  * so each tower-wide kernel is launched once per step, as in the one-process step. */
 #define TTAMM_PHASE_SCORE 256
 #define TTAMM_PHASE_TOWERS_BWD 512
+/* Gradient clipping in a sharded step (hp.grad_clip_norm > 0; grouped schedule): TOWERS_BWD then
+ * leaves the table updates out and writes this rank's squared gradient norm over the table rows it
+ * owns to *table_sumsq; after the caller's all-reduce of dense_grads and table_sumsq,
+ *   TABLES  clip_grad_norm_'s coefficient from the global norm, then the table updates
+ * and DENSE applies the same coefficient. */
+#define TTAMM_PHASE_TABLES 1024
 
 /* Device-side status word bits (written by kernels, read by the host at epoch end).  Once a
  * bit is set, every later step on that status word is skipped on the device (no parameter,
@@ -154,8 +166,11 @@ typedef struct ttamm_tower {
     int64_t feat_ld;       /* row stride in floats, multiple of 4                       */
     int32_t feat_dim;      /* F (unpadded)                                              */
     int32_t fusion;        /* TTAMM_FUSION_*                                            */
-    int32_t n_linear;      /* Linear layers in the feature encoder (0 = none)           */
-    float dropout;         /* Dropout p after each hidden ReLU (encoders.py:132-138)    */
+    int32_t n_linear;      /* Linear layers in the feature encoder; 0 with fusion !=
+                              IDENTITY = the identity feature encoder (encoders.py:114-119:
+                              f = the feature row, feat_dim == id.dim)                    */
+    float dropout;         /* Dropout p after each hidden activation (encoders.py:132-138) */
+    int32_t activation;    /* TTAMM_ACT_* of the hidden layers (encoders.py:130)          */
     ttamm_linear linear[TTAMM_MAX_LINEAR];
     ttamm_linear gate[2];  /* FeatureFusionGate.gate_network.{0,2} (encoders.py:157-162) */
     int32_t matmul_bf16;   /* 0: fp32 GEMMs (the reference).  1: "bf16 towers" (BASELINE config
@@ -222,11 +237,14 @@ typedef struct ttamm_step_args {
     uint32_t* status;     /* device status word (TTAMM_STATUS_* bits), OR-ed          */
     void* workspace;
     size_t workspace_bytes;
-    void* timing_events[6]; /* optional hipEvent_t pairs (bench roofline), NULL = off:
+    void* timing_events[12]; /* optional hipEvent_t pairs (bench roofline), NULL = off:
                                [0],[1] around the dense-group table maintenance (eager
-                               AdamW(g=0) sweep, or deferred slice replay); [2],[3] around
-                               the grouped first feature-layer forward GEMM; [4],[5] around
-                               the in-batch scoring kernel (in_batch)                    */
+                               AdamW(g=0) sweep, or the deferred slice's replay kernel);
+                               [2],[3] around the grouped first feature-layer forward GEMM;
+                               [4],[5] around the in-batch scoring kernel (in_batch);
+                               [6],[7] around the wide weight-gradient GEMM launch;
+                               [8],[9] / [10],[11] around the user / item tower's deferred
+                               catch-up replay kernel (on aux_stream when it is set)      */
     /* ---- row-sharded multi-GPU step (phase != TTAMM_PHASE_ALL) ----------------------
      * The same workspace must be passed to every phase of a step.                        */
     int32_t phase;                /* TTAMM_PHASE_* bits                                      */
@@ -246,6 +264,8 @@ typedef struct ttamm_step_args {
                                      ordered [positives; negatives (b-major)]               */
     float* item_bwd_out;          /* requester: [batch*(1+num_neg), 2*dim] (dT | dA)         */
     const float* item_bwd_in;     /* owner:     [n_item_rows, 2*dim] (dT | dA)               */
+    float* table_sumsq;           /* sharded clipping: [1] this rank's table-row squared gradient
+                                     norm (TOWERS_BWD), all-reduced by the caller before TABLES */
     float* dense_grads;           /* replicated-weight gradient arena
                                      (ttamm_dense_grad_floats floats)                        */
     /* ---- deferred exact AdamW(g = 0) on tables with last_step (see ttamm_table) ---------- */
@@ -410,6 +430,37 @@ size_t ttamm_tower_forward_workspace_size(const ttamm_tower* tower, int64_t n);
 int ttamm_tower_forward(const ttamm_tower* tower, const int64_t* idx, const int64_t* feat_idx, int64_t n,
                         int32_t augment, float* out, void* workspace, size_t workspace_bytes,
                         void* stream);
+
+/* TowerEncoder.forward under autograd (encoders.py:221-255): the training-mode forward keeps its
+ * activations in `workspace` (ttamm_tower_train_workspace_size); ttamm_tower_train_backward, given
+ * the same tower, rows, keep masks and workspace and d_out = dL/d(out) [n, dim], runs the tower's
+ * backward (gate, feature-MLP dgrad chain, one grouped weight-gradient launch) into grad_arena
+ * (ttamm_tower_grad_floats floats: per feature Linear weight [out, in] then bias [out], then the
+ * gate's / concat projection's, each piece starting at a multiple of 64 floats) and writes the
+ * ID rows' gradient per position into d_id_rows [n, dim] (nn.Embedding's sparse gradient values;
+ * duplicates not summed).  d_feat_rows [n, dim]: the feature rows' gradient, identity feature
+ * encoder only (FeatureFusionGate.forward on given rows).  keep_masks: NULL or one uint8
+ * [n, out_features] keep mask per hidden layer (NULL entries: drawn from Philox(seed, counter)).
+ * The tower's optimizer-state pointers are not read. */
+size_t ttamm_tower_grad_floats(const ttamm_tower* tower);
+size_t ttamm_tower_train_workspace_size(const ttamm_tower* tower, int64_t n);
+int ttamm_tower_train_forward(const ttamm_tower* tower, const int64_t* idx, const int64_t* feat_idx, int64_t n,
+                              const uint8_t* const* keep_masks, uint64_t seed, uint64_t counter, float* out,
+                              void* workspace, size_t workspace_bytes, void* stream);
+int ttamm_tower_train_backward(const ttamm_tower* tower, const int64_t* idx, const int64_t* feat_idx, int64_t n,
+                               const uint8_t* const* keep_masks, const float* d_out, float* grad_arena,
+                               float* d_id_rows, float* d_feat_rows, void* workspace, size_t workspace_bytes,
+                               void* stream);
+
+/* The backward of a row lookup into a dense gradient (nn.Embedding(sparse=False) / the dense
+ * mimic tables, adaptive_mimic.py:97-105; F.mse_loss's input gradient with scale = 2 / numel):
+ * dst[idx[r]] += (x[r] - y[r]) * scale * (*scale_dev) for y != NULL, x[r] * ... otherwise
+ * (idx NULL: dst row r — an elementwise scaled difference, F.mse_loss's backward);
+ * scale_dev (device float, e.g. the upstream gradient of a scalar loss) may be NULL; rows with
+ * idx[r] == skip_row (padding_idx, -1 = none) are skipped.  Float atomics. */
+int ttamm_scatter_add_rows(float* dst, int64_t dst_rows, int32_t dim, const int64_t* idx, int64_t n,
+                           const float* x, int64_t ldx, const float* y, int64_t ldy, const float* scale_dev,
+                           float scale, int64_t skip_row, void* stream);
 
 /* AdaptiveMimicMechanism._apply_aug (adaptive_mimic.py:88-95): out = base + table[idx].
  * aug_out (optional) receives table[idx]. */

@@ -76,6 +76,19 @@ class OracleModel(nn.Module):  # two_tower.py:19-38
         self.adaptive_mimic = adaptive_mimic
 
 
+def _activation(name: str) -> nn.Module:  # encoders.py:68-78 _get_activation
+    key = name.lower()
+    if key == "relu":
+        return nn.ReLU()
+    if key == "gelu":
+        return nn.GELU()
+    if key == "tanh":
+        return nn.Tanh()
+    if key == "selu":
+        return nn.SELU()
+    raise ValueError(f"Unsupported activation '{name}'")
+
+
 def build_tower(cfg: Mapping[str, Any], *, num_embeddings: int, feature_dim: int) -> OracleTower:
     """encoders.py:258-331 with the same parameter construction / init order."""
     id_cfg = cfg.get("id_embedding", {}) or {}
@@ -96,10 +109,14 @@ def build_tower(cfg: Mapping[str, Any], *, num_embeddings: int, feature_dim: int
             lin = nn.Linear(feature_dim, out)
             nn.init.xavier_uniform_(lin.weight)
             fe = FeatureEncoderWrapper(lin, out)
+        elif kind == "identity":  # encoders.py:114-119
+            if feature_dim != out:
+                raise ValueError("Identity feature encoder requires input_dim == output_dim.")
+            fe = FeatureEncoderWrapper(nn.Identity(), out)
         elif kind == "mlp":  # encoders.py:126-144
             mods: list[nn.Module] = []
             prev = feature_dim
-            act = nn.ReLU()
+            act = _activation(str(fcfg.get("activation", "relu")))  # encoders.py:68-78, one shared module
             for h in fcfg.get("hidden_dims") or []:
                 lin = nn.Linear(prev, int(h))
                 nn.init.xavier_uniform_(lin.weight)
@@ -178,6 +195,8 @@ def feature_forward(fe: FeatureEncoderWrapper, x: torch.Tensor, keep_masks: Sequ
     net = fe.network
     if isinstance(net, nn.Linear):
         return _linear(net, x, bf16)
+    if isinstance(net, nn.Identity):  # encoders.py:114-119
+        return x
     hidden = 0
     for m in net:
         if isinstance(m, nn.Dropout):

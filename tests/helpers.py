@@ -30,6 +30,8 @@ class Shape:
     padding_idx: int | None = None  # nn.Embedding padding_idx of both ID tables (encoders.py:47)
     fusion: str = "gated"  # TowerEncoder fusion (encoders.py:203): gated / sum / concat
     max_norm: float | None = None  # nn.Embedding max_norm of both ID tables (dense only, encoders.py:48-52)
+    activation: str = "relu"  # feature-MLP activation (encoders.py:68-78)
+    feature_type: str = "mlp"  # feature encoder type (encoders.py:114-144): mlp / linear / identity (F == D)
 
     def tower_cfg(self) -> dict:
         params = {"embedding_dim": self.D, "sparse": self.sparse}
@@ -41,8 +43,8 @@ class Shape:
             "type": "tower",
             "matmul_dtype": self.matmul_dtype,
             "id_embedding": {"params": params, "init": {"type": "normal", "std": 0.02}},
-            "feature_encoder": {"type": "mlp", "hidden_dims": list(self.hidden_dims), "activation": "relu",
-                                "output_dim": self.D, "dropout": self.dropout},
+            "feature_encoder": {"type": self.feature_type, "hidden_dims": list(self.hidden_dims),
+                                "activation": self.activation, "output_dim": self.D, "dropout": self.dropout},
             "fusion": self.fusion,
             "output_dim": self.D,  # the concat projection's width (encoders.py:211)
             "adaptive_mimic": {"hidden_dim": self.gate_hidden} if self.gate_hidden else {},
@@ -98,7 +100,7 @@ def make_problem(shape: Shape, *, seed: int = 1234, steps: int = 1, positives_pe
             users[:3] = shape.padding_idx
             pos[3] = shape.padding_idx
             neg[:2, :2] = shape.padding_idx
-        nh = len(shape.hidden_dims)
+        nh = len(shape.hidden_dims) if shape.feature_type == "mlp" else 0
         um = [(torch.rand((shape.B, h), generator=gen) >= shape.dropout).to(torch.uint8) for h in shape.hidden_dims][:nh]
         im = [(torch.rand((shape.B * (1 + shape.N), h), generator=gen) >= shape.dropout).to(torch.uint8)
               for h in shape.hidden_dims][:nh]

@@ -62,3 +62,32 @@ def test_sampled_candidates_follow_the_reference_rng_order():
         available = list(set(range(c1.num_items)) - set(c1.train_positive_map.get(u, set())))
         cands.update(int(n) for n in rng.choice(available, size=min(50, len(available)), replace=False).tolist())
         assert lst == list(cands), u
+
+
+def test_sampled_candidates_dense_blocked_sets_follow_cpython_order():
+    """A user blocking n / 4 items or more: CPython's set difference then builds a new, smaller
+    table whose iteration order is not ascending (n = 100 with 90 blocked iterates 96..99 before
+    90..95), so rng.choice over it picks different items than over the sorted array.  The builder
+    must follow the reference's list(set(range(n)) - blocked) order on both sides of the n / 4
+    threshold."""
+    import numpy as np
+
+    from ttamm.retrieval import sampled_candidates
+
+    n = 100
+    gen = np.random.default_rng(7)
+    for nblocked in (0, 10, 24, 25, 26, 60, 90, 99):
+        blocked = set(gen.choice(n, size=nblocked, replace=False).tolist())
+        free = sorted(set(range(n)) - blocked)
+        truth = {0: {free[0]}}
+        got = sampled_candidates([0], truth, {0: blocked}, num_items=n, candidate_samples=8,
+                                 rng=np.random.default_rng(11))[0]
+        rng = np.random.default_rng(11)
+        cands = set(truth[0])
+        available = list(set(range(n)) - blocked)
+        budget = max(0, min(8, len(available)))
+        if budget:
+            cands.update(int(x) for x in rng.choice(available, size=budget, replace=False).tolist())
+        assert got == list(cands), nblocked
+    # the non-ascending case does occur at this size (the test exercises the new-set path)
+    assert list(set(range(n)) - set(range(90))) != sorted(set(range(n)) - set(range(90)))

@@ -118,6 +118,12 @@ def _run(batches, g, ranks, W):
     (2, Shape(U=200, I=900, F=40, H=64, D=128, B=48, N=0, hidden_dims=(64,)), True, True),
     # C5 arithmetic (bf16 tower GEMMs, D = 64, H = 128) through the sharded phases
     (2, Shape(U=200, I=900, F=37, H=128, D=64, B=40, N=3, hidden_dims=(128,), matmul_dtype="bf16"), False, True),
+    # the C4 topology: 8 ranks, in-batch negatives over the all-gathered global batch (Bg = 8 x 256
+    # = 2048 positives per user), D = 128 (generic gate path)
+    (8, Shape(U=800, I=4000, F=40, H=64, D=128, B=256, N=0, hidden_dims=(64,)), True, True),
+    # 8 ranks, sampled negatives (the C2 topology at W = 8), both schedules
+    (8, Shape(U=800, I=4000, B=64, N=3), False, True),
+    (8, Shape(U=800, I=4000, B=64, N=3), False, False),
 ])
 def test_sharded_gradients_match_global_step(W, shape, in_batch, group):
     prob, batches, g, ranks = _setup(shape, W, lr=0.0, betas=(0.0, 0.999), steps=1, in_batch=in_batch, group=group)
@@ -245,3 +251,101 @@ def test_sharded_epoch_routes_pairs_to_user_owners():
             want = gsd[k][own.rank:: W] if k in TABLES else gsd[k]
             d = (v - want).abs().max().item()
             assert d <= 5e-5, f"rank {own.rank} {k}: {d:.2e}"
+
+
+def _ranks_only(shape: Shape, W: int, *, max_batch: int, in_batch: bool = False, lr: float = 1e-3):
+    prob = make_problem(shape, seed=31)
+    state = prob.model.state_dict()
+    ranks = []
+    for r in range(W):
+        own = RowOwnership(W, r)
+        st = {k: (own.shard(v) if k in TABLES else v.clone()) for k, v in state.items()}
+        m = _model(shape, own.local_count(shape.U), own.local_count(shape.I), st)
+        opts = _opts(m, lr, (0.9, 0.999))
+        local_pos = {u // W: prob.positives[u] for u in range(r, shape.U, W)}
+        eng = ShardedTrainStep(m, opts, world_size=W, rank=r, num_items=shape.I, negatives_per_positive=shape.N,
+                               positives=local_pos, user_features=own.shard(prob.user_features).cuda(),
+                               item_features=own.shard(prob.item_features).cuda(), loss_weights=LOSS_WEIGHTS,
+                               max_batch=max_batch, seed=SEED, in_batch_negatives=in_batch)
+        ranks.append((own, m, opts, eng))
+    return prob, ranks
+
+
+@pytest.mark.parametrize("in_batch", [False, True], ids=["capacity", "in-batch-unequal"])
+def test_sharded_epoch_rejects_bad_routing_on_every_rank(in_batch):
+    """epoch_program: a routed batch over max_batch, or unequal routed batches with in-batch
+    negatives, raise ValueError on EVERY rank before the step's first collective (one rank
+    raising alone would leave the others waiting in an all-to-all under RCCL)."""
+    from ttamm.sharded import epoch_program
+
+    W, b = 2, 24
+    shape = Shape(N=2 if in_batch else 5)
+    prob, ranks = _ranks_only(shape, W, max_batch=b if not in_batch else 2 * b, in_batch=in_batch)
+    # 3/4 of every source's pairs belong to rank 0's users: routed sizes (36, 12) per step
+    gen = torch.Generator().manual_seed(3)
+    per_rank = []
+    for r in range(W):
+        owned0 = torch.arange(0, shape.U, W)
+        owned1 = torch.arange(1, shape.U, W)
+        u = torch.cat([owned0[torch.randint(0, owned0.numel(), (3 * b // 4,), generator=gen)],
+                       owned1[torch.randint(0, owned1.numel(), (b // 4,), generator=gen)]])
+        i = torch.tensor([sorted(prob.positives[int(x)])[0] for x in u], dtype=torch.long)
+        per_rank.append([(u.cuda(), i.cuda())])
+
+    def catching(prog):
+        try:
+            return (yield from prog)
+        except ValueError as e:
+            return e
+
+    res = run_loopback([catching(epoch_program(eng, per_rank[r])) for r, (_, _, _, eng) in enumerate(ranks)])
+    for r in range(W):
+        assert isinstance(res[r], ValueError), (r, res[r])
+        assert ("max_batch" in str(res[r])) if not in_batch else ("same routed batch size" in str(res[r]))
+
+
+def test_sharded_poisoned_step_is_skipped_by_every_rank():
+    """An id outside rank 1's user shard in step 2: both ranks skip step 2 and 3 (the status
+    words ride with the request counts), finish raises IndexError on both, and both ranks hold
+    exactly the state after step 1 — bit for bit that of a run that stopped after step 1."""
+    W, shape = 2, Shape()
+
+    def batches(prob, steps):
+        gen = torch.Generator().manual_seed(9)
+        out = []
+        for _ in range(steps):
+            per = []
+            for r in range(W):
+                owned = torch.arange(r, shape.U, W)
+                users = owned[torch.randint(0, owned.numel(), (shape.B,), generator=gen)]
+                pos = torch.tensor([sorted(prob.positives[int(u)])[0] for u in users], dtype=torch.long)
+                per.append(((users // W).cuda(), pos.cuda()))
+            out.append(per)
+        return out
+
+    def catching(prog):
+        try:
+            return (yield from prog)
+        except (IndexError, RuntimeError) as e:
+            return e
+
+    prob, ranks = _ranks_only(shape, W, max_batch=shape.B)
+    steps = batches(prob, 3)
+    bad = steps[1][1][0].clone()
+    bad[5] = 10 ** 6  # not a row of rank 1's user shard
+    steps[1][1] = (bad, steps[1][1][1])
+    for per in steps:
+        run_loopback([eng.program(u, p) for (_, _, _, eng), (u, p) in zip(ranks, per)])
+    res = run_loopback([catching(eng.finish_program()) for (_, _, _, eng) in ranks])
+    assert all(isinstance(x, IndexError) for x in res), res
+
+    prob2, ref = _ranks_only(shape, W, max_batch=shape.B)
+    run_loopback([eng.program(u, p) for (_, _, _, eng), (u, p) in zip(ref, steps[0])])
+    run_loopback([eng.finish_program() for (_, _, _, eng) in ref])
+    for (own, m, opts, _), (_, m2, opts2, _) in zip(ranks, ref):
+        for (k, v), (_, v2) in zip(m.state_dict().items(), m2.state_dict().items()):
+            assert torch.equal(v, v2), (own.rank, k)
+        st, st2 = named_optimizer_state(m, opts), named_optimizer_state(m2, opts2)
+        for n in st:
+            assert float(st[n]["step"]) == float(st2[n]["step"]) == 1.0, (own.rank, n)
+            assert torch.equal(st[n]["exp_avg"], st2[n]["exp_avg"]), (own.rank, n)

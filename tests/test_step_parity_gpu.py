@@ -32,9 +32,22 @@ def _grads_by_name(model, opts):
         Shape(fusion="sum"),
         Shape(fusion="concat"),
         Shape(U=50, I=300, F=37, H=24, D=12, B=40, N=3, hidden_dims=(24, 16), fusion="concat"),
+        # the reference's other activations (encoders.py:68-78), with dropout (injected keep masks)
+        Shape(activation="gelu"),
+        Shape(activation="tanh"),
+        Shape(activation="selu"),
+        Shape(U=50, I=300, F=37, H=24, D=12, B=40, N=3, hidden_dims=(24, 16), activation="gelu", fusion="sum"),
+        # five hidden layers (six Linear)
+        Shape(hidden_dims=(16, 12, 20, 8, 16)),
+        Shape(hidden_dims=(16, 12, 20, 8, 16), activation="tanh", dropout=0.0),
+        # identity feature encoder (encoders.py:114-119, F == D) and a single Linear encoder
+        Shape(F=8, feature_type="identity"),
+        Shape(F=8, feature_type="identity", fusion="sum"),
+        Shape(feature_type="linear"),
     ],
     ids=["tiny", "nodrop", "odd", "2hidden", "nomimic", "dense-id", "padding", "dense-id-padding", "sum", "concat",
-         "concat-odd"],
+         "concat-odd", "gelu", "tanh", "selu", "gelu-2hidden-sum", "5hidden", "5hidden-tanh", "identity-enc",
+         "identity-enc-sum", "linear-enc"],
 )
 def test_step_gradients_match_oracle(shape):
     from gpu_helpers import run_ttamm

@@ -20,9 +20,9 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
-VALU_ISSUE_PER_S = 1024 * 2.4e9 / 4  # 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles
-# (MI355X_MICROARCH.md 'vector-instruction ISSUE cost': v_add/v_fma 4 cycles; v_sqrt/v_rcp 8, so the
-# replay's two transcendentals per element-step make this an upper bound it cannot reach)
+VALU_ISSUE_PER_S = 1024 * 2.4e9 / 2  # 256 CUs x 4 SIMD-32s, one wave64 VALU instruction per 2 cycles
+# (MI355X_MICROARCH.md "Wave scheduling" and the v_fma_f32 row: 2 cycles per SIMD-32; one wave alone
+# issues at half that, and v_sqrt / v_rcp cost more, so the replay cannot reach this upper bound)
 
 
 def short(name: str) -> str:
@@ -75,6 +75,15 @@ def main() -> None:
         k = max(l1, key=lambda n: kernels[n]["hbm_bytes_per_launch"])
         entry["l1_forward_gemm_kernel"] = k
         entry["l1_forward_gemm_bytes_per_launch"] = kernels[k]["hbm_bytes_per_launch"]
+    # the wide weight-gradient launch (XCfg<128, 192, ..., true, true, ...>, EPI_STORE = 0)
+    wg = [k for k in kernels if k.startswith("gemm_x_kernel<XCfg<128, 192, 2, 2, true, true")]
+    if wg:
+        entry["wgrad_wide_kernel"] = wg[0]
+        entry["wgrad_wide_bytes_per_launch"] = kernels[wg[0]]["hbm_bytes_per_launch"]
+    ib = [k for k in kernels if k.startswith("inbatch")]
+    if ib:
+        k = max(ib, key=lambda n: kernels[n]["hbm_bytes_per_launch"])
+        entry["inbatch_bytes_per_launch"] = kernels[k]["hbm_bytes_per_launch"]
 
     # deferred table AdamW: VALU roofline over the whole run
     rep = [k for k in valu if k.startswith("replay_kernel")]
@@ -93,8 +102,11 @@ def main() -> None:
             total_ns = sum(float(stats[k]["TotalDurationNs"]) for k in rep if k in stats)
             step_ms = total_ns / 1e6 / bench["steps"]
         es_per_step = ((U_ + I_) - (B_ + B_ * (1 + N_))) * D_
+        hbm = sum(kernels[k]["hbm_bytes_per_launch"] * kernels[k]["launches"] for k in kernels
+                  if k.startswith("replay_kernel"))
         out = {
             "kernel": "replay_kernel (deferred AdamW g=0: catch-up of touched rows + rolling slice + flushes)",
+            "hbm_bytes_per_step": round(hbm / steps),
             "bound": "valu",
             "valu_lane_instr_per_element_step": round(per_es, 2),
             "element_steps_per_step": es_per_step,

@@ -24,6 +24,14 @@ int flush_tables(const ttamm_step_args& A, hipStream_t s);
 size_t tower_forward_workspace_size(const ttamm_tower& T, int64_t n);
 int tower_forward_eval(const ttamm_tower& T, const int64_t* idx, const int64_t* fidx, int64_t n, int augment,
                        float* out, void* ws, size_t ws_bytes, hipStream_t s);
+size_t tower_grad_floats_of(const ttamm_tower& T);
+size_t tower_train_workspace_size(const ttamm_tower& T, int64_t n);
+int tower_train_forward(const ttamm_tower& T, const int64_t* idx, const int64_t* fidx, int64_t n,
+                        const uint8_t* const* keep_masks, uint64_t seed, uint64_t counter, float* out, void* ws,
+                        size_t ws_bytes, hipStream_t s);
+int tower_train_backward(const ttamm_tower& T, const int64_t* idx, const int64_t* fidx, int64_t n,
+                         const uint8_t* const* keep_masks, const float* d_out, float* grad_arena, float* d_id_rows,
+                         float* d_feat_rows, void* ws, size_t ws_bytes, hipStream_t s);
 
 }  // namespace ttamm
 
@@ -152,6 +160,40 @@ TTAMM_API int ttamm_tower_forward(const ttamm_tower* tower, const int64_t* idx, 
                                   int32_t augment, float* out, void* workspace, size_t workspace_bytes, void* stream) {
     if (!tower) return fail(TTAMM_E_INVALID, "null tower");
     return tower_forward_eval(*tower, idx, feat_idx, n, augment, out, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+TTAMM_API size_t ttamm_tower_grad_floats(const ttamm_tower* tower) { return tower ? tower_grad_floats_of(*tower) : 0; }
+
+TTAMM_API size_t ttamm_tower_train_workspace_size(const ttamm_tower* tower, int64_t n) {
+    return tower ? tower_train_workspace_size(*tower, n) : 0;
+}
+
+TTAMM_API int ttamm_tower_train_forward(const ttamm_tower* tower, const int64_t* idx, const int64_t* feat_idx,
+                                        int64_t n, const uint8_t* const* keep_masks, uint64_t seed, uint64_t counter,
+                                        float* out, void* workspace, size_t workspace_bytes, void* stream) {
+    if (!tower || (n > 0 && (!idx || !out || !workspace))) return fail(TTAMM_E_INVALID, "tower train forward: null argument");
+    g_last_error.clear();
+    return tower_train_forward(*tower, idx, feat_idx, n, keep_masks, seed, counter, out, workspace, workspace_bytes,
+                               (hipStream_t)stream);
+}
+
+TTAMM_API int ttamm_tower_train_backward(const ttamm_tower* tower, const int64_t* idx, const int64_t* feat_idx,
+                                         int64_t n, const uint8_t* const* keep_masks, const float* d_out,
+                                         float* grad_arena, float* d_id_rows, float* d_feat_rows, void* workspace,
+                                         size_t workspace_bytes, void* stream) {
+    if (!tower || (n > 0 && (!idx || !workspace))) return fail(TTAMM_E_INVALID, "tower train backward: null argument");
+    g_last_error.clear();
+    return tower_train_backward(*tower, idx, feat_idx, n, keep_masks, d_out, grad_arena, d_id_rows, d_feat_rows,
+                                workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+TTAMM_API int ttamm_scatter_add_rows(float* dst, int64_t dst_rows, int32_t dim, const int64_t* idx, int64_t n,
+                                     const float* x, int64_t ldx, const float* y, int64_t ldy, const float* scale_dev,
+                                     float scale, int64_t skip_row, void* stream) {
+    if (n > 0 && (!dst || !x || dim <= 0 || ldx < dim || (y && ldy < dim) || dst_rows <= 0 || (!idx && n > dst_rows)))
+        return fail(TTAMM_E_INVALID, "scatter_add_rows: bad arguments");
+    g_last_error.clear();
+    return launch_scatter_add_rows(dst, dim, idx, n, x, ldx, y, ldy, scale_dev, scale, skip_row, (hipStream_t)stream);
 }
 
 TTAMM_API int ttamm_mimic_augment(const float* table, int64_t table_rows, int32_t dim, const int64_t* idx, int64_t n,

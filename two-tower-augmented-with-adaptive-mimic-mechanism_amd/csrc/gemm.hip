@@ -127,6 +127,36 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 // neutral on the step, a plain-store build ran within noise of it)
 __device__ __forceinline__ void st4(float* p, float4 v) { store_nt(p, v); }
 
+// Feature-MLP activations (encoders.py:68-78, ttamm.h TTAMM_ACT_*), as ATen computes them on the
+// CPU: ReLU; GELU (approximate='none') x / 2 (1 + erf(x / sqrt 2)), d = cdf + x pdf; Tanh, d = 1 - t^2;
+// SELU scale (x > 0 ? x : alpha (exp(x) - 1)), d = x > 0 ? scale : scale alpha exp(x).  Non-ReLU
+// layers keep their pre-activation (GemmProblem::pre) for the backward.
+constexpr float kSeluAlpha = 1.6732632423543772848170429916717f;
+constexpr float kSeluScale = 1.0507009873554804934193349852946f;
+__device__ __forceinline__ float act_fwd(int act, float z) {
+    switch (act) {
+        case TTAMM_ACT_GELU: return z * 0.5f * (1.0f + erff(z * 0.70710678118654752440f));
+        case TTAMM_ACT_TANH: return tanhf(z);
+        case TTAMM_ACT_SELU: return z > 0.f ? z * kSeluScale : (expf(z) - 1.0f) * (kSeluAlpha * kSeluScale);
+        default: return z > 0.f ? z : 0.f;
+    }
+}
+__device__ __forceinline__ float act_grad(int act, float z) {
+    switch (act) {
+        case TTAMM_ACT_GELU: {
+            const float cdf = 0.5f * (1.0f + erff(z * 0.70710678118654752440f));
+            const float pdf = expf(-0.5f * z * z) * 0.39894228040143267794f;  // 1 / sqrt(2 pi)
+            return cdf + z * pdf;
+        }
+        case TTAMM_ACT_TANH: {
+            const float t = tanhf(z);
+            return 1.0f - t * t;
+        }
+        case TTAMM_ACT_SELU: return z > 0.f ? kSeluScale : expf(z) * (kSeluAlpha * kSeluScale);
+        default: return z > 0.f ? 1.f : 0.f;
+    }
+}
+
 template <int E>
 __device__ __forceinline__ void epilogue4(const KArg(GemmProblem) & P, float4 v, float4 bias4, int split, int row,
                                           int col) {
@@ -174,8 +204,17 @@ __device__ __forceinline__ void epilogue4(const KArg(GemmProblem) & P, float4 v,
         }
     } else if (E == EPI_DGRAD_HIDDEN) {
         const float4 hv = ld4(P.aux0 + (int64_t)row * P.ld_aux0 + col);
-        x[0] = hv.x > 0.f ? x[0] * P.inv_keep : 0.f, x[1] = hv.y > 0.f ? x[1] * P.inv_keep : 0.f;
-        x[2] = hv.z > 0.f ? x[2] * P.inv_keep : 0.f, x[3] = hv.w > 0.f ? x[3] * P.inv_keep : 0.f;
+        if (P.act == TTAMM_ACT_RELU) {  // aux0 = the stored hidden output: > 0 iff ReLU passed and kept
+            x[0] = hv.x > 0.f ? x[0] * P.inv_keep : 0.f, x[1] = hv.y > 0.f ? x[1] * P.inv_keep : 0.f;
+            x[2] = hv.z > 0.f ? x[2] * P.inv_keep : 0.f, x[3] = hv.w > 0.f ? x[3] * P.inv_keep : 0.f;
+        } else {  // aux0 = the pre-activation; keep bytes (injected or written by the forward)
+            const float z[4] = {hv.x, hv.y, hv.z, hv.w};
+            uint32_t km = 0xFFFFFFFFu;
+            if (P.keep_prob < 1.0f) km = *reinterpret_cast<const uint32_t*>(P.keep_mask + (int64_t)row * N + col);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                x[e] = ((km >> (8 * e)) & 0xFFu) ? x[e] * P.inv_keep * act_grad(P.act, z[e]) : 0.f;
+        }
     }
     if (E == EPI_GATE_OUT && P.C == nullptr) return;  // sharded item owner: aug is formed by the requester
     st4(P.C + (int64_t)split * P.slab_stride + (int64_t)row * P.ldc + col, make_float4(x[0], x[1], x[2], x[3]));
@@ -216,18 +255,21 @@ __device__ __forceinline__ void epilogue_hidden_pair(const KArg(GemmProblem) & P
     const uint32_t thresh = keep_threshold16(P.keep_prob);
     auto tail = [&](float4 v, const uint32_t w[2], int row) {
         float x[4] = {v.x + bias4.x, v.y + bias4.y, v.z + bias4.z, v.w + bias4.w};
-        uint32_t km = 0xFFFFFFFFu;
+        if (P.pre) st4(P.pre + (int64_t)row * P.ldc + col, make_float4(x[0], x[1], x[2], x[3]));
+        uint32_t km = 0xFFFFFFFFu, kept = 0u;
         if (drop && P.keep_mask) km = *reinterpret_cast<const uint32_t*>(P.keep_mask + (int64_t)row * P.N + col);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            float hv = x[e] > 0.f ? x[e] : 0.f;
+            float hv = P.act == TTAMM_ACT_RELU ? (x[e] > 0.f ? x[e] : 0.f) : act_fwd(P.act, x[e]);
             if (drop) {
                 const bool keep = P.keep_mask ? ((km >> (8 * e)) & 0xFFu) != 0
                                               : ((w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu) < thresh;
                 hv = hv * (keep ? P.inv_keep : 0.f);
+                kept |= keep ? (1u << (8 * e)) : 0u;
             }
             x[e] = hv;
         }
+        if (P.mask_out && drop) *reinterpret_cast<uint32_t*>(P.mask_out + (int64_t)row * P.N + col) = kept;
         st4(P.C + (int64_t)split * P.slab_stride + (int64_t)row * P.ldc + col, make_float4(x[0], x[1], x[2], x[3]));
     };
     if (oka) tail(va, wa, ra);
@@ -256,15 +298,27 @@ __device__ __forceinline__ void epilogue8_hidden(const KArg(GemmProblem) & P, fl
     }
     const uint32_t thresh = keep_threshold16(P.keep_prob);
     const uint32_t w[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+    if (P.pre) {  // non-ReLU layers: the pre-activation for the backward
+        float* pr = P.pre + (int64_t)row * P.ldc + col;
+        *reinterpret_cast<float4*>(pr) = make_float4(x[0], x[1], x[2], x[3]);
+        if (hi_ok) *reinterpret_cast<float4*>(pr + 4) = make_float4(x[4], x[5], x[6], x[7]);
+    }
+    uint32_t kept[2] = {0u, 0u};
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-        float hv = x[e] > 0.f ? x[e] : 0.f;
+        float hv = P.act == TTAMM_ACT_RELU ? (x[e] > 0.f ? x[e] : 0.f) : act_fwd(P.act, x[e]);
         if (drop) {
             const bool keep = P.keep_mask ? ((km[e >> 2] >> (8 * (e & 3))) & 0xFFu) != 0
                                           : ((w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu) < thresh;
             hv = hv * (keep ? P.inv_keep : 0.f);
+            kept[e >> 2] |= keep ? (1u << (8 * (e & 3))) : 0u;
         }
         x[e] = hv;
+    }
+    if (P.mask_out && drop) {  // the drawn keep decisions, for a non-ReLU layer's backward
+        uint8_t* mo = P.mask_out + (int64_t)row * N + col;
+        *reinterpret_cast<uint32_t*>(mo) = kept[0];
+        if (hi_ok) *reinterpret_cast<uint32_t*>(mo + 4) = kept[1];
     }
     // plain (write-back) stores: a wave's two store instructions each cover every other 16 B of
     // its rows' span, and L2 merges the halves into whole lines; non-temporal stores of the halves
@@ -701,6 +755,11 @@ __device__ __forceinline__ bf16x8 frag16(const unsigned char* plane, int r0, int
     }
 }
 
+__device__ __forceinline__ int xcd_remap(int b, int n) {  // bijective: consecutive tiles on one XCD
+    const int q = n / 8, r = n % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
 template <class CX, int E, int PL>
 __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
     constexpr int BM = CX::BM, BN = CX::BN, TM = CX::TM, TN = CX::TN, I = CX::I, J = CX::J, KT = CX::KT;
@@ -708,7 +767,10 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
     __shared__ __attribute__((aligned(16))) unsigned char lds[CX::lds_bytes(PL)];
 
     const KArg(GemmBatch)* kb = (const KArg(GemmBatch)*)(__builtin_amdgcn_kernarg_segment_ptr());
-    int tile = blockIdx.x;
+    // weight gradients (K-major A): the M-tiles of one row split are consecutive tiles; remapped
+    // onto one XCD (round-robin dispatch: blocks b and b + 8 share one) they read the split's dY
+    // chunk from that XCD's L2 once instead of once per M-tile from the fabric
+    int tile = AK ? xcd_remap(blockIdx.x, kb->total_tiles) : (int)blockIdx.x;
     int pi = 0;
 #pragma unroll 1
     for (int q = 1; q < kb->count; ++q)
@@ -1020,10 +1082,6 @@ constexpr int kB16Cld = kB16N + 4;
 constexpr int kB16Lds = 2 * kB16Stage * 2 > kB16EpiRows * kB16Cld * 4 ? 2 * kB16Stage * 2 : kB16EpiRows * kB16Cld * 4;
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ int xcd_remap(int b, int n) {  // bijective: consecutive tiles on one XCD
-    const int q = n / 8, r = n % 8, x = b % 8;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
 
 template <int E>
 __global__ __launch_bounds__(kB16Threads) void gemm_bf16_kernel(GemmBatch batch) {
@@ -1462,7 +1520,7 @@ size_t wgrad_slab_floats(int R, int M, int N, int rps) {
 
 // Weight gradients as C = X^T dY (M = n_in + 1 incl. the ones column, N = m_out, K = rows),
 // both operands K-major; one launch per tile configuration, then one fixed-order reduce.
-int launch_wgrad(WgradBatch& wb, hipStream_t s) {
+int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
     GemmBatch wide, narrow;  // m_out > 96 / <= 96
     std::memset(&wide, 0, sizeof(wide));
     std::memset(&narrow, 0, sizeof(narrow));
@@ -1527,7 +1585,10 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s) {
         g.p[g.count++] = p;
     }
     int rc;
+    const bool timed = ev && ev[0] && ev[1] && wide.count > 0;
+    if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)ev[0], s));
     if ((rc = flush(wide, true))) return rc;
+    if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)ev[1], s));
     if ((rc = flush(narrow, false))) return rc;
     if (total > 0) {
         hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, s, wb, total);

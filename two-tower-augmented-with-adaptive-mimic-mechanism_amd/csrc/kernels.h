@@ -70,6 +70,13 @@ struct GemmProblem {
     // (multiples of 8), K a multiple of 8.  Same epilogues as the fp32 kernel.
     const uint16_t* A16;
     const uint16_t* B16;
+    // feature-MLP activation (EPI_HIDDEN / EPI_DGRAD_HIDDEN; ttamm.h TTAMM_ACT_*, 0 = ReLU).  A
+    // non-ReLU EPI_HIDDEN also writes the pre-activation to `pre` [M, ldc] and, when it draws its
+    // dropout decisions, the keep bytes to `mask_out` [M, N]; its EPI_DGRAD_HIDDEN reads the
+    // pre-activation as aux0 and the keep bytes as keep_mask (keep_prob < 1).
+    int act;
+    float* pre;
+    uint8_t* mask_out;
 };
 
 constexpr int kMaxGemmProblems = 8;
@@ -114,6 +121,7 @@ struct WgradProblem {
     int bf16;              // 1: operands rounded to bf16, fp32 accumulation (the batch agrees)
 };
 constexpr int kMaxWgradProblems = 16;
+static_assert(kMaxWgradProblems >= 2 * (TTAMM_MAX_LINEAR + 2), "both towers: every Linear + the gate's two");
 struct WgradBatch {
     WgradProblem p[kMaxWgradProblems];
     int count;
@@ -128,7 +136,8 @@ inline int wgrad_class(int m_out) { return m_out > 96 ? 1 : 0; }
 // rows per split-K chunk for each class ([0] narrow, [1] wide) of a step's weight gradients
 void wgrad_rows_per_split(const WgradShape* shapes, int n, int rps[2]);
 size_t wgrad_slab_floats(int R, int M, int N, int rows_per_split);
-int launch_wgrad(WgradBatch& batch, hipStream_t s);
+// ev (optional, 2 hipEvent_t): recorded around the wide tile class's GEMM launch
+int launch_wgrad(WgradBatch& batch, hipStream_t s, void* const* ev = nullptr);
 
 // ------------------------------------------------------------------------------------
 // Fused gate forward / backward (gate.hip): fp32 towers with D == Hg in {32, 64, 96}
@@ -170,8 +179,11 @@ int launch_gate(GateArgs& a, bool backward, hipStream_t s);
 // nn.Embedding max_norm (embedding_renorm_): each distinct row of idx[0, n) whose L2 norm exceeds
 // max_norm is scaled by max_norm / (norm + 1e-7) in place; one wave per position, the first
 // wave to claim a row through mark[row] = tag does it (tags unique per call, mark zeroed once)
+// keys (optional): only positions with (keys[p] >= key_split) == key_phase take part (a sharded
+// owner's requests: the positives' lookup, key < global batch, then the negatives')
 int launch_renorm_rows(float* table, int64_t table_rows, int dim, const int64_t* idx, int64_t n, double max_norm,
-                       int32_t* mark, int32_t tag, hipStream_t s);
+                       int32_t* mark, int32_t tag, hipStream_t s, const int64_t* keys = nullptr,
+                       int64_t key_split = 0, int key_phase = 0);
 int launch_gather_rows(const float* table, int64_t table_rows, int dim, const int64_t* idx, int64_t n, float* out,
                        int64_t out_ld, hipStream_t s);
 
@@ -194,6 +206,10 @@ int launch_stage_rows(const StageArgs& a, hipStream_t s);
 // with xrow, out row r reads row xrow[r] of x and y
 int launch_add_rows(const float* x, int64_t ldx, const float* y, int64_t ldy, int64_t n, int dim, float* out,
                     int64_t ldo, hipStream_t s, const int64_t* xrow = nullptr);
+// dst[idx[r]] += (x[r] (- y[r])) * scale (* *scale_dev), skipping rows idx[r] == skip_row (float atomics)
+int launch_scatter_add_rows(float* dst, int dim, const int64_t* idx, int64_t n, const float* x, int64_t ldx,
+                            const float* y, int64_t ldy, const float* scale_dev, float scale, int64_t skip_row,
+                            hipStream_t s);
 
 // Status bits that stop every later step (ttamm.h TTAMM_STATUS_*).
 constexpr uint32_t kStatusPoison = TTAMM_STATUS_SAMPLER_EXHAUSTED | TTAMM_STATUS_INDEX_OUT_OF_RANGE;
@@ -450,16 +466,14 @@ struct ReplaySeg {
     float* v;
     int32_t* last;
     int dim;
-    // rows [row_lo, row_hi) ...
+    // rows [row_lo, row_hi), each from its own last[row] ...
     int64_t row_lo, row_hi;
-    // ... or the unique keys of a coalesced batch (keys != null): keys[seg_start[u]], u < n_unique
-    const int32_t* keys;
-    const int32_t* seg_start;
-    const int32_t* n_unique;
-    // ... or the rows lead_idx[p] of batch positions p in [row_lo, row_hi) that are their row's
-    // first occurrence (lead_first[row] == INT_MAX - p: CoalesceWs.first after the count pass)
-    const int64_t* lead_idx;
-    const int32_t* lead_first;
+    // ... or a catch-up list (list_rows != null, launch_catchup_list): list_cnt[0] rows, row r =
+    // list_rows[r] replayed from target - list_lag[r] (rows grouped by lag, longest first, so the
+    // threads of a wave share one trip count; `last` is not read — the build stamped it)
+    const int32_t* list_rows;
+    const int32_t* list_lag;
+    const int32_t* list_cnt;
 };
 constexpr int kMaxReplaySegs = 4;
 struct ReplayArgs {
@@ -468,13 +482,31 @@ struct ReplayArgs {
     const AdamConsts* hist;
     int cap;
     int32_t target;   // replay every row up to this dense step
-    int stamp;        // write last = target afterwards (row ranges, lead positions); 2: atomicMax (a concurrent
+    int stamp;        // row ranges: write last = target afterwards; 2: atomicMax (a concurrent
                       // row update may have moved a row past target)
     int decoupled;    // AdamW (decoupled weight decay) vs Adam (L2): the optimizer's, every step
     int fast_g0;      // TTAMM_G0_FAST arithmetic
     const uint32_t* status;  // poisoned: no write (null for the flush)
 };
-int launch_replay(const ReplayArgs& a, hipStream_t s);
+// ev (optional, 2 hipEvent_t): recorded around the replay kernel itself (not the stamp)
+int launch_replay(const ReplayArgs& a, hipStream_t s, void* const* ev = nullptr);
+
+// Catch-up list of a tower batch (deferred AdamW): the rows of idx[0, n) at their first
+// position (first[row] == INT_MAX - p, CoalesceWs.first after the count pass) whose
+// last[0][row] < target, grouped by lag = target - last (longest lag first), and each such
+// row stamped current (last[t][row] = target for the nlast tables: the dense-group tables of
+// one tower are replayed, stamped and updated together, so their last arrays agree).
+// cnt / fill: [cap + 1] ints, zeroed by the launcher; rows / lag: [n].
+struct CatchupList {
+    int32_t* cnt;   // [cap + 1]: [0] = rows listed, [b] = rows of lag b
+    int32_t* fill;  // [cap + 1]
+    int32_t* rows;  // [n]
+    int32_t* lag;   // [n]
+};
+size_t catchup_list_ints(int64_t n, int cap);  // workspace of one list
+void catchup_bind(CatchupList& cl, int32_t* ints, int64_t n, int cap);
+int launch_catchup_list(const int64_t* idx, int64_t n, const int32_t* first, int32_t* const* last, int nlast,
+                        int32_t target, int cap, const CatchupList& cl, const uint32_t* status, hipStream_t s);
 
 struct SweepSeg {
     float* p;
@@ -503,7 +535,7 @@ struct DenseTensor {
     const float* g;
     int64_t n;
 };
-constexpr int kMaxDenseTensors = 24;
+constexpr int kMaxDenseTensors = 2 * (2 * TTAMM_MAX_LINEAR + 4);  // both towers: each Linear weight + bias
 struct DenseAdamArgs {
     DenseTensor t[kMaxDenseTensors];
     int count;
@@ -515,6 +547,8 @@ int launch_dense_adam(const DenseAdamArgs& a, hipStream_t s);
 constexpr int kDenseSumsqBlocks = 256;
 int launch_dense_sumsq(const DenseAdamArgs& a, float* partials, hipStream_t s);
 int launch_clip_coef(const float* partials, int n, float max_norm, float* coef, hipStream_t s);
+// *out = (float) sum of partials[0, n) in double, fixed order (one block)
+int launch_sum_partials(const float* partials, int n, float* out, hipStream_t s);
 
 int launch_sparse_adam_rows(float* w, float* m, float* v, int dim, const int64_t* rows,
                             const float* grad, int64_t n, SparseConsts sp, hipStream_t s);

@@ -507,21 +507,24 @@ __global__ void step_begin_kernel(const uint32_t* status, int64_t* applied, Adam
     if (hist) hist[step % cap] = c;
 }
 
-// One thread per 4 consecutive elements of a row (dim % 4 == 0: four independent dependency
-// chains per thread sharing each step's constants); blockIdx.y = segment.  A row current to
-// step l is brought to A.target by replaying adam_elem(g = 0) with the constants of steps
-// l+1 .. target — the operations the eager sweep applies, so the bits agree.
-// The per-step constants a g = 0 replay reads (the AdamW path loads the first 24 B)
+// The per-step constants a g = 0 replay reads (the AdamW fast path loads the first 24 B)
 struct ReplayConsts {
     float decay, w1, b2, eps, neg_step, inv_bc2_sqrt, bc2_sqrt, wd, w2, pad0, pad1, pad2;
 };
 
-template <bool DECOUPLED, bool FAST>
+// One thread per V float4s of a row (dim % (4 V) == 0: 4 V independent dependency chains per
+// thread sharing each step's constants, at float4 columns q and q + dim / (4 V)); blockIdx.y =
+// segment.  A row current to step l is brought to A.target by replaying adam_elem(g = 0) with
+// the constants of steps l+1 .. target — the operations the eager sweep applies, so the bits
+// agree.  Rows come from a range (the rolling slice, the flush: untouched rows of one slice share
+// their lag) or from a catch-up list sorted by lag (launch_catchup_list), so the lanes of a wave
+// run one trip count.
+template <bool DECOUPLED, bool FAST, int V>
 __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
     const KArg(ReplayArgs)* ka = (const KArg(ReplayArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
     const KArg(ReplaySeg)& S = ka->seg[blockIdx.y];
     if (step_poisoned(ka->status)) return;
-    // the history ring unrolled twice in LDS (2 cap entries, sized at launch: ~4 KB by default),
+    // the history ring unrolled twice in LDS (2 cap entries, sized at launch: ~6 KB by default),
     // so a row's steps l+1 .. target are consecutive entries from (l + 1) % cap — no wrap test
     // and no address arithmetic beyond a pointer increment in the VALU-bound loop
     extern __shared__ ReplayConsts H2[];
@@ -531,29 +534,33 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
         H2[i] = ReplayConsts{h.decay, h.w1, h.b2, h.eps, h.neg_step, h.inv_bc2_sqrt, h.bc2_sqrt, h.wd, h.w2, 0.f, 0.f, 0.f};
     }
     __syncthreads();
-    const int dim = S.dim, dim4 = dim >> 2;
+    const int dim = S.dim;
+    const uint32_t per_row = (uint32_t)(dim >> 2) / V;  // threads per row
     const int32_t target = ka->target;
-    const bool by_key = S.keys != nullptr, by_lead = S.lead_idx != nullptr;
-    const int64_t nrows = by_key ? (int64_t)S.n_unique[0] : S.row_hi - S.row_lo;
-    const int64_t total = nrows * dim4;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = e / dim4;
-        const int q = (int)(e - r * dim4);
+    const bool by_list = S.list_rows != nullptr;
+    const uint32_t nrows = by_list ? (uint32_t)S.list_cnt[0] : (uint32_t)(S.row_hi - S.row_lo);
+    const uint32_t total = nrows * per_row;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+        const uint32_t r = e / per_row, q = e - r * per_row;
         int64_t row;
-        if (by_key) {
-            row = S.keys[S.seg_start[r]];
-        } else if (by_lead) {  // batch position r: its row, replayed once (by its first occurrence)
-            row = S.lead_idx[S.row_lo + r];
-            if (S.lead_first[row] != (int32_t)(INT_MAX - (S.row_lo + r))) continue;
+        int32_t l;
+        if (by_list) {
+            row = S.list_rows[r];
+            l = target - S.list_lag[r];
         } else {
             row = S.row_lo + r;
+            l = S.last[row];
+            if (l >= target) continue;
         }
-        const int32_t l = S.last[row];
-        if (l >= target) continue;
-        const int64_t o = row * dim + 4 * q;
-        float4 p = *reinterpret_cast<const float4*>(S.p + o);
-        float4 m = *reinterpret_cast<const float4*>(S.m + o);
-        float4 v = *reinterpret_cast<const float4*>(S.v + o);
+        const int64_t o = row * dim + 4 * (int64_t)q;
+        float4 p[V], m[V], v[V];
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const int64_t oi = o + (int64_t)(4 * per_row) * i;
+            p[i] = *reinterpret_cast<const float4*>(S.p + oi);
+            m[i] = *reinterpret_cast<const float4*>(S.m + oi);
+            v[i] = *reinterpret_cast<const float4*>(S.v + oi);
+        }
         const ReplayConsts* hc = H2 + (l + 1) % cap;
         const ReplayConsts* const hend = hc + (target - l);
         // A cold row (first moment +0.0: never given a gradient) stays cold under g = 0 (m = fma(w1,
@@ -561,11 +568,18 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
         // unchanged for every p — so its replay is p *= decay, v *= b2 per step, bit for bit what
         // the full update computes, without the two transcendentals.  Most rows of a large table
         // are cold for many steps (C4: the in-batch positives touch ~8 K of 6.25 M rows a step).
-        if (DECOUPLED && (__float_as_uint(m.x) | __float_as_uint(m.y) | __float_as_uint(m.z) | __float_as_uint(m.w)) == 0u) {
+        uint32_t mbits = 0u;
+#pragma unroll
+        for (int i = 0; i < V; ++i)
+            mbits |= __float_as_uint(m[i].x) | __float_as_uint(m[i].y) | __float_as_uint(m[i].z) | __float_as_uint(m[i].w);
+        if (DECOUPLED && mbits == 0u) {
             for (; hc != hend; ++hc) {
                 const float decay = hc->decay, b2 = hc->b2;
-                p.x = p.x * decay, p.y = p.y * decay, p.z = p.z * decay, p.w = p.w * decay;
-                v.x = v.x * b2, v.y = v.y * b2, v.z = v.z * b2, v.w = v.w * b2;
+#pragma unroll
+                for (int i = 0; i < V; ++i) {
+                    p[i].x = p[i].x * decay, p[i].y = p[i].y * decay, p[i].z = p[i].z * decay, p[i].w = p[i].w * decay;
+                    v[i].x = v[i].x * b2, v[i].y = v[i].y * b2, v[i].z = v[i].z * b2, v[i].w = v[i].w * b2;
+                }
             }
         }
         for (; hc != hend; ++hc) {
@@ -573,31 +587,112 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
             c.decay = hc->decay, c.w1 = hc->w1, c.b2 = hc->b2, c.eps = hc->eps, c.neg_step = hc->neg_step;
             c.bc2_sqrt = hc->bc2_sqrt, c.inv_bc2_sqrt = hc->inv_bc2_sqrt, c.wd = hc->wd, c.w2 = hc->w2;
             c.decoupled = DECOUPLED ? 1 : 0, c.fast_g0 = FAST ? 1 : 0;
-            adam_elem_t<DECOUPLED, true, FAST>(p.x, m.x, v.x, 0.f, c);
-            adam_elem_t<DECOUPLED, true, FAST>(p.y, m.y, v.y, 0.f, c);
-            adam_elem_t<DECOUPLED, true, FAST>(p.z, m.z, v.z, 0.f, c);
-            adam_elem_t<DECOUPLED, true, FAST>(p.w, m.w, v.w, 0.f, c);
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                adam_elem_t<DECOUPLED, true, FAST>(p[i].x, m[i].x, v[i].x, 0.f, c);
+                adam_elem_t<DECOUPLED, true, FAST>(p[i].y, m[i].y, v[i].y, 0.f, c);
+                adam_elem_t<DECOUPLED, true, FAST>(p[i].z, m[i].z, v[i].z, 0.f, c);
+                adam_elem_t<DECOUPLED, true, FAST>(p[i].w, m[i].w, v[i].w, 0.f, c);
+            }
         }
-        *reinterpret_cast<float4*>(S.p + o) = p;
-        *reinterpret_cast<float4*>(S.m + o) = m;
-        *reinterpret_cast<float4*>(S.v + o) = v;
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const int64_t oi = o + (int64_t)(4 * per_row) * i;
+            *reinterpret_cast<float4*>(S.p + oi) = p[i];
+            *reinterpret_cast<float4*>(S.m + oi) = m[i];
+            *reinterpret_cast<float4*>(S.v + oi) = v[i];
+        }
     }
 }
 
+// row ranges only: last[row] = target (stamp 1) or max(last[row], target) (stamp 2) after the
+// replay (list segments were stamped by their build)
 __global__ void stamp_kernel(ReplayArgs) {
     const KArg(ReplayArgs)* ka = (const KArg(ReplayArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
     const KArg(ReplaySeg)& S = ka->seg[blockIdx.y];
-    if (step_poisoned(ka->status)) return;
+    if (step_poisoned(ka->status) || S.list_rows != nullptr) return;
     const bool at_least = ka->stamp == 2;
     for (int64_t r = S.row_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < S.row_hi;
          r += (int64_t)gridDim.x * blockDim.x) {
-        int64_t row = r;
-        if (S.lead_idx) {  // batch positions: the row of each first occurrence
-            row = S.lead_idx[r];
-            if (S.lead_first[row] != (int32_t)(INT_MAX - r)) continue;
-        }
-        if (at_least) atomicMax(&S.last[row], ka->target);
-        else S.last[row] = ka->target;
+        if (at_least) atomicMax(&S.last[r], ka->target);
+        else S.last[r] = ka->target;
+    }
+}
+
+// ---- catch-up list (launch_catchup_list) ----------------------------------------------------
+// lag of batch position p, or 0 when p is not its row's first occurrence or the row is current
+__device__ __forceinline__ int32_t catchup_lag(const int64_t* __restrict__ idx, int64_t p, int64_t n,
+                                               const int32_t* __restrict__ first, const int32_t* __restrict__ last,
+                                               int32_t target, int64_t& row) {
+    if (p >= n) return 0;
+    row = idx[p];
+    if (first[row] != (int32_t)(INT_MAX - p)) return 0;
+    const int32_t lag = target - last[row];
+    return lag > 0 ? lag : 0;
+}
+
+// rows per lag: a block histogram in LDS, then one atomic per (block, lag); cnt[0] = all rows
+__global__ __launch_bounds__(256) void catchup_count_kernel(const int64_t* __restrict__ idx, int64_t n,
+                                                            const int32_t* __restrict__ first,
+                                                            const int32_t* __restrict__ last, int32_t target, int cap,
+                                                            int32_t* __restrict__ cnt, const uint32_t* status) {
+    __shared__ int32_t h[kMaxHistory + 1];
+    if (step_poisoned(status)) return;
+    for (int i = threadIdx.x; i <= cap; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    int64_t row = 0;
+    const int32_t lag = catchup_lag(idx, (int64_t)blockIdx.x * blockDim.x + threadIdx.x, n, first, last, target, row);
+    if (lag > 0) {
+        atomicAdd(&h[lag], 1);
+        atomicAdd(&h[0], 1);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i <= cap; i += blockDim.x)
+        if (h[i]) atomicAdd(&cnt[i], h[i]);
+}
+
+struct LastPtrs {
+    int32_t* p[2];
+};
+
+// each listed row into its lag's range of the list (longest lag first: lag b starts at
+// sum_{b' > b} cnt[b']), in block order within a lag (atomics: any order — every row's replay is
+// independent of the others), then stamped current in every table of the tower
+__global__ __launch_bounds__(256) void catchup_scatter_kernel(const int64_t* __restrict__ idx, int64_t n,
+                                                              const int32_t* __restrict__ first, LastPtrs last,
+                                                              int nlast, int32_t target, int cap,
+                                                              const int32_t* __restrict__ cnt,
+                                                              int32_t* __restrict__ fill, int32_t* __restrict__ rows,
+                                                              int32_t* __restrict__ lags, const uint32_t* status) {
+    __shared__ int32_t suf[2][kMaxHistory + 2];  // suffix sums of cnt[1..cap] (double buffered)
+    __shared__ int32_t h[kMaxHistory + 1], base[kMaxHistory + 1];
+    if (step_poisoned(status)) return;
+    const int tid = threadIdx.x;
+    for (int i = tid; i <= cap + 1; i += blockDim.x) {
+        suf[0][i] = (i >= 1 && i <= cap) ? cnt[i] : 0;
+        if (i <= cap) h[i] = 0;
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int off = 1; off <= cap; off <<= 1) {  // Hillis-Steele suffix scan
+        for (int i = tid; i <= cap + 1; i += blockDim.x)
+            suf[cur ^ 1][i] = suf[cur][i] + (i + off <= cap ? suf[cur][i + off] : 0);
+        cur ^= 1;
+        __syncthreads();
+    }
+    int64_t row = 0;
+    const int32_t lag = catchup_lag(idx, (int64_t)blockIdx.x * blockDim.x + tid, n, first, last.p[0], target, row);
+    int32_t rank = 0;
+    if (lag > 0) rank = atomicAdd(&h[lag], 1);
+    __syncthreads();
+    for (int i = tid + 1; i <= cap; i += blockDim.x)
+        if (h[i]) base[i] = atomicAdd(&fill[i], h[i]);
+    __syncthreads();
+    if (lag > 0) {
+        const int32_t slot = suf[cur][lag + 1] + base[lag] + rank;
+        rows[slot] = (int32_t)row;
+        lags[slot] = lag;
+        for (int t = 0; t < nlast; ++t) last.p[t][row] = target;
     }
 }
 
@@ -709,6 +804,19 @@ __global__ void clip_coef_kernel(const float* __restrict__ partials, int n, floa
     }
 }
 
+
+__global__ void sum_partials_kernel(const float* __restrict__ partials, int n, float* out) {
+    __shared__ double red[256];
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) acc += (double)partials[i];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = (float)red[0];
+}
 
 __global__ void sparse_adam_rows_kernel(float* __restrict__ w, float* __restrict__ m, float* __restrict__ v,
                                         int dim, const int64_t* __restrict__ rows, const float* __restrict__ grad,
@@ -915,37 +1023,77 @@ int launch_step_begin(const uint32_t* status, int64_t* applied, AdamConsts* hist
     return TTAMM_OK;
 }
 
-int launch_replay(const ReplayArgs& a, hipStream_t s) {
+template <int V>
+static void launch_replay_v(const ReplayArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    if (a.fast_g0) {
+        if (a.decoupled) hipLaunchKernelGGL((replay_kernel<true, true, V>), grid, dim3(256), lds, s, a);
+        else hipLaunchKernelGGL((replay_kernel<false, true, V>), grid, dim3(256), lds, s, a);
+    } else if (a.decoupled) {
+        hipLaunchKernelGGL((replay_kernel<true, false, V>), grid, dim3(256), lds, s, a);
+    } else {
+        hipLaunchKernelGGL((replay_kernel<false, false, V>), grid, dim3(256), lds, s, a);
+    }
+}
+
+int launch_replay(const ReplayArgs& a, hipStream_t s, void* const* ev) {
     if (a.count == 0) return TTAMM_OK;
     TTAMM_REQUIRE(a.count <= kMaxReplaySegs && a.hist && a.cap > 1 && a.cap <= kMaxHistory,
                   "replay: bad arguments");
     int64_t most = 0;
+    bool v2 = true;  // two float4s per thread when every segment's dim is a multiple of 8
+    for (int i = 0; i < a.count; ++i) v2 = v2 && a.seg[i].dim % 8 == 0;
+    const int V = v2 ? 2 : 1;
     for (int i = 0; i < a.count; ++i) {
         const ReplaySeg& g = a.seg[i];
-        TTAMM_REQUIRE(g.p && g.m && g.v && g.last, "replay: table without deferred state");
+        TTAMM_REQUIRE(g.p && g.m && g.v && (g.last || g.list_rows), "replay: table without deferred state");
+        TTAMM_REQUIRE(!g.list_rows || (g.list_lag && g.list_cnt), "replay: catch-up list incomplete");
         TTAMM_REQUIRE(g.dim % 4 == 0 && ((uintptr_t)g.p | (uintptr_t)g.m | (uintptr_t)g.v) % 16 == 0,
                       "replay: tables must be 16-byte aligned with dim % 4 == 0");
-        const int64_t n = g.row_hi - g.row_lo;  // keys: the coalesced batch size bounds n_unique
-        most = n * (g.dim / 4) > most ? n * (g.dim / 4) : most;
+        const int64_t n = g.row_hi - g.row_lo;  // lists: the batch positions bound the listed rows
+        TTAMM_REQUIRE(n >= 0 && n * (g.dim / 4) < (int64_t(1) << 31), "replay: more than 2^31 float4s in a segment");
+        most = n * (g.dim / 4 / V) > most ? n * (g.dim / 4 / V) : most;
     }
     if (most == 0) return TTAMM_OK;
     const dim3 grid(grid_for(most, 256, 16384), a.count);
     const size_t lds = (size_t)2 * a.cap * sizeof(ReplayConsts);
-    if (a.fast_g0) {
-        if (a.decoupled) hipLaunchKernelGGL((replay_kernel<true, true>), grid, dim3(256), lds, s, a);
-        else hipLaunchKernelGGL((replay_kernel<false, true>), grid, dim3(256), lds, s, a);
-    } else if (a.decoupled) {
-        hipLaunchKernelGGL((replay_kernel<true, false>), grid, dim3(256), lds, s, a);
-    } else {
-        hipLaunchKernelGGL((replay_kernel<false, false>), grid, dim3(256), lds, s, a);
-    }
+    if (ev && ev[0]) TTAMM_HIP(hipEventRecord((hipEvent_t)ev[0], s));
+    if (v2) launch_replay_v<2>(a, grid, lds, s);
+    else launch_replay_v<1>(a, grid, lds, s);
     TTAMM_LAUNCH_CHECK();
+    if (ev && ev[1]) TTAMM_HIP(hipEventRecord((hipEvent_t)ev[1], s));
     if (a.stamp) {
         int64_t rows = 0;
         for (int i = 0; i < a.count; ++i) rows = a.seg[i].row_hi - a.seg[i].row_lo > rows ? a.seg[i].row_hi - a.seg[i].row_lo : rows;
         hipLaunchKernelGGL(stamp_kernel, dim3(grid_for(rows, 256, 4096), a.count), dim3(256), 0, s, a);
         TTAMM_LAUNCH_CHECK();
     }
+    return TTAMM_OK;
+}
+
+size_t catchup_list_ints(int64_t n, int cap) { return (size_t)2 * (cap + 1) + (size_t)2 * (n > 0 ? n : 1) + 64; }
+
+void catchup_bind(CatchupList& cl, int32_t* ints, int64_t n, int cap) {
+    cl.cnt = ints;
+    cl.fill = ints ? ints + (cap + 1) : nullptr;
+    cl.rows = ints ? ints + 2 * (cap + 1) + 64 : nullptr;  // 256-B aligned past the counters
+    cl.lag = ints ? cl.rows + (n > 0 ? n : 1) : nullptr;
+}
+
+int launch_catchup_list(const int64_t* idx, int64_t n, const int32_t* first, int32_t* const* last, int nlast,
+                        int32_t target, int cap, const CatchupList& cl, const uint32_t* status, hipStream_t s) {
+    TTAMM_REQUIRE(cl.cnt && cl.fill && cl.rows && cl.lag && first && last && last[0] && nlast >= 1 && nlast <= 2,
+                  "catch-up list: bad arguments");
+    TTAMM_REQUIRE(cap > 1 && cap <= kMaxHistory && n < (int64_t(1) << 31) - 1, "catch-up list: bad sizes");
+    TTAMM_HIP(hipMemsetAsync(cl.cnt, 0, sizeof(int32_t) * 2 * (cap + 1), s));  // cnt and fill
+    if (n <= 0) return TTAMM_OK;
+    const unsigned g = (unsigned)ceil_div(n, 256);
+    hipLaunchKernelGGL(catchup_count_kernel, dim3(g), dim3(256), 0, s, idx, n, first, last[0], target, cap, cl.cnt,
+                       status);
+    TTAMM_LAUNCH_CHECK();
+    LastPtrs lp{{last[0], nlast > 1 ? last[1] : nullptr}};
+    hipLaunchKernelGGL(catchup_scatter_kernel, dim3(g), dim3(256), 0, s, idx, n, first, lp, nlast, target, cap, cl.cnt,
+                       cl.fill, cl.rows, cl.lag, status);
+    TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }
 
@@ -982,6 +1130,12 @@ int launch_dense_sumsq(const DenseAdamArgs& a, float* partials, hipStream_t s) {
 
 int launch_clip_coef(const float* partials, int n, float max_norm, float* coef, hipStream_t s) {
     hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(256), 0, s, partials, n, max_norm, coef);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_sum_partials(const float* partials, int n, float* out, hipStream_t s) {
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, partials, n, out);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

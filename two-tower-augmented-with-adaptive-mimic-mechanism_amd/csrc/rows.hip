@@ -348,10 +348,12 @@ inline unsigned grid_for(int64_t work, int threads = 256) {
 // torch embedding_renorm_ on the rows a lookup touches (encoders.py:48,58 max_norm)
 __global__ void renorm_rows_kernel(float* __restrict__ table, int64_t table_rows, int dim,
                                    const int64_t* __restrict__ idx, int64_t n, double max_norm,
-                                   int32_t* __restrict__ mark, int32_t tag) {
+                                   int32_t* __restrict__ mark, int32_t tag, const int64_t* __restrict__ keys,
+                                   int64_t key_split, int key_phase) {
     const int64_t p = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (p >= n) return;
+    if (keys && (keys[p] >= key_split) != (key_phase != 0)) return;  // the other lookup's positions
     const int64_t row = idx[p];
     if (row < 0 || row >= table_rows) return;  // reported by the staging kernel
     int claimed = 0;
@@ -372,11 +374,12 @@ __global__ void renorm_rows_kernel(float* __restrict__ table, int64_t table_rows
 }  // namespace
 
 int launch_renorm_rows(float* table, int64_t table_rows, int dim, const int64_t* idx, int64_t n, double max_norm,
-                       int32_t* mark, int32_t tag, hipStream_t s) {
+                       int32_t* mark, int32_t tag, hipStream_t s, const int64_t* keys, int64_t key_split,
+                       int key_phase) {
     if (n <= 0) return TTAMM_OK;
     TTAMM_REQUIRE(mark != nullptr && max_norm > 0.0 && tag != 0, "renorm: bad arguments");
     hipLaunchKernelGGL(renorm_rows_kernel, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, s, table, table_rows, dim, idx, n,
-                       max_norm, mark, tag);
+                       max_norm, mark, tag, keys, key_split, key_phase);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }
@@ -493,6 +496,38 @@ __global__ void add_rows_kernel(const float* __restrict__ x, int64_t ldx, const 
     }
 }
 }  // namespace
+
+namespace {
+// dst[idx[r]] += (x[r] - y[r]) * scale * (*scale_dev) (idx null: row r), rows with idx[r] != skip_row; float
+// atomics (the order of duplicate rows' adds is not fixed: torch's CUDA embedding backward and
+// index_add_ are not either).  Module-level autograd only: the fused step sums in a fixed order.
+__global__ void scatter_add_rows_kernel(float* __restrict__ dst, int dim, const int64_t* __restrict__ idx, int64_t n,
+                                        const float* __restrict__ x, int64_t ldx, const float* __restrict__ y,
+                                        int64_t ldy, const float* __restrict__ scale_dev, float scale,
+                                        int64_t skip_row) {
+    const float sc = scale_dev ? scale * *scale_dev : scale;
+    const int64_t total = n * dim;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / dim;
+        const int c = (int)(i - r * dim);
+        const int64_t row = idx ? idx[r] : r;
+        if (row == skip_row) continue;
+        float v = x[r * ldx + c];
+        if (y) v = v - y[r * ldy + c];
+        atomicAdd(dst + row * dim + c, v * sc);
+    }
+}
+}  // namespace
+
+int launch_scatter_add_rows(float* dst, int dim, const int64_t* idx, int64_t n, const float* x, int64_t ldx,
+                            const float* y, int64_t ldy, const float* scale_dev, float scale, int64_t skip_row,
+                            hipStream_t s) {
+    if (n <= 0) return TTAMM_OK;
+    hipLaunchKernelGGL(scatter_add_rows_kernel, dim3(grid_for(n * dim)), dim3(256), 0, s, dst, dim, idx, n, x, ldx, y,
+                       ldy, scale_dev, scale, skip_row);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
 
 int launch_add_rows(const float* x, int64_t ldx, const float* y, int64_t ldy, int64_t n, int dim, float* out,
                     int64_t ldo, hipStream_t s, const int64_t* xrow) {

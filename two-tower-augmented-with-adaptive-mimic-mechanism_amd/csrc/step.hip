@@ -42,8 +42,14 @@ struct TowerWs {
     int32_t* renorm_mark = nullptr;
     int32_t renorm_tag = 0;
     int64_t renorm_split = 0;  // item tower: positives [0, split) are one lookup, negatives the next
+    int64_t renorm_key_split = 0;  // sharded owner: requests with row_key < this (positives) are one lookup
     float* hid[TTAMM_MAX_LINEAR] = {};
     float* dhid[TTAMM_MAX_LINEAR] = {};
+    // non-ReLU activations: each hidden layer's pre-activation, its drawn keep bytes (dropout
+    // without an injected mask), and the keep bytes the backward reads (injected or drawn)
+    float* pre[TTAMM_MAX_LINEAR] = {};
+    uint8_t* mask[TTAMM_MAX_LINEAR] = {};
+    const uint8_t* keep[TTAMM_MAX_LINEAR] = {};
     float* ef = nullptr;    // gated: [R, 2D] = [e | f]
     float* e = nullptr;     // non-gated: [R, D]
     float* f = nullptr;     // sum fusion: [R, D]
@@ -69,6 +75,7 @@ struct TowerWs {
     float* ggb[2] = {};
     float* slab[TTAMM_MAX_LINEAR + 2] = {};
     CoalesceWs co{};
+    CatchupList cl{};  // deferred AdamW: the batch's rows to bring current, grouped by lag
     float* side_id = nullptr;
     float* side_mimic = nullptr;
     float* piece_e = nullptr;
@@ -130,6 +137,7 @@ int validate_tower(const ttamm_tower& T, const char* name, int D, bool training)
     TTAMM_REQUIRE(T.id.rows > 0, n + ": empty embedding table");
     TTAMM_REQUIRE(T.id.rows < (int64_t(1) << 31), n + ": tables of 2^31 rows or more are not supported (int32 row keys)");
     TTAMM_REQUIRE(T.n_linear >= 0 && T.n_linear <= TTAMM_MAX_LINEAR, n + ": too many feature-encoder layers");
+    TTAMM_REQUIRE(T.activation >= TTAMM_ACT_RELU && T.activation <= TTAMM_ACT_SELU, n + ": unsupported activation");
     TTAMM_REQUIRE(T.fusion >= TTAMM_FUSION_IDENTITY && T.fusion <= TTAMM_FUSION_CONCAT, n + ": unsupported fusion");
     if (T.fusion != TTAMM_FUSION_IDENTITY) {
         TTAMM_REQUIRE(T.features != nullptr && T.feat_dim > 0, n + ": fusion needs feature rows");
@@ -269,6 +277,10 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         for (int l = 0; l + 1 < T.n_linear; ++l) {
             w.hid[l] = ar.take<float>((size_t)R * T.linear[l].out_features);
             w.dhid[l] = ar.take<float>((size_t)R * T.linear[l].out_features);
+            if (T.activation != TTAMM_ACT_RELU) {
+                w.pre[l] = ar.take<float>((size_t)R * T.linear[l].out_features);
+                if (T.dropout > 0.f) w.mask[l] = ar.take<uint8_t>((size_t)R * T.linear[l].out_features);
+            }
         }
         const int Hg = T.fusion == TTAMM_FUSION_GATED ? T.gate[0].out_features : 0;
         if (uses_ef(T)) {
@@ -313,6 +325,10 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
             }
         }
         plan_coalesce(ar, w.co, R);
+        if (A.adam_history && A.history_capacity > 1) {
+            const int cap = A.history_capacity;
+            catchup_bind(w.cl, ar.take<int32_t>(catchup_list_ints(R, cap)), R, cap);
+        }
         if (needs_wpad(T)) w.wpad = ar.take<float>((size_t)T.linear[0].out_features * round4(T.linear[0].in_features));
         if (uses_w16(T)) w.w16 = ar.take<uint16_t>((size_t)T.linear[0].out_features * round8(T.linear[0].in_features));
         w.piece_e = ar.take<float>((size_t)R * D);
@@ -329,9 +345,11 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         tower(A.item, ws.item, B * (1 + N), false, B);
     ws.score_blocks = score_blocks(B);
     ws.partials = ar.take<float>((size_t)ws.score_blocks * 3);
-    if (A.hp.grad_clip_norm > 0.0 && !shard) {
+    if (A.hp.grad_clip_norm > 0.0) {
         ws.clip_on = true;
-        ws.clip_parts = rows_sumsq_blocks(B, D) + rows_sumsq_blocks(B * (1 + N), D) + kDenseSumsqBlocks;
+        // [tables' total (sharded: all-reduced)] + both towers' row partials + the dense partials
+        ws.clip_parts = 1 + rows_sumsq_blocks(B, D) + rows_sumsq_blocks(shard ? A.item_rows_capacity : B * (1 + N), D) +
+                        kDenseSumsqBlocks;
         ws.clip_partials = ar.take<float>((size_t)ws.clip_parts);
         ws.clip_coef = ar.take<float>(1);
     }
@@ -481,7 +499,14 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
         for (int k = 0; k < ntowers; ++k) {
             const ttamm_tower& t = *T[k];
             TowerWs& w = *W[k];
-            if (t.id.max_norm > 0.0 && w.R > 0) {  // nn.Embedding max_norm: renorm, then look up
+            if (t.id.max_norm > 0.0 && w.R > 0 && w.row_key && w.renorm_key_split > 0) {
+                // sharded owner: every requester's positives (keys < global batch) are the reference's
+                // first item lookup (training.py:750), the negatives its second (:776)
+                for (int ph = 0; ph < 2; ++ph)
+                    if ((rc = launch_renorm_rows(t.id.weight, t.id.rows, D, w.idx, w.R, t.id.max_norm, w.renorm_mark,
+                                                 w.renorm_tag + ph, s, w.row_key, w.renorm_key_split, ph)))
+                        return rc;
+            } else if (t.id.max_norm > 0.0 && w.R > 0) {  // nn.Embedding max_norm: renorm, then look up
                 const int64_t split = w.renorm_split > 0 && w.renorm_split < w.R ? w.renorm_split : w.R;
                 if ((rc = launch_renorm_rows(t.id.weight, t.id.rows, D, w.idx, split, t.id.max_norm, w.renorm_mark,
                                              w.renorm_tag, s)))
@@ -494,6 +519,11 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
             float* dst = uses_ef(t) ? w.ef : w.e;
             const int64_t ld = uses_ef(t) ? 2 * D : D;
             if ((rc = launch_gather_rows(t.id.weight, t.id.rows, D, w.idx, w.R, dst, ld, s))) return rc;
+            if (t.fusion != TTAMM_FUSION_IDENTITY && t.n_linear == 0 && w.R > 0) {
+                // identity feature encoder (encoders.py:114-119): f = the feature row (F == D)
+                float* fdst = uses_ef(t) ? w.ef + D : w.f;
+                if ((rc = launch_add_rows(t.features, t.feat_ld, nullptr, 0, w.R, D, fdst, ld, s, w.fidx))) return rc;
+            }
         }
         // feature encoder layers
         int maxL = 0;
@@ -546,8 +576,15 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
                     p.epi = EPI_HIDDEN;
                     p.C = w.hid[l];
                     p.ldc = L.out_features;
-                    set_dropout(p, t, bt, w.role, l, w.role == ROLE_USER ? bt.user_keep_mask[l] : bt.item_keep_mask[l]);
+                    const uint8_t* injected = w.role == ROLE_USER ? bt.user_keep_mask[l] : bt.item_keep_mask[l];
+                    set_dropout(p, t, bt, w.role, l, injected);
                     set_keys(p, w);
+                    p.act = t.activation;
+                    if (t.activation != TTAMM_ACT_RELU) {  // the backward's inputs
+                        p.pre = w.pre[l];
+                        if (t.dropout > 0.f && injected == nullptr) p.mask_out = w.mask[l];
+                        w.keep[l] = injected ? injected : w.mask[l];
+                    }
                 } else {
                     p.epi = EPI_STORE;
                     if (uses_ef(t)) {
@@ -568,12 +605,6 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
         }
     }
     if (!(part & FWD_FUSION)) return TTAMM_OK;
-    // feature encoder "identity" (no Linear): f = feature rows
-    for (int k = 0; k < ntowers; ++k) {
-        const ttamm_tower& t = *T[k];
-        if (t.fusion != TTAMM_FUSION_IDENTITY && t.n_linear == 0)
-            return fail(TTAMM_E_INVALID, "identity feature encoder is not supported by the fused step");
-    }
     // fusion
     GateArgs ga;
     const bool fused_gate = gate_group(T, W, ntowers, D, mimic, ga);
@@ -662,7 +693,9 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
 }
 
 // ---- backward ------------------------------------------------------------------------------
-int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s, int ntowers) {
+// wg_events (optional, 2 events): around the wide weight-gradient GEMM launch (bench)
+int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s, int ntowers,
+                   void* const* wg_events = nullptr) {
     int rc;
     // gate: dq, dz, dEF
     GateArgs ga;
@@ -767,6 +800,12 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
             p.ld_aux0 = L.in_features;
             const float pdrop = t.dropout;
             p.inv_keep = pdrop > 0.f ? 1.0f / (1.0f - pdrop) : 1.0f;
+            p.act = t.activation;
+            if (t.activation != TTAMM_ACT_RELU) {  // act'(pre-activation), the forward's keep bytes
+                p.aux0 = w.pre[l - 1];
+                p.keep_prob = 1.0f - pdrop;
+                p.keep_mask = pdrop > 0.f ? w.keep[l - 1] : nullptr;
+            }
             bb.add(p);
         }
         if ((rc = bb.run(s))) return rc;
@@ -854,7 +893,7 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
             wb.p[wb.count++] = p;
         }
     }
-    if ((rc = launch_wgrad(wb, s))) return rc;
+    if ((rc = launch_wgrad(wb, s, wg_events))) return rc;
     return TTAMM_OK;
 }
 
@@ -896,7 +935,6 @@ ReplaySeg replay_seg(const ttamm_table& tb) {
 // table's rows brought to `target` (every row's lag stays below the history ring).
 int replay_slice(const ttamm_tower* const* T, int n, bool mimic, const Deferred& df, int32_t target, int stamp,
                  void* const* events, hipStream_t s) {
-    int rc;
     ReplayArgs ra;
     std::memset(&ra, 0, sizeof(ra));
     ra.hist = df.hist;
@@ -918,19 +956,27 @@ int replay_slice(const ttamm_tower* const* T, int n, bool mimic, const Deferred&
             ra.seg[ra.count++] = g;
         }
     }
-    if (events && events[0]) TTAMM_HIP(hipEventRecord((hipEvent_t)events[0], s));
-    if ((rc = launch_replay(ra, s))) return rc;
-    if (events && events[1]) TTAMM_HIP(hipEventRecord((hipEvent_t)events[1], s));
-    return TTAMM_OK;
+    return launch_replay(ra, s, events);
 }
 
 // Before a tower reads its rows (part A): count the batch's rows — which marks each row's first
 // position — and, deferred, bring the dense-group rows it touches current to step - 1 (each row
-// once, by its first position).  Part B groups the rows for the row updates at the step's end.
-int tower_prepare_a(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred& df, hipStream_t s) {
+// once): the rows behind, listed by lag (the list build stamps them current — a replay that runs
+// before this step's row updates, the aux stream's slice or a flush after a poisoned step, must
+// see them current to step - 1), then one replay over the list.  Part B groups the rows for the
+// row updates at the step's end.  ev: 2 events around the replay kernel (bench).
+int tower_prepare_a(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred& df, hipStream_t s,
+                    void* const* ev = nullptr) {
     int rc;
     if ((rc = launch_coalesce_count(w.idx, w.R, t.id.rows, w.co, s))) return rc;
     if (!df.on || w.R == 0) return TTAMM_OK;
+    const ttamm_table* tabs[2];
+    const int n = dense_tables(t, mimic, tabs);
+    if (n == 0) return TTAMM_OK;
+    TTAMM_REQUIRE(w.cl.cnt != nullptr, "deferred AdamW: catch-up list workspace missing");
+    int32_t* lasts[2] = {tabs[0]->last_step, n > 1 ? tabs[1]->last_step : nullptr};
+    if ((rc = launch_catchup_list(w.idx, w.R, w.co.first, lasts, n, df.step - 1, df.cap, w.cl, df.status, s)))
+        return rc;
     ReplayArgs ra;
     std::memset(&ra, 0, sizeof(ra));
     ra.hist = df.hist;
@@ -939,29 +985,27 @@ int tower_prepare_a(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred
     ra.fast_g0 = df.fast;
     ra.status = df.status;
     ra.target = df.step - 1;
-    // stamp the caught-up rows: a replay that runs before this step's row updates (the aux
-    // stream's slice, a flush after a poisoned step) must see them current to step - 1
-    ra.stamp = 1;
-    const ttamm_table* tabs[2];
-    const int n = dense_tables(t, mimic, tabs);
+    ra.stamp = 0;  // stamped by the list build
     for (int i = 0; i < n; ++i) {
         ReplaySeg g = replay_seg(*tabs[i]);
         g.row_lo = 0;
         g.row_hi = w.R;
-        g.lead_idx = w.idx;
-        g.lead_first = w.co.first;
+        g.list_rows = w.cl.rows;
+        g.list_lag = w.cl.lag;
+        g.list_cnt = w.cl.cnt;
         ra.seg[ra.count++] = g;
     }
-    return launch_replay(ra, s);
+    return launch_replay(ra, s, ev);
 }
 
 int tower_prepare_b(const ttamm_tower& t, TowerWs& w, hipStream_t s) {
     return launch_coalesce_group(w.idx, w.R, t.id.rows, w.co, s);
 }
 
-int tower_prepare(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred& df, hipStream_t s) {
+int tower_prepare(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred& df, hipStream_t s,
+                  void* const* ev = nullptr) {
     int rc;
-    if ((rc = tower_prepare_a(t, w, mimic, df, s))) return rc;
+    if ((rc = tower_prepare_a(t, w, mimic, df, s, ev))) return rc;
     return tower_prepare_b(t, w, s);
 }
 
@@ -1000,13 +1044,18 @@ bool overlapped(const ttamm_tower* const* T, int n, const Deferred& df, hipStrea
 // catch-up) first, joined before the fusion, whose epilogue reads the mimic rows; then part B
 // (grouping), joined by table_updates.  A deferred dense ID table is read by the first gather,
 // so that case stays serial.
+// cu_events (optional): ttamm_step_args.timing_events + 8 — [0, 1] around the user tower's
+// catch-up replay, [2, 3] around the item tower's
 int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_batch& bt, int D, bool mimic,
                     const Deferred& df, hipStream_t s, hipStream_t aux, void* const* l0_events,
-                    void* const* maint_events = nullptr) {
+                    void* const* maint_events = nullptr, void* const* cu_events = nullptr) {
     int rc;
+    auto cu_ev = [&](int k) -> void* const* {
+        return cu_events ? cu_events + (W[k]->role == ROLE_USER ? 0 : 2) : nullptr;
+    };
     if (!overlapped(T, n, df, s, aux)) {
         for (int k = 0; k < n; ++k)
-            if ((rc = tower_prepare(*T[k], *W[k], mimic, df, s))) return rc;
+            if ((rc = tower_prepare(*T[k], *W[k], mimic, df, s, cu_ev(k)))) return rc;
         return tower_forward(T, W, bt, D, mimic, s, n, l0_events, FWD_ALL);
     }
     // The MLP launches are enqueued first: the prologue is a dozen small launches whose
@@ -1020,7 +1069,7 @@ int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_b
     if ((rc = tower_forward(T, W, bt, D, mimic, s, n, l0_events, FWD_MLP, late_fork ? ev[0] : nullptr))) return rc;
     TTAMM_HIP(hipStreamWaitEvent(aux, ev[0], 0));
     for (int k = 0; k < n; ++k)
-        if ((rc = tower_prepare_a(*T[k], *W[k], mimic, df, aux))) return rc;
+        if ((rc = tower_prepare_a(*T[k], *W[k], mimic, df, aux, cu_ev(k)))) return rc;
     TTAMM_HIP(hipEventRecord(ev[1], aux));
     // the fusion is enqueued before the grouping's dozen launches: enqueued after them, the host
     // still issued them when the GPU finished the MLP (~55 us idle per C2 step)
@@ -1174,23 +1223,58 @@ int dense_update(const ttamm_tower* T[2], TowerWs* W[2], const AdamConsts& ad, c
     return launch_dense_adam(dense_args(T, W, ad, status, grad_scale), s);
 }
 
+// the tables' row partials of the squared gradient norm into ws.clip_partials[1, *off)
+int clip_table_partials(const ttamm_tower* T[2], TowerWs* W[2], int D, bool mimic, const SparseConsts& sp,
+                        const AdamConsts& ad, const Deferred& df, StepWs& ws, hipStream_t s, hipStream_t aux,
+                        int* off_out) {
+    int rc;
+    if ((rc = join_grouping(s, aux))) return rc;  // the row grouping
+    int off = 1;
+    for (int k = 0; k < 2; ++k) {
+        if (!T[k] || W[k]->R <= 0) continue;
+        const RowUpdateArgs ru = row_update_args(*T[k], *W[k], D, mimic, sp, ad, df, nullptr);
+        if ((rc = launch_rows_sumsq(ru, ws.clip_partials + off, s))) return rc;
+        off += rows_sumsq_blocks(W[k]->R, D);
+    }
+    TTAMM_REQUIRE(off <= ws.clip_parts, "clip: partials overflow");
+    *off_out = off;
+    return TTAMM_OK;
+}
+
 // clip_grad_norm_(model.parameters(), max_norm) (training.py:824-825): the global gradient norm
 // over both towers' table rows and dense tensors -> ws.clip_coef, read by the optimizer kernels
 int clip_coefficient(const ttamm_tower* T[2], TowerWs* W[2], int D, bool mimic, const SparseConsts& sp,
                      const AdamConsts& ad, const Deferred& df, const ttamm_step_args& A, StepWs& ws, hipStream_t s,
                      hipStream_t aux) {
     int rc;
-    if ((rc = join_grouping(s, aux))) return rc;  // the row grouping
-    int off = 0;
-    for (int k = 0; k < 2; ++k) {
-        const RowUpdateArgs ru = row_update_args(*T[k], *W[k], D, mimic, sp, ad, df, nullptr);
-        if ((rc = launch_rows_sumsq(ru, ws.clip_partials + off, s))) return rc;
-        off += rows_sumsq_blocks(W[k]->R, D);
-    }
+    int off;
+    if ((rc = clip_table_partials(T, W, D, mimic, sp, ad, df, ws, s, aux, &off))) return rc;
     if ((rc = launch_dense_sumsq(dense_args(T, W, ad, A.status, nullptr), ws.clip_partials + off, s))) return rc;
     off += kDenseSumsqBlocks;
     TTAMM_REQUIRE(off <= ws.clip_parts, "clip: partials overflow");
-    return launch_clip_coef(ws.clip_partials, off, (float)A.hp.grad_clip_norm, ws.clip_coef, s);
+    return launch_clip_coef(ws.clip_partials + 1, off - 1, (float)A.hp.grad_clip_norm, ws.clip_coef, s);
+}
+
+// sharded clipping, TOWERS_BWD: this rank's share of the squared gradient norm over the table
+// rows it owns (its users', its items' — every requester's contributions to a row summed first),
+// into *A.table_sumsq for the caller's all-reduce
+int clip_table_share(const ttamm_tower* T[2], TowerWs* W[2], int D, bool mimic, const SparseConsts& sp,
+                     const AdamConsts& ad, const Deferred& df, const ttamm_step_args& A, StepWs& ws, hipStream_t s,
+                     hipStream_t aux) {
+    int rc;
+    int off;
+    if ((rc = clip_table_partials(T, W, D, mimic, sp, ad, df, ws, s, aux, &off))) return rc;
+    return launch_sum_partials(ws.clip_partials + 1, off - 1, A.table_sumsq, s);
+}
+
+// sharded clipping, TABLES: clip_grad_norm_'s coefficient from the all-reduced table share and the
+// (all-reduced) replicated-weight gradients
+int clip_coefficient_sharded(const ttamm_tower* T[2], TowerWs* W[2], const AdamConsts& ad, const ttamm_step_args& A,
+                             StepWs& ws, hipStream_t s) {
+    int rc;
+    TTAMM_HIP(hipMemcpyAsync(ws.clip_partials, A.table_sumsq, sizeof(float), hipMemcpyDeviceToDevice, s));
+    if ((rc = launch_dense_sumsq(dense_args(T, W, ad, A.status, nullptr), ws.clip_partials + 1, s))) return rc;
+    return launch_clip_coef(ws.clip_partials, 1 + kDenseSumsqBlocks, (float)A.hp.grad_clip_norm, ws.clip_coef, s);
 }
 
 // Deferred mode is all-or-nothing over the dense-group tables of both towers.
@@ -1256,10 +1340,11 @@ int validate_step(const ttamm_step_args& A) {
     for (const ttamm_tower* t : {&A.user, &A.item})
         if (t->id.max_norm > 0.0) {
             TTAMM_REQUIRE(t->id.optimizer == TTAMM_OPT_DENSE, "max_norm is not supported when using sparse embeddings.");
-            TTAMM_REQUIRE(!sharded(A), "max_norm embeddings are not implemented in the row-sharded step");
         }
     if (A.hp.grad_clip_norm > 0.0) {
-        TTAMM_REQUIRE(!sharded(A), "gradient clipping is not implemented in the row-sharded step");
+        TTAMM_REQUIRE(!sharded(A) || !(A.phase & (TTAMM_PHASE_USER | TTAMM_PHASE_ITEM_BWD)),
+                      "gradient clipping in the row-sharded step needs the grouped schedule (SCORE / TOWERS_BWD)");
+        TTAMM_REQUIRE(!sharded(A) || A.table_sumsq != nullptr, "sharded gradient clipping needs table_sumsq");
         TTAMM_REQUIRE(A.user.id.optimizer == TTAMM_OPT_DENSE && A.item.id.optimizer == TTAMM_OPT_DENSE,
                       "gradient clipping needs dense ID tables (clip_grad_norm_ cannot take the sparse gradients "
                       "of sparse ID tables)");
@@ -1268,7 +1353,7 @@ int validate_step(const ttamm_step_args& A) {
                   "row_base / global_batch out of range");
     if (!sharded(A)) return TTAMM_OK;
     const int ph = A.phase;
-    TTAMM_REQUIRE((ph & ~1023) == 0, "unknown phase bits");
+    TTAMM_REQUIRE((ph & ~2047) == 0, "unknown phase bits");
     TTAMM_REQUIRE(!((ph & TTAMM_PHASE_USER) && (ph & (TTAMM_PHASE_SCORE | TTAMM_PHASE_TOWERS_BWD))),
                   "USER and SCORE / TOWERS_BWD are alternatives");
     TTAMM_REQUIRE(A.in_batch || (ph & (TTAMM_PHASE_INBATCH_SRC | TTAMM_PHASE_INBATCH)) == 0,
@@ -1327,6 +1412,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         I.dA = A.item_bwd_in ? A.item_bwd_in + D : nullptr;
         I.dA_ld = 2 * D;
         I.dA_split = I.R;  // every row's mimic gradient is shipped in (dT | dA)
+        I.renorm_key_split = Bg;  // request keys: positives [0, Bg), negatives from Bg on
         neg = A.b.neg_items;
     } else {
         I.idx = I.fidx = I.idx_own;
@@ -1396,22 +1482,29 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     hipStream_t aux = static_cast<hipStream_t>(A.aux_stream);
     if (!shard) {
         df.slice_on_aux = df.on && overlapped(T, 2, df, s, aux) && !std::getenv("TTAMM_SLICE_MAIN");
-        if ((rc = prepare_forward(T, W, 2, A.b, D, mimic, df, s, aux, A.timing_events + 2, A.timing_events))) return rc;
+        if ((rc = prepare_forward(T, W, 2, A.b, D, mimic, df, s, aux, A.timing_events + 2, A.timing_events,
+                                  A.timing_events + 8)))
+            return rc;
     } else {
         const ttamm_tower* Ti[2] = {&A.item, nullptr};
         TowerWs* Wi[2] = {&I, nullptr};
         const int both = TTAMM_PHASE_ITEM_FWD | TTAMM_PHASE_USER_FWD;
         if ((ph & both) == both && I.R > 0) {  // grouped: both towers' launches at once
-            if ((rc = prepare_forward(T, W, 2, A.b, D, mimic, df, s, aux, A.timing_events + 2))) return rc;
+            if ((rc = prepare_forward(T, W, 2, A.b, D, mimic, df, s, aux, A.timing_events + 2, nullptr,
+                                      A.timing_events + 8)))
+                return rc;
         } else if (ph & TTAMM_PHASE_ITEM_FWD) {
             if (I.R > 0) {
-                if ((rc = prepare_forward(Ti, Wi, 1, A.b, D, mimic, df, s, aux, A.timing_events + 2))) return rc;
+                if ((rc = prepare_forward(Ti, Wi, 1, A.b, D, mimic, df, s, aux, A.timing_events + 2, nullptr,
+                                          A.timing_events + 8)))
+                    return rc;
             } else if ((rc = tower_prepare(A.item, I, mimic, df, s))) {
                 return rc;
             }
         }
         if ((ph & TTAMM_PHASE_USER_FWD) && !((ph & both) == both && I.R > 0))
-            if ((rc = prepare_forward(T, W, 1, A.b, D, mimic, df, s, aux, nullptr))) return rc;
+            if ((rc = prepare_forward(T, W, 1, A.b, D, mimic, df, s, aux, nullptr, nullptr, A.timing_events + 8)))
+                return rc;
     }
     // ---- in-batch negatives: S = U P^T, its BCE, dU and dP ------------------------------------
     const int64_t ib_cols = ws.ib_on ? (shard ? Bg : B) : 0;  // positives every user is scored against
@@ -1518,7 +1611,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         }
         if (!shard) {
             // ---- the whole backward + optimizers in one process --------------------------------
-            if ((rc = tower_backward(T, W, D, s, 2))) return rc;
+            if ((rc = tower_backward(T, W, D, s, 2, A.timing_events + 6))) return rc;
             if (ws.clip_on && (rc = clip_coefficient(T, W, D, mimic, sp, ad, df, A, ws, s, aux))) return rc;
             if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, s, aux, ws.clip_coef))) return rc;
             return dense_update(T, W, ad, A.status, s, ws.clip_coef);
@@ -1531,20 +1624,29 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     // ---- grouped: both towers' backward and table updates ------------------------------------
     if (ph & TTAMM_PHASE_TOWERS_BWD) {
         if (I.R > 0) {
-            if ((rc = tower_backward(T, W, D, s, 2))) return rc;
+            if ((rc = tower_backward(T, W, D, s, 2, A.timing_events + 6))) return rc;
         } else {
             if ((rc = tower_backward(T, W, D, s, 1))) return rc;
             const size_t n = tower_grad_floats(A.item);
             if (n) TTAMM_HIP(hipMemsetAsync(I.gw[0] ? I.gw[0] : I.ggw[0], 0, n * sizeof(float), s));
         }
-        if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, s, aux))) return rc;
+        if (ws.clip_on) {  // the table updates wait for the global norm (TABLES, after the all-reduce)
+            if ((rc = clip_table_share(T, W, D, mimic, sp, ad, df, A, ws, s, aux))) return rc;
+        } else if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, s, aux))) {
+            return rc;
+        }
+    }
+    // ---- sharded clipping: the deferred table updates, scaled by clip_grad_norm_'s coefficient --
+    if ((ph & TTAMM_PHASE_TABLES) && ws.clip_on) {
+        if ((rc = clip_coefficient_sharded(T, W, ad, A, ws, s))) return rc;
+        if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, s, aux, ws.clip_coef))) return rc;
     }
     // ---- item-side backward on the owner ------------------------------------------------------
     if (ph & TTAMM_PHASE_ITEM_BWD) {
         const ttamm_tower* Ti[2] = {&A.item, nullptr};
         TowerWs* Wi[2] = {&I, nullptr};
         if (I.R > 0) {
-            if ((rc = tower_backward(Ti, Wi, D, s, 1))) return rc;
+            if ((rc = tower_backward(Ti, Wi, D, s, 1, A.timing_events + 6))) return rc;
         } else {
             // no requests: this rank's item-tower gradient share is zero
             const size_t n = tower_grad_floats(A.item);
@@ -1553,7 +1655,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         if ((rc = table_updates(Ti, Wi, 1, D, mimic, sp, ad, df, A.timing_events, s, aux))) return rc;
     }
     if (ph & TTAMM_PHASE_DENSE)
-        if ((rc = dense_update(T, W, ad, A.status, s))) return rc;
+        if ((rc = dense_update(T, W, ad, A.status, s, ws.clip_on ? ws.clip_coef : nullptr))) return rc;
     return TTAMM_OK;
 }
 
@@ -1680,6 +1782,153 @@ int tower_forward_eval(const ttamm_tower& T, const int64_t* idx, const int64_t* 
     TowerWs* WW[2] = {&w, nullptr};
     const bool mimic = augment && T.mimic.weight;
     if ((rc = tower_forward(TT, WW, bt, D, mimic, s, 1))) return rc;
+    return TTAMM_OK;
+}
+
+
+// ---- training-mode tower forward / backward (module-level autograd) ------------------------
+// TowerEncoder.forward under autograd (encoders.py:221-255) in two calls: the forward keeps its
+// activations in the workspace, the backward (same tower, rows and workspace) runs the tower's
+// backward kernels — gate, dgrad chain, one grouped weight-gradient launch — into the caller's
+// gradient arena (tower_grad_floats: per Linear weight then bias, 256-B aligned pieces) and
+// writes the ID rows' gradient per position (and, identity feature encoder, the feature rows').
+namespace {
+void plan_tower_train(Arena& ar, const ttamm_tower& T, int64_t n, TowerWs& w) {
+    const int D = T.id.dim;
+    w.role = ROLE_USER;
+    w.R = n;
+    w.idx_own = ar.take<int64_t>(n);
+    for (int l = 0; l + 1 < T.n_linear; ++l) {
+        w.hid[l] = ar.take<float>((size_t)n * T.linear[l].out_features);
+        w.dhid[l] = ar.take<float>((size_t)n * T.linear[l].out_features);
+        if (T.activation != TTAMM_ACT_RELU) {
+            w.pre[l] = ar.take<float>((size_t)n * T.linear[l].out_features);
+            if (T.dropout > 0.f) w.mask[l] = ar.take<uint8_t>((size_t)n * T.linear[l].out_features);
+        }
+    }
+    if (uses_ef(T)) {
+        w.ef = ar.take<float>((size_t)n * 2 * D);
+        w.dEF = ar.take<float>((size_t)n * 2 * D);
+    } else {
+        w.e = ar.take<float>((size_t)n * D);
+        w.f = ar.take<float>((size_t)n * D);
+    }
+    if (T.fusion == TTAMM_FUSION_GATED) {
+        const int Hg = T.gate[0].out_features;
+        w.z = ar.take<float>((size_t)n * Hg);
+        w.dz = ar.take<float>((size_t)n * Hg);
+        w.g = ar.take<float>((size_t)n * D);
+        w.dq = ar.take<float>((size_t)n * D);
+    }
+    WgradShape shapes[TTAMM_MAX_LINEAR + 2];
+    const int ns = wgrad_shapes(T, n, shapes);
+    int rps[2] = {512, 512};
+    if (ns) wgrad_rows_per_split(shapes, ns, rps);
+    w.wgrad_rps[0] = rps[0];
+    w.wgrad_rps[1] = rps[1];
+    if (T.fusion != TTAMM_FUSION_IDENTITY) {
+        for (int l = 0; l < T.n_linear; ++l) {
+            const ttamm_linear& L = T.linear[l];
+            w.slab[l] = ar.take<float>(wgrad_slab_floats((int)n, L.out_features, L.in_features,
+                                                         w.wgrad_rps[wgrad_class(L.out_features)]));
+        }
+        for (int q = 0; q < fusion_linears(T); ++q) {
+            const ttamm_linear& L = T.gate[q];
+            w.slab[TTAMM_MAX_LINEAR + q] = ar.take<float>(
+                wgrad_slab_floats((int)n, L.out_features, L.in_features, w.wgrad_rps[wgrad_class(L.out_features)]));
+        }
+    }
+    if (needs_wpad(T)) w.wpad = ar.take<float>((size_t)T.linear[0].out_features * round4(T.linear[0].in_features));
+    if (T.id.max_norm > 0.0) w.renorm_mark = ar.take<int32_t>(T.id.rows);
+}
+
+int bind_tower_train(const ttamm_tower& T, const int64_t* idx, const int64_t* fidx, int64_t n, void* wsp,
+                     size_t ws_bytes, TowerWs& w) {
+    Arena ar{static_cast<char*>(wsp), ws_bytes, 0, false};
+    plan_tower_train(ar, T, n, w);
+    TTAMM_REQUIRE(ar.ok(), "workspace too small for the training tower forward / backward");
+    w.idx = w.idx_own;
+    w.fidx = fidx == idx ? w.idx_own : fidx;  // caller-gathered feature rows: fidx = null (row r)
+    w.key_split = n;
+    return TTAMM_OK;
+}
+}  // namespace
+
+size_t tower_grad_floats_of(const ttamm_tower& T) { return tower_grad_floats(T); }
+
+size_t tower_train_workspace_size(const ttamm_tower& T, int64_t n) {
+    Arena ar{nullptr, 0, 0, true};
+    TowerWs w;
+    plan_tower_train(ar, T, n, w);
+    return ar.off + 256;
+}
+
+int tower_train_forward(const ttamm_tower& T, const int64_t* idx, const int64_t* fidx, int64_t n,
+                        const uint8_t* const* keep_masks, uint64_t seed, uint64_t counter, float* out, void* wsp,
+                        size_t ws_bytes, hipStream_t s) {
+    const int D = T.id.dim;
+    int rc;
+    if ((rc = validate_tower(T, "tower", D, false))) return rc;
+    if (n <= 0) return TTAMM_OK;
+    TowerWs w;
+    if ((rc = bind_tower_train(T, idx, fidx, n, wsp, ws_bytes, w))) return rc;
+    {  // ids outside the table read row 0 (the Python mirror raises IndexError before calling)
+        StageArgs st;
+        std::memset(&st, 0, sizeof(st));
+        st.seg[st.count++] = StageSeg{idx, w.idx_own, n, T.id.rows};
+        if ((rc = launch_stage_rows(st, s))) return rc;
+    }
+    if (w.renorm_mark) {
+        TTAMM_HIP(hipMemsetAsync(w.renorm_mark, 0, (size_t)T.id.rows * sizeof(int32_t), s));
+        w.renorm_tag = 1;
+    }
+    w.t = out;
+    w.t_ld = D;
+    ttamm_batch bt;
+    std::memset(&bt, 0, sizeof(bt));
+    bt.seed = seed;
+    bt.counter = counter;
+    for (int l = 0; keep_masks && l + 1 < T.n_linear; ++l) bt.user_keep_mask[l] = keep_masks[l];
+    const ttamm_tower* TT[2] = {&T, nullptr};
+    TowerWs* WW[2] = {&w, nullptr};
+    return tower_forward(TT, WW, bt, D, false, s, 1);
+}
+
+int tower_train_backward(const ttamm_tower& T, const int64_t* idx, const int64_t* fidx, int64_t n,
+                         const uint8_t* const* keep_masks, const float* d_out, float* grad_arena, float* d_id_rows,
+                         float* d_feat_rows, void* wsp, size_t ws_bytes, hipStream_t s) {
+    const int D = T.id.dim;
+    int rc;
+    if ((rc = validate_tower(T, "tower", D, false))) return rc;
+    const size_t ng = tower_grad_floats(T);
+    if (n <= 0) {
+        if (ng) TTAMM_HIP(hipMemsetAsync(grad_arena, 0, ng * sizeof(float), s));
+        return TTAMM_OK;
+    }
+    TTAMM_REQUIRE(d_out && (ng == 0 || grad_arena), "tower backward: d_out / grad_arena missing");
+    TowerWs w;
+    if ((rc = bind_tower_train(T, idx, fidx, n, wsp, ws_bytes, w))) return rc;
+    w.dT = d_out;
+    w.dT_ld = D;
+    float* cur = grad_arena;
+    carve_grads(T, w, cur);
+    // non-ReLU layers read the forward's keep bytes: the injected masks again, or the ones the
+    // forward drew into the workspace
+    for (int l = 0; l + 1 < T.n_linear; ++l) w.keep[l] = keep_masks && keep_masks[l] ? keep_masks[l] : w.mask[l];
+    const ttamm_tower* TT[2] = {&T, nullptr};
+    TowerWs* WW[2] = {&w, nullptr};
+    if (T.fusion != TTAMM_FUSION_IDENTITY)
+        if ((rc = tower_backward(TT, WW, D, s, 1))) return rc;
+    // d(ID rows): [e | f] towers take dEF[:, :D]; sum / identity fusion pass dT to e
+    const float* de = uses_ef(T) ? w.dEF : d_out;
+    const int64_t ld_de = uses_ef(T) ? 2 * D : D;
+    if (d_id_rows && (rc = launch_add_rows(de, ld_de, nullptr, 0, n, D, d_id_rows, D, s))) return rc;
+    if (d_feat_rows) {  // identity feature encoder: f = the feature row, its gradient is dEF[:, D:] / dT
+        TTAMM_REQUIRE(T.n_linear == 0 && T.fusion != TTAMM_FUSION_IDENTITY,
+                      "tower backward: feature-row gradients exist for the identity feature encoder only");
+        const float* df = uses_ef(T) ? w.dEF + D : d_out;
+        if ((rc = launch_add_rows(df, ld_de, nullptr, 0, n, D, d_feat_rows, D, s))) return rc;
+    }
     return TTAMM_OK;
 }
 

@@ -18,11 +18,13 @@ TTAMM_E_INVALID = 1
 TTAMM_E_RUNTIME = 2
 TTAMM_E_HIP = 3
 
-MAX_LINEAR = 4
+MAX_LINEAR = 6
 FUSION_IDENTITY, FUSION_SUM, FUSION_GATED, FUSION_CONCAT = 0, 1, 2, 3
+ACT_RELU, ACT_GELU, ACT_TANH, ACT_SELU = 0, 1, 2, 3  # ttamm.h TTAMM_ACT_*
 OPT_SPARSE_ADAM, OPT_DENSE = 0, 1
 STATUS_SAMPLER_EXHAUSTED = 1
 STATUS_INDEX_OUT_OF_RANGE = 2
+STATUS_POISON = STATUS_SAMPLER_EXHAUSTED | STATUS_INDEX_OUT_OF_RANGE  # bits that stop every later step
 
 _NATIVE_DIR = Path(__file__).resolve().parent / "_native"
 LIB_PATH = _NATIVE_DIR / "libttamm.so"
@@ -73,6 +75,7 @@ class Tower(ctypes.Structure):
         ("fusion", c_i32),
         ("n_linear", c_i32),
         ("dropout", c_f),
+        ("activation", c_i32),
         ("linear", Linear * MAX_LINEAR),
         ("gate", Linear * 2),
         ("matmul_bf16", c_i32),
@@ -131,7 +134,7 @@ class StepArgs(ctypes.Structure):
         ("status", c_vp),
         ("workspace", c_vp),
         ("workspace_bytes", ctypes.c_size_t),
-        ("timing_events", c_vp * 6),
+        ("timing_events", c_vp * 12),
         # row-sharded multi-GPU step (ttamm.h TTAMM_PHASE_*)
         ("phase", c_i32),
         ("row_base", c_i64),
@@ -145,6 +148,7 @@ class StepArgs(ctypes.Structure):
         ("item_fwd_in", c_vp),
         ("item_bwd_out", c_vp),
         ("item_bwd_in", c_vp),
+        ("table_sumsq", c_vp),
         ("dense_grads", c_vp),
         # deferred exact AdamW(g = 0) on tables with last_step
         ("adam_history", c_vp),
@@ -165,7 +169,7 @@ class StepArgs(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 16  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 19  # ttamm.h TTAMM_ABI_VERSION
 G0_EXACT = 0  # ttamm.h TTAMM_G0_EXACT
 G0_FAST = 1  # ttamm.h TTAMM_G0_FAST
 
@@ -181,6 +185,7 @@ PHASE_INBATCH_SRC = 64
 PHASE_INBATCH = 128
 PHASE_SCORE = 256
 PHASE_TOWERS_BWD = 512
+PHASE_TABLES = 1024
 
 
 # Symbol table: name -> (restype, argtypes).  tests/ check every one is exported and that this
@@ -215,6 +220,21 @@ SIGNATURES = {
     "ttamm_tower_forward": (
         ctypes.c_int,
         [ctypes.POINTER(Tower), c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, ctypes.c_size_t, c_vp],
+    ),
+    "ttamm_tower_grad_floats": (ctypes.c_size_t, [ctypes.POINTER(Tower)]),
+    "ttamm_tower_train_workspace_size": (ctypes.c_size_t, [ctypes.POINTER(Tower), c_i64]),
+    "ttamm_tower_train_forward": (
+        ctypes.c_int,
+        [ctypes.POINTER(Tower), c_vp, c_vp, c_i64, c_vp, ctypes.c_uint64, ctypes.c_uint64, c_vp, c_vp,
+         ctypes.c_size_t, c_vp],
+    ),
+    "ttamm_tower_train_backward": (
+        ctypes.c_int,
+        [ctypes.POINTER(Tower), c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_size_t, c_vp],
+    ),
+    "ttamm_scatter_add_rows": (
+        ctypes.c_int,
+        [c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, ctypes.c_float, c_i64, c_vp],
     ),
     "ttamm_mimic_augment": (ctypes.c_int, [c_vp, c_i64, c_i32, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "ttamm_mse_loss": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),

@@ -2,9 +2,10 @@
 
 Same parameters (``user_augmented.weight``, ``item_augmented.weight``), same init and the
 same error conventions (adaptive_mimic.py:20-105).  The row gathers, the augmentation add
-and the MSE reductions run on the MI355X through libttamm.  Inside training the whole
-mechanism (gather, add, stop-grad MSE, gradients, full-table AdamW) is fused into the step
-(``ttamm_train_step``); this module's own forward is the inference / evaluation path.
+and the MSE reductions run on the MI355X through libttamm, with autograd (ttamm/autograd.py:
+the dense table gradients by ttamm_scatter_add_rows) when the reference's own loop calls the
+module.  Inside ``ttamm.train_one_epoch`` the whole mechanism (gather, add, stop-grad MSE,
+gradients, full-table AdamW) is fused into the step instead (``ttamm_train_step``).
 """
 
 from __future__ import annotations
@@ -64,17 +65,17 @@ class AdaptiveMimicMechanism(nn.Module):
         if indices.dtype != torch.long:
             raise ValueError("Adaptive mimic indices must be torch.long tensors.")
         _lib.require_rocm(reference, "AdaptiveMimicMechanism")
-        if torch.is_grad_enabled() and (table.weight.requires_grad or reference.requires_grad):
-            raise RuntimeError(
-                "ttamm AdaptiveMimicMechanism is inference-only outside the fused training step; "
-                "use ttamm.train_one_epoch or torch.no_grad()"
-            )
         flat = indices.reshape(-1).contiguous()
         _lib.check_index_range(flat, table.num_embeddings)
         base = reference.reshape(flat.numel(), -1)
         if base.shape[1] != self.embedding_dim:
             raise ValueError("Adaptive mimic: embedding width does not match the augmentation tables.")
         base = base.contiguous()
+        if torch.is_grad_enabled() and (table.weight.requires_grad or reference.requires_grad):
+            from .autograd import ApplyAugFunction
+
+            out, rows = ApplyAugFunction.apply(table.weight, flat, base)
+            return out.reshape(reference.shape), rows.reshape(reference.shape)
         out = torch.empty_like(base)
         rows = torch.empty_like(base)
         lib = _lib.load()
@@ -88,7 +89,14 @@ class AdaptiveMimicMechanism(nn.Module):
 
 
 def _mse(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """F.mse_loss(x, y), reduction 'mean' (y is detached by the callers, adaptive_mimic.py:66-67)."""
     xs, ys = x.contiguous(), y.contiguous()
+    if xs.shape != ys.shape:
+        raise ValueError("ttamm: mse_loss input and target shapes differ")
+    if torch.is_grad_enabled() and xs.requires_grad:
+        from .autograd import MSEFunction
+
+        return MSEFunction.apply(xs.reshape(xs.shape[0], -1), ys.reshape(ys.shape[0], -1))
     out = torch.empty((), dtype=torch.float32, device=x.device)
     _lib.check(_lib.load().ttamm_mse_loss(xs.data_ptr(), ys.data_ptr(), xs.numel(), out.data_ptr(),
                                           _lib.stream_handle(x.device)))

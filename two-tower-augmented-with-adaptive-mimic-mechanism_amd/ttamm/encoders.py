@@ -7,10 +7,11 @@ match the reference (encoders.py:19-331) so configs and checkpoints carry over:
     feature_encoder.network.{i}.{weight,bias}          (nn.Sequential MLP, encoders.py:102-146)
     adaptive_mimic.gate_network.{0,2}.{weight,bias}    (FeatureFusionGate, encoders.py:149-168)
 
-``TowerEncoder.forward`` executes on the MI355X through libttamm (``ttamm_tower_forward``:
-ID-row gather, MFMA feature MLP and the gated fusion in fused gfx950 kernels).  Training
-goes through the fused step (``ttamm.training.train_one_epoch``); a forward that would need
-autograd raises instead of silently falling back to PyTorch ops.
+``TowerEncoder.forward`` executes on the MI355X through libttamm: in eval mode / under no_grad
+``ttamm_tower_forward`` (ID-row gather, MFMA feature MLP and the fusion in fused gfx950 kernels);
+under autograd ``ttamm_tower_train_forward`` / ``_backward`` wrapped in a torch.autograd.Function
+(ttamm/autograd.py), so the reference's own loop body can call the modules and ``backward()``.
+The fast training path is the fused step (``ttamm.training.train_one_epoch``).
 """
 
 from __future__ import annotations
@@ -151,9 +152,14 @@ class FeatureFusionGate(nn.Module):
         )
 
     def forward(self, id_repr: torch.Tensor, feature_repr: torch.Tensor) -> torch.Tensor:
-        raise RuntimeError(
-            "FeatureFusionGate runs fused inside TowerEncoder.forward / the training step on MI355X"
-        )
+        """gate * id + (1 - gate) * feature (encoders.py:164-168) on the fused gate kernels, with
+        autograd to both inputs and the gate's parameters (ttamm/autograd.py gate_forward)."""
+        from .autograd import gate_forward
+
+        _lib.require_rocm(id_repr, "FeatureFusionGate")
+        shape = id_repr.shape
+        out = gate_forward(self, id_repr.reshape(-1, shape[-1]), feature_repr.reshape(-1, shape[-1]))
+        return out.reshape(shape)
 
 
 class TowerEncoder(nn.Module):
@@ -275,28 +281,47 @@ def _matmul_dtype(name: str) -> str:
     raise ValueError(f"Unsupported matmul_dtype: {name} (fp32 or bf16)")
 
 
+_ACT_CODE = {nn.ReLU: _lib.ACT_RELU, nn.GELU: _lib.ACT_GELU, nn.Tanh: _lib.ACT_TANH, nn.SELU: _lib.ACT_SELU}
+
+
 def feature_layers(tower: TowerEncoder) -> tuple[list[nn.Linear], float]:
-    """The Linear layers of the feature encoder and its dropout p.  Raises for encoder
-    shapes the fused kernels do not implement (non-ReLU activations, identity encoders)."""
+    """The Linear layers of the feature encoder (none for the identity encoder) and its
+    dropout p (encoders.py:102-146)."""
+    return _feature_net(tower)[:2]
+
+
+def feature_activation(tower: TowerEncoder) -> int:
+    """ttamm.h TTAMM_ACT_* of the feature MLP's hidden layers (encoders.py:68-78, :130)."""
+    return _feature_net(tower)[2]
+
+
+def _feature_net(tower: TowerEncoder) -> tuple[list[nn.Linear], float, int]:
     if tower.feature_encoder is None or tower.fusion == "identity":
-        return [], 0.0
+        return [], 0.0, _lib.ACT_RELU
     net = tower.feature_encoder.network
     if isinstance(net, nn.Linear):
-        return [net], 0.0
+        return [net], 0.0, _lib.ACT_RELU
+    if isinstance(net, nn.Identity):  # encoders.py:114-119: f = the feature row
+        return [], 0.0, _lib.ACT_RELU
     if not isinstance(net, nn.Sequential):
-        raise NotImplementedError("ttamm: identity feature encoders are not implemented on the MI355X path")
+        raise NotImplementedError(f"ttamm: feature encoder {type(net).__name__} is not implemented")
     linears: list[nn.Linear] = []
     p = 0.0
+    act = _lib.ACT_RELU
     for m in net:
         if isinstance(m, nn.Linear):
             linears.append(m)
         elif isinstance(m, nn.Dropout):
             p = float(m.p)
-        elif not isinstance(m, nn.ReLU):
-            raise NotImplementedError(f"ttamm: activation {type(m).__name__} is not implemented (ReLU only)")
+        elif type(m) in _ACT_CODE:
+            if isinstance(m, nn.GELU) and m.approximate != "none":
+                raise NotImplementedError("ttamm: GELU(approximate='tanh') is not implemented")
+            act = _ACT_CODE[type(m)]
+        else:
+            raise NotImplementedError(f"ttamm: activation {type(m).__name__} is not implemented")
     if len(linears) > _lib.MAX_LINEAR:
         raise NotImplementedError(f"ttamm: at most {_lib.MAX_LINEAR} feature-encoder layers")
-    return linears, p
+    return linears, p, act
 
 
 def _linear_struct(layer: nn.Linear, state: Mapping[int, Mapping[str, torch.Tensor]] | None = None) -> _lib.Linear:
@@ -354,7 +379,7 @@ def describe_tower(
             s.mimic.exp_avg_sq = st["exp_avg_sq"].data_ptr()
     s.fusion = _FUSION_CODE[tower.fusion]
     s.matmul_bf16 = 1 if getattr(tower, "matmul_dtype", "fp32") == "bf16" else 0
-    linears, p = feature_layers(tower)
+    linears, p, act = _feature_net(tower)
     if s.fusion != _lib.FUSION_IDENTITY:
         if features is None:
             raise ValueError("ttamm: this tower fuses feature rows; features are required")
@@ -364,6 +389,7 @@ def describe_tower(
         s.feat_ld = int(feat_ld if feat_ld is not None else features.stride(0))
         s.feat_dim = features.shape[1]
         s.dropout = p
+        s.activation = act
         s.n_linear = len(linears)
         for i, layer in enumerate(linears):
             s.linear[i] = _linear_struct(layer, state)
@@ -383,23 +409,30 @@ def tower_forward(
     features: torch.Tensor | None,
     mimic_table: torch.Tensor | None = None,
 ) -> torch.Tensor:
-    """TowerEncoder.forward (eval semantics) on the MI355X; optionally adds the mimic rows."""
+    """TowerEncoder.forward on the MI355X (encoders.py:221-255); optionally adds the mimic rows
+    (eval path only).  Under autograd (a parameter requires grad) or in train mode with dropout,
+    the training forward runs (ttamm/autograd.py: activations kept for the backward)."""
     _lib.require_rocm(indices, "TowerEncoder.forward")
     if indices.dtype != torch.long:
         raise ValueError("ttamm: indices must be torch.long")
-    if torch.is_grad_enabled() and any(p.requires_grad for p in tower.parameters()):
-        raise RuntimeError(
-            "ttamm TowerEncoder.forward is inference-only on MI355X; train with ttamm.train_one_epoch "
-            "(the fused step) or call under torch.no_grad()"
-        )
-    if tower.training and feature_layers(tower)[1] > 0:
-        raise RuntimeError("ttamm TowerEncoder.forward runs in eval mode; call tower.eval() first")
     if features is not None and tower.fusion == "identity":
         features = None
     use_features = tower.fusion != "identity" and features is not None
     idx = indices.reshape(-1).contiguous()
     _lib.check_index_range(idx, tower.num_embeddings)
     n = idx.numel()
+    train = (torch.is_grad_enabled() and any(p.requires_grad for p in tower.parameters())) or \
+        (tower.training and feature_layers(tower)[1] > 0)
+    if train and mimic_table is None:
+        from .autograd import tower_train_forward
+
+        feats = None
+        if use_features:
+            feats = features.reshape(-1, features.shape[-1])
+            if feats.shape[0] != n:
+                raise ValueError("ttamm: features must have one row per index")
+        out = tower_train_forward(tower, idx, feats)
+        return out.reshape(*indices.shape, tower.id_dim)
     out = torch.empty((n, tower.id_dim), dtype=torch.float32, device=idx.device)
     if not use_features and tower.fusion != "identity":
         # the reference falls back to the ID embedding when features are absent (encoders.py:228-231)

@@ -179,15 +179,23 @@ def sampled_candidates(users: Sequence[int], truth: Mapping[int, set[int]], bloc
     """Candidate lists of _retrieve_with_sampling (training.py:979-987), drawing from ``rng`` in
     the reference's order (one rng.choice per user, users ascending as DataFrame.groupby yields
     them): the user's ground truth plus up to ``candidate_samples`` distinct unblocked items.
-    ``list(set(range(n)) - blocked)`` iterates in ascending order (CPython stores small ints at
-    their own hash slot, and the set's table is larger than n), so the sorted setdiff is the same
-    array and rng.choice picks the same items.  The list order is the reference's set order."""
+    The reference draws from ``list(set(range(n)) - blocked)``, whose order is CPython's: when
+    len(blocked) < n / 4 (set_difference's copy-and-discard path, (n >> 2) > len(blocked)) it is
+    ascending (small ints sit at their own hash slot of a table larger than n), so the sorted
+    setdiff is the same array and rng.choice picks the same items; otherwise CPython builds a new,
+    smaller table whose order is not ascending, and the reference's expression itself is
+    evaluated.  The list order is the reference's set order."""
     everything = np.arange(num_items, dtype=np.int64)
     lists: list[list[int]] = []
     for u in users:
         cands = set(truth[u])
-        b = blocked.get(int(u), ())
-        avail = everything if not b else np.setdiff1d(everything, np.fromiter(b, dtype=np.int64), assume_unique=False)
+        b = set(blocked.get(int(u), ()))
+        if not b:
+            avail = everything
+        elif (num_items >> 2) > len(b):
+            avail = np.setdiff1d(everything, np.fromiter(b, dtype=np.int64), assume_unique=False)
+        else:  # CPython's new-set path: the reference's own expression, in its iteration order
+            avail = np.fromiter(set(range(num_items)) - b, dtype=np.int64)
         if avail.size:
             budget = max(0, min(int(candidate_samples), int(avail.size)))
             if budget > 0:

@@ -77,6 +77,13 @@ class RowOwnership:
         """This rank's rows of a global table (a copy, contiguous)."""
         return full[self.rank :: self.world_size].contiguous()
 
+    def local_padding_idx(self, padding_idx: int | None) -> int | None:
+        """The shard's nn.Embedding padding_idx for a table whose global padding row is
+        ``padding_idx`` (encoders.py:47): its local row on the owner, None on every other rank."""
+        if padding_idx is None or int(padding_idx) % self.world_size != self.rank:
+            return None
+        return int(padding_idx) // self.world_size
+
 
 # ---------------------------------------------------------------------------------------
 # collectives as requests
@@ -196,6 +203,51 @@ class TorchComm:
             return stop.value
 
 
+class MirrorComm:
+    """Serves ONE rank's collectives as if the other W - 1 ranks ran the same program on the same
+    data relabelled (rank s's traffic to rank d is this rank's traffic to rank d - s + rank):
+    an all-to-all returns this rank's own send chunks (the chunk "from" rank s is the one this
+    rank sends to rank 2 rank - s, so every split agrees with the count exchange), an
+    all-gather W copies of ``send``, a reduce-scatter this rank's chunk, an all-reduce the tensor
+    unchanged.  The rank then does exactly the per-rank work of a W-rank step — W x its own
+    item requests as owner, the W B-row all-gathered in-batch positives — with no interconnect
+    traffic.  A measurement device (``bench.py --emulate-world``), not a numerically meaningful
+    run: the values are not those of any W-rank job."""
+
+    def __init__(self, world_size: int, rank: int = 0) -> None:
+        if world_size < 1 or not 0 <= rank < world_size:
+            raise ValueError("ttamm: bad (world_size, rank)")
+        self.world, self.rank = int(world_size), int(rank)
+
+    def __call__(self, req: Any) -> Any:
+        W, me = self.world, self.rank
+        if isinstance(req, AllToAll):
+            chunks = list(torch.split(req.send, req.send_splits))
+            got = torch.cat([chunks[(2 * me - s) % W] for s in range(W)])
+            if got.shape[0] != sum(req.recv_splits):
+                raise RuntimeError("mirror: recv splits do not match the mirrored sends")
+            if req.out is not None:
+                got = req.out.copy_(got)
+            return (None, got) if req.async_op else got
+        if isinstance(req, Wait):
+            return req.handle[1]
+        if isinstance(req, AllGather):
+            return torch.cat([req.send] * W)
+        if isinstance(req, ReduceScatter):
+            return req.send.chunk(W)[me].contiguous()
+        if isinstance(req, AllReduce):
+            return req.tensor
+        raise TypeError(f"unknown collective request {req!r}")
+
+    def run(self, program: Program) -> Any:
+        res = None
+        try:
+            while True:
+                res = self(program.send(res))
+        except StopIteration as stop:
+            return stop.value
+
+
 def run_loopback(programs: Sequence[Program]) -> list[Any]:
     """Run W SPMD programs in one process, serving their collectives jointly.  Rank order is
     the reduction order of AllReduce (fixed, deterministic)."""
@@ -264,6 +316,8 @@ class Route:
     recv_counts: list[int]  # requests from each requester
     rows: torch.Tensor  # owner side: local rows requested [n_recv]
     keys: torch.Tensor  # owner side: global request positions [n_recv]
+    own_status: int = 0  # this rank's status word after SAMPLE (when piggybacked)
+    peer_status: int = 0  # OR of the other ranks' status words
 
 
 def device_route(lib: Any, world: int, id0: torch.Tensor, id1: torch.Tensor | None = None,
@@ -290,20 +344,32 @@ Router = Callable[..., "tuple[torch.Tensor, torch.Tensor, torch.Tensor]"]  # dev
 
 
 def route_requests(own: RowOwnership, router: Router, pos: torch.Tensor, negs: torch.Tensor, key0: int,
-                   key1: int) -> Program:
+                   key1: int, status: torch.Tensor | None = None) -> Program:
     """Program: send (local row, key) of every requested item ([pos; negs], keys key0 + j for
     positives, key1 + j for negatives) to its owner.  Returns a Route.  One host sync (the
-    counts, which size the variable all-to-all); none at world size 1."""
+    counts, which size the variable all-to-all); none at world size 1.  ``status`` (the rank's
+    device status word): rides along with the counts, so every rank learns whether any rank's
+    step is poisoned (Route.peer_status) before any of them writes state."""
     W = own.world_size
     n = pos.numel() + negs.numel()
-    cnt = torch.empty(2 * W, dtype=torch.long, device=pos.device)
-    packed, slot, _ = router(W, pos, negs, None, key0, key1, counts_out=cnt[:W])
+    counts = torch.empty(W, dtype=torch.long, device=pos.device)
+    packed, slot, _ = router(W, pos, negs, None, key0, key1, counts_out=counts)
     if W == 1:
         return Route(slot, [n], [n], packed[:, 0].contiguous(), packed[:, 1].contiguous())
-    yield AllToAll(cnt[:W], [1] * W, [1] * W, out=cnt[W:])
-    c = cnt.tolist()
-    got = yield AllToAll(packed, c[:W], c[W:])
-    return Route(slot, c[:W], c[W:], got[:, 0].contiguous(), got[:, 1].contiguous())
+    send = torch.zeros((W, 2), dtype=torch.long, device=pos.device)  # (count to d, my status)
+    send[:, 0] = counts
+    if status is not None:
+        send[:, 1] = status.to(torch.long)
+    recv = torch.empty_like(send)
+    yield AllToAll(send, [1] * W, [1] * W, out=recv)
+    c = torch.cat([send.reshape(-1), recv.reshape(-1)]).tolist()
+    sent, got_c = c[0:2 * W:2], c[2 * W::2]
+    peers = 0
+    for r, st in enumerate(c[2 * W + 1::2]):
+        if r != own.rank:
+            peers |= int(st)
+    got = yield AllToAll(packed, sent, got_c)
+    return Route(slot, sent, got_c, got[:, 0].contiguous(), got[:, 1].contiguous(), int(c[1]), peers)
 
 
 # ---------------------------------------------------------------------------------------
@@ -317,16 +383,23 @@ class ShardedTrainStep(FusedTrainStep):
 
     Every rank must call ``step`` with the same batch size (the global batch is W x B, rank r's
     interactions are global positions [r B, (r+1) B)); ``step`` and ``finish`` are collective.
+
+    Reference options (encoders.py:47-58, training.py:824-825):
+      * padding_idx: the shard's ID table carries the padding row as a LOCAL row on its owner
+        only (``RowOwnership.local_padding_idx``); it gets no gradient there, as in one process;
+      * max_norm (dense ID tables): the owner renorms the rows looked up for every requester's
+        positives, then for their negatives — the reference's two item lookups (training.py:750,
+        :776) — and each rank its own users;
+      * gradient_clip_norm (dense ID tables, grouped schedule): the table updates wait for the
+        global norm — each rank's share over the table rows it owns rides in the gradient
+        all-reduce (TTAMM_PHASE_TABLES), so every rank applies clip_grad_norm_'s one coefficient.
     """
 
     def __init__(self, model, optimizers, *, world_size: int, rank: int, num_items: int,
                  comm: Callable[[Program], Any] | None = None, group_towers: bool = True, **kw: Any) -> None:
-        for enc in (model.user_encoder, model.item_encoder):
-            if enc.embedding.padding_idx is not None:
-                # a global padding id lives on one owner as a local row: not mapped here
-                raise NotImplementedError("ttamm: padding_idx is not implemented in the row-sharded step")
-            if enc.embedding.max_norm is not None:
-                raise NotImplementedError("ttamm: max_norm embeddings are not implemented in the row-sharded step")
+        clip = kw.get("gradient_clip_norm")
+        if clip is not None and clip > 0 and not group_towers:
+            raise NotImplementedError("ttamm: gradient clipping in the row-sharded step needs group_towers=True")
         self.own = RowOwnership(world_size, rank)
         self.comm = comm
         # True: both towers' forward in one set of grouped launches, then the (t | a) exchange;
@@ -347,11 +420,14 @@ class ShardedTrainStep(FusedTrainStep):
         args.item_rows_capacity = self.capacity
         args.num_items_global = self.num_items
         n_grad = int(self.lib.ttamm_dense_grad_floats(ctypes.byref(args)))
-        # gradient arena + this rank's loss share: one all-reduce carries both
-        self.arena = torch.zeros(n_grad + 5, dtype=torch.float32, device=self.device)  # + loss_out[5]
+        # gradient arena + this rank's loss share (+ its table-row squared gradient norm when
+        # clipping): one all-reduce carries them all
+        self.arena = torch.zeros(n_grad + 6, dtype=torch.float32, device=self.device)  # + loss_out[5] + sumsq
         self.n_grad = n_grad
-        self.loss_out = self.arena[n_grad:]
+        self.loss_out = self.arena[n_grad:n_grad + 5]
+        self.clip = args.hp.grad_clip_norm > 0
         args.loss_out = self.loss_out.data_ptr()
+        args.table_sumsq = self.arena[n_grad + 5:].data_ptr()
         args.dense_grads = self.arena.data_ptr()
         D = self.model.user_encoder.embedding.weight.shape[1]
         self.D = D
@@ -387,14 +463,22 @@ class ShardedTrainStep(FusedTrainStep):
             raise ValueError("ttamm: in-batch negatives need the same batch size on every rank")
         a.row_base = base
         a.global_batch = Bg
-        ev = list(timing_events or []) + [None] * 6
-        for i in range(6):
+        nev = len(a.timing_events)
+        ev = list(timing_events or []) + [None] * nev
+        for i in range(nev):
             a.timing_events[i] = None
         self._hparams()
         negs = neg_items.reshape(-1) if neg_items is not None else self.neg_buffer[: B * N]
         self._phase(_lib.PHASE_SAMPLE)
         # ---- route the item requests [positives; negatives] to their owners -----------------
-        route = yield from route_requests(self.own, self.router, pos_items.reshape(-1), negs, base, Bg + base * N)
+        route = yield from route_requests(self.own, self.router, pos_items.reshape(-1), negs, base, Bg + base * N,
+                                          status=self.status)
+        if route.peer_status and not route.own_status:
+            # another rank's step is poisoned (an id outside its table, sampler exhaustion):
+            # poison this rank's step too, before it writes any state, so every rank keeps the
+            # state after the same last good step; SAMPLE already counted the step here
+            self.status.bitwise_or_(route.peer_status & _lib.STATUS_POISON)
+            self.steps_applied.sub_(1)
         n = route.rows.numel()
         self.item_rows_seen += n
         if n > self.capacity:
@@ -405,7 +489,8 @@ class ShardedTrainStep(FusedTrainStep):
         a.item_slot = route.slot.data_ptr()  # exchange buffers stay in owner-grouped order
         a.item_fwd_out = self.fwd_out.data_ptr()
         R = B * (1 + N)
-        a.timing_events[2], a.timing_events[3] = ev[2], ev[3]
+        for i in (2, 3, 8, 9, 10, 11):  # first-layer GEMM, catch-up replays
+            a.timing_events[i] = ev[i]
         if W == 1:  # no exchange: the requester's buffers are the owner's
             self._phase(_lib.PHASE_ITEM_FWD | _lib.PHASE_USER_FWD if self.group_towers else _lib.PHASE_ITEM_FWD)
             if not self.group_towers:
@@ -420,7 +505,8 @@ class ShardedTrainStep(FusedTrainStep):
                                out=self.fwd_in[:R])
             self._phase(_lib.PHASE_USER_FWD)
             back = yield Wait(h)
-        a.timing_events[2] = a.timing_events[3] = None
+        for i in (2, 3, 8, 9, 10, 11):
+            a.timing_events[i] = None
         a.item_fwd_in = back.data_ptr()
         a.item_bwd_out = self.bwd_out.data_ptr()
         ib = ()
@@ -444,11 +530,16 @@ class ShardedTrainStep(FusedTrainStep):
         else:
             bwd_in = yield AllToAll(self.bwd_out[:R], route.send_counts, route.recv_counts)
         a.item_bwd_in = bwd_in.data_ptr()
-        a.timing_events[0], a.timing_events[1] = ev[0], ev[1]
+        for i in (0, 1, 6, 7):  # table maintenance, wide weight-gradient GEMM
+            a.timing_events[i] = ev[i]
         self._phase(_lib.PHASE_TOWERS_BWD if self.group_towers else _lib.PHASE_ITEM_BWD)
-        a.timing_events[0] = a.timing_events[1] = None
+        for i in (6, 7):
+            a.timing_events[i] = None
         if W > 1:
             yield AllReduce(self.arena)
+        if self.clip:  # the table updates under the global clip coefficient
+            self._phase(_lib.PHASE_TABLES)
+        a.timing_events[0] = a.timing_events[1] = None
         self._phase(_lib.PHASE_DENSE)
         self.steps_done += 1
         # keep the step's device buffers alive until the stream has consumed them
@@ -462,8 +553,9 @@ class ShardedTrainStep(FusedTrainStep):
 
     def finish_program(self) -> Program:
         """Collective finish: global epoch loss (sum of the ranks' shares).  A status error on
-        any rank (an out-of-range id, sampler exhaustion) raises on every rank; each rank's own
-        tables hold the state after its last good step."""
+        any rank (an out-of-range id, sampler exhaustion) raises on every rank, and every rank
+        holds the state after the same last good step: the status words ride with each step's
+        request counts, so a poisoned step is skipped by all ranks before any writes state."""
         flags = torch.stack([(self.status & b) != 0 for b in (1, 2)]).reshape(-1).to(torch.float32)
         yield AllReduce(flags)
         self.status.bitwise_or_((flags[0] > 0).to(torch.int32) + 2 * (flags[1] > 0).to(torch.int32))
@@ -511,8 +603,16 @@ def epoch_program(engine: ShardedTrainStep, batches: Any) -> Program:
     rank = own.rank
     for users, items in batches:
         u, i, sizes = yield from route_pairs(own, engine.router, users, items)
+        # every rank holds the same sizes (the all-gathered count matrix): they all raise here,
+        # before the step's first collective, instead of one rank leaving the others waiting in it
         if min(sizes) == 0:
             raise ValueError("ttamm: a rank received no interactions for this step")
+        if max(sizes) > engine.max_batch:
+            raise ValueError(f"ttamm: a routed batch of {max(sizes)} interactions exceeds the sharded step's "
+                             f"max_batch={engine.max_batch} (size it for the largest per-rank share of a step)")
+        if engine.in_batch and len(set(sizes)) > 1:
+            raise ValueError("ttamm: in-batch negatives need the same routed batch size on every rank "
+                             f"(routed sizes {sizes}); feed each rank its own users' interactions instead")
         yield from engine.program(u, i, row_base=sum(sizes[:rank]), global_batch=sum(sizes))
     return (yield from engine.finish_program())
 

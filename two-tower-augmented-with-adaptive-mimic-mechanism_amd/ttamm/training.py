@@ -122,7 +122,7 @@ class FusedTrainStep:
         num_items: int | None = None,
         deferred_adamw: bool = True,
         replay_slices: int = 64,
-        table_adamw_math: str = "fast",
+        table_adamw_math: str = "exact",
         overlap: bool = True,
         aux_cus: int | None = None,
         item_category_tensor: torch.Tensor | None = None,
@@ -305,7 +305,9 @@ class FusedTrainStep:
         self.dense_step0 = int(self._adam_steps[0]["step"].item()) if self._adam_steps else 0
         self.sparse_step0 = int(self._sparse_steps[0]["step"]) if self._sparse_steps else 0
         # arithmetic of the g = 0 AdamW updates of untouched table rows (ttamm.h table_g0_math):
-        # "exact" = IEEE sqrt / division, bit-identical to torch; "fast" = v_sqrt / v_rcp
+        # "exact" (default) = IEEE sqrt / division, bit-identical to torch's AdamW; "fast" =
+        # v_sqrt / v_rcp (<= 1 ulp each): exp_avg / exp_avg_sq stay bit-identical, a warm row's
+        # parameter moves by the same update term within a few ulp per step
         if table_adamw_math not in ("exact", "fast"):
             raise ValueError("ttamm: table_adamw_math must be 'exact' or 'fast'")
         args.table_g0_math = _lib.G0_FAST if table_adamw_math == "fast" else _lib.G0_EXACT
@@ -403,7 +405,7 @@ class FusedTrainStep:
             return
         a = self.args
         ev = list(timing_events or [])
-        for i in range(6):
+        for i in range(len(a.timing_events)):
             a.timing_events[i] = ev[i] if i < len(ev) else None
         self._hparams()
         _lib.check(self.lib.ttamm_train_step(ctypes.byref(a), _lib.stream_handle(self.device)))
@@ -506,6 +508,8 @@ class _IdentityView(nn.Module):
         self.feature_encoder = None
         self.embedding = tower.embedding
         self.matmul_dtype = tower.matmul_dtype
+        self.id_dim = tower.id_dim
+        self.num_embeddings = tower.num_embeddings
 
 
 def train_one_epoch(
@@ -527,6 +531,7 @@ def train_one_epoch(
     batch_hook: Callable[[int, torch.Tensor, torch.Tensor], tuple[Any, Any]] | None = None,
     step_losses: list | None = None,
     in_batch_negatives: bool = False,
+    table_adamw_math: str = "exact",
 ) -> float:
     """Drop-in for ``_train_one_epoch`` (training.py:700-833) executed on the MI355X.
 
@@ -538,7 +543,9 @@ def train_one_epoch(
       step_losses: receives each step's device loss vector [total, bce, mimic_user, mimic_item,
           category_alignment] (no host synchronisation inside the loop).
     ``in_batch_negatives`` selects ttamm's in-batch mode (FusedTrainStep; BASELINE C2/C4), with
-    ``negatives_per_positive`` sampled negatives on top (0 allowed)."""
+    ``negatives_per_positive`` sampled negatives on top (0 allowed).  ``table_adamw_math``: the
+    g = 0 AdamW arithmetic of untouched mimic-table rows — "exact" (default, bit-identical to
+    torch) or "fast" (FusedTrainStep)."""
     model.train()
     if not isinstance(criterion, nn.BCEWithLogitsLoss) or criterion.reduction != "mean" or \
             criterion.weight is not None or criterion.pos_weight is not None:
@@ -561,6 +568,7 @@ def train_one_epoch(
                 max_batch=max(int(size), users.numel()),
                 item_category_tensor=item_category_tensor, major_category_id=major_category_id,
                 in_batch_negatives=in_batch_negatives, gradient_clip_norm=gradient_clip_norm,
+                table_adamw_math=table_adamw_math,
             )
         neg = masks = None
         if batch_hook is not None:
