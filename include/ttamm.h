@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 19
+#define TTAMM_ABI_VERSION 20
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -104,6 +104,17 @@ extern "C" {
  *   TABLES  clip_grad_norm_'s coefficient from the global norm, then the table updates
  * and DENSE applies the same coefficient. */
 #define TTAMM_PHASE_TABLES 1024
+/* Category-alignment loss in a sharded step (item_categories set, lambda > 0): L_cal is taken
+ * over the GLOBAL batch's item rows (training.py:541-579 on cat[positives; negatives] of all
+ * ranks), so after the (t | a) exchange and before SCORE / USER,
+ *   CAL_STATS    requester: per-category sums and row counts of its requests -> cal_stats
+ *                [all-reduce (sum): cal_stats]
+ *   CAL_SCATTER  requester: centered scatter of its rows about the global means -> cal_scatter
+ *                [all-reduce (sum): cal_scatter]
+ * and SCORE / USER form the covariances, L_cal and G, and add the gradient of this rank's rows
+ * into item_bwd_out.  The rank with row_base 0 carries lambda * L_cal in its loss share. */
+#define TTAMM_PHASE_CAL_STATS 2048
+#define TTAMM_PHASE_CAL_SCATTER 4096
 
 /* Device-side status word bits (written by kernels, read by the host at epoch end).  Once a
  * bit is set, every later step on that status word is skipped on the device (no parameter,
@@ -279,8 +290,9 @@ typedef struct ttamm_step_args {
      * tower reads depend only on the indices; with an aux stream they run there, overlapping
      * the feature-MLP GEMMs, and `stream` waits for them before the first table read. */
     void* aux_stream;
-    /* ---- category-alignment loss (training.py:530-579, :805-820; one-process step only) ----
+    /* ---- category-alignment loss (training.py:530-579, :805-820; sharded: TTAMM_PHASE_CAL_*) ----
      * item_categories: [item.id.rows] int64 category id per item, each in [0, num_categories)
+     * (sharded: [num_items_global], every rank holds the global tensor)
      * (_build_item_category_tensor, training.py:582-610); NULL (or lambda 0) = no L_cal.       */
     const int64_t* item_categories;
     int64_t num_categories;
@@ -314,6 +326,11 @@ typedef struct ttamm_step_args {
      * owner-grouped order ttamm_route_rows produced, so the all-to-alls move the buffers as
      * they are (no permutation pass). */
     const int64_t* item_slot;
+    /* ---- sharded category alignment (TTAMM_PHASE_CAL_*): the caller's all-reduce buffers ------
+     * cal_stats [num_categories * (dim + 1)] floats, cal_scatter [num_categories * dim * dim]
+     * floats; the step zeroes and fills them between the caller's all-reduces.              */
+    float* cal_stats;
+    float* cal_scatter;
 } ttamm_step_args;
 
 #define TTAMM_G0_EXACT 0
@@ -335,6 +352,19 @@ int ttamm_train_step(const ttamm_step_args* args, void* stream);
 /* Size (floats) of the replicated-weight gradient arena of a sharded step: both towers'
  * feature-encoder and gate weight+bias gradients, contiguous (the all-reduce buffer). */
 int64_t ttamm_dense_grad_floats(const ttamm_step_args* args);
+
+/* Row grouping of a batch of row ids — the gradient coalescing every row-table update of the
+ * step runs (torch's grad.coalesce(), _functional.py:44, and the index_add order of the
+ * embedding backward, training.py:822): the unique rows, in first-occurrence order (sorted = 0)
+ * or ascending (sorted = 1, table_rows <= 65536), each with its batch positions ascending.
+ * Outputs: keys_out[n] / positions_out[n] (the row and batch position of each slot),
+ * seg_start_out[n + 1] (row u's slots are [seg_start[u], seg_start[u + 1])), n_unique_out[1].
+ * idx must hold ids in [0, table_rows).  The workspace (ttamm_coalesce_workspace_bytes) must be
+ * zero-filled before its first use; every call leaves its per-row scratch zero again. */
+size_t ttamm_coalesce_workspace_bytes(int64_t n, int64_t table_rows);
+int ttamm_coalesce_rows(const int64_t* idx, int64_t n, int64_t table_rows, int32_t sorted, int32_t* keys_out,
+                        int32_t* positions_out, int32_t* seg_start_out, int32_t* n_unique_out, void* workspace,
+                        size_t workspace_bytes, void* stream);
 
 /* ---- exact inner-product retrieval + top-k -------------------------------
  * Replaces faiss.IndexFlatIP.search + the candidate filter of _evaluate_model

@@ -2,7 +2,9 @@
 GPU against the one-process fused step over the global batch (as tests/test_sharded_gpu.py):
 padding_idx (the padding row local to its owner), max_norm ID tables (the owner renorms every
 requester's positives, then their negatives), gradient_clip_norm (the table updates wait for the
-all-reduced global norm).  One step at lr = 0 / betas (0, 0.999) — every gradient at 1e-5 — and
+all-reduced global norm), the category-alignment loss over the global batch (per-category sums
+and centered scatters all-reduced between TTAMM_PHASE_CAL_STATS / CAL_SCATTER, the reference's
+default loss weight raised so its gradient is visible).  One step at lr = 0 / betas (0, 0.999) — every gradient at 1e-5 — and
 three real steps — parameters within 5e-5 absolute."""
 
 from __future__ import annotations
@@ -56,8 +58,20 @@ def _shard_cfg(shape: Shape, own: RowOwnership) -> dict:
     return cfg
 
 
-def _run(shape: Shape, W: int, *, lr: float, betas, steps: int, clip: float | None):
+CAL_WEIGHTS = {**LOSS_WEIGHTS, "category_alignment": 2.0}
+
+
+def _categories(I: int, C: int = 4, major_share: float = 0.4, seed: int = 9) -> torch.Tensor:
+    g = torch.Generator().manual_seed(seed)
+    cats = torch.randint(1, C, (I,), generator=g)
+    cats[torch.rand(I, generator=g) < major_share] = 0
+    return cats
+
+
+def _run(shape: Shape, W: int, *, lr: float, betas, steps: int, clip: float | None, cal: bool = False):
     prob = make_problem(shape, seed=77)
+    lw = CAL_WEIGHTS if cal else LOSS_WEIGHTS
+    cat_kw = dict(item_category_tensor=_categories(shape.I).cuda(), major_category_id=0) if cal else {}
     state = prob.model.state_dict()
     gen = torch.Generator().manual_seed(5)
     batches = []
@@ -77,7 +91,8 @@ def _run(shape: Shape, W: int, *, lr: float, betas, steps: int, clip: float | No
     gopts = _opts(gm, lr, betas)
     geng = ttamm.FusedTrainStep(gm, gopts, negatives_per_positive=shape.N, positives=prob.positives,
                                 user_features=prob.user_features.cuda(), item_features=prob.item_features.cuda(),
-                                loss_weights=LOSS_WEIGHTS, max_batch=W * shape.B, seed=SEED, gradient_clip_norm=clip)
+                                loss_weights=lw, max_batch=W * shape.B, seed=SEED, gradient_clip_norm=clip,
+                                **cat_kw)
     ranks = []
     for r in range(W):
         own = RowOwnership(W, r)
@@ -87,8 +102,8 @@ def _run(shape: Shape, W: int, *, lr: float, betas, steps: int, clip: float | No
         local_pos = {u // W: prob.positives[u] for u in range(r, shape.U, W)}
         eng = ShardedTrainStep(m, opts, world_size=W, rank=r, num_items=shape.I, negatives_per_positive=shape.N,
                                positives=local_pos, user_features=own.shard(prob.user_features).cuda(),
-                               item_features=own.shard(prob.item_features).cuda(), loss_weights=LOSS_WEIGHTS,
-                               max_batch=shape.B, seed=SEED, gradient_clip_norm=clip)
+                               item_features=own.shard(prob.item_features).cuda(), loss_weights=lw,
+                               max_batch=shape.B, seed=SEED, gradient_clip_norm=clip, **cat_kw)
         ranks.append((own, m, opts, eng))
     glosses, rlosses = [], []
     for per_rank in batches:
@@ -102,23 +117,29 @@ def _run(shape: Shape, W: int, *, lr: float, betas, steps: int, clip: float | No
 
 
 CASES = [
-    (2, Shape(padding_idx=5), None),
-    (3, Shape(sparse=False, padding_idx=4), None),
-    (2, Shape(sparse=False, max_norm=0.05), None),
-    (3, Shape(sparse=False, max_norm=0.05, N=3), None),
-    (2, Shape(sparse=False), 0.05),
-    (3, Shape(sparse=False), 100.0),
-    (2, Shape(sparse=False, max_norm=0.05, padding_idx=6), 0.05),
+    (2, Shape(padding_idx=5), None, False),
+    (3, Shape(sparse=False, padding_idx=4), None, False),
+    (2, Shape(sparse=False, max_norm=0.05), None, False),
+    (3, Shape(sparse=False, max_norm=0.05, N=3), None, False),
+    (2, Shape(sparse=False), 0.05, False),
+    (3, Shape(sparse=False), 100.0, False),
+    (2, Shape(sparse=False, max_norm=0.05, padding_idx=6), 0.05, False),
+    (2, Shape(), None, True),
+    (3, Shape(N=3), None, True),
+    (3, Shape(sparse=False, max_norm=0.05, padding_idx=6), 0.05, True),
 ]
-IDS = ["padding-w2", "dense-padding-w3", "max-norm-w2", "max-norm-w3", "clip-w2", "noclip-w3", "all-w2"]
+IDS = ["padding-w2", "dense-padding-w3", "max-norm-w2", "max-norm-w3", "clip-w2", "noclip-w3", "all-w2",
+       "cal-w2", "cal-w3", "cal-all-w3"]
 
 
-@pytest.mark.parametrize("W,shape,clip", CASES, ids=IDS)
-def test_sharded_options_gradients_match_global_step(W, shape, clip):
-    (gm, gopts), ranks, gl, rl = _run(shape, W, lr=0.0, betas=(0.0, 0.999), steps=1, clip=clip)
-    for key in ("total", "bce", "mimic_user", "mimic_item"):
+@pytest.mark.parametrize("W,shape,clip,cal", CASES, ids=IDS)
+def test_sharded_options_gradients_match_global_step(W, shape, clip, cal):
+    (gm, gopts), ranks, gl, rl = _run(shape, W, lr=0.0, betas=(0.0, 0.999), steps=1, clip=clip, cal=cal)
+    if cal:
+        assert gl[0]["category_alignment"] > 0
+    for key in ("total", "bce", "mimic_user", "mimic_item", "category_alignment"):
         for r in range(W):
-            assert abs(rl[0][r][key] - gl[0][key]) <= 1e-5 * max(abs(gl[0][key]), 1e-12), key
+            assert abs(rl[0][r][key] - gl[0][key]) <= 1e-5 * max(abs(gl[0][key]), 1e-12), (key, rl[0][r][key], gl[0][key])
     gstate = named_optimizer_state(gm, gopts)
     for own, m, opts, _ in ranks:
         for name, st in named_optimizer_state(m, opts).items():
@@ -133,10 +154,10 @@ def test_sharded_options_gradients_match_global_step(W, shape, clip):
                 assert rel_err(m.state_dict()[k], gsd[k][own.rank:: W]) <= 1e-6, (own.rank, k)
 
 
-@pytest.mark.parametrize("W,shape,clip", [CASES[0], CASES[3], CASES[4], CASES[6]],
-                         ids=["padding-w2", "max-norm-w3", "clip-w2", "all-w2"])
-def test_sharded_options_three_steps_match_global_step(W, shape, clip):
-    (gm, _), ranks, gl, rl = _run(shape, W, lr=1e-3, betas=(0.9, 0.999), steps=3, clip=clip)
+@pytest.mark.parametrize("W,shape,clip,cal", [CASES[0], CASES[3], CASES[4], CASES[6], CASES[8], CASES[9]],
+                         ids=["padding-w2", "max-norm-w3", "clip-w2", "all-w2", "cal-w3", "cal-all-w3"])
+def test_sharded_options_three_steps_match_global_step(W, shape, clip, cal):
+    (gm, _), ranks, gl, rl = _run(shape, W, lr=1e-3, betas=(0.9, 0.999), steps=3, clip=clip, cal=cal)
     for s in range(3):
         assert abs(rl[s][0]["total"] - gl[s]["total"]) <= 1e-5 * abs(gl[s]["total"])
     gsd = gm.state_dict()

@@ -4,6 +4,8 @@
 
 #include <vector>
 
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace ttamm {
@@ -193,7 +195,40 @@ TTAMM_API int ttamm_scatter_add_rows(float* dst, int64_t dst_rows, int32_t dim, 
     if (n > 0 && (!dst || !x || dim <= 0 || ldx < dim || (y && ldy < dim) || dst_rows <= 0 || (!idx && n > dst_rows)))
         return fail(TTAMM_E_INVALID, "scatter_add_rows: bad arguments");
     g_last_error.clear();
-    return launch_scatter_add_rows(dst, dim, idx, n, x, ldx, y, ldy, scale_dev, scale, skip_row, (hipStream_t)stream);
+    return launch_scatter_add_rows(dst, dst_rows, dim, idx, n, x, ldx, y, ldy, scale_dev, scale, skip_row,
+                                   (hipStream_t)stream);
+}
+
+TTAMM_API size_t ttamm_coalesce_workspace_bytes(int64_t n, int64_t table_rows) {
+    if (n < 0 || table_rows <= 0) return 0;
+    const size_t tiles = (size_t)std::max<int64_t>(n, 257);
+    return sizeof(int32_t) * (coalesce_scratch_ints(table_rows) + 2 * (size_t)n + 2 * tiles);
+}
+
+TTAMM_API int ttamm_coalesce_rows(const int64_t* idx, int64_t n, int64_t table_rows, int32_t sorted, int32_t* keys_out,
+                                  int32_t* positions_out, int32_t* seg_start_out, int32_t* n_unique_out,
+                                  void* workspace, size_t workspace_bytes, void* stream) {
+    if (n < 0 || table_rows <= 0 || !n_unique_out || !seg_start_out || (n > 0 && (!idx || !keys_out || !positions_out)) ||
+        !workspace || workspace_bytes < ttamm_coalesce_workspace_bytes(n, table_rows))
+        return fail(TTAMM_E_INVALID, "coalesce_rows: bad arguments");
+    g_last_error.clear();
+    CoalesceWs co{};
+    int32_t* w = static_cast<int32_t*>(workspace);
+    coalesce_bind_scratch(co, w, table_rows);
+    w += coalesce_scratch_ints(table_rows);
+    co.vals_tmp = w;
+    w += n;
+    co.lead = w;
+    w += n;
+    co.lead_cnt = w;
+    w += std::max<int64_t>(n, 257);
+    co.seglong = w;
+    co.keys_out = keys_out;
+    co.vals_out = positions_out;
+    co.seg_start = seg_start_out;
+    co.n_unique = n_unique_out;
+    co.sorted = sorted ? 1 : 0;
+    return launch_coalesce(idx, n, table_rows, co, (hipStream_t)stream);
 }
 
 TTAMM_API int ttamm_mimic_augment(const float* table, int64_t table_rows, int32_t dim, const int64_t* idx, int64_t n,

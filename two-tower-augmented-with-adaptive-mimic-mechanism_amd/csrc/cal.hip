@@ -17,6 +17,14 @@
 //   piece sums -> means -> piece centered scatter tiles (64 x 64 per block) -> covariances ->
 //   per-category squared distances -> loss -> G_major -> per-row gradients added into the
 //   item rows' dT (and dA for positives: the augmented embedding is t + a).
+//
+// Row-sharded step (slot space = category ids, CalArgs::gstats set): the global batch is the
+// union of the ranks' request rows, so the statistics are global and only the rows are local:
+//   CAL_STATS   local piece sums -> gstats[c] = (sum of c's rows | count)    [all-reduce]
+//   CAL_SCATTER global means -> local centered scatter of c's rows -> gscat[c] [all-reduce]
+//   SCORE       cov_c = gscat[c] / (n_c - 1) in place, distances, L_cal, G, and the gradients of
+//               this rank's rows (global n_c and means), added into its (dT | dA) exchange rows.
+// Every rank computes the same loss and G from the same all-reduced sums.
 #include "kernels.h"
 
 namespace ttamm {
@@ -43,11 +51,14 @@ __device__ __forceinline__ int total_pieces(const CalArgs& A) {
     return A.pstart[last] + A.pcount[last];
 }
 
-// catrow[r] = category of item row r
+// catrow[r] = category of item row r (rows [split, R) from idx1 when given; an id outside
+// [0, idx_rows) — a poisoned step writes nothing — reads item 0's category)
 __global__ void cal_rows_kernel(CalArgs A) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= A.R) return;
-    int64_t c = A.categories[A.idx[r]];
+    int64_t id = A.idx1 && r >= A.split ? A.idx1[r - A.split] : A.idx[r];
+    if (id < 0 || id >= A.idx_rows) id = 0;
+    int64_t c = A.categories[id];
     c = c < 0 ? 0 : (c >= A.num_categories ? A.num_categories - 1 : c);
     A.catrow[r] = c;
 }
@@ -73,18 +84,34 @@ __device__ __forceinline__ bool piece_rows(const CalArgs& A, int p, int& u, int&
 
 __device__ __forceinline__ int seg_len(const CalArgs& A, int u) { return A.co.seg_start[u + 1] - A.co.seg_start[u]; }
 
-__device__ __forceinline__ const float* row_ptr(const CalArgs& A, int k) {
-    return A.x + (int64_t)A.co.vals_out[k] * A.ld_x;
+// the category of local segment u (segment keys are the rows' categories)
+__device__ __forceinline__ int64_t seg_cat(const CalArgs& A, int u) { return A.co.keys_out[A.co.seg_start[u]]; }
+
+// slot space: local segments (one process) or category ids (sharded, gstats set)
+__device__ __forceinline__ int slot_of(const CalArgs& A, int u) { return A.gstats ? (int)seg_cat(A, u) : u; }
+
+__device__ __forceinline__ int slot_count(const CalArgs& A, int q) {
+    if (A.gstats) return (int)A.gstats[(int64_t)q * (A.D + 1) + A.D];
+    return q < A.co.n_unique[0] ? seg_len(A, q) : 0;
+}
+
+// the exchange-buffer row of request row j
+__device__ __forceinline__ int64_t buf_row(const CalArgs& A, int64_t j) { return A.slot ? A.slot[j] : j; }
+
+// element col of sorted row k: x (+ xa, the mimic rows of the sharded exchange buffer)
+__device__ __forceinline__ float row_val(const CalArgs& A, int k, int col) {
+    const int64_t o = buf_row(A, A.co.vals_out[k]) * A.ld_x + col;
+    return A.xa ? A.x[o] + A.xa[o] : A.x[o];
 }
 
 // psum[p][d] = sum of the piece's rows (row order)
 __global__ void cal_piece_sum_kernel(CalArgs A) {
     int u, k0, k1;
     if (!piece_rows(A, blockIdx.x, u, k0, k1)) return;
-    if (seg_len(A, u) < 2) return;
+    if (!A.gstats && seg_len(A, u) < 2) return;
     for (int d = threadIdx.x; d < A.D; d += blockDim.x) {
         float s = 0.f;
-        for (int k = k0; k < k1; ++k) s += row_ptr(A, k)[d];
+        for (int k = k0; k < k1; ++k) s += row_val(A, k, d);
         A.psum[(int64_t)blockIdx.x * A.D + d] = s;
     }
 }
@@ -103,13 +130,38 @@ __global__ void cal_mean_kernel(CalArgs A) {
     }
 }
 
+// sharded: gstats[c] = (sum of the segment's piece sums, piece order | row count); the buffer is
+// zeroed first, categories absent here stay 0 for the all-reduce
+__global__ void cal_stats_kernel(CalArgs A) {
+    const int u = blockIdx.x;
+    if (u >= A.co.n_unique[0]) return;
+    const int q0 = A.pstart[u], q1 = q0 + A.pcount[u];
+    float* g = A.gstats + seg_cat(A, u) * (A.D + 1);
+    for (int d = threadIdx.x; d < A.D; d += blockDim.x) {
+        float s = 0.f;
+        for (int q = q0; q < q1; ++q) s += A.psum[(int64_t)q * A.D + d];
+        g[d] = s;
+    }
+    if (threadIdx.x == 0) g[A.D] = (float)seg_len(A, u);
+}
+
+// sharded: mean[u] = the global mean of segment u's category (all-reduced gstats)
+__global__ void cal_gmean_kernel(CalArgs A) {
+    const int u = blockIdx.x;
+    if (u >= A.co.n_unique[0]) return;
+    const float* g = A.gstats + seg_cat(A, u) * (A.D + 1);
+    const float n = g[A.D];
+    if (n < 2.f) return;
+    for (int d = threadIdx.x; d < A.D; d += blockDim.x) A.mean[(int64_t)u * A.D + d] = g[d] / n;
+}
+
 // pslab[p][i][j] = sum over the piece's rows of (x_i - mean_i)(x_j - mean_j), one 64 x 64
 // tile of (i, j) per block (blockIdx.y); 256 threads x (4 x 4) entries
 __global__ __launch_bounds__(256) void cal_piece_scatter_kernel(CalArgs A) {
     __shared__ float xs[kRowsStage][2 * kTile + 4];
     int u, k0, k1;
     if (!piece_rows(A, blockIdx.x, u, k0, k1)) return;
-    if (seg_len(A, u) < 2) return;
+    if (slot_count(A, slot_of(A, u)) < 2) return;
     const int D = A.D;
     const int nt = (D + kTile - 1) / kTile;
     const int I0 = (blockIdx.y / nt) * kTile, J0 = (blockIdx.y % nt) * kTile;
@@ -123,7 +175,7 @@ __global__ __launch_bounds__(256) void cal_piece_scatter_kernel(CalArgs A) {
             const int r = e / (2 * kTile), c = e % (2 * kTile);
             const int col = c < kTile ? I0 + c : J0 + (c - kTile);
             float v = 0.f;
-            if (r < nr && col < D) v = row_ptr(A, kb + r)[col] - mu[col];
+            if (r < nr && col < D) v = row_val(A, kb + r, col) - mu[col];
             xs[r][c] = v;
         }
         __syncthreads();
@@ -165,8 +217,34 @@ __global__ void cal_cov_kernel(CalArgs A) {
     A.cov[u * DD + e] = s / (float)(n - 1);
 }
 
-// the segment of the major category, or -1 (keys of the unique segments are ascending)
+// sharded: gscat[c] = sum of segment u's piece scatters (piece order); zeroed first
+__global__ void cal_seg_scatter_kernel(CalArgs A) {
+    const int u = blockIdx.y;
+    if (u >= A.co.n_unique[0]) return;
+    if (slot_count(A, slot_of(A, u)) < 2) return;
+    const int64_t DD = (int64_t)A.D * A.D;
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= DD) return;
+    const int q0 = A.pstart[u], q1 = q0 + A.pcount[u];
+    float s = 0.f;
+    for (int q = q0; q < q1; ++q) s += A.pslab[(int64_t)q * DD + e];
+    A.cov[seg_cat(A, u) * DD + e] = s;
+}
+
+// sharded: cov[c] = gscat[c] / (n_c - 1) in place (all-reduced scatter sums, global counts)
+__global__ void cal_cov_dense_kernel(CalArgs A) {
+    const int c = blockIdx.y;
+    const int n = slot_count(A, c);
+    if (n < 2) return;
+    const int64_t DD = (int64_t)A.D * A.D;
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= DD) return;
+    A.cov[c * DD + e] = A.cov[c * DD + e] / (float)(n - 1);
+}
+
+// the slot of the major category, or -1 (keys of the unique segments are ascending)
 __device__ int major_segment(const CalArgs& A) {
+    if (A.gstats) return slot_count(A, (int)A.major) > 0 ? (int)A.major : -1;
     const int nu = A.co.n_unique[0];
     int lo = 0, hi = nu - 1;
     while (lo <= hi) {
@@ -179,18 +257,21 @@ __device__ int major_segment(const CalArgs& A) {
     return -1;
 }
 
-// the reference's early exits (training.py:552-563): <= 1 category, < 2 major rows
+// the reference's early exits (training.py:552-563): <= 1 category, < 2 major rows (with a
+// single category nothing is compared either, so the sharded slot space skips that count)
 __device__ bool cal_active(const CalArgs& A, int uM) {
-    return A.co.n_unique[0] > 1 && uM >= 0 && seg_len(A, uM) >= 2;
+    return (A.gstats || A.co.n_unique[0] > 1) && uM >= 0 && slot_count(A, uM) >= 2;
 }
+
+__device__ __forceinline__ int num_slots(const CalArgs& A) { return A.gstats ? (int)A.num_categories : A.nseg_max; }
 
 // part[u] = ||cov_u - cov_major||^2 for every compared category (flag[u] = 1)
 __global__ __launch_bounds__(256) void cal_dist_kernel(CalArgs A) {
     __shared__ float red[256];
     const int u = blockIdx.x;
-    if (u >= A.nseg_max) return;
+    if (u >= num_slots(A)) return;
     const int uM = major_segment(A);
-    const bool on = u < A.co.n_unique[0] && cal_active(A, uM) && u != uM && seg_len(A, u) >= 2;
+    const bool on = cal_active(A, uM) && u != uM && slot_count(A, u) >= 2;
     float s = 0.f;
     if (on) {
         const int64_t DD = (int64_t)A.D * A.D;
@@ -218,7 +299,7 @@ __global__ void cal_loss_kernel(CalArgs A) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     float loss = 0.f;
     int compared = 0;
-    for (int u = 0; u < A.nseg_max; ++u)
+    for (int u = 0; u < num_slots(A); ++u)
         if (A.flag[u]) {
             loss = loss + A.part[u];
             ++compared;
@@ -238,7 +319,7 @@ __global__ void cal_gmajor_kernel(CalArgs A) {
     const float cm = A.cov[uM * DD + e];
     const float scale = 2.0f / (float)compared;
     float g = 0.f;
-    for (int u = 0; u < A.nseg_max; ++u)
+    for (int u = 0; u < num_slots(A); ++u)
         if (A.flag[u]) g -= scale * (A.cov[u * DD + e] - cm);
     A.gmajor[e] = g;
 }
@@ -255,22 +336,23 @@ __global__ __launch_bounds__(128) void cal_row_grad_kernel(CalArgs A) {
     const int compared = (int)A.out[1];
     if (compared == 0) return;
     const int uM = major_segment(A);
-    if (u != uM && !A.flag[u]) return;
+    const int q = slot_of(A, u);
+    if (q != uM && !A.flag[q]) return;
     const int D = A.D;
     const int64_t DD = (int64_t)D * D;
     const int J0 = blockIdx.y * kGradCols;
     float* Gs = lds;                           // [D][kGradCols]
     float* xs = lds + (int64_t)D * kGradCols;  // [16][D]
     const float scale = 2.0f / (float)compared;
-    const float* cu = A.cov + u * DD;
+    const float* cu = A.cov + q * DD;
     const float* cm = A.cov + uM * DD;
     for (int e = threadIdx.x; e < D * kGradCols; e += blockDim.x) {
         const int i = e / kGradCols, j = J0 + e % kGradCols;
         float g = 0.f;
-        if (j < D) g = u == uM ? A.gmajor[(int64_t)i * D + j] : scale * (cu[(int64_t)i * D + j] - cm[(int64_t)i * D + j]);
+        if (j < D) g = q == uM ? A.gmajor[(int64_t)i * D + j] : scale * (cu[(int64_t)i * D + j] - cm[(int64_t)i * D + j]);
         Gs[e] = g;
     }
-    const float coef = A.lambda * (2.0f / (float)(seg_len(A, u) - 1));
+    const float coef = A.lambda * (2.0f / (float)(slot_count(A, q) - 1));
     const float* mu = A.mean + (int64_t)u * D;
     const int rl = threadIdx.x / 8, cg = threadIdx.x % 8;
     for (int kb = k0; kb < k1; kb += 16) {
@@ -278,7 +360,7 @@ __global__ __launch_bounds__(128) void cal_row_grad_kernel(CalArgs A) {
         __syncthreads();
         for (int e = threadIdx.x; e < 16 * D; e += blockDim.x) {
             const int r = e / D, c = e % D;
-            xs[e] = r < nr ? row_ptr(A, kb + r)[c] - mu[c] : 0.f;
+            xs[e] = r < nr ? row_val(A, kb + r, c) - mu[c] : 0.f;
         }
         __syncthreads();
         const int col = J0 + 4 * cg;
@@ -289,11 +371,12 @@ __global__ __launch_bounds__(128) void cal_row_grad_kernel(CalArgs A) {
 #pragma unroll
                 for (int w = 0; w < 4; ++w) o[w] = fmaf(xv, Gs[i * kGradCols + 4 * cg + w], o[w]);
             }
-            const int64_t row = A.co.vals_out[kb + rl];
+            const int64_t j = A.co.vals_out[kb + rl];
+            const int64_t row = buf_row(A, j);
             float* dt = A.dT + row * A.ld_d + col;
 #pragma unroll
             for (int w = 0; w < 4; ++w) dt[w] += coef * o[w];
-            if (A.dA && row < A.dA_rows) {
+            if (A.dA && j < A.dA_rows) {
                 float* da = A.dA + row * A.ld_d + col;
 #pragma unroll
                 for (int w = 0; w < 4; ++w) da[w] += coef * o[w];
@@ -307,8 +390,10 @@ inline unsigned blocks_for(int64_t n, int t = 256) { return (unsigned)ceil_div(n
 }  // namespace
 
 int cal_max_pieces(int64_t R, int64_t nseg_max) { return (int)(ceil_div(R, kPiece) + nseg_max); }
+size_t cal_stats_floats(int64_t num_categories, int D) { return (size_t)num_categories * (D + 1); }
+size_t cal_scatter_floats(int64_t num_categories, int D) { return (size_t)num_categories * D * D; }
 
-int launch_category_alignment(const CalArgs& a, hipStream_t s) {
+int launch_cal_local(const CalArgs& a, hipStream_t s) {
     TTAMM_REQUIRE(a.D % 4 == 0 && a.D <= 256, "category alignment: embedding dim must be a multiple of 4, <= 256");
     TTAMM_REQUIRE(a.R > 0 && a.nseg_max > 0 && a.nseg_max <= 65535, "category alignment: bad batch / category count");
     int rc;
@@ -320,27 +405,64 @@ int launch_category_alignment(const CalArgs& a, hipStream_t s) {
     TTAMM_LAUNCH_CHECK();
     if ((rc = launch_block_exclusive_scan(a.pcount, a.pstart, a.nseg_max, s))) return rc;
     const unsigned pieces = (unsigned)cal_max_pieces(a.R, a.nseg_max);
-    const unsigned nt = (unsigned)ceil_div(a.D, kTile);
     hipLaunchKernelGGL(cal_piece_sum_kernel, dim3(pieces), dim3(256), 0, s, a);
     TTAMM_LAUNCH_CHECK();
-    hipLaunchKernelGGL(cal_mean_kernel, dim3((unsigned)a.nseg_max), dim3(256), 0, s, a);
+    if (a.gstats) {
+        TTAMM_HIP(hipMemsetAsync(a.gstats, 0, sizeof(float) * cal_stats_floats(a.num_categories, a.D), s));
+        hipLaunchKernelGGL(cal_stats_kernel, dim3((unsigned)a.nseg_max), dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(cal_mean_kernel, dim3((unsigned)a.nseg_max), dim3(256), 0, s, a);
+    }
     TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_cal_scatter(const CalArgs& a, hipStream_t s) {
+    const unsigned pieces = (unsigned)cal_max_pieces(a.R, a.nseg_max);
+    const unsigned nt = (unsigned)ceil_div(a.D, kTile);
+    const int64_t DD = (int64_t)a.D * a.D;
+    if (a.gstats) {
+        hipLaunchKernelGGL(cal_gmean_kernel, dim3((unsigned)a.nseg_max), dim3(256), 0, s, a);
+        TTAMM_LAUNCH_CHECK();
+    }
     hipLaunchKernelGGL(cal_piece_scatter_kernel, dim3(pieces, nt * nt), dim3(256), 0, s, a);
     TTAMM_LAUNCH_CHECK();
-    const int64_t DD = (int64_t)a.D * a.D;
-    hipLaunchKernelGGL(cal_cov_kernel, dim3(blocks_for(DD), (unsigned)a.nseg_max), dim3(256), 0, s, a);
+    if (a.gstats) {
+        TTAMM_HIP(hipMemsetAsync(a.cov, 0, sizeof(float) * cal_scatter_floats(a.num_categories, a.D), s));
+        hipLaunchKernelGGL(cal_seg_scatter_kernel, dim3(blocks_for(DD), (unsigned)a.nseg_max), dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(cal_cov_kernel, dim3(blocks_for(DD), (unsigned)a.nseg_max), dim3(256), 0, s, a);
+    }
     TTAMM_LAUNCH_CHECK();
-    hipLaunchKernelGGL(cal_dist_kernel, dim3((unsigned)a.nseg_max), dim3(256), 0, s, a);
+    return TTAMM_OK;
+}
+
+int launch_cal_finish(const CalArgs& a, hipStream_t s) {
+    const int64_t DD = (int64_t)a.D * a.D;
+    const unsigned slots = (unsigned)(a.gstats ? a.num_categories : a.nseg_max);
+    if (a.gstats) {
+        hipLaunchKernelGGL(cal_cov_dense_kernel, dim3(blocks_for(DD), slots), dim3(256), 0, s, a);
+        TTAMM_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(cal_dist_kernel, dim3(slots), dim3(256), 0, s, a);
     TTAMM_LAUNCH_CHECK();
     hipLaunchKernelGGL(cal_loss_kernel, dim3(1), dim3(64), 0, s, a);
     TTAMM_LAUNCH_CHECK();
     if (a.dT == nullptr) return TTAMM_OK;  // loss only
     hipLaunchKernelGGL(cal_gmajor_kernel, dim3(blocks_for(DD)), dim3(256), 0, s, a);
     TTAMM_LAUNCH_CHECK();
+    const unsigned pieces = (unsigned)cal_max_pieces(a.R, a.nseg_max);
     const size_t lds = sizeof(float) * ((size_t)a.D * kGradCols + 16 * (size_t)a.D);
     hipLaunchKernelGGL(cal_row_grad_kernel, dim3(pieces, (unsigned)ceil_div(a.D, kGradCols)), dim3(128), lds, s, a);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
+}
+
+int launch_category_alignment(const CalArgs& a, hipStream_t s) {
+    int rc;
+    if ((rc = launch_cal_local(a, s))) return rc;
+    if ((rc = launch_cal_scatter(a, s))) return rc;
+    return launch_cal_finish(a, s);
 }
 
 }  // namespace ttamm

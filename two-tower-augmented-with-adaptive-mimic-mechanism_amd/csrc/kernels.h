@@ -206,10 +206,11 @@ int launch_stage_rows(const StageArgs& a, hipStream_t s);
 // with xrow, out row r reads row xrow[r] of x and y
 int launch_add_rows(const float* x, int64_t ldx, const float* y, int64_t ldy, int64_t n, int dim, float* out,
                     int64_t ldo, hipStream_t s, const int64_t* xrow = nullptr);
-// dst[idx[r]] += (x[r] (- y[r])) * scale (* *scale_dev), skipping rows idx[r] == skip_row (float atomics)
-int launch_scatter_add_rows(float* dst, int dim, const int64_t* idx, int64_t n, const float* x, int64_t ldx,
-                            const float* y, int64_t ldy, const float* scale_dev, float scale, int64_t skip_row,
-                            hipStream_t s);
+// dst[idx[r]] += (x[r] (- y[r])) * scale (* *scale_dev), skipping rows idx[r] == skip_row and
+// rows outside [0, dst_rows) (float atomics)
+int launch_scatter_add_rows(float* dst, int64_t dst_rows, int dim, const int64_t* idx, int64_t n, const float* x,
+                            int64_t ldx, const float* y, int64_t ldy, const float* scale_dev, float scale,
+                            int64_t skip_row, hipStream_t s);
 
 // Status bits that stop every later step (ttamm.h TTAMM_STATUS_*).
 constexpr uint32_t kStatusPoison = TTAMM_STATUS_SAMPLER_EXHAUSTED | TTAMM_STATUS_INDEX_OUT_OF_RANGE;
@@ -359,7 +360,13 @@ int launch_coalesce(const int64_t* idx, int64_t n, int64_t table_rows, CoalesceW
 struct CalArgs {
     const float* x;             // augmented item rows [R, ld_x] = cat[positives; negatives]
     int64_t ld_x;
+    const float* xa;            // sharded: the mimic rows (row value = x + xa); null: x is t + a
+    const int64_t* slot;        // sharded: exchange-buffer row of request row r; null: row r
     const int64_t* idx;         // item id of row r
+    const int64_t* idx1;        // sharded: item ids of rows [split, R) (the negatives); null: idx
+    int64_t split;
+    int64_t idx_rows;           // ids outside [0, idx_rows) read item 0's category
+    float* gstats;              // sharded: [num_categories, D + 1] (sums | count), all-reduced
     const int64_t* categories;  // [items] category id (training.py:582-610)
     int64_t num_categories;
     int64_t major;              // major_category_id
@@ -374,17 +381,23 @@ struct CalArgs {
     float* psum;                // [pieces, D]
     float* mean;                // [nseg_max, D]
     float* pslab;               // [pieces, D, D]
-    float* cov;                 // [nseg_max, D, D]
-    float* part;                // [nseg_max]
-    int32_t* flag;              // [nseg_max]
+    float* cov;                 // [nseg_max, D, D]; sharded: [num_categories, D, D], all-reduced
+    float* part;                // [slots]: nseg_max, sharded num_categories
+    int32_t* flag;              // [slots]
     float* gmajor;              // [D, D]
     float* out;                 // [2]: L_cal, compared
     float* dT;                  // item rows' dT [R, ld_d] (+= lambda dX); null: loss only
-    float* dA;                  // positive rows' dA [dA_rows, ld_d] (+=), may be null
+    float* dA;                  // dA of request rows < dA_rows [., ld_d] (+=), may be null
     int64_t ld_d;
     int64_t dA_rows;
 };
 int cal_max_pieces(int64_t R, int64_t nseg_max);
+size_t cal_stats_floats(int64_t num_categories, int D);    // sharded gstats
+size_t cal_scatter_floats(int64_t num_categories, int D);  // sharded cov / scatter sums
+// the three stages (sharded: the caller all-reduces gstats after the first, cov after the second)
+int launch_cal_local(const CalArgs& a, hipStream_t s);
+int launch_cal_scatter(const CalArgs& a, hipStream_t s);
+int launch_cal_finish(const CalArgs& a, hipStream_t s);
 // exclusive prefix sum of n ints by one block (n up to ~1M; used for small arrays)
 int launch_block_exclusive_scan(const int32_t* in, int32_t* out, int64_t n, hipStream_t s);
 int launch_category_alignment(const CalArgs& a, hipStream_t s);

@@ -236,9 +236,8 @@ __global__ void co_fill_kernel(const int64_t* __restrict__ idx, int64_t n, int b
 // batch order), the long-segment flags, and the row's scratch back to zero.  One thread per
 // segment sorts up to kOrderSmall positions in registers (nearly every row of a batch occurs
 // once or a few times); longer segments (hot rows) are listed in `big` and ranked by whole
-// blocks, through LDS up to kOrderLds positions.
+// blocks (co_order_big_kernel).
 constexpr int kOrderSmall = 16;
-constexpr int kOrderLds = 4096;
 
 __device__ __forceinline__ void co_reset(const CoalesceWs& W, int32_t key) {
     W.cnt[key] = 0;
@@ -276,29 +275,80 @@ __global__ __launch_bounds__(256) void co_order_small_kernel(CoalesceWs W, int32
     co_reset(W, W.keys_out[k0]);
 }
 
+// Long segments: the positions are distinct integers, so each one's rank within the segment is
+// the number of the segment's positions below it — a bitmap over the segment's position range in
+// LDS, per-word prefix popcounts, one lookup per position: O(range / 32 + L) per segment (a
+// Zipf-hot item of a C2 batch spans ~50K positions: 1.5K words).  A range wider than the bitmap
+// falls back to counting ranks (L^2 / threads).
+constexpr int kBitWords = 6144;  // position range up to 196,608 (48 KB of LDS with the prefixes)
 __global__ __launch_bounds__(256) void co_order_big_kernel(CoalesceWs W, const int32_t* __restrict__ big,
                                                            const int32_t* __restrict__ n_big) {
-    __shared__ int32_t sv[kOrderLds];
+    __shared__ uint32_t bits[kBitWords];
+    __shared__ int32_t pre[kBitWords];
+    __shared__ int32_t sf[4], sc[4], smin[4], smax[4];
     const int nb = n_big[0];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int b = blockIdx.x; b < nb; b += gridDim.x) {
         const int32_t u = big[b];
         const int32_t k0 = W.seg_start[u], k1 = W.seg_start[u + 1], L = k1 - k0;
         const int32_t longseg = L > kCoalescePiece ? 1 : 0;
-        const bool in_lds = L <= kOrderLds;
-        __syncthreads();
-        if (in_lds)
-            for (int32_t j = threadIdx.x; j < L; j += blockDim.x) sv[j] = W.vals_tmp[k0 + j];
-        __syncthreads();
+        // the segment's position range
+        int32_t lo = INT_MAX, hi = -1;
         for (int32_t j = threadIdx.x; j < L; j += blockDim.x) {
-            const int32_t v = in_lds ? sv[j] : W.vals_tmp[k0 + j];
-            int32_t rank = 0;
-            if (in_lds)
-                for (int32_t i = 0; i < L; ++i) rank += sv[i] < v ? 1 : 0;
-            else
-                for (int32_t i = k0; i < k1; ++i) rank += W.vals_tmp[i] < v ? 1 : 0;
-            W.vals_out[k0 + rank] = v;
-            W.seglong[k0 + j] = longseg;
+            const int32_t v = W.vals_tmp[k0 + j];
+            lo = min(lo, v);
+            hi = max(hi, v);
         }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            lo = min(lo, __shfl_xor(lo, o, 64));
+            hi = max(hi, __shfl_xor(hi, o, 64));
+        }
+        __syncthreads();  // the previous segment's LDS reads are done
+        if (lane == 0) {
+            smin[wv] = lo;
+            smax[wv] = hi;
+        }
+        __syncthreads();
+        lo = min(min(smin[0], smin[1]), min(smin[2], smin[3]));
+        hi = max(max(smax[0], smax[1]), max(smax[2], smax[3]));
+        const int32_t nw = ((hi - lo) >> 5) + 1;
+        if (nw <= kBitWords) {
+            for (int32_t w = threadIdx.x; w < nw; w += blockDim.x) bits[w] = 0u;
+            __syncthreads();
+            for (int32_t j = threadIdx.x; j < L; j += blockDim.x) {
+                const int32_t d = W.vals_tmp[k0 + j] - lo;
+                atomicOr(&bits[d >> 5], 1u << (d & 31));
+            }
+            __syncthreads();
+            // exclusive prefix of the words' popcounts: contiguous chunks per thread, block scan
+            const int32_t chunk = (nw + (int32_t)blockDim.x - 1) / (int32_t)blockDim.x;
+            const int32_t w0 = min(nw, (int32_t)threadIdx.x * chunk), w1 = min(nw, w0 + chunk);
+            int32_t c = 0;
+            for (int32_t w = w0; w < w1; ++w) c += __popc(bits[w]);
+            int32_t f = 0, ci = c;
+            block_scan2(f, ci, sf, sc);
+            int32_t run = ci - c;
+            for (int32_t w = w0; w < w1; ++w) {
+                pre[w] = run;
+                run += __popc(bits[w]);
+            }
+            __syncthreads();
+            for (int32_t j = threadIdx.x; j < L; j += blockDim.x) {
+                const int32_t v = W.vals_tmp[k0 + j];
+                const int32_t d = v - lo;
+                const int32_t r = pre[d >> 5] + __popc(bits[d >> 5] & ((1u << (d & 31)) - 1u));
+                W.vals_out[k0 + r] = v;
+            }
+        } else {
+            for (int32_t j = threadIdx.x; j < L; j += blockDim.x) {
+                const int32_t v = W.vals_tmp[k0 + j];
+                int32_t rank = 0;
+                for (int32_t i = k0; i < k1; ++i) rank += W.vals_tmp[i] < v ? 1 : 0;
+                W.vals_out[k0 + rank] = v;
+            }
+        }
+        for (int32_t j = threadIdx.x; j < L; j += blockDim.x) W.seglong[k0 + j] = longseg;
         if (threadIdx.x == 0) co_reset(W, W.keys_out[k0]);
     }
 }

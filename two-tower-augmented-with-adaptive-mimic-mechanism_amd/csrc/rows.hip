@@ -504,14 +504,14 @@ namespace {
 __global__ void scatter_add_rows_kernel(float* __restrict__ dst, int dim, const int64_t* __restrict__ idx, int64_t n,
                                         const float* __restrict__ x, int64_t ldx, const float* __restrict__ y,
                                         int64_t ldy, const float* __restrict__ scale_dev, float scale,
-                                        int64_t skip_row) {
+                                        int64_t skip_row, int64_t dst_rows) {
     const float sc = scale_dev ? scale * *scale_dev : scale;
     const int64_t total = n * dim;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = i / dim;
         const int c = (int)(i - r * dim);
         const int64_t row = idx ? idx[r] : r;
-        if (row == skip_row) continue;
+        if (row == skip_row || row < 0 || row >= dst_rows) continue;  // never write outside dst
         float v = x[r * ldx + c];
         if (y) v = v - y[r * ldy + c];
         atomicAdd(dst + row * dim + c, v * sc);
@@ -519,12 +519,12 @@ __global__ void scatter_add_rows_kernel(float* __restrict__ dst, int dim, const 
 }
 }  // namespace
 
-int launch_scatter_add_rows(float* dst, int dim, const int64_t* idx, int64_t n, const float* x, int64_t ldx,
-                            const float* y, int64_t ldy, const float* scale_dev, float scale, int64_t skip_row,
-                            hipStream_t s) {
+int launch_scatter_add_rows(float* dst, int64_t dst_rows, int dim, const int64_t* idx, int64_t n, const float* x,
+                            int64_t ldx, const float* y, int64_t ldy, const float* scale_dev, float scale,
+                            int64_t skip_row, hipStream_t s) {
     if (n <= 0) return TTAMM_OK;
     hipLaunchKernelGGL(scatter_add_rows_kernel, dim3(grid_for(n * dim)), dim3(256), 0, s, dst, dim, idx, n, x, ldx, y,
-                       ldy, scale_dev, scale, skip_row);
+                       ldy, scale_dev, scale, skip_row, dst_rows);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

@@ -235,7 +235,7 @@ int wgrad_shapes(const ttamm_tower& T, int64_t R, WgradShape* out) {
 void plan_scratch(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
     coalesce_bind_scratch(ws.user.co, ar.take<int32_t>(coalesce_scratch_ints(A.user.id.rows)), A.user.id.rows);
     coalesce_bind_scratch(ws.item.co, ar.take<int32_t>(coalesce_scratch_ints(A.item.id.rows)), A.item.id.rows);
-    if (cal_enabled(A) && !sharded(A)) {
+    if (cal_enabled(A)) {
         const int64_t ncat = std::min<int64_t>(A.num_categories, 65535);
         coalesce_bind_scratch(ws.cal.co, ar.take<int32_t>(coalesce_scratch_ints(ncat)), ncat);
     }
@@ -365,13 +365,16 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         ws.ib_du = ar.take<float>((size_t)B * D);
         if (!shard) ws.ib_dp = ar.take<float>((size_t)B * D);
     }
-    if (cal_enabled(A) && !shard) {
+    if (cal_enabled(A)) {
+        // one process: the batch's item rows; sharded: this requester's rows, with the per-category
+        // sums and scatters in the caller's all-reduce buffers (slot space = category ids)
         CalArgs& c = ws.cal;
         ws.cal_on = true;
         const int64_t R = B * (1 + N);
         c.R = R;
         c.D = D;
         c.nseg_max = (int)std::min<int64_t>(R, std::max<int64_t>(1, std::min<int64_t>(A.num_categories, 65535)));
+        const int64_t slots = shard ? A.num_categories : c.nseg_max;
         const int pieces = cal_max_pieces(R, c.nseg_max);
         c.catrow = ar.take<int64_t>(R);
         plan_coalesce(ar, c.co, R);
@@ -381,9 +384,14 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         c.psum = ar.take<float>((size_t)pieces * D);
         c.mean = ar.take<float>((size_t)c.nseg_max * D);
         c.pslab = ar.take<float>((size_t)pieces * D * D);
-        c.cov = ar.take<float>((size_t)c.nseg_max * D * D);
-        c.part = ar.take<float>(c.nseg_max);
-        c.flag = ar.take<int32_t>(c.nseg_max);
+        if (shard) {
+            c.gstats = A.cal_stats;
+            c.cov = A.cal_scatter;
+        } else {
+            c.cov = ar.take<float>((size_t)c.nseg_max * D * D);
+        }
+        c.part = ar.take<float>(slots);
+        c.flag = ar.take<int32_t>(slots);
         c.gmajor = ar.take<float>((size_t)D * D);
         c.out = ar.take<float>(2);
     }
@@ -1305,6 +1313,32 @@ int deferred_of(const ttamm_step_args& A, Deferred& df) {
     return TTAMM_OK;
 }
 
+// the category-alignment rows of this step: one process, the item tower's augmented rows
+// [positives; negatives]; sharded requester, its requests' (t | a) exchange rows and global ids
+CalArgs& bind_cal(const ttamm_step_args& A, StepWs& ws, const TowerWs& I, int64_t B, int D, bool mimic) {
+    CalArgs& c = ws.cal;
+    if (sharded(A)) {
+        c.x = A.item_fwd_in;
+        c.xa = mimic ? A.item_fwd_in + D : nullptr;
+        c.ld_x = 2 * D;
+        c.slot = A.item_slot;
+        c.idx = A.b.pos_items;
+        c.idx1 = A.b.neg_items;
+        c.split = B;
+        c.idx_rows = A.num_items_global > 0 ? A.num_items_global : A.item.id.rows;
+    } else {
+        c.x = I.aug;
+        c.ld_x = D;
+        c.idx = I.idx;
+        c.idx_rows = A.item.id.rows;
+    }
+    c.categories = A.item_categories;
+    c.num_categories = A.num_categories;
+    c.major = A.major_category;
+    c.lambda = (float)A.hp.lambda_category_alignment;
+    return c;
+}
+
 int validate_step(const ttamm_step_args& A) {
     const int D = A.user.id.dim;
     int rc;
@@ -1315,7 +1349,12 @@ int validate_step(const ttamm_step_args& A) {
     TTAMM_REQUIRE(A.user.matmul_bf16 == A.item.matmul_bf16, "user and item towers must share one matmul precision");
     TTAMM_REQUIRE(A.b.batch > 0, "empty batch");
     if (cal_enabled(A)) {
-        TTAMM_REQUIRE(!sharded(A), "the category-alignment loss is not implemented in the row-sharded step");
+        TTAMM_REQUIRE(!sharded(A) || (A.cal_stats && A.cal_scatter),
+                      "the row-sharded category-alignment loss needs cal_stats and cal_scatter");
+        TTAMM_REQUIRE(!sharded(A) || !(A.phase & (TTAMM_PHASE_CAL_STATS | TTAMM_PHASE_CAL_SCATTER |
+                                                  TTAMM_PHASE_SCORE | TTAMM_PHASE_USER)) ||
+                          (A.item_fwd_in && (A.b.num_neg == 0 || A.b.neg_items)),
+                      "the row-sharded category-alignment loss needs item_fwd_in and b.neg_items");
         TTAMM_REQUIRE(A.num_categories > 0 && A.num_categories <= 65535,
                       "category alignment: num_categories must be in [1, 65535]");
         TTAMM_REQUIRE(A.major_category >= 0 && A.major_category < A.num_categories,
@@ -1353,7 +1392,7 @@ int validate_step(const ttamm_step_args& A) {
                   "row_base / global_batch out of range");
     if (!sharded(A)) return TTAMM_OK;
     const int ph = A.phase;
-    TTAMM_REQUIRE((ph & ~2047) == 0, "unknown phase bits");
+    TTAMM_REQUIRE((ph & ~8191) == 0, "unknown phase bits");
     TTAMM_REQUIRE(!((ph & TTAMM_PHASE_USER) && (ph & (TTAMM_PHASE_SCORE | TTAMM_PHASE_TOWERS_BWD))),
                   "USER and SCORE / TOWERS_BWD are alternatives");
     TTAMM_REQUIRE(A.in_batch || (ph & (TTAMM_PHASE_INBATCH_SRC | TTAMM_PHASE_INBATCH)) == 0,
@@ -1540,6 +1579,11 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         if ((rc = launch_inbatch(a, s))) return rc;
         if (ev[0] && ev[1]) TTAMM_HIP(hipEventRecord((hipEvent_t)ev[1], s));
     }
+    // ---- sharded category alignment: global per-category sums, then centered scatters ---------
+    if (shard && ws.cal_on && (ph & TTAMM_PHASE_CAL_STATS))
+        if ((rc = launch_cal_local(bind_cal(A, ws, I, B, D, mimic), s))) return rc;
+    if (shard && ws.cal_on && (ph & TTAMM_PHASE_CAL_SCATTER))
+        if ((rc = launch_cal_scatter(bind_cal(A, ws, I, B, D, mimic), s))) return rc;
     // ---- score + loss (fwd + bwd seeds), user-side backward ---------------------------------
     if (ph & (TTAMM_PHASE_USER | TTAMM_PHASE_SCORE)) {
         ScoreArgs sa;
@@ -1587,24 +1631,25 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         }
         if ((rc = launch_score_loss(sa, s))) return rc;
         if (ws.cal_on) {  // + lambda * L_cal over cat[positives; negatives] (training.py:805-820)
-            CalArgs& c = ws.cal;
-            c.x = I.aug;
-            c.ld_x = D;
-            c.idx = I.idx;
-            c.categories = A.item_categories;
-            c.num_categories = A.num_categories;
-            c.major = A.major_category;
-            c.lambda = (float)A.hp.lambda_category_alignment;
-            c.dT = I.dT_own;
-            c.dA = mimic ? I.dA_own : nullptr;
-            c.ld_d = D;
-            c.dA_rows = B;
-            if ((rc = launch_category_alignment(c, s))) return rc;
+            CalArgs& c = bind_cal(A, ws, I, B, D, mimic);
+            if (shard) {
+                c.dT = A.item_bwd_out;
+                c.dA = mimic ? A.item_bwd_out + D : nullptr;
+                c.ld_d = 2 * D;
+                c.dA_rows = c.R;  // every request ships its own dA
+                if ((rc = launch_cal_finish(c, s))) return rc;
+            } else {
+                c.dT = I.dT_own;
+                c.dA = mimic ? I.dA_own : nullptr;
+                c.ld_d = D;
+                c.dA_rows = B;
+                if ((rc = launch_category_alignment(c, s))) return rc;
+            }
         }
         if (A.loss_out) {
             if ((rc = launch_loss_finalize(ws.partials, ws.score_blocks, ws.ib_on ? ws.ib.loss_part : nullptr,
                                            ws.ib_on ? ws.ib_parts : 0, bce_count, B, Bg, D, sa.lambda_u, sa.lambda_i,
-                                           sa.mimic, ws.cal_on ? ws.cal.out : nullptr,
+                                           sa.mimic, ws.cal_on && A.row_base == 0 ? ws.cal.out : nullptr,
                                            (float)A.hp.lambda_category_alignment, A.loss_out, A.loss_accum, A.status,
                                            s)))
                 return rc;

@@ -166,10 +166,12 @@ class StepArgs(ctypes.Structure):
         ("inbatch_dp", c_vp),
         ("table_g0_math", c_i32),
         ("item_slot", c_vp),
+        ("cal_stats", c_vp),
+        ("cal_scatter", c_vp),
     ]
 
 
-ABI_VERSION = 19  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 20  # ttamm.h TTAMM_ABI_VERSION
 G0_EXACT = 0  # ttamm.h TTAMM_G0_EXACT
 G0_FAST = 1  # ttamm.h TTAMM_G0_FAST
 
@@ -186,6 +188,8 @@ PHASE_INBATCH = 128
 PHASE_SCORE = 256
 PHASE_TOWERS_BWD = 512
 PHASE_TABLES = 1024
+PHASE_CAL_STATS = 2048
+PHASE_CAL_SCATTER = 4096
 
 
 # Symbol table: name -> (restype, argtypes).  tests/ check every one is exported and that this
@@ -241,6 +245,11 @@ SIGNATURES = {
     "ttamm_sample_negatives": (
         ctypes.c_int,
         [c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp],
+    ),
+    "ttamm_coalesce_workspace_bytes": (ctypes.c_size_t, [c_i64, c_i64]),
+    "ttamm_coalesce_rows": (
+        ctypes.c_int,
+        [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_size_t, c_vp],
     ),
     "ttamm_sparse_adam_rows": (
         ctypes.c_int,

@@ -436,6 +436,13 @@ class ShardedTrainStep(FusedTrainStep):
             args.global_batch = W * self.max_batch
             self.ib_local = torch.empty((self.max_batch, D), dtype=torch.float32, device=self.device)
             self.ib_dp_all = torch.empty((W * self.max_batch, D), dtype=torch.float32, device=self.device)
+        self.cal = self.item_categories is not None
+        if self.cal:  # the global per-category sums / scatters (TTAMM_PHASE_CAL_*), all-reduced
+            ncat = int(args.num_categories)
+            self.cal_stats = torch.zeros(ncat * (D + 1), dtype=torch.float32, device=self.device)
+            self.cal_scatter = torch.zeros(ncat * D * D, dtype=torch.float32, device=self.device)
+            args.cal_stats = self.cal_stats.data_ptr()
+            args.cal_scatter = self.cal_scatter.data_ptr()
         self.fwd_in = torch.empty((R, 2 * D), dtype=torch.float32, device=self.device)
         self.bwd_out = torch.empty((R, 2 * D), dtype=torch.float32, device=self.device)
 
@@ -523,6 +530,14 @@ class ShardedTrainStep(FusedTrainStep):
             dp = yield ReduceScatter(self.ib_dp_all[: W * B])
             a.inbatch_dp = dp.data_ptr()
             ib = (gathered, dp)
+        if self.cal:
+            # ---- category alignment over the global batch: per-category sums, then scatters -------
+            self._phase(_lib.PHASE_CAL_STATS)
+            if W > 1:
+                yield AllReduce(self.cal_stats)
+            self._phase(_lib.PHASE_CAL_SCATTER)
+            if W > 1:
+                yield AllReduce(self.cal_scatter)
         # ---- scores; (dT | dA) to the owners; backward -------------------------------------------
         self._phase(_lib.PHASE_SCORE if self.group_towers else _lib.PHASE_USER)
         if W == 1:

@@ -271,7 +271,7 @@ class FusedTrainStep:
         if item_category_tensor is not None and major_category_id is not None and \
                 args.hp.lambda_category_alignment > 0:
             cats = item_category_tensor.to(self.device, torch.long).contiguous()
-            if cats.numel() != ie.num_embeddings:
+            if cats.numel() != self.num_items:  # sharded: the global tensor on every rank
                 raise ValueError("ttamm: item_category_tensor must hold one category per item")
             ncat = int(cats.max().item()) + 1 if cats.numel() else 0
             if int(cats.min().item()) < 0 or not 0 <= int(major_category_id) < ncat:
