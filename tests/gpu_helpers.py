@@ -14,7 +14,7 @@ def ttamm_model_from(prob: Problem, device="cuda"):
     torch.manual_seed(0)
     ue = ttamm.build_tower_encoder(cfg, num_embeddings=s.U, feature_dim=s.F, device=device)
     ie = ttamm.build_tower_encoder(cfg, num_embeddings=s.I, feature_dim=s.F, device=device)
-    mm = ttamm.AdaptiveMimicMechanism(num_users=s.U, num_items=s.I, embedding_dim=s.D).to(device) if s.mimic else None
+    mm = ttamm.AdaptiveMimicMechanism(num_users=s.U, num_items=s.I, embedding_dim=s.P).to(device) if s.mimic else None
     model = ttamm.TwoTowerModel(ue, ie, similarity=ttamm.DotProductSimilarity(), adaptive_mimic=mm)
     missing = model.load_state_dict({k: v.to(device) for k, v in prob.model.state_dict().items()}, strict=True)
     assert not missing.missing_keys and not missing.unexpected_keys

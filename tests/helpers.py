@@ -32,6 +32,16 @@ class Shape:
     max_norm: float | None = None  # nn.Embedding max_norm of both ID tables (dense only, encoders.py:48-52)
     activation: str = "relu"  # feature-MLP activation (encoders.py:68-78)
     feature_type: str = "mlp"  # feature encoder type (encoders.py:114-144): mlp / linear / identity (F == D)
+    feature_out: int | None = None  # feature encoder output_dim (None: D)
+    concat_out: int | None = -1  # concat output_dim: -1 = D, None = the reference default D + feature_out
+
+    @property
+    def P(self) -> int:
+        """The tower output width (encoders.py:211-219): the mimic tables and scores are this wide."""
+        if self.fusion != "concat":
+            return self.D
+        fo = self.feature_out or self.D
+        return self.D + fo if self.concat_out is None else (self.D if self.concat_out == -1 else self.concat_out)
 
     def tower_cfg(self) -> dict:
         params = {"embedding_dim": self.D, "sparse": self.sparse}
@@ -44,9 +54,11 @@ class Shape:
             "matmul_dtype": self.matmul_dtype,
             "id_embedding": {"params": params, "init": {"type": "normal", "std": 0.02}},
             "feature_encoder": {"type": self.feature_type, "hidden_dims": list(self.hidden_dims),
-                                "activation": self.activation, "output_dim": self.D, "dropout": self.dropout},
+                                "activation": self.activation, "output_dim": self.feature_out or self.D,
+                                "dropout": self.dropout},
             "fusion": self.fusion,
-            "output_dim": self.D,  # the concat projection's width (encoders.py:211)
+            # the concat projection's width (encoders.py:211-212; None = embedding + feature width)
+            "output_dim": self.D if self.concat_out == -1 else self.concat_out,
             "adaptive_mimic": {"hidden_dim": self.gate_hidden} if self.gate_hidden else {},
         }
 

@@ -65,7 +65,7 @@ def _ttamm_model(prob, shape):
     cfg = shape.tower_cfg()
     ue = ttamm.build_tower_encoder(cfg, num_embeddings=shape.U, feature_dim=shape.F, device="cuda")
     ie = ttamm.build_tower_encoder(cfg, num_embeddings=shape.I, feature_dim=shape.F, device="cuda")
-    mm = ttamm.AdaptiveMimicMechanism(num_users=shape.U, num_items=shape.I, embedding_dim=shape.D).cuda() \
+    mm = ttamm.AdaptiveMimicMechanism(num_users=shape.U, num_items=shape.I, embedding_dim=shape.P).cuda() \
         if shape.mimic else None
     model = ttamm.TwoTowerModel(ue, ie, similarity=ttamm.DotProductSimilarity(), adaptive_mimic=mm)
     model.load_state_dict({k: v.cuda() for k, v in prob.model.state_dict().items()}, strict=True)
@@ -98,12 +98,13 @@ SHAPES = [
     Shape(dropout=0.0, sparse=False),
     Shape(dropout=0.0, fusion="sum"),
     Shape(dropout=0.0, fusion="concat"),
+    Shape(dropout=0.0, fusion="concat", feature_out=12, concat_out=20),
     Shape(dropout=0.0, activation="gelu", hidden_dims=(16, 12)),
     Shape(dropout=0.0, mimic=False),
     Shape(dropout=0.0, padding_idx=5),
     Shape(U=64, I=512, F=605, H=192, D=96, B=96, N=5, hidden_dims=(192,), dropout=0.0),
 ]
-IDS = ["gated", "dense-id", "sum", "concat", "gelu-2hidden", "nomimic", "padding", "c2-dims"]
+IDS = ["gated", "dense-id", "sum", "concat", "concat-out20", "gelu-2hidden", "nomimic", "padding", "c2-dims"]
 
 
 @pytest.mark.parametrize("shape", SHAPES, ids=IDS)

@@ -28,7 +28,7 @@ SEED = 4242
 def _model(cfg, shape: Shape, U: int, I: int, state: dict):
     ue = ttamm.build_tower_encoder(cfg, num_embeddings=U, feature_dim=shape.F, device="cuda")
     ie = ttamm.build_tower_encoder(cfg, num_embeddings=I, feature_dim=shape.F, device="cuda")
-    mm = ttamm.AdaptiveMimicMechanism(num_users=U, num_items=I, embedding_dim=shape.D).cuda()
+    mm = ttamm.AdaptiveMimicMechanism(num_users=U, num_items=I, embedding_dim=shape.P).cuda()
     m = ttamm.TwoTowerModel(ue, ie, similarity=ttamm.DotProductSimilarity(), adaptive_mimic=mm)
     m.load_state_dict({k: v.cuda() for k, v in state.items()}, strict=True)
     return m
@@ -127,9 +127,10 @@ CASES = [
     (2, Shape(), None, True),
     (3, Shape(N=3), None, True),
     (3, Shape(sparse=False, max_norm=0.05, padding_idx=6), 0.05, True),
+    (2, Shape(fusion="concat", feature_out=12, concat_out=20), None, True),
 ]
 IDS = ["padding-w2", "dense-padding-w3", "max-norm-w2", "max-norm-w3", "clip-w2", "noclip-w3", "all-w2",
-       "cal-w2", "cal-w3", "cal-all-w3"]
+       "cal-w2", "cal-w3", "cal-all-w3", "concat-out20-cal-w2"]
 
 
 @pytest.mark.parametrize("W,shape,clip,cal", CASES, ids=IDS)

@@ -32,6 +32,11 @@ def _grads_by_name(model, opts):
         Shape(fusion="sum"),
         Shape(fusion="concat"),
         Shape(U=50, I=300, F=37, H=24, D=12, B=40, N=3, hidden_dims=(24, 16), fusion="concat"),
+        # concat with the reference's default output_dim (embedding + feature width, encoders.py:212),
+        # and with a feature width and output_dim of their own (the mimic tables output-wide)
+        Shape(fusion="concat", concat_out=None),
+        Shape(U=50, I=300, F=37, H=24, D=12, B=40, N=3, hidden_dims=(24,), fusion="concat", feature_out=20, concat_out=28),
+        Shape(fusion="concat", feature_out=12, concat_out=20, sparse=False, mimic=False),
         # the reference's other activations (encoders.py:68-78), with dropout (injected keep masks)
         Shape(activation="gelu"),
         Shape(activation="tanh"),
@@ -46,7 +51,7 @@ def _grads_by_name(model, opts):
         Shape(feature_type="linear"),
     ],
     ids=["tiny", "nodrop", "odd", "2hidden", "nomimic", "dense-id", "padding", "dense-id-padding", "sum", "concat",
-         "concat-odd", "gelu", "tanh", "selu", "gelu-2hidden-sum", "5hidden", "5hidden-tanh", "identity-enc",
+         "concat-odd", "concat-default-out", "concat-out28", "concat-out20-dense-nomimic", "gelu", "tanh", "selu", "gelu-2hidden-sum", "5hidden", "5hidden-tanh", "identity-enc",
          "identity-enc-sum", "linear-enc"],
 )
 def test_step_gradients_match_oracle(shape):

@@ -389,12 +389,13 @@ __global__ __launch_bounds__(64 * kRowWaves) void piece_sum_kernel(RowUpdateArgs
     __builtin_amdgcn_wave_barrier();
     const int D = A.dim;
     const bool mimic = A.mimic.weight != nullptr;
+    const bool idt = A.id.weight != nullptr;  // (a mimic-only pass leaves the ID table out)
     for (int d = lane; d < D; d += 64) {
         float ve[kPiece], va[kPiece];
 #pragma unroll
         for (int p = 0; p < kPiece; ++p) {  // issue every load of the chunk before adding
             const int64_t r = srows[w][p];
-            ve[p] = p < cnt ? A.dE[r * A.ld_dE + d] : 0.f;
+            ve[p] = (idt && p < cnt) ? A.dE[r * A.ld_dE + d] : 0.f;
             va[p] = (mimic && p < cnt) ? dA_row(A, r)[d] : 0.f;
         }
         float ge = 0.f, ga = 0.f;
@@ -405,7 +406,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void piece_sum_kernel(RowUpdateArgs
                 ge += ve[p];
                 ga += va[p];
                 if ((last_mask >> p) & 1ull) {
-                    A.piece_e[(k0 + start) * D + d] = ge;
+                    if (idt) A.piece_e[(k0 + start) * D + d] = ge;
                     if (mimic) A.piece_a[(k0 + start) * D + d] = ga;
                     ge = ga = 0.f;
                     start = p + 1;
@@ -433,6 +434,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArg
     const int64_t key = A.keys[k0];
     const int D = A.dim;
     const bool mimic = A.mimic.weight != nullptr;
+    const bool idt = A.id.weight != nullptr;  // (a mimic-only pass leaves the ID table out)
     const bool direct = k1 - k0 <= kPiece;
     auto each = [](float4& p, float4& m, float4& v, float4 g, auto&& f) {
         f(p.x, m.x, v.x, g.x);
@@ -443,28 +445,33 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArg
     for (int d = 4 * sub; d < D; d += 4 * lpr) {
         // the table rows first: they do not depend on the gradient sums below
         const int64_t o = key * D + d;
-        float4 ip = ldf4(A.id.weight + o), im = ldf4(A.id.exp_avg + o), iv = ldf4(A.id.exp_avg_sq + o);
+        float4 ip = make_float4(0.f, 0.f, 0.f, 0.f), im = ip, iv = ip;
+        if (idt) {
+            ip = ldf4(A.id.weight + o);
+            im = ldf4(A.id.exp_avg + o);
+            iv = ldf4(A.id.exp_avg_sq + o);
+        }
         float4 mp = make_float4(0.f, 0.f, 0.f, 0.f), mm = mp, mv = mp;
         if (mimic) {
             mp = ldf4(A.mimic.weight + o);
             mm = ldf4(A.mimic.exp_avg + o);
             mv = ldf4(A.mimic.exp_avg_sq + o);
         }
-        float4 ge, ga = make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 ge = make_float4(0.f, 0.f, 0.f, 0.f), ga = ge;
         if (direct) {  // the row's contributions in batch order
             const int64_t r0 = A.rows[k0];
-            ge = ldf4(A.dE + r0 * A.ld_dE + d);
+            if (idt) ge = ldf4(A.dE + r0 * A.ld_dE + d);
             if (mimic) ga = ldf4(dA_row(A, r0) + d);
             for (int64_t k = k0 + 1; k < k1; ++k) {
                 const int64_t r = A.rows[k];
-                ge = addf4(ge, ldf4(A.dE + r * A.ld_dE + d));
+                if (idt) ge = addf4(ge, ldf4(A.dE + r * A.ld_dE + d));
                 if (mimic) ga = addf4(ga, ldf4(dA_row(A, r) + d));
             }
         } else {  // pieces (piece_sum_kernel), then the pieces in order
-            ge = ldf4(A.piece_e + k0 * D + d);
+            if (idt) ge = ldf4(A.piece_e + k0 * D + d);
             if (mimic) ga = ldf4(A.piece_a + k0 * D + d);
             for (int64_t k = (k0 / kPiece + 1) * kPiece; k < k1; k += kPiece) {
-                ge = addf4(ge, ldf4(A.piece_e + k * D + d));
+                if (idt) ge = addf4(ge, ldf4(A.piece_e + k * D + d));
                 if (mimic) ga = addf4(ga, ldf4(A.piece_a + k * D + d));
             }
         }
@@ -477,13 +484,15 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArg
         // gradient at all, so the row is left as it is; AdamW: a zero gradient row)
         const bool pad = A.id.has_padding_idx && key == A.id.padding_idx;
         if (pad) ge = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM) {
+        if (!idt) {
+            // mimic-only pass
+        } else if (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM) {
             if (!pad)
                 each(ip, im, iv, ge, [&](float& p, float& m, float& v, float g) { sparse_adam_elem(p, m, v, g, A.sp); });
         } else {
             each(ip, im, iv, ge, [&](float& p, float& m, float& v, float g) { adam_elem(p, m, v, g, A.ad); });
         }
-        if (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM && pad) {
+        if (!idt || (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM && pad)) {
             // untouched
         } else if (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM || A.id.last_step) {
             // SparseAdam, or deferred mode: the row was caught up before the forward
@@ -511,7 +520,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArg
         }
     }
     if (sub == 0) {
-        if (A.id.optimizer != TTAMM_OPT_SPARSE_ADAM && A.id.last_step) A.id.last_step[key] = A.dense_step;
+        if (idt && A.id.optimizer != TTAMM_OPT_SPARSE_ADAM && A.id.last_step) A.id.last_step[key] = A.dense_step;
         if (mimic && A.mimic.last_step) A.mimic.last_step[key] = A.dense_step;
     }
 }
@@ -1036,7 +1045,7 @@ int launch_block_exclusive_scan(const int32_t* in, int32_t* out, int64_t n, hipS
 int launch_row_update(const RowUpdateArgs& args, hipStream_t s) {
     if (args.n <= 0) return TTAMM_OK;
     RowUpdateArgs a = args;
-    TTAMM_REQUIRE(a.dim % 4 == 0 && a.ld_dE % 4 == 0 && (!a.mimic.weight || a.ld_dA % 4 == 0),
+    TTAMM_REQUIRE(a.dim % 4 == 0 && (!a.id.weight || a.ld_dE % 4 == 0) && (!a.mimic.weight || a.ld_dA % 4 == 0),
                   "row update: dim and gradient leading dims must be multiples of 4");
     a.lanes_per_row = 1;
     while (a.lanes_per_row < a.dim / 4 && a.lanes_per_row < 64) a.lanes_per_row *= 2;

@@ -12,8 +12,11 @@
 // tile.  A lane appends (score, id) to its query's candidate buffer only when the score reaches
 // the query's running threshold (the k-th best so far) and the item is not blocked; a wave
 // compacts a query's buffer (bitonic sort in registers, keep k) before it could overflow.
+// D <= 128 runs the same scheme on split-bf16 MFMA (retrieval_x_kernel: fp32-level scores at
+// 2.6x the fp32 MFMA rate; TTAMM_RETRIEVAL_FP32=1 keeps the fp32 kernel for comparison).
 // Pass 2 (retrieval_merge_kernel): one wave per query merges the partitions' top-k lists.
 #include <cfloat>
+#include <cstdlib>
 #include <cstring>
 
 #include "kernels.h"
@@ -209,7 +212,14 @@ __global__ __launch_bounds__(256) void retrieval_partial_kernel(RetrievalArgs A)
                                                                   q == 0 ? b4.x : q == 1 ? b4.y : q == 2 ? b4.z : b4.w,
                                                                   acc[m], 0, 0, 0);
         }
-        if (qvalid) {
+        // most tiles hold no score at or above the lane's threshold once it has warmed up: one max
+        // over the lane's scores skips the per-score filter
+        float mx = -INFINITY;
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, acc[m][r]);
+        if (qvalid && mx >= my_tau) {
 #pragma unroll
             for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -230,6 +240,175 @@ __global__ __launch_bounds__(256) void retrieval_partial_kernel(RetrievalArgs A)
     }
     __syncthreads();
     for (int q = w; q < kRQ; q += 4) {
+        const int64_t g = q0 + q;
+        if (g >= A.nq) continue;
+        float* os = A.part_s + (g * A.parts + blockIdx.y) * A.k;
+        int* oi = A.part_i + (g * A.parts + blockIdx.y) * A.k;
+        compact_query(bs, bi, cnt, tau, q, A.k, os, oi, A.k);
+    }
+}
+
+// Split-bf16 variant (D <= 128): every fp32 score as six v_mfma_f32_32x32x16_bf16 products of
+// (hi, mid, lo) bf16 planes (x = hi + mid + lo exactly to ~24 bits; the small terms accumulated
+// first, as the tower GEMMs of gemm.hip) — fp32-level accuracy, and exact whenever the operands
+// are small integers (the hi plane holds them, the other planes are 0).  A block of 8 waves owns
+// 256 queries, each wave 32 of them, their planes held in registers as MFMA B fragments for the
+// whole padded K; the partition's items stream through double-buffered LDS planes in 64-item
+// tiles (fp32 loads of the next tile in flight, split in registers, then written).  Query tiles
+// 4x the fp32 kernel's cut the item re-reads (one pass over the partition per 256 queries).
+constexpr int kXQ = 256;    // queries per block
+constexpr int kXThreads = 512;
+
+typedef __bf16 bf16x8r __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4r __attribute__((ext_vector_type(4)));
+typedef float f32x4r __attribute__((ext_vector_type(4)));
+
+// x -> (hi, mid, lo) bf16 quadruples (gemm.hip split_bf16<3>)
+__device__ __forceinline__ void split3(float4 v, uint2 (&out)[3]) {
+    const f32x4r x = {v.x, v.y, v.z, v.w};
+    const bf16x4r hi = __builtin_convertvector(x, bf16x4r);
+    const f32x4r r = x - __builtin_convertvector(hi, f32x4r);
+    const bf16x4r mid = __builtin_convertvector(r, bf16x4r);
+    const f32x4r r2 = r - __builtin_convertvector(mid, f32x4r);
+    out[0] = __builtin_bit_cast(uint2, hi);
+    out[1] = __builtin_bit_cast(uint2, mid);
+    out[2] = __builtin_bit_cast(uint2, __builtin_convertvector(r2, bf16x4r));
+}
+
+// byte offset of k values [c, c + 4) (c < 16) of item row `row` in a 32-B-row plane: 16-B halves
+// swapped on rows with bit 3 set, so the 16 rows of a ds_read_b128 lane group hit distinct bank
+// quads (gemm.hip mn_off<32>)
+__device__ __forceinline__ int xoff(int row, int c) { return row * 32 + (((c >> 3) ^ ((row >> 3) & 1)) << 4) + (c & 4) * 2; }
+
+template <int KS, int IT>
+__global__ __launch_bounds__(kXThreads) void retrieval_x_kernel(RetrievalArgs A) {
+    constexpr int MT = IT / 32;           // 32-item MFMA tiles per wave
+    constexpr int PLANE = IT * 32;        // one k-step plane: IT rows x 16 bf16
+    constexpr int BUF = 3 * KS * PLANE;   // (hi, mid, lo) x k-steps
+    constexpr int C4 = 4 * KS;            // float4 chunks per padded row
+    constexpr int LOADS = (IT * C4 + kXThreads - 1) / kXThreads;
+    extern __shared__ __attribute__((aligned(16))) float lds_f[];  // 2 * BUF bytes
+    unsigned char* lds = reinterpret_cast<unsigned char*>(lds_f);
+    __shared__ int cnt[kXQ];
+    __shared__ float tau[kXQ];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5;
+    const int D = A.D;
+    const int64_t q0 = (int64_t)blockIdx.x * kXQ;
+    const int64_t i_begin = (int64_t)blockIdx.y * A.items_per_part;
+    const int64_t i_end = i_begin + A.items_per_part < A.ni ? i_begin + A.items_per_part : A.ni;
+    const int64_t blk = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+    float* bs = A.buf_s + blk * kXQ * kRCap;
+    int* bi = A.buf_i + blk * kXQ * kRCap;
+    if (tid < kXQ) {
+        cnt[tid] = 0;
+        tau[tid] = -INFINITY;
+    }
+    const int myq = w * 32 + (lane & 31);
+    const int64_t gq = q0 + myq;
+    const bool qvalid = gq < A.nq;
+    int64_t blo = 0, bhi = 0;
+    if (A.boff && qvalid) {
+        blo = A.boff[gq];
+        bhi = A.boff[gq + 1];
+    }
+    // this lane's B fragments: query myq, k = 16 ks + 8 h + [0, 8), zero past D
+    bf16x8r qf[3][KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+        uint2 lo3[3], hi3[3];
+        const int k0 = 16 * ks + 8 * h;
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+        if (qvalid && k0 < D) a = *reinterpret_cast<const float4*>(A.Q + gq * A.ldq + k0);
+        if (qvalid && k0 + 4 < D) b = *reinterpret_cast<const float4*>(A.Q + gq * A.ldq + k0 + 4);
+        split3(a, lo3);
+        split3(b, hi3);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) qf[p][ks] = __builtin_bit_cast(bf16x8r, make_uint4(lo3[p].x, lo3[p].y, hi3[p].x, hi3[p].y));
+    }
+    // item tile staging: chunk e -> (row e / C4, k 4 (e % C4)); zero past D and past the partition
+    float4 pf[LOADS];
+    auto load_tile = [&](int64_t t0) {
+#pragma unroll
+        for (int it = 0; it < LOADS; ++it) {
+            const int e = tid + it * kXThreads;
+            const int r = e / C4, c = (e - r * C4) * 4;
+            pf[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e < IT * C4 && c < D && t0 + r < i_end) pf[it] = *reinterpret_cast<const float4*>(A.X + (t0 + r) * A.ldx + c);
+        }
+    };
+    auto store_tile = [&](int buf) {
+        unsigned char* base = lds + buf * BUF;
+#pragma unroll
+        for (int it = 0; it < LOADS; ++it) {
+            const int e = tid + it * kXThreads;
+            if (e >= IT * C4) continue;
+            const int r = e / C4, c = (e - r * C4) * 4;
+            uint2 v[3];
+            split3(pf[it], v);
+            const int off = (c >> 4) * PLANE + xoff(r, c & 15);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(base + p * KS * PLANE + off) = v[p];
+        }
+    };
+    int buf = 0;
+    if (i_begin < i_end) {
+        load_tile(i_begin);
+        store_tile(0);
+    }
+    for (int64_t t0 = i_begin; t0 < i_end; t0 += IT) {
+        __syncthreads();  // tile t0 is in LDS buffer `buf`; thresholds and counts are current
+        if (t0 + IT < i_end) load_tile(t0 + IT);
+        const float my_tau = tau[myq];
+        const unsigned char* base = lds + buf * BUF;
+        f32x16 acc[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                bf16x8r af[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    af[p] = *reinterpret_cast<const bf16x8r*>(base + (p * KS + ks) * PLANE +
+                                                              xoff(32 * m + (lane & 31), 8 * h));
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], qf[1][ks], acc[m], 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], qf[0][ks], acc[m], 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], qf[2][ks], acc[m], 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], qf[0][ks], acc[m], 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], qf[1][ks], acc[m], 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], qf[0][ks], acc[m], 0, 0, 0);
+            }
+        }
+        float mx = -INFINITY;  // the per-score filter only when some score can pass
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, acc[m][r]);
+        if (qvalid && mx >= my_tau) {
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int64_t item = t0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const float sc = acc[m][r];
+                    if (item < i_end && sc >= my_tau && !(bhi > blo && is_blocked(A.bval, blo, bhi, item))) {
+                        const int slot = atomicAdd(&cnt[myq], 1);
+                        bs[myq * kRCap + slot] = sc;  // slot < kRCap: cnt <= kRCap - IT before the tile
+                        bi[myq * kRCap + slot] = (int)item;
+                    }
+                }
+        }
+        __syncthreads();  // all scores of the tile are in; the other buffer is free
+        for (int q = w; q < kXQ; q += kXThreads / 64)
+            if (cnt[q] > kRCap - IT) compact_query(bs, bi, cnt, tau, q, A.k, nullptr, nullptr, 0);
+        if (t0 + IT < i_end) store_tile(buf ^ 1);
+        buf ^= 1;
+    }
+    __syncthreads();
+    for (int q = w; q < kXQ; q += kXThreads / 64) {
         const int64_t g = q0 + q;
         if (g >= A.nq) continue;
         float* os = A.part_s + (g * A.parts + blockIdx.y) * A.k;
@@ -264,8 +443,8 @@ __global__ __launch_bounds__(64) void retrieval_merge_kernel(RetrievalArgs A, fl
     }
 }
 
-int pick_parts(int64_t nq, int64_t ni, int k) {
-    const int64_t qtiles = (nq + kRQ - 1) / kRQ;
+int pick_parts(int64_t nq, int64_t ni, int k, int qb = kRQ) {
+    const int64_t qtiles = (nq + qb - 1) / qb;
     int64_t parts = (2048 + qtiles - 1) / qtiles;  // aim for >= 2048 blocks (8 per CU)
     const int64_t by_items = (ni + 4 * kRI - 1) / (4 * kRI);  // >= 4 tiles per partition
     if (parts > by_items) parts = by_items;
@@ -377,12 +556,38 @@ int launch_normalize_rows(float* x, int64_t n, int dim, int64_t ld, hipStream_t 
     return TTAMM_OK;
 }
 
+template <int KS, int IT>
+int launch_x(const RetrievalArgs& A, dim3 grid, hipStream_t s) {
+    constexpr int lds = 2 * 3 * KS * IT * 32;
+    static bool attr_set = false;
+    if (!attr_set) {
+        TTAMM_HIP(hipFuncSetAttribute((const void*)retrieval_x_kernel<KS, IT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      lds));
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((retrieval_x_kernel<KS, IT>), grid, dim3(kXThreads), lds, s, A);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+template <int KS>
+int launch_x_ks(const RetrievalArgs& A, dim3 grid, bool wide, hipStream_t s) {
+    if constexpr (KS <= 6) {
+        if (wide) return launch_x<KS, 128>(A, grid, s);
+    }
+    return launch_x<KS, 64>(A, grid, s);
+}
+
+// the split-bf16 kernel's query block (dim <= 128), else the fp32 kernel's
+bool retrieval_split(int dim) { return dim <= 128 && std::getenv("TTAMM_RETRIEVAL_FP32") == nullptr; }
+int retrieval_qb(int dim) { return retrieval_split(dim) ? kXQ : kRQ; }
+
 size_t retrieval_workspace_bytes(int64_t nq, int64_t ni, int dim, int k) {
-    (void)dim;
     if (nq <= 0 || k <= 0) return 256;
-    const int parts = pick_parts(nq, ni, k);
-    const int64_t blocks = ((nq + kRQ - 1) / kRQ) * parts;
-    const size_t buf = (size_t)blocks * kRQ * kRCap * (sizeof(float) + sizeof(int));
+    const int qb = retrieval_qb(dim);
+    const int parts = pick_parts(nq, ni, k, qb);
+    const int64_t blocks = ((nq + qb - 1) / qb) * parts;
+    const size_t buf = (size_t)blocks * qb * kRCap * (sizeof(float) + sizeof(int));
     const size_t part = (size_t)nq * parts * k * (sizeof(float) + sizeof(int));
     return buf + part + 4 * 256;
 }
@@ -412,9 +617,10 @@ int launch_retrieval_topk(const float* Q, int64_t nq, int64_t ldq, const float* 
     A.boff = boff;
     A.bval = bval;
     A.k = k;
-    A.parts = pick_parts(nq, ni, k);
+    const int qb = retrieval_qb(dim);
+    A.parts = pick_parts(nq, ni, k, qb);
     A.items_per_part = ni > 0 ? ((ni + A.parts - 1) / A.parts + 127) / 128 * 128 : 0;
-    const int64_t qtiles = (nq + kRQ - 1) / kRQ;
+    const int64_t qtiles = (nq + qb - 1) / qb;
     const int64_t blocks = qtiles * A.parts;
     char* p = static_cast<char*>(ws);
     auto take = [&](size_t bytes) {
@@ -422,27 +628,46 @@ int launch_retrieval_topk(const float* Q, int64_t nq, int64_t ldq, const float* 
         p += (bytes + 255) / 256 * 256;
         return r;
     };
-    A.buf_s = reinterpret_cast<float*>(take((size_t)blocks * kRQ * kRCap * sizeof(float)));
-    A.buf_i = reinterpret_cast<int*>(take((size_t)blocks * kRQ * kRCap * sizeof(int)));
+    A.buf_s = reinterpret_cast<float*>(take((size_t)blocks * qb * kRCap * sizeof(float)));
+    A.buf_i = reinterpret_cast<int*>(take((size_t)blocks * qb * kRCap * sizeof(int)));
     A.part_s = reinterpret_cast<float*>(take((size_t)nq * A.parts * k * sizeof(float)));
     A.part_i = reinterpret_cast<int*>(take((size_t)nq * A.parts * k * sizeof(int)));
-    // 128-item tiles (twice the MFMA work per barrier) when the LDS and the buffer allow
-    const bool wide = dim <= 128 && k <= kRCap - 128;
-    const int IT = wide ? 128 : kRI;
-    const size_t lds = (size_t)(kRQ + IT) * (dim + 4) * sizeof(float);
-    auto kern = wide ? (const void*)retrieval_partial_kernel<128, 128> : (const void*)retrieval_partial_kernel<64, 256>;
-    static bool attr_set[2] = {false, false};
-    if (!attr_set[wide]) {
-        TTAMM_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024));
-        attr_set[wide] = true;
+    if (retrieval_split(dim)) {
+        const dim3 grid((unsigned)qtiles, (unsigned)A.parts);
+        // 128-item tiles (twice the MFMA work per barrier and per load latency) when the candidate
+        // buffer (k <= 128) and the LDS (two buffers of 3 x 128 x 16 KS bf16: KS <= 6) allow
+        const bool wide = k <= kRCap - 128;
+        int rc = TTAMM_OK;
+        switch ((dim + 15) / 16) {
+            case 1: rc = launch_x_ks<1>(A, grid, wide, s); break;
+            case 2: rc = launch_x_ks<2>(A, grid, wide, s); break;
+            case 3: rc = launch_x_ks<3>(A, grid, wide, s); break;
+            case 4: rc = launch_x_ks<4>(A, grid, wide, s); break;
+            case 5: rc = launch_x_ks<5>(A, grid, wide, s); break;
+            case 6: rc = launch_x_ks<6>(A, grid, wide, s); break;
+            case 7: rc = launch_x_ks<7>(A, grid, wide, s); break;
+            default: rc = launch_x_ks<8>(A, grid, wide, s); break;
+        }
+        if (rc) return rc;
+    } else {
+        // 128-item tiles (twice the MFMA work per barrier) when the LDS and the buffer allow
+        const bool wide = dim <= 128 && k <= kRCap - 128;
+        const int IT = wide ? 128 : kRI;
+        const size_t lds = (size_t)(kRQ + IT) * (dim + 4) * sizeof(float);
+        auto kern = wide ? (const void*)retrieval_partial_kernel<128, 128> : (const void*)retrieval_partial_kernel<64, 256>;
+        static bool attr_set[2] = {false, false};
+        if (!attr_set[wide]) {
+            TTAMM_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024));
+            attr_set[wide] = true;
+        }
+        if (wide)
+            hipLaunchKernelGGL((retrieval_partial_kernel<128, 128>), dim3((unsigned)qtiles, (unsigned)A.parts), dim3(256),
+                               lds, s, A);
+        else
+            hipLaunchKernelGGL((retrieval_partial_kernel<64, 256>), dim3((unsigned)qtiles, (unsigned)A.parts), dim3(256),
+                               lds, s, A);
+        TTAMM_LAUNCH_CHECK();
     }
-    if (wide)
-        hipLaunchKernelGGL((retrieval_partial_kernel<128, 128>), dim3((unsigned)qtiles, (unsigned)A.parts), dim3(256),
-                           lds, s, A);
-    else
-        hipLaunchKernelGGL((retrieval_partial_kernel<64, 256>), dim3((unsigned)qtiles, (unsigned)A.parts), dim3(256),
-                           lds, s, A);
-    TTAMM_LAUNCH_CHECK();
     hipLaunchKernelGGL(retrieval_merge_kernel, dim3((unsigned)nq), dim3(64), 0, s, A, out_s, out_i);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;

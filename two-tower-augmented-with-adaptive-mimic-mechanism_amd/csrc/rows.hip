@@ -178,6 +178,13 @@ __device__ __forceinline__ float item_aug_at(const ScoreArgs& A, int64_t r, int 
     return A.a_item ? t + A.a_item[r * A.ld_item + d] : t;
 }
 
+// NCH = ceil(D / 64) chunks per lane.  Every row the wave reads is requested before the first
+// reduction (the positive, the user's mimic terms, then the negatives in groups of kScoreNG):
+// one memory latency per group instead of one per row, and the NG dot-product reductions
+// interleave.  Sums keep the chunk order of the scalar loop (lane partials over c, then the
+// butterfly), so the results are those of the one-row-at-a-time form.
+constexpr int kScoreNG = 8;
+template <int NCH>
 __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs A) {
     __shared__ float red[kScoreWaves][3];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -190,19 +197,33 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
     float bce = 0.f, mse_u = 0.f, mse_i = 0.f;
     if (b < B) {
         const int64_t pb = A.item_slot ? A.item_slot[b] : b;  // the positive's item row
-        const int nch = (D + 63) / 64;
-        float u[kMaxDChunks], p[kMaxDChunks], du[kMaxDChunks];
-        float dot = 0.f;
+        bool ok[NCH];
+        float u[NCH], p[NCH], du[NCH], dpos[NCH];
+        float au[NCH], tp[NCH], ap[NCH], tu[NCH], ibp[NCH], ibu[NCH];
 #pragma unroll
-        for (int c = 0; c < kMaxDChunks; ++c) {
-            u[c] = p[c] = du[c] = 0.f;
+        for (int c = 0; c < NCH; ++c) {
             const int d = c * 64 + lane;
-            if (c < nch && d < D) {
+            ok[c] = d < D;
+            u[c] = p[c] = au[c] = tp[c] = ap[c] = tu[c] = ibp[c] = ibu[c] = 0.f;
+            if (ok[c]) {
                 u[c] = A.user_aug[b * D + d];
                 p[c] = item_aug_at(A, pb, d);
-                dot += u[c] * p[c];
+                if (A.mimic) {
+                    au[c] = A.a_user[b * D + d];
+                    tp[c] = A.t_item[pb * A.ld_item + d];
+                    ap[c] = A.a_item[pb * A.ld_item + d];
+                    tu[c] = A.t_user[b * D + d];
+                }
+                if (ib) {
+                    ibp[c] = A.ib_dp[b * A.ib_ld + d];
+                    ibu[c] = A.ib_du[b * D + d];
+                }
             }
         }
+        float dot = 0.f;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+            if (ok[c]) dot += u[c] * p[c];
         const float sp = wave_sum(dot);
         float dsp = 0.f;
         if (!ib) {
@@ -210,54 +231,65 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
             bce += bce_logit(sp, 1.0f);
         }
         // positive item row: dT_pos = ds+ * u ; user: ds+ * p   (in-batch: the S = U P^T terms)
-        float dpos[kMaxDChunks];
 #pragma unroll
-        for (int c = 0; c < kMaxDChunks; ++c) {
+        for (int c = 0; c < NCH; ++c) {
             const int d = c * 64 + lane;
             dpos[c] = 0.f;
-            if (c < nch && d < D) {
-                dpos[c] = ib ? A.ib_dp[b * A.ib_ld + d] : dsp * u[c];
+            du[c] = 0.f;
+            if (ok[c]) {
+                dpos[c] = ib ? ibp[c] : dsp * u[c];
                 A.dT_item[pb * ldi + d] = dpos[c];
-                du[c] = ib ? A.ib_du[b * D + d] : dsp * p[c];
+                du[c] = ib ? ibu[c] : dsp * p[c];
             }
         }
-        for (int j = 0; j < N; ++j) {
-            const int64_t nr = A.item_slot ? A.item_slot[B + b * N + j] : B + b * N + j;
-            float nv[kMaxDChunks];
-            float dn = 0.f;
+        for (int j0 = 0; j0 < N; j0 += kScoreNG) {
+            const int ng = N - j0 < kScoreNG ? N - j0 : kScoreNG;
+            int64_t nr[kScoreNG];
+            float nv[kScoreNG][NCH];
 #pragma unroll
-            for (int c = 0; c < kMaxDChunks; ++c) {
-                nv[c] = 0.f;
-                const int d = c * 64 + lane;
-                if (c < nch && d < D) {
-                    nv[c] = item_aug_at(A, nr, d);
-                    dn += u[c] * nv[c];
+            for (int jj = 0; jj < kScoreNG; ++jj) {
+                nr[jj] = 0;
+                if (jj < ng) {
+                    const int64_t q = B + b * N + j0 + jj;
+                    nr[jj] = A.item_slot ? A.item_slot[q] : q;
                 }
-            }
-            const float sn = wave_sum(dn);
-            const float dsn = (1.0f / (1.0f + expf(-sn)) - 0.0f) * inv_numel;
-            bce += bce_logit(sn, 0.0f);
 #pragma unroll
-            for (int c = 0; c < kMaxDChunks; ++c) {
-                const int d = c * 64 + lane;
-                if (c < nch && d < D) {
-                    const float g = dsn * u[c];
-                    A.dT_item[nr * ldi + d] = g;
-                    if (A.mimic && A.dA_all) A.dA_item[nr * ldi + d] = g;
-                    du[c] += dsn * nv[c];
+                for (int c = 0; c < NCH; ++c) nv[jj][c] = (jj < ng && ok[c]) ? item_aug_at(A, nr[jj], c * 64 + lane) : 0.f;
+            }
+            float sn[kScoreNG];
+#pragma unroll
+            for (int jj = 0; jj < kScoreNG; ++jj) {
+                float dn = 0.f;
+#pragma unroll
+                for (int c = 0; c < NCH; ++c)
+                    if (ok[c]) dn += u[c] * nv[jj][c];
+                sn[jj] = jj < ng ? wave_sum(dn) : 0.f;
+            }
+#pragma unroll
+            for (int jj = 0; jj < kScoreNG; ++jj) {
+                if (jj >= ng) continue;
+                const float dsn = (1.0f / (1.0f + expf(-sn[jj])) - 0.0f) * inv_numel;
+                bce += bce_logit(sn[jj], 0.0f);
+#pragma unroll
+                for (int c = 0; c < NCH; ++c) {
+                    const int d = c * 64 + lane;
+                    if (ok[c]) {
+                        const float g = dsn * u[c];
+                        A.dT_item[nr[jj] * ldi + d] = g;
+                        if (A.mimic && A.dA_all) A.dA_item[nr[jj] * ldi + d] = g;
+                        du[c] += dsn * nv[jj][c];
+                    }
                 }
             }
         }
         const float norm = 2.0f / (float)(A.Bg * D);
 #pragma unroll
-        for (int c = 0; c < kMaxDChunks; ++c) {
+        for (int c = 0; c < NCH; ++c) {
             const int d = c * 64 + lane;
-            if (c < nch && d < D) {
+            if (ok[c]) {
                 A.dT_user[b * D + d] = du[c];
                 if (A.mimic) {
-                    const float au = A.a_user[b * D + d], tp = A.t_item[pb * A.ld_item + d];
-                    const float ap = A.a_item[pb * A.ld_item + d], tu = A.t_user[b * D + d];
-                    const float xu = au - tp, xi = ap - tu;
+                    const float xu = au[c] - tp[c], xi = ap[c] - tu[c];
                     mse_u += xu * xu;
                     mse_i += xi * xi;
                     A.dA_user[b * D + d] = du[c] + norm * xu * A.lambda_u;
@@ -461,7 +493,15 @@ int launch_score_loss(const ScoreArgs& a, hipStream_t s) {
     TTAMM_REQUIRE(a.D <= 64 * kMaxDChunks, "score: embedding dim too large (max 512)");
     TTAMM_REQUIRE(a.N >= (a.ib_du ? 0 : 1) && a.N <= kMaxNeg, "score: negatives_per_positive out of range");
     if (a.B <= 0) return TTAMM_OK;
-    hipLaunchKernelGGL(score_loss_kernel, dim3(a.blocks), dim3(64 * kScoreWaves), 0, s, a);
+    const dim3 g(a.blocks), t(64 * kScoreWaves);
+    switch ((a.D + 63) / 64) {
+        case 1: hipLaunchKernelGGL(score_loss_kernel<1>, g, t, 0, s, a); break;
+        case 2: hipLaunchKernelGGL(score_loss_kernel<2>, g, t, 0, s, a); break;
+        case 3: hipLaunchKernelGGL(score_loss_kernel<3>, g, t, 0, s, a); break;
+        case 4: hipLaunchKernelGGL(score_loss_kernel<4>, g, t, 0, s, a); break;
+        case 5: case 6: hipLaunchKernelGGL(score_loss_kernel<6>, g, t, 0, s, a); break;
+        default: hipLaunchKernelGGL(score_loss_kernel<8>, g, t, 0, s, a); break;
+    }
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

@@ -123,6 +123,13 @@ bool uses_ef(const ttamm_tower& T) { return T.fusion == TTAMM_FUSION_GATED || T.
 int fusion_linears(const ttamm_tower& T) {
     return T.fusion == TTAMM_FUSION_GATED ? 2 : T.fusion == TTAMM_FUSION_CONCAT ? 1 : 0;
 }
+// widths of a tower: the ID rows (Did), the feature encoder's output (Fo), the [e | f] rows of
+// gated / concat fusion (Did + Fo) and the tower output (concat: the projection's output_dim,
+// encoders.py:211-217; otherwise Did).  Everything downstream of the tower (scores, mimic
+// tables, the exchange rows) is output-wide; only concat lets the output differ from Did.
+int fo_dim(const ttamm_tower& T) { return T.n_linear ? T.linear[T.n_linear - 1].out_features : T.feat_dim; }
+int efw(const ttamm_tower& T) { return T.id.dim + fo_dim(T); }
+int out_dim(const ttamm_tower& T) { return T.fusion == TTAMM_FUSION_CONCAT ? T.gate[0].out_features : T.id.dim; }
 bool needs_wpad(const ttamm_tower& T) {
     return T.fusion != TTAMM_FUSION_IDENTITY && T.n_linear > 0 && T.linear[0].in_features % 4 != 0;
 }
@@ -132,8 +139,8 @@ int validate_tower(const ttamm_tower& T, const char* name, int D, bool training)
     std::string n(name);
     TTAMM_REQUIRE(T.id.weight, n + ": embedding table missing");
     if (training) TTAMM_REQUIRE(T.id.exp_avg && T.id.exp_avg_sq, n + ": embedding optimizer state missing");
-    TTAMM_REQUIRE(T.id.dim == D, n + ": embedding dim mismatch");
-    TTAMM_REQUIRE(D % 4 == 0, n + ": ttamm requires embedding_dim % 4 == 0");
+    TTAMM_REQUIRE(T.fusion == TTAMM_FUSION_CONCAT || T.id.dim == D, n + ": embedding dim mismatch");
+    TTAMM_REQUIRE(D % 4 == 0 && T.id.dim % 4 == 0, n + ": ttamm requires embedding_dim % 4 == 0");
     TTAMM_REQUIRE(T.id.rows > 0, n + ": empty embedding table");
     TTAMM_REQUIRE(T.id.rows < (int64_t(1) << 31), n + ": tables of 2^31 rows or more are not supported (int32 row keys)");
     TTAMM_REQUIRE(T.n_linear >= 0 && T.n_linear <= TTAMM_MAX_LINEAR, n + ": too many feature-encoder layers");
@@ -157,10 +164,12 @@ int validate_tower(const ttamm_tower& T, const char* name, int D, bool training)
             TTAMM_REQUIRE(L.in_features == tower_in_dim(T, l), n + ": feature-encoder layer shapes do not chain");
             TTAMM_REQUIRE(L.out_features % 4 == 0, n + ": ttamm requires feature-encoder widths % 4 == 0");
         }
-        const int fo = T.n_linear ? T.linear[T.n_linear - 1].out_features : T.feat_dim;
-        TTAMM_REQUIRE(fo == D,
-                      n + ": Feature encoder output dimension must equal embedding dimension for 'sum', 'gated' or "
-                          "'concat' fusion.");
+        const int fo = fo_dim(T);
+        if (T.fusion == TTAMM_FUSION_CONCAT)
+            TTAMM_REQUIRE(fo % 4 == 0, n + ": ttamm requires the feature encoder's output width % 4 == 0");
+        else
+            TTAMM_REQUIRE(fo == D, n + ": Feature encoder output dimension must match id embedding dimension for "
+                                       "'sum' or 'gated' fusion.");
         TTAMM_REQUIRE(T.dropout >= 0.f && T.dropout < 1.f, n + ": dropout must be in [0, 1)");
     }
     if (T.fusion == TTAMM_FUSION_GATED) {
@@ -180,8 +189,8 @@ int validate_tower(const ttamm_tower& T, const char* name, int D, bool training)
         if (training)
             TTAMM_REQUIRE(P.weight_exp_avg && P.weight_exp_avg_sq && P.bias_exp_avg && P.bias_exp_avg_sq,
                           n + ": concat projection optimizer state missing");
-        TTAMM_REQUIRE(P.in_features == 2 * D && P.out_features == D,
-                      n + ": concat projection must map [e | f] (2 x embedding dim) to the embedding dim");
+        TTAMM_REQUIRE(P.in_features == efw(T) && P.out_features == D,
+                      n + ": concat projection must map [e | f] (embedding dim + feature output) to the output dim");
     }
     return TTAMM_OK;
 }
@@ -258,7 +267,7 @@ void plan_coalesce(Arena& ar, CoalesceWs& co, int64_t R) {
 int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
     const int64_t B = A.b.batch;
     const int N = A.b.num_neg;
-    const int D = A.user.id.dim;
+    const int D = out_dim(A.user);
     const bool mimic = A.mimic_enabled != 0;
     const bool shard = sharded(A);
     plan_scratch(ar, A, ws);
@@ -284,8 +293,8 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         }
         const int Hg = T.fusion == TTAMM_FUSION_GATED ? T.gate[0].out_features : 0;
         if (uses_ef(T)) {
-            w.ef = ar.take<float>((size_t)R * 2 * D);
-            w.dEF = ar.take<float>((size_t)R * 2 * D);
+            w.ef = ar.take<float>((size_t)R * efw(T));
+            w.dEF = ar.take<float>((size_t)R * efw(T));
         }
         if (T.fusion == TTAMM_FUSION_GATED) {
             w.z = ar.take<float>((size_t)R * Hg);
@@ -331,9 +340,9 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         }
         if (needs_wpad(T)) w.wpad = ar.take<float>((size_t)T.linear[0].out_features * round4(T.linear[0].in_features));
         if (uses_w16(T)) w.w16 = ar.take<uint16_t>((size_t)T.linear[0].out_features * round8(T.linear[0].in_features));
-        w.piece_e = ar.take<float>((size_t)R * D);
+        w.piece_e = ar.take<float>((size_t)R * T.id.dim);
         if (mimic) w.piece_a = ar.take<float>((size_t)R * D);
-        if (T.id.optimizer == TTAMM_OPT_DENSE) w.side_id = ar.take<float>((size_t)R * 3 * D);
+        if (T.id.optimizer == TTAMM_OPT_DENSE) w.side_id = ar.take<float>((size_t)R * 3 * T.id.dim);
         if (mimic) w.side_mimic = ar.take<float>((size_t)R * 3 * D);
     };
     ws.user.role = ROLE_USER;
@@ -348,7 +357,8 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
     if (A.hp.grad_clip_norm > 0.0) {
         ws.clip_on = true;
         // [tables' total (sharded: all-reduced)] + both towers' row partials + the dense partials
-        ws.clip_parts = 1 + rows_sumsq_blocks(B, D) + rows_sumsq_blocks(shard ? A.item_rows_capacity : B * (1 + N), D) +
+        ws.clip_parts = 1 + rows_sumsq_blocks(B, A.user.id.dim) +
+                        rows_sumsq_blocks(shard ? A.item_rows_capacity : B * (1 + N), A.item.id.dim) +
                         kDenseSumsqBlocks;
         ws.clip_partials = ar.take<float>((size_t)ws.clip_parts);
         ws.clip_coef = ar.take<float>(1);
@@ -511,26 +521,27 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
                 // sharded owner: every requester's positives (keys < global batch) are the reference's
                 // first item lookup (training.py:750), the negatives its second (:776)
                 for (int ph = 0; ph < 2; ++ph)
-                    if ((rc = launch_renorm_rows(t.id.weight, t.id.rows, D, w.idx, w.R, t.id.max_norm, w.renorm_mark,
+                    if ((rc = launch_renorm_rows(t.id.weight, t.id.rows, t.id.dim, w.idx, w.R, t.id.max_norm, w.renorm_mark,
                                                  w.renorm_tag + ph, s, w.row_key, w.renorm_key_split, ph)))
                         return rc;
             } else if (t.id.max_norm > 0.0 && w.R > 0) {  // nn.Embedding max_norm: renorm, then look up
                 const int64_t split = w.renorm_split > 0 && w.renorm_split < w.R ? w.renorm_split : w.R;
-                if ((rc = launch_renorm_rows(t.id.weight, t.id.rows, D, w.idx, split, t.id.max_norm, w.renorm_mark,
+                if ((rc = launch_renorm_rows(t.id.weight, t.id.rows, t.id.dim, w.idx, split, t.id.max_norm, w.renorm_mark,
                                              w.renorm_tag, s)))
                     return rc;
                 if (split < w.R &&
-                    (rc = launch_renorm_rows(t.id.weight, t.id.rows, D, w.idx + split, w.R - split, t.id.max_norm,
+                    (rc = launch_renorm_rows(t.id.weight, t.id.rows, t.id.dim, w.idx + split, w.R - split, t.id.max_norm,
                                              w.renorm_mark, w.renorm_tag + 1, s)))
                     return rc;
             }
             float* dst = uses_ef(t) ? w.ef : w.e;
-            const int64_t ld = uses_ef(t) ? 2 * D : D;
-            if ((rc = launch_gather_rows(t.id.weight, t.id.rows, D, w.idx, w.R, dst, ld, s))) return rc;
+            const int64_t ld = uses_ef(t) ? efw(t) : t.id.dim;
+            if ((rc = launch_gather_rows(t.id.weight, t.id.rows, t.id.dim, w.idx, w.R, dst, ld, s))) return rc;
             if (t.fusion != TTAMM_FUSION_IDENTITY && t.n_linear == 0 && w.R > 0) {
-                // identity feature encoder (encoders.py:114-119): f = the feature row (F == D)
-                float* fdst = uses_ef(t) ? w.ef + D : w.f;
-                if ((rc = launch_add_rows(t.features, t.feat_ld, nullptr, 0, w.R, D, fdst, ld, s, w.fidx))) return rc;
+                // identity feature encoder (encoders.py:114-119): f = the feature row
+                float* fdst = uses_ef(t) ? w.ef + t.id.dim : w.f;
+                if ((rc = launch_add_rows(t.features, t.feat_ld, nullptr, 0, w.R, fo_dim(t), fdst, ld, s, w.fidx)))
+                    return rc;
             }
         }
         // feature encoder layers
@@ -596,8 +607,8 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
                 } else {
                     p.epi = EPI_STORE;
                     if (uses_ef(t)) {
-                        p.C = w.ef + D;
-                        p.ldc = 2 * D;
+                        p.C = w.ef + t.id.dim;
+                        p.ldc = efw(t);
                     } else {
                         p.C = w.f;
                         p.ldc = D;
@@ -627,12 +638,12 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
             GemmProblem p = gp_base();
             p.bf16 = t.matmul_bf16;
             p.A = w.ef;
-            p.lda = 2 * D;
+            p.lda = efw(t);
             p.B = t.gate[0].weight;
-            p.ldb = 2 * D;
+            p.ldb = efw(t);
             p.M = (int)w.R;
             p.N = D;
-            p.K = 2 * D;
+            p.K = efw(t);
             p.bias = t.gate[0].bias;
             p.epi = EPI_STORE;
             p.C = w.t;
@@ -760,15 +771,15 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
         q.bf16 = t.matmul_bf16;
         q.A = w.dT;
         q.lda = w.dT_ld;
-        q.B = t.gate[0].weight;  // [D, 2D] = [K, N]
-        q.ldb = 2 * D;
+        q.B = t.gate[0].weight;  // [D, Did + Fo] = [K, N]
+        q.ldb = efw(t);
         q.b_kn = 1;
         q.M = (int)w.R;
-        q.N = 2 * D;
+        q.N = efw(t);
         q.K = D;
         q.epi = EPI_STORE;
         q.C = w.dEF;
-        q.ldc = 2 * D;
+        q.ldc = efw(t);
         b2.add(q);
     }
     if ((rc = b1.run(s))) return rc;
@@ -789,8 +800,8 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
             GemmProblem p = gp_base();
             p.bf16 = t.matmul_bf16;
             if (l == t.n_linear - 1) {
-                p.A = uses_ef(t) ? w.dEF + D : w.dT;
-                p.lda = uses_ef(t) ? 2 * D : w.dT_ld;
+                p.A = uses_ef(t) ? w.dEF + t.id.dim : w.dT;
+                p.lda = uses_ef(t) ? efw(t) : w.dT_ld;
             } else {
                 p.A = w.dhid[l];
                 p.lda = L.out_features;
@@ -862,10 +873,10 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
             pp.dY = w.dT;
             pp.ld_dy = w.dT_ld;
             pp.X = w.ef;
-            pp.ld_x = 2 * D;
+            pp.ld_x = efw(t);
             pp.R = (int)w.R;
             pp.M = D;
-            pp.N = 2 * D;
+            pp.N = efw(t);
             pp.grad_w = w.ggw[0];
             pp.grad_b = w.ggb[0];
             pp.slab = w.slab[TTAMM_MAX_LINEAR];
@@ -877,8 +888,8 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
             WgradProblem p{};
             p.bf16 = t.matmul_bf16;
             if (l == t.n_linear - 1) {
-                p.dY = uses_ef(t) ? w.dEF + D : w.dT;
-                p.ld_dy = uses_ef(t) ? 2 * D : w.dT_ld;
+                p.dY = uses_ef(t) ? w.dEF + t.id.dim : w.dT;
+                p.ld_dy = uses_ef(t) ? efw(t) : w.dT_ld;
             } else {
                 p.dY = w.dhid[l];
                 p.ld_dy = L.out_features;
@@ -1112,7 +1123,7 @@ RowUpdateArgs row_update_args(const ttamm_tower& t, TowerWs& w, int D, bool mimi
     RowUpdateArgs ru;
     std::memset(&ru, 0, sizeof(ru));
     ru.n = w.R;
-    ru.dim = D;
+    ru.dim = t.id.dim;  // == D unless concat fusion has another output_dim (tower_optimizer_rows)
     ru.n_unique = w.co.n_unique;
     ru.seg_start = w.co.seg_start;
     ru.keys = w.co.keys_out;
@@ -1120,7 +1131,7 @@ RowUpdateArgs row_update_args(const ttamm_tower& t, TowerWs& w, int D, bool mimi
     ru.seglong = w.co.seglong;
     if (uses_ef(t)) {
         ru.dE = w.dEF;
-        ru.ld_dE = 2 * D;
+        ru.ld_dE = efw(t);
     } else {
         ru.dE = w.dT;
         ru.ld_dE = w.dT_ld;
@@ -1146,7 +1157,20 @@ RowUpdateArgs row_update_args(const ttamm_tower& t, TowerWs& w, int D, bool mimi
 }
 int tower_optimizer_rows(const ttamm_tower& t, TowerWs& w, int D, bool mimic, const SparseConsts& sp,
                          const AdamConsts& ad, const Deferred& df, hipStream_t s, const float* grad_scale) {
-    return launch_row_update(row_update_args(t, w, D, mimic, sp, ad, df, grad_scale), s);
+    const RowUpdateArgs ru = row_update_args(t, w, D, mimic, sp, ad, df, grad_scale);
+    if (!mimic || t.id.dim == D) return launch_row_update(ru, s);
+    // concat with output_dim != embedding_dim: the ID rows and the (output-wide) mimic rows differ
+    // in width, so the two tables are updated by two passes over the same row grouping
+    RowUpdateArgs a = ru, b = ru;
+    std::memset(&a.mimic, 0, sizeof(a.mimic));
+    a.piece_a = a.side_mimic = nullptr;
+    std::memset(&b.id, 0, sizeof(b.id));
+    b.dE = nullptr;
+    b.piece_e = b.side_id = nullptr;
+    b.dim = D;
+    int rc;
+    if ((rc = launch_row_update(a, s))) return rc;
+    return launch_row_update(b, s);
 }
 void add_seg(SweepArgs& sw, const ttamm_table& tb) {
     sw.seg[sw.count].p = tb.weight;
@@ -1189,7 +1213,7 @@ int table_updates(const ttamm_tower* T[2], TowerWs* W[2], int n, int D, bool mim
                                           df.status, s)))
                 return rc;
         if (t.id.optimizer == TTAMM_OPT_DENSE)
-            if ((rc = launch_side_scatter(w.co.n_unique, w.co.keys_out, w.co.seg_start, w.side_id, w.R, D, t.id,
+            if ((rc = launch_side_scatter(w.co.n_unique, w.co.keys_out, w.co.seg_start, w.side_id, w.R, t.id.dim, t.id,
                                           df.status, s)))
                 return rc;
     }
@@ -1242,7 +1266,7 @@ int clip_table_partials(const ttamm_tower* T[2], TowerWs* W[2], int D, bool mimi
         if (!T[k] || W[k]->R <= 0) continue;
         const RowUpdateArgs ru = row_update_args(*T[k], *W[k], D, mimic, sp, ad, df, nullptr);
         if ((rc = launch_rows_sumsq(ru, ws.clip_partials + off, s))) return rc;
-        off += rows_sumsq_blocks(W[k]->R, D);
+        off += rows_sumsq_blocks(W[k]->R, T[k]->id.dim);
     }
     TTAMM_REQUIRE(off <= ws.clip_parts, "clip: partials overflow");
     *off_out = off;
@@ -1340,13 +1364,17 @@ CalArgs& bind_cal(const ttamm_step_args& A, StepWs& ws, const TowerWs& I, int64_
 }
 
 int validate_step(const ttamm_step_args& A) {
-    const int D = A.user.id.dim;
+    const int D = out_dim(A.user);
     int rc;
     TTAMM_REQUIRE(A.table_g0_math == TTAMM_G0_EXACT || A.table_g0_math == TTAMM_G0_FAST,
                   "table_g0_math must be TTAMM_G0_EXACT or TTAMM_G0_FAST");
     if ((rc = validate_tower(A.user, "user_encoder", D, true))) return rc;
     if ((rc = validate_tower(A.item, "item_encoder", D, true))) return rc;
+    TTAMM_REQUIRE(out_dim(A.item) == D, "User and item encoders must produce embeddings with the same dimension.");
     TTAMM_REQUIRE(A.user.matmul_bf16 == A.item.matmul_bf16, "user and item towers must share one matmul precision");
+    if (A.hp.grad_clip_norm > 0.0 && A.mimic_enabled)
+        TTAMM_REQUIRE(A.user.id.dim == D && A.item.id.dim == D,
+                      "gradient clipping with a concat output_dim other than the embedding dim is not supported");
     TTAMM_REQUIRE(A.b.batch > 0, "empty batch");
     if (cal_enabled(A)) {
         TTAMM_REQUIRE(!sharded(A) || (A.cal_stats && A.cal_scatter),
@@ -1359,7 +1387,7 @@ int validate_step(const ttamm_step_args& A) {
                       "category alignment: num_categories must be in [1, 65535]");
         TTAMM_REQUIRE(A.major_category >= 0 && A.major_category < A.num_categories,
                       "category alignment: major_category out of range");
-        TTAMM_REQUIRE(A.user.id.dim <= 256, "category alignment: embedding dim must be <= 256");
+        TTAMM_REQUIRE(D <= 256, "category alignment: embedding dim must be <= 256");
     }
     if (A.in_batch) {
         TTAMM_REQUIRE(A.b.num_neg >= 0, "num_negatives must be >= 0 with in-batch negatives");
@@ -1417,7 +1445,7 @@ int validate_step(const ttamm_step_args& A) {
 int run_step(const ttamm_step_args& A, hipStream_t s) {
     int rc;
     if ((rc = validate_step(A))) return rc;
-    const int D = A.user.id.dim;
+    const int D = out_dim(A.user);
     const bool mimic = A.mimic_enabled != 0;
     const bool shard = sharded(A);
     const int ph = shard ? A.phase : 255;
@@ -1756,10 +1784,10 @@ int flush_tables(const ttamm_step_args& A, hipStream_t s) {
 // ---- eval-mode tower forward (TowerEncoder.forward + augment) -----------------------------
 size_t tower_forward_workspace_size(const ttamm_tower& T, int64_t n) {
     Arena ar{nullptr, 0, 0, true};
-    const int D = T.id.dim;
+    const int D = out_dim(T);
     for (int l = 0; l + 1 < T.n_linear; ++l) ar.take<float>((size_t)n * T.linear[l].out_features);
-    ar.take<float>((size_t)n * 2 * D);  // ef / e
-    ar.take<float>((size_t)n * D);      // f
+    ar.take<float>((size_t)n * efw(T));  // ef / e
+    ar.take<float>((size_t)n * D);       // f
     if (T.fusion == TTAMM_FUSION_GATED) ar.take<float>((size_t)n * T.gate[0].out_features);
     for (int q = 0; q < 3; ++q) ar.take<float>((size_t)n * D);  // g, t, a
     ar.take<int64_t>(n);                                         // range-checked ids
@@ -1770,7 +1798,7 @@ size_t tower_forward_workspace_size(const ttamm_tower& T, int64_t n) {
 
 int tower_forward_eval(const ttamm_tower& T, const int64_t* idx, const int64_t* fidx, int64_t n, int augment,
                        float* out, void* wsp, size_t ws_bytes, hipStream_t s) {
-    const int D = T.id.dim;
+    const int D = out_dim(T);
     int rc;
     if ((rc = validate_tower(T, "tower", D, false))) return rc;
     if (augment && T.mimic.weight)
@@ -1782,7 +1810,7 @@ int tower_forward_eval(const ttamm_tower& T, const int64_t* idx, const int64_t* 
     w.idx = idx;
     w.fidx = fidx;
     for (int l = 0; l + 1 < T.n_linear; ++l) w.hid[l] = ar.take<float>((size_t)n * T.linear[l].out_features);
-    float* efbuf = ar.take<float>((size_t)n * 2 * D);
+    float* efbuf = ar.take<float>((size_t)n * efw(T));
     float* fbuf = ar.take<float>((size_t)n * D);
     float* zbuf = T.fusion == TTAMM_FUSION_GATED ? ar.take<float>((size_t)n * T.gate[0].out_features) : nullptr;
     float* gbuf = ar.take<float>((size_t)n * D);
@@ -1839,7 +1867,7 @@ int tower_forward_eval(const ttamm_tower& T, const int64_t* idx, const int64_t* 
 // writes the ID rows' gradient per position (and, identity feature encoder, the feature rows').
 namespace {
 void plan_tower_train(Arena& ar, const ttamm_tower& T, int64_t n, TowerWs& w) {
-    const int D = T.id.dim;
+    const int D = out_dim(T);
     w.role = ROLE_USER;
     w.R = n;
     w.idx_own = ar.take<int64_t>(n);
@@ -1852,8 +1880,8 @@ void plan_tower_train(Arena& ar, const ttamm_tower& T, int64_t n, TowerWs& w) {
         }
     }
     if (uses_ef(T)) {
-        w.ef = ar.take<float>((size_t)n * 2 * D);
-        w.dEF = ar.take<float>((size_t)n * 2 * D);
+        w.ef = ar.take<float>((size_t)n * efw(T));
+        w.dEF = ar.take<float>((size_t)n * efw(T));
     } else {
         w.e = ar.take<float>((size_t)n * D);
         w.f = ar.take<float>((size_t)n * D);
@@ -1911,7 +1939,7 @@ size_t tower_train_workspace_size(const ttamm_tower& T, int64_t n) {
 int tower_train_forward(const ttamm_tower& T, const int64_t* idx, const int64_t* fidx, int64_t n,
                         const uint8_t* const* keep_masks, uint64_t seed, uint64_t counter, float* out, void* wsp,
                         size_t ws_bytes, hipStream_t s) {
-    const int D = T.id.dim;
+    const int D = out_dim(T);
     int rc;
     if ((rc = validate_tower(T, "tower", D, false))) return rc;
     if (n <= 0) return TTAMM_OK;
@@ -1942,7 +1970,8 @@ int tower_train_forward(const ttamm_tower& T, const int64_t* idx, const int64_t*
 int tower_train_backward(const ttamm_tower& T, const int64_t* idx, const int64_t* fidx, int64_t n,
                          const uint8_t* const* keep_masks, const float* d_out, float* grad_arena, float* d_id_rows,
                          float* d_feat_rows, void* wsp, size_t ws_bytes, hipStream_t s) {
-    const int D = T.id.dim;
+    const int D = out_dim(T);
+    const int Did = T.id.dim;
     int rc;
     if ((rc = validate_tower(T, "tower", D, false))) return rc;
     const size_t ng = tower_grad_floats(T);
@@ -1964,15 +1993,16 @@ int tower_train_backward(const ttamm_tower& T, const int64_t* idx, const int64_t
     TowerWs* WW[2] = {&w, nullptr};
     if (T.fusion != TTAMM_FUSION_IDENTITY)
         if ((rc = tower_backward(TT, WW, D, s, 1))) return rc;
-    // d(ID rows): [e | f] towers take dEF[:, :D]; sum / identity fusion pass dT to e
+    // d(ID rows): [e | f] towers take dEF[:, :Did]; sum / identity fusion pass dT to e
     const float* de = uses_ef(T) ? w.dEF : d_out;
-    const int64_t ld_de = uses_ef(T) ? 2 * D : D;
-    if (d_id_rows && (rc = launch_add_rows(de, ld_de, nullptr, 0, n, D, d_id_rows, D, s))) return rc;
-    if (d_feat_rows) {  // identity feature encoder: f = the feature row, its gradient is dEF[:, D:] / dT
+    const int64_t ld_de = uses_ef(T) ? efw(T) : D;
+    if (d_id_rows && (rc = launch_add_rows(de, ld_de, nullptr, 0, n, Did, d_id_rows, Did, s))) return rc;
+    if (d_feat_rows) {  // identity feature encoder: f = the feature row, its gradient is dEF[:, Did:] / dT
         TTAMM_REQUIRE(T.n_linear == 0 && T.fusion != TTAMM_FUSION_IDENTITY,
                       "tower backward: feature-row gradients exist for the identity feature encoder only");
-        const float* df = uses_ef(T) ? w.dEF + D : d_out;
-        if ((rc = launch_add_rows(df, ld_de, nullptr, 0, n, D, d_feat_rows, D, s))) return rc;
+        const float* df = uses_ef(T) ? w.dEF + Did : d_out;
+        const int fo = fo_dim(T);
+        if ((rc = launch_add_rows(df, ld_de, nullptr, 0, n, fo, d_feat_rows, fo, s))) return rc;
     }
     return TTAMM_OK;
 }

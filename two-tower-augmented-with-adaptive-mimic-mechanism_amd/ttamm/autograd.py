@@ -95,7 +95,7 @@ class _TowerRun:
         self.feature_grad = feature_grad
 
     def forward(self) -> torch.Tensor:
-        D = self.tower.id_dim
+        D = getattr(self.tower, "output_dim", self.tower.id_dim)  # concat: the projection's width
         out = torch.empty((self.n, D), dtype=torch.float32, device=self.idx.device)
         _lib.check(self.lib.ttamm_tower_train_forward(
             ctypes.byref(self.desc), _ptr(self.idx), None, self.n, self.mask_arr, self.seed, self.counter,
@@ -105,12 +105,13 @@ class _TowerRun:
     def backward(self, d_out: torch.Tensor) -> tuple[torch.Tensor | None, ...]:
         tower = self.tower
         D = tower.id_dim
+        fo = self.feats.shape[1] if self.feature_grad else 0  # identity feature encoder: F wide
         dev = self.idx.device
         params = tower_params(tower)
         n_arena = int(self.lib.ttamm_tower_grad_floats(ctypes.byref(self.desc)))
         arena = torch.empty(max(1, n_arena), dtype=torch.float32, device=dev)
         d_rows = torch.empty((self.n, D), dtype=torch.float32, device=dev)
-        d_feat = torch.empty((self.n, D), dtype=torch.float32, device=dev) if self.feature_grad else None
+        d_feat = torch.empty((self.n, fo), dtype=torch.float32, device=dev) if self.feature_grad else None
         _lib.check(self.lib.ttamm_tower_train_backward(
             ctypes.byref(self.desc), _ptr(self.idx), None, self.n, self.mask_arr, _ptr(d_out), _ptr(arena),
             _ptr(d_rows), _ptr(d_feat), _ptr(self.ws), self.ws.numel(), _lib.stream_handle(dev)))

@@ -348,9 +348,6 @@ def describe_tower(
     state: Mapping[int, Mapping[str, torch.Tensor]] | None = None,
     id_optimizer: int = _lib.OPT_SPARSE_ADAM,
 ) -> _lib.Tower:
-    if tower.fusion == "concat" and tower.projection.out_features != tower.id_dim:
-        # the step's score / mimic rows are embedding-dim wide (AdaptiveMimicMechanism needs it)
-        raise NotImplementedError("ttamm: 'concat' fusion needs output_dim == embedding_dim")
     if tower.embedding.max_norm is not None and float(tower.embedding.norm_type) != 2.0:
         raise NotImplementedError("ttamm: max_norm embeddings with norm_type != 2")
     s = _lib.Tower()
@@ -432,8 +429,8 @@ def tower_forward(
             if feats.shape[0] != n:
                 raise ValueError("ttamm: features must have one row per index")
         out = tower_train_forward(tower, idx, feats)
-        return out.reshape(*indices.shape, tower.id_dim)
-    out = torch.empty((n, tower.id_dim), dtype=torch.float32, device=idx.device)
+        return out.reshape(*indices.shape, out.shape[-1])
+    out = torch.empty((n, tower.output_dim if use_features else tower.id_dim), dtype=torch.float32, device=idx.device)
     if not use_features and tower.fusion != "identity":
         # the reference falls back to the ID embedding when features are absent (encoders.py:228-231)
         lib = _lib.load()
@@ -473,4 +470,4 @@ def tower_forward(
             ws.data_ptr(), ws_bytes, _lib.stream_handle(idx.device),
         )
     )
-    return out.reshape(*indices.shape, tower.id_dim)
+    return out.reshape(*indices.shape, out.shape[-1])

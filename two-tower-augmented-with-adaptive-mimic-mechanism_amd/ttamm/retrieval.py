@@ -30,11 +30,11 @@ def _encode(tower: TowerEncoder, mimic_table: torch.Tensor | None, rows: torch.T
     dev = rows.device
     n = rows.numel()
     D = tower.id_dim
-    out = torch.empty((n, D), dtype=torch.float32, device=dev)
+    feats = _pad_features(features) if tower.fusion != "identity" else None
+    out = torch.empty((n, tower.output_dim if feats is not None else D), dtype=torch.float32, device=dev)
     if n == 0:
         return out
     _lib.check_index_range(rows, tower.num_embeddings)
-    feats = _pad_features(features) if tower.fusion != "identity" else None
     if tower.fusion != "identity" and feats is None:
         # no features: the reference falls back to the ID embedding (encoders.py:228-231)
         _lib.check(lib.ttamm_gather_rows(tower.embedding.weight.data_ptr(), tower.num_embeddings, D, rows.data_ptr(),

@@ -429,7 +429,7 @@ class ShardedTrainStep(FusedTrainStep):
         args.loss_out = self.loss_out.data_ptr()
         args.table_sumsq = self.arena[n_grad + 5:].data_ptr()
         args.dense_grads = self.arena.data_ptr()
-        D = self.model.user_encoder.embedding.weight.shape[1]
+        D = self.model.user_encoder.output_dim  # the tower output (= embedding dim unless concat sets another)
         self.D = D
         self.fwd_out = torch.empty((self.capacity, 2 * D), dtype=torch.float32, device=self.device)
         if self.in_batch:  # all-gathered positives: the workspace is sized for the global batch

@@ -509,6 +509,7 @@ class _IdentityView(nn.Module):
         self.embedding = tower.embedding
         self.matmul_dtype = tower.matmul_dtype
         self.id_dim = tower.id_dim
+        self.output_dim = tower.id_dim
         self.num_embeddings = tower.num_embeddings
 
 
