@@ -259,7 +259,7 @@ struct ScoreArgs {
     const float* ib_dp;
     int64_t ib_ld;
 };
-int score_blocks(int64_t B);
+int score_blocks(int64_t B, int D);  // [blocks, 3] partials of launch_score_loss
 int launch_score_loss(const ScoreArgs& a, hipStream_t s);
 // bce = (sum of the score partials + sum of ib_partials) / bce_count
 int launch_loss_finalize(const float* partials, int blocks, const float* ib_partials, int ib_blocks, int64_t bce_count,

@@ -15,6 +15,7 @@
 // The result equals one dense AdamW step over the full dense gradient.
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cmath>
 
 #include "kernels.h"
@@ -664,6 +665,117 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
     }
 }
 
+// The same replay with the per-step constants in scalar registers.  A wave whose active lanes
+// share one start step l (the slice: untouched rows of a slice share their lag; the catch-up
+// lists: sorted by lag) reads step k's constants once for the wave with s_load from the history
+// ring (constant address space, wave-uniform index), the next step's load issued before the
+// current step's arithmetic — no LDS ring fill, no per-lane ds_read and pointer arithmetic in
+// the VALU-bound loop.  Waves whose lanes straddle two lags take each lane's constants with
+// vector loads (a few waves per launch).  Arithmetic and constants are replay_kernel's, bit for
+// bit.
+template <bool DECOUPLED, bool FAST>
+__device__ __forceinline__ void replay_steps_g0(float4& p, float4& m, float4& v, const AdamConsts& c) {
+    adam_elem_t<DECOUPLED, true, FAST>(p.x, m.x, v.x, 0.f, c);
+    adam_elem_t<DECOUPLED, true, FAST>(p.y, m.y, v.y, 0.f, c);
+    adam_elem_t<DECOUPLED, true, FAST>(p.z, m.z, v.z, 0.f, c);
+    adam_elem_t<DECOUPLED, true, FAST>(p.w, m.w, v.w, 0.f, c);
+}
+
+template <typename H>
+__device__ __forceinline__ AdamConsts consts_at(H h) {
+    AdamConsts c;
+    c.decay = h->decay, c.w1 = h->w1, c.b2 = h->b2, c.eps = h->eps, c.neg_step = h->neg_step;
+    c.bc2_sqrt = h->bc2_sqrt, c.inv_bc2_sqrt = h->inv_bc2_sqrt, c.wd = h->wd, c.w2 = h->w2;
+    c.decoupled = 0, c.fast_g0 = 0;
+    return c;
+}
+
+template <bool DECOUPLED, bool FAST, int V>
+__global__ __launch_bounds__(256) void replay_s_kernel(ReplayArgs) {
+    const KArg(ReplayArgs)* ka = (const KArg(ReplayArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
+    const KArg(ReplaySeg)& S = ka->seg[blockIdx.y];
+    if (step_poisoned(ka->status)) return;
+    const KArg(AdamConsts)* hist = (const KArg(AdamConsts)*)ka->hist;
+    const int cap = ka->cap;
+    const int dim = S.dim;
+    const uint32_t per_row = (uint32_t)(dim >> 2) / V;  // threads per row
+    const int32_t target = ka->target;
+    const bool by_list = S.list_rows != nullptr;
+    const uint32_t nrows = by_list ? (uint32_t)S.list_cnt[0] : (uint32_t)(S.row_hi - S.row_lo);
+    const uint32_t total = nrows * per_row;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+        const uint32_t r = e / per_row, q = e - r * per_row;
+        int64_t row;
+        int32_t l;
+        if (by_list) {
+            row = S.list_rows[r];
+            l = target - S.list_lag[r];
+        } else {
+            row = S.row_lo + r;
+            l = S.last[row];
+            if (l >= target) continue;
+        }
+        const int64_t o = row * dim + 4 * (int64_t)q;
+        float4 p[V], m[V], v[V];
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const int64_t oi = o + (int64_t)(4 * per_row) * i;
+            p[i] = *reinterpret_cast<const float4*>(S.p + oi);
+            m[i] = *reinterpret_cast<const float4*>(S.m + oi);
+            v[i] = *reinterpret_cast<const float4*>(S.v + oi);
+        }
+        uint32_t mbits = 0u;
+#pragma unroll
+        for (int i = 0; i < V; ++i)
+            mbits |= __float_as_uint(m[i].x) | __float_as_uint(m[i].y) | __float_as_uint(m[i].z) | __float_as_uint(m[i].w);
+        const bool cold = DECOUPLED && mbits == 0u;  // see replay_kernel: p *= decay, v *= b2
+        const int32_t l0 = __builtin_amdgcn_readfirstlane(l);
+        if (__builtin_amdgcn_ballot_w64(l != l0) == 0) {
+            // wave-uniform start step: constants in SGPRs, step k + 1's loaded during step k
+            const int32_t n = target - l0;
+            int j = (l0 + 1) % cap;
+            if (cold) {
+                float decay = hist[j].decay, b2 = hist[j].b2;
+                for (int32_t k = 0; k < n; ++k) {
+                    j = j + 1 == cap ? 0 : j + 1;
+                    const float nd = hist[j].decay, nb = hist[j].b2;
+#pragma unroll
+                    for (int i = 0; i < V; ++i) {
+                        p[i].x = p[i].x * decay, p[i].y = p[i].y * decay, p[i].z = p[i].z * decay, p[i].w = p[i].w * decay;
+                        v[i].x = v[i].x * b2, v[i].y = v[i].y * b2, v[i].z = v[i].z * b2, v[i].w = v[i].w * b2;
+                    }
+                    decay = nd, b2 = nb;
+                }
+            } else {
+                AdamConsts c = consts_at(hist + j);
+                for (int32_t k = 0; k < n; ++k) {
+                    j = j + 1 == cap ? 0 : j + 1;
+                    const AdamConsts nc = consts_at(hist + j);
+#pragma unroll
+                    for (int i = 0; i < V; ++i) replay_steps_g0<DECOUPLED, FAST>(p[i], m[i], v[i], c);
+                    c = nc;
+                }
+            }
+        } else {
+            // lanes of two or more start steps: per-lane constants
+            int j = (l + 1) % cap;
+            for (int32_t k = l; k < target; ++k) {
+                const AdamConsts c = consts_at((const AdamConsts*)ka->hist + j);
+                j = j + 1 == cap ? 0 : j + 1;
+#pragma unroll
+                for (int i = 0; i < V; ++i) replay_steps_g0<DECOUPLED, FAST>(p[i], m[i], v[i], c);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const int64_t oi = o + (int64_t)(4 * per_row) * i;
+            *reinterpret_cast<float4*>(S.p + oi) = p[i];
+            *reinterpret_cast<float4*>(S.m + oi) = m[i];
+            *reinterpret_cast<float4*>(S.v + oi) = v[i];
+        }
+    }
+}
+
 // row ranges only: last[row] = target (stamp 1) or max(last[row], target) (stamp 2) after the
 // replay (list segments were stamped by their build)
 __global__ void stamp_kernel(ReplayArgs) {
@@ -1084,6 +1196,23 @@ int launch_step_begin(const uint32_t* status, int64_t* applied, AdamConsts* hist
 
 template <int V>
 static void launch_replay_v(const ReplayArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    // TTAMM_REPLAY_SCALAR=1: constants in scalar registers (replay_s_kernel); default: the
+    // history ring staged in LDS per block (replay_kernel)
+    static const bool scalar = [] {
+        const char* e = getenv("TTAMM_REPLAY_SCALAR");
+        return e && e[0] == '1';
+    }();
+    if (scalar) {
+        if (a.fast_g0) {
+            if (a.decoupled) hipLaunchKernelGGL((replay_s_kernel<true, true, V>), grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((replay_s_kernel<false, true, V>), grid, dim3(256), 0, s, a);
+        } else if (a.decoupled) {
+            hipLaunchKernelGGL((replay_s_kernel<true, false, V>), grid, dim3(256), 0, s, a);
+        } else {
+            hipLaunchKernelGGL((replay_s_kernel<false, false, V>), grid, dim3(256), 0, s, a);
+        }
+        return;
+    }
     if (a.fast_g0) {
         if (a.decoupled) hipLaunchKernelGGL((replay_kernel<true, true, V>), grid, dim3(256), lds, s, a);
         else hipLaunchKernelGGL((replay_kernel<false, true, V>), grid, dim3(256), lds, s, a);

@@ -313,6 +313,148 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
     }
 }
 
+// The same scores, gradients and loss terms with G lanes per interaction (64 / G interactions
+// per wave) and NV float4 columns per lane (D = 4 G NV: lane s of a group holds columns
+// 4 (s + G i) .. + 3, so a group's loads of one row are G consecutive 16-B pieces): 16-B loads
+// and stores instead of 4-B ones, all lanes busy at D = 96, and each dot product reduced over
+// log2 G lanes instead of 64.  Used when D % (4 G) == 0; the lane partials are summed over
+// i and then across the group (a different order from score_loss_kernel's chunk sums).
+__device__ __forceinline__ float group_sum(float v, int G) {
+    for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float dot4(float4 a, float4 b) { return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w; }
+__device__ __forceinline__ float4 scale4(float s, float4 a) { return make_float4(s * a.x, s * a.y, s * a.z, s * a.w); }
+__device__ __forceinline__ float4 fma4(float s, float4 a, float4 c) {
+    return make_float4(c.x + s * a.x, c.y + s * a.y, c.z + s * a.z, c.w + s * a.w);
+}
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float4 addf4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+
+template <int G, int NV>
+__global__ __launch_bounds__(64 * kScoreWaves) void score_loss_v_kernel(ScoreArgs A) {
+    constexpr int NG = NV <= 3 ? 8 : 4;  // negatives in flight per group
+    __shared__ float red[kScoreWaves][3];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, s = lane % G;
+    const int64_t b = ((int64_t)blockIdx.x * kScoreWaves + w) * (64 / G) + lane / G;
+    constexpr int D = 4 * G * NV;
+    const int N = A.N;
+    const int64_t B = A.B, ldi = A.ld_dti, ldt = A.ld_item;
+    const float inv_numel = A.inv_numel;
+    const bool ib = A.ib_du != nullptr;
+    float bce = 0.f, mse_u = 0.f, mse_i = 0.f;
+    if (b < B) {
+        const int64_t pb = A.item_slot ? A.item_slot[b] : b;
+        auto item_row = [&](int64_t r, int c) {
+            if (A.item_aug) return ld4(A.item_aug + r * ldt + c);
+            const float4 t = ld4(A.t_item + r * ldt + c);
+            return A.a_item ? addf4(t, ld4(A.a_item + r * ldt + c)) : t;
+        };
+        const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 u[NV], p[NV], au[NV], tp[NV], ap[NV], tu[NV], ibp[NV], ibu[NV];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const int c = 4 * (s + G * i);
+            u[i] = ld4(A.user_aug + b * D + c);
+            p[i] = item_row(pb, c);
+            au[i] = tp[i] = ap[i] = tu[i] = ibp[i] = ibu[i] = z4;
+            if (A.mimic) {
+                au[i] = ld4(A.a_user + b * D + c);
+                tp[i] = ld4(A.t_item + pb * ldt + c);
+                ap[i] = ld4(A.a_item + pb * ldt + c);
+                tu[i] = ld4(A.t_user + b * D + c);
+            }
+            if (ib) {
+                ibp[i] = ld4(A.ib_dp + b * A.ib_ld + c);
+                ibu[i] = ld4(A.ib_du + b * D + c);
+            }
+        }
+        float dot = 0.f;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) dot += dot4(u[i], p[i]);
+        const float sp = group_sum(dot, G);
+        float dsp = 0.f;
+        if (!ib) {
+            dsp = (1.0f / (1.0f + expf(-sp)) - 1.0f) * inv_numel;
+            bce += bce_logit(sp, 1.0f);
+        }
+        float4 du[NV], dpos[NV];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            dpos[i] = ib ? ibp[i] : scale4(dsp, u[i]);
+            du[i] = ib ? ibu[i] : scale4(dsp, p[i]);
+            st4(A.dT_item + pb * ldi + 4 * (s + G * i), dpos[i]);
+        }
+        for (int j0 = 0; j0 < N; j0 += NG) {
+            const int ng = N - j0 < NG ? N - j0 : NG;
+            int64_t nr[NG];
+            float4 nv[NG][NV];
+#pragma unroll
+            for (int jj = 0; jj < NG; ++jj) {
+                nr[jj] = 0;
+                if (jj < ng) {
+                    const int64_t q = B + b * N + j0 + jj;
+                    nr[jj] = A.item_slot ? A.item_slot[q] : q;
+                }
+#pragma unroll
+                for (int i = 0; i < NV; ++i) nv[jj][i] = jj < ng ? item_row(nr[jj], 4 * (s + G * i)) : z4;
+            }
+            float sn[NG];
+#pragma unroll
+            for (int jj = 0; jj < NG; ++jj) {
+                float dn = 0.f;
+#pragma unroll
+                for (int i = 0; i < NV; ++i) dn += dot4(u[i], nv[jj][i]);
+                sn[jj] = group_sum(dn, G);
+            }
+#pragma unroll
+            for (int jj = 0; jj < NG; ++jj) {
+                if (jj >= ng) continue;
+                const float dsn = (1.0f / (1.0f + expf(-sn[jj])) - 0.0f) * inv_numel;
+                bce += bce_logit(sn[jj], 0.0f);
+#pragma unroll
+                for (int i = 0; i < NV; ++i) {
+                    const int c = 4 * (s + G * i);
+                    const float4 g = scale4(dsn, u[i]);
+                    st4(A.dT_item + nr[jj] * ldi + c, g);
+                    if (A.mimic && A.dA_all) st4(A.dA_item + nr[jj] * ldi + c, g);
+                    du[i] = fma4(dsn, nv[jj][i], du[i]);
+                }
+            }
+        }
+        const float norm = 2.0f / (float)(A.Bg * D);
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const int c = 4 * (s + G * i);
+            st4(A.dT_user + b * D + c, du[i]);
+            if (A.mimic) {
+                const float4 xu = make_float4(au[i].x - tp[i].x, au[i].y - tp[i].y, au[i].z - tp[i].z, au[i].w - tp[i].w);
+                const float4 xi = make_float4(ap[i].x - tu[i].x, ap[i].y - tu[i].y, ap[i].z - tu[i].z, ap[i].w - tu[i].w);
+                mse_u += dot4(xu, xu);
+                mse_i += dot4(xi, xi);
+                st4(A.dA_user + b * D + c, fma4(norm * A.lambda_u, xu, du[i]));
+                st4(A.dA_item + pb * ldi + c, fma4(norm * A.lambda_i, xi, dpos[i]));
+            }
+        }
+    }
+    // every lane of a group holds the group's BCE terms: count them once
+    bce = wave_sum(s == 0 ? bce : 0.f);
+    mse_u = wave_sum(mse_u);
+    mse_i = wave_sum(mse_i);
+    if (lane == 0) {
+        red[w][0] = bce;
+        red[w][1] = mse_u;
+        red[w][2] = mse_i;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        float t = 0.f;
+        for (int i = 0; i < kScoreWaves; ++i) t += red[i][threadIdx.x];
+        A.partials[blockIdx.x * 3 + threadIdx.x] = t;
+    }
+}
+
 // Deterministic final reduction of the per-block partials; total loss as in training.py:798-803.
 __global__ void loss_finalize_kernel(const float* __restrict__ partials, int blocks, const float* __restrict__ ib_partials,
                                      int ib_blocks, int64_t bce_count, int64_t B, int64_t Bg, int D,
@@ -489,11 +631,32 @@ int launch_gate_dq(const float* dT, int64_t ld_dT, const float* ef, const float*
     return TTAMM_OK;
 }
 
+static int score_group(int D);
 int launch_score_loss(const ScoreArgs& a, hipStream_t s) {
     TTAMM_REQUIRE(a.D <= 64 * kMaxDChunks, "score: embedding dim too large (max 512)");
     TTAMM_REQUIRE(a.N >= (a.ib_du ? 0 : 1) && a.N <= kMaxNeg, "score: negatives_per_positive out of range");
     if (a.B <= 0) return TTAMM_OK;
     const dim3 g(a.blocks), t(64 * kScoreWaves);
+    TTAMM_REQUIRE(a.blocks == score_blocks(a.B, a.D), "score: partials sized for another batch");
+    // 16-B aligned rows: every leading dimension a multiple of 4 floats
+    const uintptr_t ptrs = (uintptr_t)a.user_aug | (uintptr_t)a.item_aug | (uintptr_t)a.t_user | (uintptr_t)a.t_item |
+                           (uintptr_t)a.a_user | (uintptr_t)a.a_item | (uintptr_t)a.dT_user | (uintptr_t)a.dT_item |
+                           (uintptr_t)a.dA_user | (uintptr_t)a.dA_item | (uintptr_t)a.ib_du | (uintptr_t)a.ib_dp;
+    const bool al = ptrs % 16 == 0 && a.ld_item % 4 == 0 && a.ld_dti % 4 == 0 && (!a.ib_dp || a.ib_ld % 4 == 0);
+    if (al && score_group(a.D)) {
+        switch (a.D) {
+            case 32: hipLaunchKernelGGL((score_loss_v_kernel<8, 1>), g, t, 0, s, a); break;
+            case 64: hipLaunchKernelGGL((score_loss_v_kernel<8, 2>), g, t, 0, s, a); break;
+            case 96: hipLaunchKernelGGL((score_loss_v_kernel<8, 3>), g, t, 0, s, a); break;
+            case 128: hipLaunchKernelGGL((score_loss_v_kernel<8, 4>), g, t, 0, s, a); break;
+            case 192: hipLaunchKernelGGL((score_loss_v_kernel<16, 3>), g, t, 0, s, a); break;
+            case 256: hipLaunchKernelGGL((score_loss_v_kernel<16, 4>), g, t, 0, s, a); break;
+            case 384: hipLaunchKernelGGL((score_loss_v_kernel<16, 6>), g, t, 0, s, a); break;
+            default: hipLaunchKernelGGL((score_loss_v_kernel<16, 8>), g, t, 0, s, a); break;
+        }
+        TTAMM_LAUNCH_CHECK();
+        return TTAMM_OK;
+    }
     switch ((a.D + 63) / 64) {
         case 1: hipLaunchKernelGGL(score_loss_kernel<1>, g, t, 0, s, a); break;
         case 2: hipLaunchKernelGGL(score_loss_kernel<2>, g, t, 0, s, a); break;
@@ -506,7 +669,16 @@ int launch_score_loss(const ScoreArgs& a, hipStream_t s) {
     return TTAMM_OK;
 }
 
-int score_blocks(int64_t B) { return (int)ceil_div(B, kScoreWaves); }
+// lanes per interaction of score_loss_v_kernel for this D, or 0 (score_loss_kernel)
+static int score_group(int D) {
+    if (D == 32 || D == 64 || D == 96 || D == 128) return 8;
+    if (D == 192 || D == 256 || D == 384 || D == 512) return 16;
+    return 0;
+}
+int score_blocks(int64_t B, int D) {
+    const int G = score_group(D);
+    return (int)ceil_div(B, G ? (int64_t)kScoreWaves * (64 / G) : kScoreWaves);
+}
 
 int launch_loss_finalize(const float* partials, int blocks, const float* ib_partials, int ib_blocks, int64_t bce_count,
                          int64_t B, int64_t Bg, int D, float lu, float li, int mimic, const float* cal, float lcal,

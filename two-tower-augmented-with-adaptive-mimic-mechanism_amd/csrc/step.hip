@@ -352,7 +352,7 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         tower(A.item, ws.item, A.item_rows_capacity, true, 0);
     else
         tower(A.item, ws.item, B * (1 + N), false, B);
-    ws.score_blocks = score_blocks(B);
+    ws.score_blocks = score_blocks(B, D);
     ws.partials = ar.take<float>((size_t)ws.score_blocks * 3);
     if (A.hp.grad_clip_norm > 0.0) {
         ws.clip_on = true;
