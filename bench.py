@@ -496,6 +496,15 @@ def main() -> None:
             ach = es_per_step * per_es / 64 / (rep_ms * 1e-3)
             ent["achieved"] = round(ach, 0)
             ent["frac"] = round(ach / VALU_WAVE_INSTR_PEAK, 4)
+        cyc = rv.get("issue_cycles_per_step")
+        if cyc and rep_ms > 0:
+            # the same work priced per instruction at its measured sustained issue cost
+            # (v_sqrt / v_rcp 8.4 SIMD cycles, other VALU 4.08: profiles/r03_valu_issue_rates.txt)
+            ent["issue_roofline"] = {
+                "issue_cycles_per_step": cyc, "unit": "SIMD cycles at 2.4 GHz",
+                "available_per_step": round(rep_ms * 1e-3 * 1024 * 2.4e9),
+                "frac": round(cyc / (rep_ms * 1e-3 * 1024 * 2.4e9), 4),
+                "cost_model": rv.get("issue_cost_model")}
         kernels.insert(0, ent)
         maint = ent
     else:

@@ -14,7 +14,9 @@ launches; every launch's output is checked bit-exact against torch.index_select.
 
 Algorithmic bytes per row: dim*4 read (the table row) + dim*4 written + 8 (int64 index).
 `read_frac` prices the table-row reads alone against 8 TB/s (the north_star's "HBM-read
-roofline"); `frac` prices all algorithmic bytes."""
+roofline"); `frac` prices all algorithmic bytes.  `bulk_read_only` is the product's read-only
+gather of a 50M x 128 table: ttamm_candidate_topk scoring uniform random candidate rows by id
+(the sampled-candidate evaluation), 4 B written per 512 B row read."""
 
 from __future__ import annotations
 
@@ -72,6 +74,45 @@ def run(lib, L, table: torch.Tensor, idx: torch.Tensor, reps: int) -> dict:
             "frac": round(total_b / ms / 1e6 / HBM_PEAK_GBS, 4), "bit_exact": exact}
 
 
+def run_candidates(lib, L, table: torch.Tensor, nq: int, per_q: int, reps: int, gen: torch.Generator,
+                   k: int = 20) -> dict:
+    """ttamm_candidate_topk (the sampled-candidate evaluation, training.py:974-1009) over `nq`
+    queries with `per_q` uniform candidate rows each: every candidate is one random row of the
+    table read by index (its only HBM traffic besides 8 B of id), scored and ranked in LDS.
+    Checked against torch: the top-k positions of a sample of queries."""
+    dev = table.device
+    rows, D = table.shape
+    q = torch.randn((nq, D), generator=gen, device=dev, dtype=torch.float32)
+    cand = torch.randint(0, rows, (nq * per_q,), generator=gen, device=dev)
+    off = torch.arange(0, nq * per_q + 1, per_q, device=dev, dtype=torch.long)
+    out_s = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    out_p = torch.empty((nq, k), dtype=torch.long, device=dev)
+    sp = torch.cuda.current_stream().cuda_stream
+
+    def launch():
+        L.check(lib.ttamm_candidate_topk(q.data_ptr(), nq, D, table.data_ptr(), rows, D, D, off.data_ptr(),
+                                         cand.data_ptr(), per_q, 0, k, out_s.data_ptr(), out_p.data_ptr(), sp))
+
+    for _ in range(2):
+        launch()
+    torch.cuda.synchronize()
+    sample = torch.arange(0, nq, max(1, nq // 512), device=dev)
+    ref = (table[cand.view(nq, per_q)[sample]] * q[sample, None, :]).sum(-1)
+    ref_top = torch.topk(ref, k, dim=1).values
+    score_err = float((out_s[sample] - ref_top).abs().max() / ref_top.abs().max())
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(reps):
+        launch()
+    ev1.record()
+    torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1) / reps
+    read_b = nq * per_q * D * 4
+    return {"queries": nq, "candidates_per_query": per_q, "rows_read": nq * per_q, "avg_launch_ms": round(ms, 4),
+            "read_GBps": round(read_b / ms / 1e6, 1), "read_frac": round(read_b / ms / 1e6 / HBM_PEAK_GBS, 4),
+            "topk_score_rel_err_vs_torch": score_err}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=50_000_000)
@@ -80,6 +121,8 @@ def main() -> None:
     ap.add_argument("--neg", type=int, default=5)
     ap.add_argument("--bulk", type=int, default=2_000_000)
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--cand-queries", type=int, default=200_000)
+    ap.add_argument("--cand-per-query", type=int, default=101)
     args = ap.parse_args()
 
     from ttamm import _lib as L
@@ -98,6 +141,8 @@ def main() -> None:
         uni = torch.randint(0, args.rows, (n,), generator=gen, device=dev)
         zipf = zipf_rows(n, args.rows, 1.05, gen, dev)
         results[name] = {"uniform": run(lib, L, table, uni, args.reps), "zipf": run(lib, L, table, zipf, args.reps)}
+    results["bulk_read_only"] = {"candidate_topk_uniform": run_candidates(lib, L, table, args.cand_queries,
+                                                                         args.cand_per_query, 5, gen)}
     line = {
         "metric": "C4 embedding row gather (ttamm_gather_rows), HBM read roofline",
         "config": {"table": f"{args.rows} x {args.dim} fp32", "step_rows": step_rows,

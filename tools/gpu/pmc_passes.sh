@@ -12,7 +12,7 @@ run_pass() {  # name, counters...
 }
 run_pass fetch FETCH_SIZE
 run_pass write WRITE_SIZE
-run_pass valu SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU
+run_pass valu SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_WAVES SQ_INSTS_SALU
 timeout -s KILL 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/stats -o run -- python3 bench.py --no-cpu-baseline $BENCH_ARGS > gpurun_out/stats_bench.json 2> gpurun_out/stats.err
 find gpurun_out/stats -name "*kernel_stats.csv" -exec cp {} gpurun_out/stats_kernel_stats.csv \;
 rm -rf gpurun_out/stats

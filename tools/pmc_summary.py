@@ -23,6 +23,11 @@ sys.path.insert(0, str(ROOT))
 VALU_ISSUE_PER_S = 1024 * 2.4e9 / 2  # 256 CUs x 4 SIMD-32s, one wave64 VALU instruction per 2 cycles
 # (MI355X_MICROARCH.md "Wave scheduling" and the v_fma_f32 row: 2 cycles per SIMD-32; one wave alone
 # issues at half that, and v_sqrt / v_rcp cost more, so the replay cannot reach this upper bound)
+SIMD_CYCLES_PER_S = 1024 * 2.4e9
+# measured sustained issue costs with 8 waves per SIMD (csrc/tools/valu_bench.cpp,
+# profiles/r03_valu_issue_rates.txt), SIMD cycles at 2.4 GHz per wave64 instruction
+COST_TRANS = 8.43  # v_sqrt_f32 8.46, v_rcp_f32 8.39
+COST_OTHER = 4.08  # v_fma_f32 (the cheapest measured; v_pk_mul_f32 4.78, v_pk_fma_f32 5.21)
 
 
 def short(name: str) -> str:
@@ -46,6 +51,7 @@ def main() -> None:
     fetch = per_kernel(src / "pmc_fetch.csv", "FETCH_SIZE")
     write = per_kernel(src / "pmc_write.csv", "WRITE_SIZE")
     valu = per_kernel(src / "pmc_valu.csv", "SQ_INSTS_VALU")
+    trans = per_kernel(src / "pmc_valu.csv", "SQ_INSTS_VALU_TRANS_F32")
     stats = {short(r["Name"]): r for r in csv.DictReader((src / "stats_kernel_stats.csv").open())}
     bench = json.loads((src / "stats_bench.json").read_text())
 
@@ -117,6 +123,17 @@ def main() -> None:
             achieved = es_per_step * per_es / 64 / (step_ms * 1e-3)
             out["achieved_wave_instr_per_s"] = round(achieved, 0)
             out["frac"] = round(achieved / VALU_ISSUE_PER_S, 4)
+        if trans:
+            # issue-cycle roofline: every VALU instruction priced at its measured sustained cost
+            tr = sum(sum(trans[k]) for k in rep)
+            cycles = tr * COST_TRANS + (instr - tr) * COST_OTHER
+            out["valu_wave_instr_per_step"] = round(instr / steps)
+            out["trans_wave_instr_per_step"] = round(tr / steps)
+            out["issue_cycles_per_step"] = round(cycles / steps)
+            out["issue_cost_model"] = {"trans_f32": COST_TRANS, "other": COST_OTHER,
+                                       "source": "profiles/r03_valu_issue_rates.txt (csrc/tools/valu_bench.cpp)"}
+            if step_ms:
+                out["issue_frac"] = round(cycles / steps / (step_ms * 1e-3 * SIMD_CYCLES_PER_S), 4)
         entry["replay_valu_roofline"] = out
 
     path = ROOT / "profiles" / "pmc_traffic.json"

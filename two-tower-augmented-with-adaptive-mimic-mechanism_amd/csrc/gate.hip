@@ -41,19 +41,27 @@ __device__ __forceinline__ void stg4(float* p, f4v v) { store_nt(p, make_float4(
 __device__ __forceinline__ float sigmoid_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
 // acc[ob] += W[16 (ob0 + ob) + li][16 t + 4 q + r] * b[t][r] over k-tiles t < NK
+// The A fragments of k-tile t + 1 are read from LDS while k-tile t's MFMAs issue (two register
+// sets), so the MFMA chain does not stop for an LDS round trip at every k-tile.
 template <int NO, int NK, int LD>
 __device__ __forceinline__ void tile_gemm(const float* w_lds, int ob0, const f4v (&b)[NK], f4v (&acc)[NO], int li,
                                           int q) {
+    f4v w[2][NO];
+    const float* base = w_lds + (16 * ob0 + li) * LD + 4 * q;
+#pragma unroll
+    for (int ob = 0; ob < NO; ++ob) w[0][ob] = lds4(base + 16 * ob * LD);
 #pragma unroll
     for (int t = 0; t < NK; ++t) {
-        f4v w[NO];
+        const int cur = t & 1;
+        if (t + 1 < NK) {
 #pragma unroll
-        for (int ob = 0; ob < NO; ++ob) w[ob] = lds4(w_lds + (16 * (ob0 + ob) + li) * LD + 16 * t + 4 * q);
+            for (int ob = 0; ob < NO; ++ob) w[cur ^ 1][ob] = lds4(base + 16 * ob * LD + 16 * (t + 1));
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int ob = 0; ob < NO; ++ob)
-                acc[ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[ob][r], b[t][r], acc[ob], 0, 0, 0);
+                acc[ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[cur][ob][r], b[t][r], acc[ob], 0, 0, 0);
         // keep the scheduler from hoisting every k-tile's LDS reads to the top (register spills)
         __builtin_amdgcn_sched_barrier(0);
     }

@@ -224,6 +224,34 @@ int launch_combine(const float* e, int64_t ld_e, const float* f, int64_t ld_f, c
                    hipStream_t s);
 int launch_pad_rows(const float* src, int64_t rows, int cols, int64_t ld_src, float* dst, int ld_dst,
                     hipStream_t s);
+// the same over up to two segments in one launch (the two towers)
+struct GatherSeg {
+    const float* table;
+    int64_t rows;
+    int dim;
+    const int64_t* idx;
+    int64_t n;
+    float* out;
+    int64_t out_ld;
+};
+struct GatherSegs {
+    GatherSeg seg[2];
+    int count;
+};
+int launch_gather_rows_segs(const GatherSegs& g, hipStream_t s);
+struct PadSeg {
+    const float* src;
+    int64_t rows;
+    int cols;
+    int64_t ld_src;
+    float* dst;
+    int ld_dst;
+};
+struct PadSegs {
+    PadSeg seg[2];
+    int count;
+};
+int launch_pad_rows_segs(const PadSegs& p, hipStream_t s);
 int launch_mse(const float* x, const float* y, int64_t n, float* out, hipStream_t s);
 // dq = (dT*e - dT*f) * (1-g) * g   (gate backward through the sigmoid)
 int launch_gate_dq(const float* dT, int64_t ld_dT, const float* ef, const float* g, int64_t n, int dim,

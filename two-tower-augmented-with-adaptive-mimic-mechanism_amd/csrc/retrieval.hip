@@ -531,6 +531,81 @@ __global__ __launch_bounds__(256) void candidate_topk_kernel(const float* __rest
     }
 }
 
+// The same scores with G lanes per candidate row and NV float4 columns per lane (dim = 4 G NV),
+// U candidates per lane group in flight: each row is 16-B loads by G lanes, reduced over
+// log2 G lanes.  The block's 256 / G groups keep 256 U / G random rows in flight — the rows
+// are the HBM traffic of this kernel (a gather of the item-vector table by candidate id).
+template <int G, int NV>
+__global__ __launch_bounds__(256) void candidate_topk_v_kernel(const float* __restrict__ Q, int64_t ldq,
+                                                               const float* __restrict__ X, int64_t ni, int64_t ldx,
+                                                               const int64_t* __restrict__ coff,
+                                                               const int64_t* __restrict__ crow, int cosine, int k,
+                                                               float* __restrict__ out_s, int64_t* __restrict__ out_p) {
+    constexpr int GPB = 256 / G, U = 2;
+    __shared__ float sc[kCandCap];
+    const int s = threadIdx.x % G, grp = threadIdx.x / G;
+    const int64_t q = blockIdx.x;
+    const int64_t c0 = coff[q];
+    const int nc = (int)(coff[q + 1] - c0);
+    float4 qv[NV];
+    float qq = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        qv[i] = *reinterpret_cast<const float4*>(Q + q * ldq + 4 * (s + G * i));
+        qq += qv[i].x * qv[i].x + qv[i].y * qv[i].y + qv[i].z * qv[i].z + qv[i].w * qv[i].w;
+    }
+    for (int o = G / 2; o > 0; o >>= 1) qq += __shfl_xor(qq, o, 64);
+    const float qn = fmaxf(sqrtf(qq), 1e-12f);
+    for (int cb = grp; cb < nc; cb += GPB * U) {
+        int64_t r[U];
+        float4 x[U][NV];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int c = cb + u * GPB;
+            r[u] = c < nc ? crow[c0 + c] : -1;
+            if (r[u] >= ni) r[u] = -1;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int i = 0; i < NV; ++i)
+                x[u][i] = r[u] >= 0 ? *reinterpret_cast<const float4*>(X + r[u] * ldx + 4 * (s + G * i))
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            float dot = 0.f, ss = 0.f;
+#pragma unroll
+            for (int i = 0; i < NV; ++i) {
+                dot += qv[i].x * x[u][i].x + qv[i].y * x[u][i].y + qv[i].z * x[u][i].z + qv[i].w * x[u][i].w;
+                ss += x[u][i].x * x[u][i].x + x[u][i].y * x[u][i].y + x[u][i].z * x[u][i].z + x[u][i].w * x[u][i].w;
+            }
+            for (int o = G / 2; o > 0; o >>= 1) {
+                dot += __shfl_xor(dot, o, 64);
+                ss += __shfl_xor(ss, o, 64);
+            }
+            const int c = cb + u * GPB;
+            if (s == 0 && c < nc) sc[c] = cosine ? dot / (qn * fmaxf(sqrtf(ss), 1e-12f)) : dot;
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
+        const float v = sc[c];
+        int rank = 0;
+        for (int o = 0; o < nc; ++o) {
+            const float w = sc[o];
+            rank += (w > v || (w == v && o < c)) ? 1 : 0;
+        }
+        if (rank < k) {
+            out_s[q * k + rank] = v;
+            out_p[q * k + rank] = c;
+        }
+    }
+    for (int r = nc + threadIdx.x; r < k; r += blockDim.x) {
+        out_s[q * k + r] = -INFINITY;
+        out_p[q * k + r] = -1;
+    }
+}
+
 }  // namespace
 
 int launch_candidate_topk(const float* Q, int64_t nq, int64_t ldq, const float* X, int64_t ni, int64_t ldx, int dim,
@@ -541,8 +616,20 @@ int launch_candidate_topk(const float* Q, int64_t nq, int64_t ldq, const float* 
     TTAMM_REQUIRE(max_candidates >= 0 && max_candidates <= kCandCap, "candidate_topk: at most 4096 candidates per query");
     if (nq == 0) return TTAMM_OK;
     TTAMM_REQUIRE(Q && coff && out_s && out_p && (crow || max_candidates == 0), "candidate_topk: null pointer");
-    hipLaunchKernelGGL(candidate_topk_kernel, dim3((unsigned)nq), dim3(256), 0, s, Q, ldq, X, ni, ldx, dim, coff, crow,
-                       cosine, k, out_s, out_p);
+    const bool al = ((uintptr_t)Q | (uintptr_t)X) % 16 == 0 && ldq % 4 == 0 && ldx % 4 == 0;
+    const dim3 g((unsigned)nq), t(256);
+#define TTAMM_CAND(G, NV) \
+    hipLaunchKernelGGL((candidate_topk_v_kernel<G, NV>), g, t, 0, s, Q, ldq, X, ni, ldx, coff, crow, cosine, k, out_s, out_p)
+    if (al && dim == 32) TTAMM_CAND(8, 1);
+    else if (al && dim == 64) TTAMM_CAND(8, 2);
+    else if (al && dim == 96) TTAMM_CAND(8, 3);
+    else if (al && dim == 128) TTAMM_CAND(8, 4);
+    else if (al && dim == 256) TTAMM_CAND(16, 4);
+    else if (al && dim == 512) TTAMM_CAND(16, 8);
+    else
+        hipLaunchKernelGGL(candidate_topk_kernel, g, t, 0, s, Q, ldq, X, ni, ldx, dim, coff, crow, cosine, k, out_s,
+                           out_p);
+#undef TTAMM_CAND
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

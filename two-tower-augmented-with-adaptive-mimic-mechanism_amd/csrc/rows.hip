@@ -72,6 +72,41 @@ __global__ __launch_bounds__(256) void gather_rows_wide(const float4* __restrict
     }
 }
 
+// gather_rows_wide over up to two (table, idx, out) segments of one row width, blockIdx.y =
+// segment: the user and item towers' ID rows in one launch
+template <int D4>
+__global__ __launch_bounds__(256) void gather_rows_wide_seg(GatherSegs) {
+    const KArg(GatherSegs)* ka = (const KArg(GatherSegs)*)(__builtin_amdgcn_kernarg_segment_ptr());
+    const KArg(GatherSeg)& S = ka->seg[blockIdx.y];
+    constexpr int RPW = WideGather<D4>::RPW, I = WideGather<D4>::I;
+    const float4* table = reinterpret_cast<const float4*>(S.table);
+    float4* out = reinterpret_cast<float4*>(S.out);
+    const int64_t n = S.n, rows = S.rows, out_ld4 = S.out_ld / 4;
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t r0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW; r0 < n;
+         r0 += nwaves * RPW) {
+        int64_t src[I];
+#pragma unroll
+        for (int u = 0; u < I; ++u) {
+            const int64_t r = r0 + (u * 64 + lane) / D4;
+            src[u] = r < n ? checked_row(S.idx[r], rows) : -1;
+        }
+        float4 v[I];
+#pragma unroll
+        for (int u = 0; u < I; ++u) {
+            v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (src[u] >= 0) v[u] = table[src[u] * D4 + (u * 64 + lane) % D4];
+        }
+#pragma unroll
+        for (int u = 0; u < I; ++u) {
+            const int e = u * 64 + lane;
+            const int64_t r = r0 + e / D4;
+            if (r < n) store_nt(out + r * out_ld4 + e % D4, v[u]);
+        }
+    }
+}
+
 __global__ void gather_rows_scalar(const float* __restrict__ table, int64_t rows, int dim,
                                    const int64_t* __restrict__ idx, int64_t n, float* __restrict__ out, int64_t out_ld) {
     const int64_t total = n * dim;
@@ -135,6 +170,19 @@ __global__ void pad_rows_kernel(const float* __restrict__ src, int64_t rows, int
         const int64_t r = i / ld_dst;
         const int c = (int)(i - r * ld_dst);
         dst[i] = c < cols ? src[r * ld_src + c] : 0.f;
+    }
+}
+
+// pad_rows_kernel over up to two segments (blockIdx.y): both towers' first-layer weights
+__global__ void pad_rows_seg_kernel(PadSegs) {
+    const KArg(PadSegs)* ka = (const KArg(PadSegs)*)(__builtin_amdgcn_kernarg_segment_ptr());
+    const KArg(PadSeg)& S = ka->seg[blockIdx.y];
+    const int64_t total = S.rows * S.ld_dst;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / S.ld_dst;
+        const int c = (int)(i - r * S.ld_dst);
+        S.dst[i] = c < S.cols ? S.src[r * S.ld_src + c] : 0.f;
     }
 }
 
@@ -593,6 +641,61 @@ int launch_gather_rows(const float* table, int64_t table_rows, int dim, const in
         hipLaunchKernelGGL(gather_rows_scalar, dim3(grid_for(n * dim)), dim3(256), 0, s, table, table_rows, dim, idx,
                            n, out, out_ld);
     }
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_gather_rows_segs(const GatherSegs& g, hipStream_t s) {
+    TTAMM_REQUIRE(g.count >= 0 && g.count <= 2, "gather: at most two segments");
+    bool one = g.count == 2;
+    int d4 = 0;
+    int64_t most = 0;
+    for (int i = 0; i < g.count; ++i) {
+        const GatherSeg& q = g.seg[i];
+        one = one && q.dim == g.seg[0].dim && q.dim % 4 == 0 && q.out_ld % 4 == 0 &&
+              ((uintptr_t)q.table | (uintptr_t)q.out) % 16 == 0;
+        d4 = q.dim / 4;
+        most = q.n > most ? q.n : most;
+    }
+    auto seg = [&](auto K) {
+        constexpr int D4 = decltype(K)::value;
+        const int64_t rows_per_block = (int64_t)WideGather<D4>::RPW * 4;
+        int64_t blocks = ceil_div(most, rows_per_block);
+        if (blocks > 8192) blocks = 8192;
+        hipLaunchKernelGGL(gather_rows_wide_seg<D4>, dim3((unsigned)blocks, 2), dim3(256), 0, s, g);
+        return true;
+    };
+    bool done = false;
+    if (one && most > 0) {
+        switch (d4) {
+            case 8: done = seg(std::integral_constant<int, 8>{}); break;
+            case 16: done = seg(std::integral_constant<int, 16>{}); break;
+            case 24: done = seg(std::integral_constant<int, 24>{}); break;
+            case 32: done = seg(std::integral_constant<int, 32>{}); break;
+            case 48: done = seg(std::integral_constant<int, 48>{}); break;
+            case 64: done = seg(std::integral_constant<int, 64>{}); break;
+            default: break;
+        }
+    }
+    if (done) {
+        TTAMM_LAUNCH_CHECK();
+        return TTAMM_OK;
+    }
+    for (int i = 0; i < g.count; ++i) {
+        const GatherSeg& q = g.seg[i];
+        const int rc = launch_gather_rows(q.table, q.rows, q.dim, q.idx, q.n, q.out, q.out_ld, s);
+        if (rc) return rc;
+    }
+    return TTAMM_OK;
+}
+
+int launch_pad_rows_segs(const PadSegs& p, hipStream_t s) {
+    TTAMM_REQUIRE(p.count >= 0 && p.count <= 2, "pad rows: at most two segments");
+    if (p.count == 0) return TTAMM_OK;
+    int64_t most = 0;
+    for (int i = 0; i < p.count; ++i) most = p.seg[i].rows * p.seg[i].ld_dst > most ? p.seg[i].rows * p.seg[i].ld_dst : most;
+    if (most == 0) return TTAMM_OK;
+    hipLaunchKernelGGL(pad_rows_seg_kernel, dim3(grid_for(most), p.count), dim3(256), 0, s, p);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

@@ -513,7 +513,9 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
                   int ntowers, void* const* l0_events = nullptr, int part = FWD_ALL, hipEvent_t after_l0 = nullptr) {
     int rc;
     if (part & FWD_MLP) {
-        // ID rows -> e (ef[:, :D] when gated)
+        // ID rows -> e (ef[:, :D] when gated): both towers' gathers in one launch
+        GatherSegs gs;
+        gs.count = 0;
         for (int k = 0; k < ntowers; ++k) {
             const ttamm_tower& t = *T[k];
             TowerWs& w = *W[k];
@@ -536,7 +538,7 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
             }
             float* dst = uses_ef(t) ? w.ef : w.e;
             const int64_t ld = uses_ef(t) ? efw(t) : t.id.dim;
-            if ((rc = launch_gather_rows(t.id.weight, t.id.rows, t.id.dim, w.idx, w.R, dst, ld, s))) return rc;
+            gs.seg[gs.count++] = GatherSeg{t.id.weight, t.id.rows, t.id.dim, w.idx, w.R, dst, ld};
             if (t.fusion != TTAMM_FUSION_IDENTITY && t.n_linear == 0 && w.R > 0) {
                 // identity feature encoder (encoders.py:114-119): f = the feature row
                 float* fdst = uses_ef(t) ? w.ef + t.id.dim : w.f;
@@ -544,12 +546,15 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
                     return rc;
             }
         }
+        if ((rc = launch_gather_rows_segs(gs, s))) return rc;
         // feature encoder layers
         int maxL = 0;
         for (int k = 0; k < ntowers; ++k)
             if (T[k]->fusion != TTAMM_FUSION_IDENTITY) maxL = T[k]->n_linear > maxL ? T[k]->n_linear : maxL;
         for (int l = 0; l < maxL; ++l) {
             Batcher bb;
+            PadSegs pads;  // first-layer weights padded to 16-B rows, both towers in one launch
+            pads.count = 0;
             for (int k = 0; k < ntowers; ++k) {
                 const ttamm_tower& t = *T[k];
                 TowerWs& w = *W[k];
@@ -576,9 +581,8 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
                     p.B16 = w.w16;
                     p.ldb = kp;
                 } else if (l == 0 && w.wpad) {
-                    if ((rc = launch_pad_rows(L.weight, L.out_features, L.in_features, L.in_features, w.wpad,
-                                              round4(L.in_features), s)))
-                        return rc;
+                    pads.seg[pads.count++] = PadSeg{L.weight, L.out_features, L.in_features, L.in_features, w.wpad,
+                                                    round4(L.in_features)};
                     p.B = w.wpad;
                     p.ldb = round4(L.in_features);
                 }
@@ -616,6 +620,7 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
                 }
                 bb.add(p);
             }
+            if ((rc = launch_pad_rows_segs(pads, s))) return rc;
             const bool timed = l == 0 && l0_events && l0_events[0] && l0_events[1];
             if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)l0_events[0], s));
             if ((rc = bb.run(s))) return rc;
