@@ -484,8 +484,10 @@ def main() -> None:
                "kernel": "replay_kernel (deferred AdamW g=0): rolling slice + user / item catch-up lists + the "
                          "closing flush's share, per step",
                "ms_per_step": round(rep_ms, 4),
-               "parts_ms_per_step": {"slice": round(slice_ms, 4), "catchup_user": round(cu_user_ms, 4),
-                                     "catchup_item": round(cu_item_ms, 4), "closing_flush_share": round(flush_share, 4)},
+               # the catch-up of both towers' touched rows is one replay launch (user + item
+               # events when the towers are prepared separately)
+               "parts_ms_per_step": {"slice": round(slice_ms, 4), "catchup": round(cu_user_ms + cu_item_ms, 4),
+                                     "closing_flush_share": round(flush_share, 4)},
                "element_steps_per_step": es_per_step, "unit": "wave-instr/s", "peak": VALU_WAVE_INSTR_PEAK,
                "valu_lane_instr_per_element_step": per_es,
                "note": "achieved = element-steps per step x VALU lane-instructions per element-step (SQ_INSTS_VALU "

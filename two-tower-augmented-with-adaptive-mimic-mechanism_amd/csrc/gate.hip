@@ -23,6 +23,8 @@
 // supplies k-slot q).  The A fragment of that step is W[16*ob + li][16t + 4q + r]: four
 // consecutive floats of an LDS row, one ds_read_b128 per four MFMAs.  All four r-steps of a
 // k-tile are issued across the output tiles, so consecutive MFMAs never share an accumulator.
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace ttamm {
@@ -67,6 +69,81 @@ __device__ __forceinline__ void tile_gemm(const float* w_lds, int ob0, const f4v
     }
 }
 
+// ---- split-bf16 form of the wider GEMM of each direction (G1 forward, G1^T backward) ----------
+// The fp32 weight is staged once per block as three bf16 planes (hi, mid, lo: hi + mid + lo = w
+// exactly, gemm.hip split_bf16) and each product is six v_mfma_f32_16x16x32_bf16 (hh, hm, mh,
+// hl, lh, mm), accumulated in fp32: 6 x 16 cycles per 16 x 16 x 32 step against 8 x 32 cycles of
+// v_mfma_f32_16x16x4_f32 for the same product.  The 32 k-slots of step t are, for lane group q,
+// columns {32 t + 4 q + j, 32 t + 16 + 4 q + j : j < 4} — exactly the two float4s the lane holds
+// from load_row (its k-tiles 2t and 2t + 1) — so the B operand is the lane's own registers,
+// split in place, and the weight planes are laid out [t][q][row][8 slots] (one ds_read_b128 per
+// plane and fragment, 16 lanes reading 256 contiguous bytes).
+typedef __bf16 g_bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 g_bf16x4 __attribute__((ext_vector_type(4)));
+typedef float g_f32x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split8(f4v a, f4v b, g_bf16x8& h, g_bf16x8& m, g_bf16x8& l) {
+    const g_f32x8 x = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    h = __builtin_convertvector(x, g_bf16x8);
+    const g_f32x8 r = x - __builtin_convertvector(h, g_f32x8);
+    m = __builtin_convertvector(r, g_bf16x8);
+    l = __builtin_convertvector(r - __builtin_convertvector(m, g_f32x8), g_bf16x8);
+}
+
+// byte offset of slot (t, q, j) of weight row f in one plane of an [NT][4][NF][8] image
+template <int NF>
+__device__ __forceinline__ int xw_off(int t, int q, int f, int j) {
+    return ((t * 4 + q) * NF + f) * 16 + j * 2;
+}
+// slot of k index c (k-step t, lane group q, slot j)
+__device__ __forceinline__ void xw_slot(int c, int& t, int& q, int& j) {
+    t = c >> 5;
+    const int r = c & 31;
+    q = (r & 15) >> 2;
+    j = ((r >> 4) << 2) | (r & 3);
+}
+// split 4 consecutive weights (the same t, q, consecutive j) into the three planes
+template <int NF, int PLANE>
+__device__ __forceinline__ void xw_store4(unsigned char* img, int t, int q, int f, int j0, f4v w) {
+    const f4v hf = w;
+    const g_bf16x4 h = __builtin_convertvector(hf, g_bf16x4);
+    const f4v r = hf - __builtin_convertvector(h, f4v);
+    const g_bf16x4 m = __builtin_convertvector(r, g_bf16x4);
+    const g_bf16x4 l = __builtin_convertvector(r - __builtin_convertvector(m, f4v), g_bf16x4);
+    const int off = xw_off<NF>(t, q, f, j0);
+    *reinterpret_cast<g_bf16x4*>(img + off) = h;
+    *reinterpret_cast<g_bf16x4*>(img + PLANE + off) = m;
+    *reinterpret_cast<g_bf16x4*>(img + 2 * PLANE + off) = l;
+}
+
+// acc[ob] += W[16 (ob0 + ob) + li][k] * b[k] over the NT k-steps of 32 (b: 2 NT float4s of the
+// lane, load_row layout), W from its three-plane image ([NT][4][NF][8] bf16 per plane)
+template <int NO, int NT, int NF>
+__device__ __forceinline__ void tile_gemm_x(const unsigned char* img, int ob0, const f4v* b, f4v (&acc)[NO], int li,
+                                            int q) {
+    constexpr int PLANE = NT * 4 * NF * 16;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        g_bf16x8 bh, bm, bl;
+        split8(b[2 * t], b[2 * t + 1], bh, bm, bl);
+        const unsigned char* base = img + xw_off<NF>(t, q, 16 * ob0 + li, 0);
+#pragma unroll
+        for (int ob = 0; ob < NO; ++ob) {
+            const unsigned char* p = base + ob * 16 * 16;
+            const g_bf16x8 ah = *reinterpret_cast<const g_bf16x8*>(p);
+            const g_bf16x8 am = *reinterpret_cast<const g_bf16x8*>(p + PLANE);
+            const g_bf16x8 al = *reinterpret_cast<const g_bf16x8*>(p + 2 * PLANE);
+            acc[ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, acc[ob], 0, 0, 0);  // small terms first
+            acc[ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc[ob], 0, 0, 0);
+            acc[ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc[ob], 0, 0, 0);
+            acc[ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, acc[ob], 0, 0, 0);
+            acc[ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, acc[ob], 0, 0, 0);
+            acc[ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc[ob], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 template <int N>
 __device__ __forceinline__ void zero(f4v (&a)[N]) {
 #pragma unroll
@@ -92,6 +169,12 @@ struct GateCfg {
     static constexpr int B_LDS = HG * B_LD1 + 2 * D * B_LD2;
     static_assert(D % 16 == 0 && HG % 16 == 0, "16-feature tiles");
     static_assert(F_LDS * 4 <= 163840 && B_LDS * 4 <= 163840, "the gate matrices must fit one CU's LDS");
+    // split-bf16: G1 (forward, [HG] rows x 2D k) / G1^T (backward, [2D] rows x HG k) as three bf16
+    // planes, 2 B x 3 per weight; G2 / G2^T stay fp32 (the 16x16x4 f32 GEMM)
+    static constexpr int X1_BYTES = 3 * 2 * (2 * D) * HG;
+    static constexpr int XF_BYTES = X1_BYTES + 4 * (D * F_LD2 + HG + D);
+    static constexpr int XB_BYTES = X1_BYTES + 4 * (HG * B_LD1);
+    static constexpr bool X_OK = (2 * D) % 32 == 0 && HG % 32 == 0 && XF_BYTES <= 163840 && XB_BYTES <= 163840;
 };
 
 // this block's tower and its index among the tower's blocks
@@ -104,15 +187,17 @@ __device__ __forceinline__ int gate_tower(const KArg(GateArgs) * ka, int& bidx) 
     return 0;
 }
 
-template <int D, int HG>
+template <int D, int HG, bool X>
 __global__ __launch_bounds__(kGateThreads) void gate_fwd_kernel(GateArgs) {
     using C = GateCfg<D, HG>;
-    __shared__ __attribute__((aligned(16))) float lds[C::F_LDS];
+    constexpr int NX = (2 * D) / 32;  // split: k-steps of the first GEMM
+    __shared__ __attribute__((aligned(16))) float lds[X ? C::XF_BYTES / 4 : C::F_LDS];
     const KArg(GateArgs)* ka = (const KArg(GateArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
     int bidx;
     const KArg(GateTower)& T = ka->tw[gate_tower(ka, bidx)];
-    float* g1s = lds;
-    float* g2s = g1s + HG * C::F_LD1;
+    float* g1s = lds;  // fp32 G1, or (X) its three bf16 planes
+    unsigned char* img = reinterpret_cast<unsigned char*>(lds);
+    float* g2s = X ? reinterpret_cast<float*>(img + C::X1_BYTES) : g1s + HG * C::F_LD1;
     float* c1s = g2s + D * C::F_LD2;
     float* c2s = c1s + HG;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -135,7 +220,14 @@ __global__ __launch_bounds__(kGateThreads) void gate_fwd_kernel(GateArgs) {
         const int e = e0 + (int)threadIdx.x;
         if (e < N1) {
             const int i = e / (2 * D / 4), c = 4 * (e % (2 * D / 4));
-            *reinterpret_cast<f4v*>(g1s + i * C::F_LD1 + c) = ldg4(T.G1 + (int64_t)i * 2 * D + c);
+            const f4v w = ldg4(T.G1 + (int64_t)i * 2 * D + c);
+            if constexpr (X) {
+                int t, q4, j;
+                xw_slot(c, t, q4, j);
+                xw_store4<HG, C::X1_BYTES / 3>(img, t, q4, i, j, w);
+            } else {
+                *reinterpret_cast<f4v*>(g1s + i * C::F_LD1 + c) = w;
+            }
         }
     }
 #pragma unroll
@@ -151,12 +243,12 @@ __global__ __launch_bounds__(kGateThreads) void gate_fwd_kernel(GateArgs) {
     for (; s < nslab; s += stride) {
         const int64_t row = s * 16 + li;
         const bool ok = row < R;
-        const int64_t rr = ok ? row : R - 1;
         f4v a[C::TD];  // mimic rows for the epilogue, requested before the MFMA chain
         if (T.table) load_row(a, T.table, D, arow, q);
         f4v z[C::TH];
         zero(z);
-        tile_gemm<C::TH, C::TE, C::F_LD1>(g1s, 0, ef, z, li, q);  // z^T = G1 . ef^T
+        if constexpr (X) tile_gemm_x<C::TH, NX, HG>(img, 0, ef, z, li, q);  // z^T = G1 . ef^T
+        else tile_gemm<C::TH, C::TE, C::F_LD1>(g1s, 0, ef, z, li, q);
         // the next slab's rows, in flight during the rest of this one
         f4v nx[C::TE];
         int64_t arow_n = 0;
@@ -210,15 +302,17 @@ __global__ __launch_bounds__(kGateThreads) void gate_fwd_kernel(GateArgs) {
     }
 }
 
-template <int D, int HG>
+template <int D, int HG, bool X>
 __global__ __launch_bounds__(kGateThreads) void gate_bwd_kernel(GateArgs) {
     using C = GateCfg<D, HG>;
-    __shared__ __attribute__((aligned(16))) float lds[C::B_LDS];
+    constexpr int NX = HG / 32;  // split: k-steps of the dEF GEMM
+    __shared__ __attribute__((aligned(16))) float lds[X ? C::XB_BYTES / 4 : C::B_LDS];
     const KArg(GateArgs)* ka = (const KArg(GateArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
     int bidx;
     const KArg(GateTower)& T = ka->tw[gate_tower(ka, bidx)];
-    float* g2t = lds;                  // G2^T [HG][D]
-    float* g1t = lds + HG * C::B_LD1;  // G1^T [2D][HG]
+    unsigned char* img = reinterpret_cast<unsigned char*>(lds);  // (X) G1^T as three bf16 planes
+    float* g2t = X ? reinterpret_cast<float*>(img + C::X1_BYTES) : lds;  // G2^T [HG][D]
+    float* g1t = lds + HG * C::B_LD1;                                    // G1^T [2D][HG]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
     const int64_t R = T.R;
@@ -242,8 +336,26 @@ __global__ __launch_bounds__(kGateThreads) void gate_bwd_kernel(GateArgs) {
         if (e < N1) {
             const int j = e / (2 * D / 4), c = 4 * (e % (2 * D / 4));  // G1 [HG][2D]
             const f4v v = ldg4(T.G1 + (int64_t)j * 2 * D + c);
+            if constexpr (X) {  // hidden unit j is k slot (t, q4, js) of rows c .. c + 3
+                int t, q4, js;
+                xw_slot(j, t, q4, js);
+                constexpr int PL = C::X1_BYTES / 3;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) g1t[(c + i) * C::B_LD2 + j] = v[i];
+                for (int i = 0; i < 4; ++i) {
+                    const float w = v[i];
+                    const __bf16 h = (__bf16)w;
+                    const float r = w - (float)h;
+                    const __bf16 m = (__bf16)r;
+                    const __bf16 l = (__bf16)(r - (float)m);
+                    const int off = xw_off<2 * D>(t, q4, c + i, js);
+                    *reinterpret_cast<__bf16*>(img + off) = h;
+                    *reinterpret_cast<__bf16*>(img + PL + off) = m;
+                    *reinterpret_cast<__bf16*>(img + 2 * PL + off) = l;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) g1t[(c + i) * C::B_LD2 + j] = v[i];
+            }
         }
     }
     __syncthreads();
@@ -283,7 +395,8 @@ __global__ __launch_bounds__(kGateThreads) void gate_bwd_kernel(GateArgs) {
         for (int half = 0; half < 2; ++half) {
             f4v de[C::TD];
             zero(de);
-            tile_gemm<C::TD, C::TH, C::B_LD2>(g1t, half * C::TD, dz, de, li, q);
+            if constexpr (X) tile_gemm_x<C::TD, NX, 2 * D>(img, half * C::TD, dz, de, li, q);
+            else tile_gemm<C::TD, C::TH, C::B_LD2>(g1t, half * C::TD, dz, de, li, q);
             if (ok) {
 #pragma unroll
                 for (int ob = 0; ob < C::TD; ++ob) {
@@ -323,8 +436,20 @@ int gate_blocks(GateArgs& a) {
 template <int D, int HG>
 int launch_gate_t(GateArgs& a, bool backward, hipStream_t s) {
     const int blocks = gate_blocks(a);
-    if (backward) hipLaunchKernelGGL((gate_bwd_kernel<D, HG>), dim3(blocks), dim3(kGateThreads), 0, s, a);
-    else hipLaunchKernelGGL((gate_fwd_kernel<D, HG>), dim3(blocks), dim3(kGateThreads), 0, s, a);
+    // TTAMM_GATE_SPLIT=1: the 2D-wide GEMM on split-bf16 MFMA.  Measured at C2 (D = 96): forward
+    // 64 -> 62 us, backward 67 -> 79 us, step 0.726 -> 0.758 ms (profiles/r03_c2_gate_split_s17.txt):
+    // the kernels are not MFMA-bound (SQ: ~31 % MFMA busy, profiles/r03_c2_pmc_sq_s13.json) and the
+    // split variant runs at the 256-VGPR limit, so both GEMMs stay on v_mfma_f32_16x16x4_f32
+    static const bool split = std::getenv("TTAMM_GATE_SPLIT") != nullptr;
+    constexpr bool XOK = GateCfg<D, HG>::X_OK;
+    if (XOK && split) {
+        if (backward) hipLaunchKernelGGL((gate_bwd_kernel<D, HG, XOK>), dim3(blocks), dim3(kGateThreads), 0, s, a);
+        else hipLaunchKernelGGL((gate_fwd_kernel<D, HG, XOK>), dim3(blocks), dim3(kGateThreads), 0, s, a);
+        TTAMM_LAUNCH_CHECK();
+        return TTAMM_OK;
+    }
+    if (backward) hipLaunchKernelGGL((gate_bwd_kernel<D, HG, false>), dim3(blocks), dim3(kGateThreads), 0, s, a);
+    else hipLaunchKernelGGL((gate_fwd_kernel<D, HG, false>), dim3(blocks), dim3(kGateThreads), 0, s, a);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

@@ -549,6 +549,30 @@ void catchup_bind(CatchupList& cl, int32_t* ints, int64_t n, int cap);
 int launch_catchup_list(const int64_t* idx, int64_t n, const int32_t* first, int32_t* const* last, int nlast,
                         int32_t target, int cap, const CatchupList& cl, const uint32_t* status, hipStream_t s);
 
+// Part A of both towers' step prologue in three launches: the coalesce count of each tower's
+// batch (as launch_coalesce_count; it also zeroes the tower's catch-up list counters), then —
+// for towers with a list (list_cnt != null: deferred dense-group tables) — the catch-up list
+// (as launch_catchup_list, cnt / fill = list_cnt[0 .. cap], list_cnt[cap + 1 .. 2 cap + 1]).
+struct PrepSeg {
+    const int64_t* idx;
+    int64_t n;
+    int32_t* cnt;    // CoalesceWs cnt / first
+    int32_t* first;
+    int32_t* list_cnt;  // CatchupList cnt (fill follows it) or null
+    int32_t* list_rows;
+    int32_t* list_lag;
+    int32_t* last[2];
+    int nlast;
+};
+struct PrepSegs {
+    PrepSeg seg[2];
+    int count;
+    int32_t target;
+    int cap;
+    const uint32_t* status;
+};
+int launch_prepare_segs(const PrepSegs& a, hipStream_t s);
+
 struct SweepSeg {
     float* p;
     float* m;

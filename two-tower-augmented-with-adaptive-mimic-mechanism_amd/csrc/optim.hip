@@ -103,6 +103,20 @@ __global__ void co_count_kernel(const int64_t* __restrict__ idx, int64_t n, int3
     atomicMax(&first[key], (int32_t)(INT_MAX - p));
 }
 
+// co_count_kernel over up to two towers (blockIdx.y = tower); each tower's first block also
+// zeroes its catch-up list counters (CatchupList cnt + fill), which the next launch reads
+__global__ void co_count_seg_kernel(PrepSegs) {
+    const KArg(PrepSegs)* ka = (const KArg(PrepSegs)*)(__builtin_amdgcn_kernarg_segment_ptr());
+    const KArg(PrepSeg)& S = ka->seg[blockIdx.y];
+    if (blockIdx.x == 0 && S.list_cnt)
+        for (int i = threadIdx.x; i < 2 * (ka->cap + 1); i += blockDim.x) S.list_cnt[i] = 0;  // cnt, fill
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= S.n) return;
+    const int64_t key = S.idx[p];
+    atomicAdd(&S.cnt[key], 1);
+    atomicMax(&S.first[key], (int32_t)(INT_MAX - p));
+}
+
 // Entry i of the segment scan: (flag, count) — a position's leader flag and its row's count,
 // or (sorted mode, entries = the key range) whether key i occurs and its count.
 __device__ __forceinline__ void co_entry(int by_key, int64_t i, const int64_t* __restrict__ idx,
@@ -803,12 +817,9 @@ __device__ __forceinline__ int32_t catchup_lag(const int64_t* __restrict__ idx, 
 }
 
 // rows per lag: a block histogram in LDS, then one atomic per (block, lag); cnt[0] = all rows
-__global__ __launch_bounds__(256) void catchup_count_kernel(const int64_t* __restrict__ idx, int64_t n,
-                                                            const int32_t* __restrict__ first,
-                                                            const int32_t* __restrict__ last, int32_t target, int cap,
-                                                            int32_t* __restrict__ cnt, const uint32_t* status) {
-    __shared__ int32_t h[kMaxHistory + 1];
-    if (step_poisoned(status)) return;
+__device__ __forceinline__ void catchup_count_block(const int64_t* __restrict__ idx, int64_t n,
+                                                    const int32_t* __restrict__ first, const int32_t* __restrict__ last,
+                                                    int32_t target, int cap, int32_t* __restrict__ cnt, int32_t* h) {
     for (int i = threadIdx.x; i <= cap; i += blockDim.x) h[i] = 0;
     __syncthreads();
     int64_t row = 0;
@@ -822,6 +833,24 @@ __global__ __launch_bounds__(256) void catchup_count_kernel(const int64_t* __res
         if (h[i]) atomicAdd(&cnt[i], h[i]);
 }
 
+__global__ __launch_bounds__(256) void catchup_count_kernel(const int64_t* __restrict__ idx, int64_t n,
+                                                            const int32_t* __restrict__ first,
+                                                            const int32_t* __restrict__ last, int32_t target, int cap,
+                                                            int32_t* __restrict__ cnt, const uint32_t* status) {
+    __shared__ int32_t h[kMaxHistory + 1];
+    if (step_poisoned(status)) return;
+    catchup_count_block(idx, n, first, last, target, cap, cnt, h);
+}
+
+// both towers' lists in one launch (blockIdx.y = tower)
+__global__ __launch_bounds__(256) void catchup_count_seg_kernel(PrepSegs) {
+    const KArg(PrepSegs)* ka = (const KArg(PrepSegs)*)(__builtin_amdgcn_kernarg_segment_ptr());
+    const KArg(PrepSeg)& S = ka->seg[blockIdx.y];
+    __shared__ int32_t h[kMaxHistory + 1];
+    if (step_poisoned(ka->status) || S.list_cnt == nullptr) return;
+    catchup_count_block(S.idx, S.n, S.first, S.last[0], ka->target, ka->cap, S.list_cnt, h);
+}
+
 struct LastPtrs {
     int32_t* p[2];
 };
@@ -829,15 +858,12 @@ struct LastPtrs {
 // each listed row into its lag's range of the list (longest lag first: lag b starts at
 // sum_{b' > b} cnt[b']), in block order within a lag (atomics: any order — every row's replay is
 // independent of the others), then stamped current in every table of the tower
-__global__ __launch_bounds__(256) void catchup_scatter_kernel(const int64_t* __restrict__ idx, int64_t n,
-                                                              const int32_t* __restrict__ first, LastPtrs last,
-                                                              int nlast, int32_t target, int cap,
-                                                              const int32_t* __restrict__ cnt,
-                                                              int32_t* __restrict__ fill, int32_t* __restrict__ rows,
-                                                              int32_t* __restrict__ lags, const uint32_t* status) {
-    __shared__ int32_t suf[2][kMaxHistory + 2];  // suffix sums of cnt[1..cap] (double buffered)
-    __shared__ int32_t h[kMaxHistory + 1], base[kMaxHistory + 1];
-    if (step_poisoned(status)) return;
+__device__ __forceinline__ void catchup_scatter_block(const int64_t* __restrict__ idx, int64_t n,
+                                                      const int32_t* __restrict__ first, int32_t* const* last,
+                                                      int nlast, int32_t target, int cap,
+                                                      const int32_t* __restrict__ cnt, int32_t* __restrict__ fill,
+                                                      int32_t* __restrict__ rows, int32_t* __restrict__ lags,
+                                                      int32_t (*suf)[kMaxHistory + 2], int32_t* h, int32_t* base) {
     const int tid = threadIdx.x;
     for (int i = tid; i <= cap + 1; i += blockDim.x) {
         suf[0][i] = (i >= 1 && i <= cap) ? cnt[i] : 0;
@@ -852,7 +878,7 @@ __global__ __launch_bounds__(256) void catchup_scatter_kernel(const int64_t* __r
         __syncthreads();
     }
     int64_t row = 0;
-    const int32_t lag = catchup_lag(idx, (int64_t)blockIdx.x * blockDim.x + tid, n, first, last.p[0], target, row);
+    const int32_t lag = catchup_lag(idx, (int64_t)blockIdx.x * blockDim.x + tid, n, first, last[0], target, row);
     int32_t rank = 0;
     if (lag > 0) rank = atomicAdd(&h[lag], 1);
     __syncthreads();
@@ -863,8 +889,31 @@ __global__ __launch_bounds__(256) void catchup_scatter_kernel(const int64_t* __r
         const int32_t slot = suf[cur][lag + 1] + base[lag] + rank;
         rows[slot] = (int32_t)row;
         lags[slot] = lag;
-        for (int t = 0; t < nlast; ++t) last.p[t][row] = target;
+        for (int t = 0; t < nlast; ++t) last[t][row] = target;
     }
+}
+
+__global__ __launch_bounds__(256) void catchup_scatter_kernel(const int64_t* __restrict__ idx, int64_t n,
+                                                              const int32_t* __restrict__ first, LastPtrs last,
+                                                              int nlast, int32_t target, int cap,
+                                                              const int32_t* __restrict__ cnt,
+                                                              int32_t* __restrict__ fill, int32_t* __restrict__ rows,
+                                                              int32_t* __restrict__ lags, const uint32_t* status) {
+    __shared__ int32_t suf[2][kMaxHistory + 2];  // suffix sums of cnt[1..cap] (double buffered)
+    __shared__ int32_t h[kMaxHistory + 1], base[kMaxHistory + 1];
+    if (step_poisoned(status)) return;
+    catchup_scatter_block(idx, n, first, last.p, nlast, target, cap, cnt, fill, rows, lags, suf, h, base);
+}
+
+__global__ __launch_bounds__(256) void catchup_scatter_seg_kernel(PrepSegs) {
+    const KArg(PrepSegs)* ka = (const KArg(PrepSegs)*)(__builtin_amdgcn_kernarg_segment_ptr());
+    const KArg(PrepSeg)& S = ka->seg[blockIdx.y];
+    __shared__ int32_t suf[2][kMaxHistory + 2];
+    __shared__ int32_t h[kMaxHistory + 1], base[kMaxHistory + 1];
+    if (step_poisoned(ka->status) || S.list_cnt == nullptr) return;
+    int32_t* last[2] = {S.last[0], S.last[1]};
+    catchup_scatter_block(S.idx, S.n, S.first, last, S.nlast, ka->target, ka->cap, S.list_cnt,
+                          S.list_cnt + (ka->cap + 1), S.list_rows, S.list_lag, suf, h, base);
 }
 
 __global__ void side_scatter_kernel(const int32_t* __restrict__ n_unique, const int32_t* __restrict__ keys,
@@ -1281,6 +1330,30 @@ int launch_catchup_list(const int64_t* idx, int64_t n, const int32_t* first, int
     LastPtrs lp{{last[0], nlast > 1 ? last[1] : nullptr}};
     hipLaunchKernelGGL(catchup_scatter_kernel, dim3(g), dim3(256), 0, s, idx, n, first, lp, nlast, target, cap, cl.cnt,
                        cl.fill, cl.rows, cl.lag, status);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+int launch_prepare_segs(const PrepSegs& a, hipStream_t s) {
+    TTAMM_REQUIRE(a.count >= 1 && a.count <= 2, "prepare: one or two towers");
+    int64_t most = 0;
+    bool lists = false;
+    for (int i = 0; i < a.count; ++i) {
+        const PrepSeg& g = a.seg[i];
+        TTAMM_REQUIRE(g.idx && g.cnt && g.first && g.n >= 0 && g.n < (int64_t(1) << 31) - 1, "prepare: bad tower");
+        TTAMM_REQUIRE(!g.list_cnt || (g.list_rows && g.list_lag && g.last[0] && g.nlast >= 1 && g.nlast <= 2 &&
+                                      a.cap > 1 && a.cap <= kMaxHistory),
+                      "prepare: catch-up list incomplete");
+        most = g.n > most ? g.n : most;
+        lists = lists || g.list_cnt;
+    }
+    const unsigned g = (unsigned)std::max<int64_t>(1, ceil_div(most, 256));
+    hipLaunchKernelGGL(co_count_seg_kernel, dim3(g, a.count), dim3(256), 0, s, a);
+    TTAMM_LAUNCH_CHECK();
+    if (!lists || most == 0) return TTAMM_OK;
+    hipLaunchKernelGGL(catchup_count_seg_kernel, dim3(g, a.count), dim3(256), 0, s, a);
+    TTAMM_LAUNCH_CHECK();
+    hipLaunchKernelGGL(catchup_scatter_seg_kernel, dim3(g, a.count), dim3(256), 0, s, a);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

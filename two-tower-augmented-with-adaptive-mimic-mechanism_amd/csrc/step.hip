@@ -934,6 +934,12 @@ struct Deferred {
     // one-process step with the aux stream: the rolling slice runs there (replay_slice_aux)
     // instead of at the end of the main stream's step
     bool slice_on_aux = false;
+    // TTAMM_SLICE_LATE=1: launched when the main stream reaches the table updates (overlapping
+    // the memory-bound row updates and the next step's prologue) rather than behind the grouping
+    // (overlapping the backward GEMMs).  Measured at C2: the weight-gradient GEMM runs uncontended
+    // (132 -> 76 us) but the row updates slow by as much, step 0.7326 vs 0.7280 ms
+    // (profiles/r03_c2_slice_late_vs_early_s16.txt) — so behind the grouping stays the default.
+    bool slice_late = false;
 };
 
 // The tables of a tower that belong to the dense (AdamW) group.
@@ -1022,6 +1028,63 @@ int tower_prepare_a(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred
     return launch_replay(ra, s, ev);
 }
 
+// tower_prepare_a of `n` towers in four launches (launch_prepare_segs: the counts, the catch-up
+// lists' counts and scatters; then one replay over every tower's list) instead of 5-6 per tower:
+// the aux stream's prologue is a chain of small launches that the gate waits for.
+// ev: 2 events around the replay kernel (bench).
+int towers_prepare_a(const ttamm_tower* const* T, TowerWs* const* W, int n, bool mimic, const Deferred& df,
+                     hipStream_t s, void* const* ev = nullptr) {
+    PrepSegs ps;
+    std::memset(&ps, 0, sizeof(ps));
+    ps.target = df.step - 1;
+    ps.cap = df.cap;
+    ps.status = df.status;
+    ReplayArgs ra;
+    std::memset(&ra, 0, sizeof(ra));
+    ra.hist = df.hist;
+    ra.cap = df.cap;
+    ra.decoupled = df.decoupled;
+    ra.fast_g0 = df.fast;
+    ra.status = df.status;
+    ra.target = df.step - 1;
+    ra.stamp = 0;  // stamped by the list build
+    for (int k = 0; k < n; ++k) {
+        const ttamm_tower& t = *T[k];
+        TowerWs& w = *W[k];
+        const int64_t rows = t.id.rows;
+        TTAMM_REQUIRE(rows < (int64_t(1) << 31) && w.co.key_range >= rows && w.co.cnt && w.co.first,
+                      "coalesce: per-row scratch missing");
+        TTAMM_REQUIRE(!w.co.sorted || rows <= 65536, "coalesce: sorted grouping needs <= 65536 keys");
+        PrepSeg& g = ps.seg[ps.count++];
+        g.idx = w.idx;
+        g.n = w.R;
+        g.cnt = w.co.cnt;
+        g.first = w.co.first;
+        if (!df.on || w.R == 0) continue;
+        const ttamm_table* tabs[2];
+        const int nt = dense_tables(t, mimic, tabs);
+        if (nt == 0) continue;
+        TTAMM_REQUIRE(w.cl.cnt != nullptr, "deferred AdamW: catch-up list workspace missing");
+        g.list_cnt = w.cl.cnt;
+        g.list_rows = w.cl.rows;
+        g.list_lag = w.cl.lag;
+        g.nlast = nt;
+        for (int i = 0; i < nt; ++i) {
+            g.last[i] = tabs[i]->last_step;
+            ReplaySeg r = replay_seg(*tabs[i]);
+            r.row_lo = 0;
+            r.row_hi = w.R;
+            r.list_rows = w.cl.rows;
+            r.list_lag = w.cl.lag;
+            r.list_cnt = w.cl.cnt;
+            ra.seg[ra.count++] = r;
+        }
+    }
+    int rc;
+    if ((rc = launch_prepare_segs(ps, s))) return rc;
+    return launch_replay(ra, s, ev);
+}
+
 int tower_prepare_b(const ttamm_tower& t, TowerWs& w, hipStream_t s) {
     return launch_coalesce_group(w.idx, w.R, t.id.rows, w.co, s);
 }
@@ -1035,24 +1098,25 @@ int tower_prepare(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred& 
 
 // Fork / join events of the aux stream, one set per host thread and device (reused across
 // steps: a wait binds to the record that precedes it).  [0] fork, [1] rows current (before the
-// fusion), [2] rows grouped (before the table updates).
-int aux_events(hipEvent_t ev[3]) {
+// fusion), [2] rows grouped (before the table updates), [3] main stream at the table updates
+// (the late slice's start).
+int aux_events(hipEvent_t ev[4]) {
     struct Set {
         int dev;
-        hipEvent_t e[3];
+        hipEvent_t e[4];
     };
     thread_local std::vector<Set> cache;
     int dev = 0;
     TTAMM_HIP(hipGetDevice(&dev));
     for (const Set& p : cache)
         if (p.dev == dev) {
-            for (int i = 0; i < 3; ++i) ev[i] = p.e[i];
+            for (int i = 0; i < 4; ++i) ev[i] = p.e[i];
             return TTAMM_OK;
         }
-    Set p{dev, {nullptr, nullptr, nullptr}};
-    for (int i = 0; i < 3; ++i) TTAMM_HIP(hipEventCreateWithFlags(&p.e[i], hipEventDisableTiming));
+    Set p{dev, {nullptr, nullptr, nullptr, nullptr}};
+    for (int i = 0; i < 4; ++i) TTAMM_HIP(hipEventCreateWithFlags(&p.e[i], hipEventDisableTiming));
     cache.push_back(p);
-    for (int i = 0; i < 3; ++i) ev[i] = p.e[i];
+    for (int i = 0; i < 4; ++i) ev[i] = p.e[i];
     return TTAMM_OK;
 }
 
@@ -1069,7 +1133,8 @@ bool overlapped(const ttamm_tower* const* T, int n, const Deferred& df, hipStrea
 // (grouping), joined by table_updates.  A deferred dense ID table is read by the first gather,
 // so that case stays serial.
 // cu_events (optional): ttamm_step_args.timing_events + 8 — [0, 1] around the user tower's
-// catch-up replay, [2, 3] around the item tower's
+// catch-up replay, [2, 3] around the item tower's (overlapped: [0, 1] around the one replay of
+// both towers' lists)
 int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_batch& bt, int D, bool mimic,
                     const Deferred& df, hipStream_t s, hipStream_t aux, void* const* l0_events,
                     void* const* maint_events = nullptr, void* const* cu_events = nullptr) {
@@ -1084,7 +1149,7 @@ int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_b
     }
     // The MLP launches are enqueued first: the prologue is a dozen small launches whose
     // host-side enqueue would otherwise hold the GEMMs back behind the host.
-    hipEvent_t ev[3];
+    hipEvent_t ev[4];
     if ((rc = aux_events(ev))) return rc;
     // bf16 towers: the prologue starts after the first layer's GEMM (its one-block-per-CU tiles
     // otherwise wait for CUs behind the catch-up replay); fp32 towers: at once
@@ -1092,8 +1157,7 @@ int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_b
     if (!late_fork) TTAMM_HIP(hipEventRecord(ev[0], s));
     if ((rc = tower_forward(T, W, bt, D, mimic, s, n, l0_events, FWD_MLP, late_fork ? ev[0] : nullptr))) return rc;
     TTAMM_HIP(hipStreamWaitEvent(aux, ev[0], 0));
-    for (int k = 0; k < n; ++k)
-        if ((rc = tower_prepare_a(*T[k], *W[k], mimic, df, aux, cu_ev(k)))) return rc;
+    if ((rc = towers_prepare_a(T, W, n, mimic, df, aux, cu_ev(0)))) return rc;
     TTAMM_HIP(hipEventRecord(ev[1], aux));
     // the fusion is enqueued before the grouping's dozen launches: enqueued after them, the host
     // still issued them when the GPU finished the MLP (~55 us idle per C2 step)
@@ -1102,7 +1166,7 @@ int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_b
     for (int k = 0; k < n; ++k)
         if ((rc = tower_prepare_b(*T[k], *W[k], aux))) return rc;
     TTAMM_HIP(hipEventRecord(ev[2], aux));
-    if (df.slice_on_aux) {
+    if (df.slice_on_aux && !df.slice_late) {
         // The previous step's slice (target step - 1), behind this step's catch-up on the aux
         // stream, overlapping the main stream's GEMMs instead of closing the step.  The rows this
         // batch touches are current to step - 1 after the catch-up, so the slice skips them and
@@ -1116,7 +1180,7 @@ int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_b
 // the row updates need the grouping (prepare part B), possibly still running on the aux stream
 int join_grouping(hipStream_t s, hipStream_t aux) {
     if (aux == nullptr || aux == s) return TTAMM_OK;
-    hipEvent_t ev[3];
+    hipEvent_t ev[4];
     int rc;
     if ((rc = aux_events(ev))) return rc;
     TTAMM_HIP(hipStreamWaitEvent(s, ev[2], 0));
@@ -1193,6 +1257,16 @@ int table_updates(const ttamm_tower* T[2], TowerWs* W[2], int n, int D, bool mim
                   const float* grad_scale = nullptr) {
     int rc;
     if ((rc = join_grouping(s, aux))) return rc;
+    if (df.on && df.slice_on_aux && df.slice_late) {
+        // the previous step's slice (target step - 1, as in prepare_forward), started on the aux
+        // stream now: the catch-up and the grouping before it on that stream, the row updates
+        // beside it (the rows they touch are current to step - 1, so the slice skips them)
+        hipEvent_t ev[4];
+        if ((rc = aux_events(ev))) return rc;
+        TTAMM_HIP(hipEventRecord(ev[3], s));
+        TTAMM_HIP(hipStreamWaitEvent(aux, ev[3], 0));
+        if ((rc = replay_slice(T, n, mimic, df, df.step - 1, 2, events, aux))) return rc;
+    }
     for (int k = 0; k < n; ++k)
         if ((rc = tower_optimizer_rows(*T[k], *W[k], D, mimic, sp, ad, df, s, grad_scale))) return rc;
     if (df.on) {
@@ -1554,6 +1628,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     hipStream_t aux = static_cast<hipStream_t>(A.aux_stream);
     if (!shard) {
         df.slice_on_aux = df.on && overlapped(T, 2, df, s, aux) && !std::getenv("TTAMM_SLICE_MAIN");
+        df.slice_late = df.slice_on_aux && std::getenv("TTAMM_SLICE_LATE") != nullptr;
         if ((rc = prepare_forward(T, W, 2, A.b, D, mimic, df, s, aux, A.timing_events + 2, A.timing_events,
                                   A.timing_events + 8)))
             return rc;
