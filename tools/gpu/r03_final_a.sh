@@ -17,6 +17,8 @@ find gpurun_out/stats -name "*kernel_stats.csv" -exec cp {} gpurun_out/stats_ker
 rm -rf gpurun_out/stats
 timeout -k 10 300 python -u tools/bench_retrieval.py > gpurun_out/fa_c3.json 2> gpurun_out/fa_c3.err || { echo C3_FAIL; tail -5 gpurun_out/fa_c3.err; exit 1; }
 cat gpurun_out/fa_c3.json
+timeout -k 10 400 python -u bench.py --no-cpu-baseline --negatives in-batch > gpurun_out/fa_c2_inbatch.json 2> gpurun_out/fa_c2_inbatch.err || { echo IB_FAIL; tail -5 gpurun_out/fa_c2_inbatch.err; exit 1; }
+timeout -k 10 400 python -u bench.py --no-cpu-baseline --exact-table-math > gpurun_out/fa_c2_exact.json 2> gpurun_out/fa_c2_exact.err || { echo EX_FAIL; tail -5 gpurun_out/fa_c2_exact.err; exit 1; }
 for c in c4 c5; do
   timeout -k 10 400 python -u bench.py --config $c --no-cpu-baseline > gpurun_out/fa_$c.json 2> gpurun_out/fa_$c.err || { echo ${c}_FAIL; tail -5 gpurun_out/fa_$c.err; exit 1; }
 done
@@ -24,6 +26,6 @@ timeout -k 10 400 python -u bench.py --config c4 --emulate-world 8 --steps 40 --
 timeout -k 10 400 python -u bench.py --config c2 --emulate-world 8 --steps 100 --warmup 3 > gpurun_out/fa_c2_emu8.json 2> gpurun_out/fa_c2_emu8.err || { echo EMU2_FAIL; tail -20 gpurun_out/fa_c2_emu8.err; exit 1; }
 python3 -c "
 import json
-for f in ('fa_c4','fa_c5','fa_c4_emu8','fa_c2_emu8'):
+for f in ('fa_c2_inbatch','fa_c2_exact','fa_c4','fa_c5','fa_c4_emu8','fa_c2_emu8'):
     d=json.load(open('gpurun_out/'+f+'.json')); print(f, d['value'], d['ms_per_step'], d['roofline']['kernel'][:40], d['roofline'].get('frac'))"
 echo "pytest rc=$rc"

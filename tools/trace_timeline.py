@@ -7,10 +7,13 @@ import sys
 from collections import defaultdict
 
 rows = list(csv.DictReader(open(sys.argv[1])))
-marker = sys.argv[2] if len(sys.argv) > 2 else "sample_negatives_kernel"
+marker = sys.argv[2] if len(sys.argv) > 2 else None
 for r in rows:
     r["s"], r["e"] = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
 rows.sort(key=lambda r: r["s"])
+if marker is None:  # the step's first kernel: the fused prologue (round 3) or the sampler before it
+    marker = next((m for m in ("step_prologue_kernel", "sample_negatives_kernel")
+                   if any(m in r["Kernel_Name"] for r in rows)), "step_prologue_kernel")
 starts = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
 if len(starts) < 3:
     sys.exit(f"marker {marker} found {len(starts)} times")

@@ -266,12 +266,12 @@ __global__ __launch_bounds__(kGateThreads) void gate_fwd_kernel(GateArgs) {
                 const float v = z[ob][r] + c1[r];
                 z[ob][r] = v > 0.f ? v : 0.f;
             }
-            if (ok) stg4(T.z + row * HG + 16 * ob + 4 * q, z[ob]);
+            if (ok && !ka->ablate) stg4(T.z + row * HG + 16 * ob + 4 * q, z[ob]);
         }
         f4v x[C::TD];
         zero(x);
         tile_gemm<C::TD, C::TH, C::F_LD2>(g2s, 0, z, x, li, q);  // (pre-sigmoid)^T = G2 . z^T
-        if (ok) {
+        if (ok && !ka->ablate) {
 #pragma unroll
             for (int ob = 0; ob < C::TD; ++ob) {
                 const int col = 16 * ob + 4 * q;
@@ -379,7 +379,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_bwd_kernel(GateArgs) {
                     const float dg = d[t][r] * ef[t][r] - d[t][r] * ef[C::TD + t][r];
                     dq[t][r] = dg * (1.0f - g[t][r]) * g[t][r];
                 }
-                if (ok) stg4(T.dq + row * D + 16 * t + 4 * q, dq[t]);
+                if (ok && !ka->ablate) stg4(T.dq + row * D + 16 * t + 4 * q, dq[t]);
             }
             zero(dz);
             tile_gemm<C::TH, C::TD, C::B_LD1>(g2t, 0, dq, dz, li, q);  // dz^T = G2^T . dq^T
@@ -388,7 +388,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_bwd_kernel(GateArgs) {
         for (int ob = 0; ob < C::TH; ++ob) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) dz[ob][r] = zr[ob][r] > 0.f ? dz[ob][r] : 0.f;
-            if (ok) stg4(T.dz + row * HG + 16 * ob + 4 * q, dz[ob]);
+            if (ok && !ka->ablate) stg4(T.dz + row * HG + 16 * ob + 4 * q, dz[ob]);
         }
         // dEF^T = G1^T . dz^T + [dT g | dT (1 - g)], in two halves (e part, f part)
 #pragma unroll
@@ -397,7 +397,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_bwd_kernel(GateArgs) {
             zero(de);
             if constexpr (X) tile_gemm_x<C::TD, NX, 2 * D>(img, half * C::TD, dz, de, li, q);
             else tile_gemm<C::TD, C::TH, C::B_LD2>(g1t, half * C::TD, dz, de, li, q);
-            if (ok) {
+            if (ok && !ka->ablate) {
 #pragma unroll
                 for (int ob = 0; ob < C::TD; ++ob) {
 #pragma unroll
@@ -459,6 +459,8 @@ int launch_gate_t(GateArgs& a, bool backward, hipStream_t s) {
 bool gate_fused_supported(int D, int HG) { return D == HG && (D == 32 || D == 64 || D == 96); }
 
 int launch_gate(GateArgs& a, bool backward, hipStream_t s) {
+    static const bool ablate = std::getenv("TTAMM_GATE_ABLATE") != nullptr;
+    a.ablate = ablate ? 1 : 0;
     TTAMM_REQUIRE(a.count >= 1 && a.count <= 2 && gate_fused_supported(a.D, a.HG), "fused gate: unsupported shape");
     for (int i = 0; i < a.count; ++i) TTAMM_REQUIRE(a.tw[i].R > 0, "fused gate: empty tower");
     switch (a.D) {

@@ -168,6 +168,7 @@ struct GateArgs {
     GateTower tw[2];
     int count;
     int D, HG;
+    int ablate;  // developer timing ablation (TTAMM_GATE_ABLATE=1: no output stores); set by launch_gate
 };
 bool gate_fused_supported(int D, int HG);
 int launch_gate(GateArgs& a, bool backward, hipStream_t s);
@@ -631,5 +632,30 @@ int launch_sample_negatives(const int64_t* users, int64_t batch, int num_neg, in
                             const int64_t* pos_offsets, const int64_t* pos_values, uint64_t seed,
                             uint64_t counter, int64_t slot_base, int64_t* out, int64_t* out2, uint32_t* status,
                             hipStream_t s);  // out2: optional second copy
+
+// The step's prologue in one launch: staging (StageArgs), the negative sampler (when num_neg > 0;
+// as launch_sample_negatives, users = the RAW batch ids, range-checked against user_rows) and,
+// by the last block, launch_step_begin's work.  done: a uint32 in the zeroed workspace.
+struct PrologueArgs {
+    const int64_t* users;
+    int64_t user_rows;
+    int64_t batch;
+    int num_neg;
+    uint64_t num_items;
+    const int64_t* pos_offsets;
+    const int64_t* pos_values;
+    uint32_t k0, k1;
+    uint64_t counter;
+    int64_t slot_base;
+    int64_t* out;
+    int64_t* out2;
+    uint32_t* done;
+    int64_t* applied;
+    AdamConsts* hist;
+    int cap;
+    int64_t step;
+    AdamConsts c;
+};
+int launch_step_prologue(const StageArgs& st, const PrologueArgs& pa, hipStream_t s);
 
 }  // namespace ttamm

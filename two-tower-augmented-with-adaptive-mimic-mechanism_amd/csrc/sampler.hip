@@ -27,15 +27,12 @@ __device__ __forceinline__ bool is_positive(const int64_t* __restrict__ vals, in
     return false;
 }
 
-__global__ void sample_negatives_kernel(const int64_t* __restrict__ users, int64_t batch, int num_neg,
-                                        uint64_t num_items, const int64_t* __restrict__ pos_offsets,
-                                        const int64_t* __restrict__ pos_values, uint32_t k0, uint32_t k1,
-                                        uint64_t counter, int64_t slot_base, int64_t* __restrict__ out,
-                                        int64_t* __restrict__ out2, uint32_t* __restrict__ status) {
-    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (slot >= batch * num_neg) return;
-    const int64_t b = slot / num_neg;
-    const int64_t u = users[b];
+// slot `slot` of the batch's negatives for user row u (a staged, in-range id)
+__device__ __forceinline__ void sample_slot(int64_t slot, int64_t u, uint64_t num_items,
+                                            const int64_t* __restrict__ pos_offsets,
+                                            const int64_t* __restrict__ pos_values, uint32_t k0, uint32_t k1,
+                                            uint64_t counter, int64_t slot_base, int64_t* __restrict__ out,
+                                            int64_t* __restrict__ out2, uint32_t* __restrict__ status) {
     int64_t lo = 0, hi = 0;
     if (pos_offsets) {
         lo = pos_offsets[u];
@@ -58,7 +55,92 @@ __global__ void sample_negatives_kernel(const int64_t* __restrict__ users, int64
     if (!ok) atomicOr(status, TTAMM_STATUS_SAMPLER_EXHAUSTED);
 }
 
+__global__ void sample_negatives_kernel(const int64_t* __restrict__ users, int64_t batch, int num_neg,
+                                        uint64_t num_items, const int64_t* __restrict__ pos_offsets,
+                                        const int64_t* __restrict__ pos_values, uint32_t k0, uint32_t k1,
+                                        uint64_t counter, int64_t slot_base, int64_t* __restrict__ out,
+                                        int64_t* __restrict__ out2, uint32_t* __restrict__ status) {
+    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= batch * num_neg) return;
+    sample_slot(slot, users[slot / num_neg], num_items, pos_offsets, pos_values, k0, k1, counter, slot_base, out, out2,
+                status);
+}
+
+// The step's prologue in one launch (blockIdx.y < st.count: staging segment y, as
+// stage_rows_kernel; y == st.count: the sampler, reading user b's id from the raw batch with the
+// staging's range check, so it needs no staged copy; both grid-stride), and the last block to
+// finish runs
+// step_begin_kernel's work with every block's status bits visible (a completion counter in the
+// zero-initialised workspace, reset by that block).
+struct StepPrologue {
+    StageArgs st;
+    PrologueArgs pa;
+};
+__global__ void step_prologue_kernel(StepPrologue) {
+    const KArg(StepPrologue)* kp = (const KArg(StepPrologue)*)(__builtin_amdgcn_kernarg_segment_ptr());
+    const KArg(StageArgs)* st = &kp->st;
+    const KArg(PrologueArgs)* pa = &kp->pa;
+    const int y = blockIdx.y;
+    if (y < st->count) {
+        const KArg(StageSeg)& S = st->seg[y];
+        bool bad = false;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < S.n; i += (int64_t)gridDim.x * blockDim.x) {
+            const int64_t v = S.in[i];
+            const bool ok = v >= 0 && v < S.rows;
+            bad |= !ok;
+            if (S.out) S.out[i] = ok ? v : 0;
+        }
+        if (st->status && __ballot(bad) != 0ull && (threadIdx.x & 63) == 0)
+            atomicOr(st->status, TTAMM_STATUS_INDEX_OUT_OF_RANGE);
+    } else {
+        const int64_t slots = pa->batch * pa->num_neg;
+        for (int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; slot < slots;
+             slot += (int64_t)gridDim.x * blockDim.x) {
+            const int64_t v = pa->users[slot / pa->num_neg];
+            const int64_t u = (v >= 0 && v < pa->user_rows) ? v : 0;
+            sample_slot(slot, u, pa->num_items, pa->pos_offsets, pa->pos_values, pa->k0, pa->k1, pa->counter,
+                        pa->slot_base, pa->out, pa->out2, st->status);
+        }
+    }
+    // completion: the last block counts the step and publishes its AdamW constants
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    __threadfence();
+    const uint32_t blocks = gridDim.x * gridDim.y;
+    if (atomicAdd(pa->done, 1u) != blocks - 1) return;
+    __threadfence();
+    *pa->done = 0u;
+    const uint32_t status = st->status ? atomicOr(st->status, 0u) : 0u;
+    if (status & kStatusPoison) return;
+    if (pa->applied) pa->applied[0] += 1;
+    if (pa->hist) {
+        AdamConsts c;
+        c.decay = pa->c.decay, c.w1 = pa->c.w1, c.b2 = pa->c.b2, c.w2 = pa->c.w2, c.eps = pa->c.eps;
+        c.neg_step = pa->c.neg_step, c.bc2_sqrt = pa->c.bc2_sqrt, c.inv_bc2_sqrt = pa->c.inv_bc2_sqrt;
+        c.wd = pa->c.wd, c.decoupled = pa->c.decoupled, c.fast_g0 = pa->c.fast_g0;
+        pa->hist[pa->step % pa->cap] = c;
+    }
+}
+
 }  // namespace
+
+int launch_step_prologue(const StageArgs& st, const PrologueArgs& pa, hipStream_t s) {
+    TTAMM_REQUIRE(st.count >= 0 && st.count <= kMaxStageSegs && pa.done, "step prologue: bad arguments");
+    TTAMM_REQUIRE(pa.num_neg == 0 || (pa.num_items > 1 && pa.users), "step prologue: sampler arguments");
+    TTAMM_REQUIRE(!pa.hist || (pa.cap > 1 && pa.cap <= kMaxAdamHistory), "adam history: capacity must be in [2, 512]");
+    int64_t most = pa.batch * pa.num_neg;
+    for (int i = 0; i < st.count; ++i) most = st.seg[i].n > most ? st.seg[i].n : most;
+    // both parts grid-stride: 64 blocks per part keep the closing counter's atomics few (one per
+    // block) while a C2 batch is still ~2.5 staging elements or sampler slots per thread
+    int64_t gx = ceil_div(most, 256);
+    if (gx > 64) gx = 64;
+    if (gx < 1) gx = 1;
+    const unsigned gy = (unsigned)st.count + (pa.num_neg > 0 ? 1u : 0u);
+    TTAMM_REQUIRE(gy >= 1 && gx * gy < (int64_t(1) << 31), "step prologue: grid too large");
+    hipLaunchKernelGGL(step_prologue_kernel, dim3((unsigned)gx, gy), dim3(256), 0, s, StepPrologue{st, pa});
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
 
 int launch_sample_negatives(const int64_t* users, int64_t batch, int num_neg, int64_t num_items,
                             const int64_t* pos_offsets, const int64_t* pos_values, uint64_t seed, uint64_t counter,

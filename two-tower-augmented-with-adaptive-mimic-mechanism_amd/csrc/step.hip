@@ -88,6 +88,7 @@ struct TowerWs {
 struct StepWs {
     TowerWs user, item;
     float* partials = nullptr;
+    uint32_t* prologue_done = nullptr;  // completion counter of step_prologue_kernel (zero between calls)
     int score_blocks = 0;
     // in-batch negatives (ttamm_step_args.in_batch)
     bool ib_on = false;
@@ -354,6 +355,7 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         tower(A.item, ws.item, B * (1 + N), false, B);
     ws.score_blocks = score_blocks(B, D);
     ws.partials = ar.take<float>((size_t)ws.score_blocks * 3);
+    ws.prologue_done = ar.take<uint32_t>(1);
     if (A.hp.grad_clip_norm > 0.0) {
         ws.clip_on = true;
         // [tables' total (sharded: all-reduced)] + both towers' row partials + the dense partials
@@ -939,6 +941,8 @@ struct Deferred {
     // (overlapping the backward GEMMs).  Measured at C2: the weight-gradient GEMM runs uncontended
     // (132 -> 76 us) but the row updates slow by as much, step 0.7326 vs 0.7280 ms
     // (profiles/r03_c2_slice_late_vs_early_s16.txt) — so behind the grouping stays the default.
+    // (Started once the gate backward is enqueued, overlapping dgrad + the weight gradients
+    // instead of the gate backward: 0.745 vs 0.712-0.720 ms, profiles/r03_c2_slice_point_s20.txt.)
     bool slice_late = false;
 };
 
@@ -1604,18 +1608,34 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
                 st.seg[st.count++] = StageSeg{A.b.neg_items, nullptr, B * N, num_items};
         }
         TTAMM_REQUIRE(A.status != nullptr, "the training step needs a status word");
-        if ((rc = launch_stage_rows(st, s))) return rc;
+        // staging, the sampler and the step's count + AdamW constants (unless a status error
+        // stops it) in one launch
+        TTAMM_REQUIRE(!(A.b.sample_negatives && N > 0) || num_items > 1, "num_items must be greater than one.");
+        PrologueArgs pa;
+        std::memset(&pa, 0, sizeof(pa));
         if (A.b.sample_negatives && N > 0) {
             // one process: into the item tower's rows and (when given) the caller's buffer
-            if ((rc = launch_sample_negatives(U.idx_own, B, N, num_items, A.b.pos_offsets, A.b.pos_values, A.b.seed,
-                                              A.b.counter, A.row_base * N, neg,
-                                              (!shard && A.b.neg_items != neg) ? A.b.neg_items : nullptr, A.status,
-                                              s)))
-                return rc;
+            pa.users = A.b.users;
+            pa.user_rows = A.user.id.rows;
+            pa.batch = B;
+            pa.num_neg = N;
+            pa.num_items = (uint64_t)num_items;
+            pa.pos_offsets = A.b.pos_offsets;
+            pa.pos_values = A.b.pos_values;
+            pa.k0 = (uint32_t)A.b.seed;
+            pa.k1 = (uint32_t)(A.b.seed >> 32);
+            pa.counter = A.b.counter;
+            pa.slot_base = A.row_base * N;
+            pa.out = neg;
+            pa.out2 = (!shard && A.b.neg_items != neg) ? A.b.neg_items : nullptr;
         }
-        // count the step and publish its AdamW constants, unless a status error stops it
-        if ((rc = launch_step_begin(A.status, A.steps_applied, df.on ? df.hist : nullptr, df.cap, df.step, ad, s)))
-            return rc;
+        pa.done = ws.prologue_done;
+        pa.applied = A.steps_applied;
+        pa.hist = df.on ? df.hist : nullptr;
+        pa.cap = df.on ? df.cap : 2;
+        pa.step = df.step;
+        pa.c = ad;
+        if ((rc = launch_step_prologue(st, pa, s))) return rc;
     }
     if (shard && (ph & TTAMM_PHASE_ITEM_FWD) && I.R > 0) {  // owner: stage the requested local rows
         StageArgs st;
