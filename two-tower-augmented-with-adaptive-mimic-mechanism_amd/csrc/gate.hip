@@ -158,6 +158,39 @@ __device__ __forceinline__ void load_row(f4v (&v)[N], const float* base, int64_t
     for (int t = 0; t < N; ++t) v[t] = ldg4(p + 16 * t);
 }
 
+// Row-contiguous stores of a slab's [16 rows x 16 NO] block held in the MFMA output layout
+// (lane (li, q): row li, columns 16 ob + 4 q .. + 3, one float4 per ob): through the wave's LDS
+// scratch, eight rows at a time, so a store instruction writes whole row segments (1 KB per
+// instruction at NO = 6) instead of 16 rows x 64 B.  The direct form of these stores bounded the
+// gate kernels (their time without any output store: 64 -> 42 us forward, 65 -> 49 us backward,
+// profiles/r03_c2_gate_store_ablation_s22.txt).
+constexpr int kSlabScratch = 8 * (96 + 4);  // floats per wave: eight rows of up to 96 + 4 pad
+template <int NO>
+__device__ __forceinline__ void store_slab(float* scr, const f4v (&v)[NO], float* out, int64_t ld, int64_t row0,
+                                           int64_t R, int lane) {
+    constexpr int W = 16 * NO, LDW = W + 4, C4 = W / 4, PER = 8 * C4 / 64;
+    static_assert(8 * LDW <= kSlabScratch && (8 * C4) % 64 == 0, "slab scratch");
+    const int li = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        if ((li >> 3) == half) {
+#pragma unroll
+            for (int ob = 0; ob < NO; ++ob) *reinterpret_cast<f4v*>(scr + (li & 7) * LDW + 16 * ob + 4 * q) = v[ob];
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes are done
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int idx = lane + 64 * k, r = idx / C4, c = idx - r * C4;
+            const f4v val = *reinterpret_cast<const f4v*>(scr + r * LDW + 4 * c);
+            const int64_t grow = row0 + 8 * half + r;
+            if (grow < R) stg4(out + grow * ld + 4 * c, val);
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // the reads are done before the next half's writes
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 template <int D, int HG>
 struct GateCfg {
     static constexpr int TD = D / 16, TH = HG / 16, TE = 2 * D / 16;  // 16-feature tiles
@@ -191,7 +224,8 @@ template <int D, int HG, bool X>
 __global__ __launch_bounds__(kGateThreads) void gate_fwd_kernel(GateArgs) {
     using C = GateCfg<D, HG>;
     constexpr int NX = (2 * D) / 32;  // split: k-steps of the first GEMM
-    __shared__ __attribute__((aligned(16))) float lds[X ? C::XF_BYTES / 4 : C::F_LDS];
+    // !X: each wave's slab-store scratch after the matrices (store_slab)
+    __shared__ __attribute__((aligned(16))) float lds[X ? C::XF_BYTES / 4 : C::F_LDS + kGateWaves * kSlabScratch];
     const KArg(GateArgs)* ka = (const KArg(GateArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
     int bidx;
     const KArg(GateTower)& T = ka->tw[gate_tower(ka, bidx)];
@@ -202,6 +236,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_fwd_kernel(GateArgs) {
     float* c2s = c1s + HG;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
+    float* scr = lds + C::F_LDS + wave * kSlabScratch;  // (!X)
     const int64_t R = T.R;
     const int64_t nslab = (R + 15) / 16;
     const int64_t stride = (int64_t)T.blocks * kGateWaves;
@@ -266,12 +301,38 @@ __global__ __launch_bounds__(kGateThreads) void gate_fwd_kernel(GateArgs) {
                 const float v = z[ob][r] + c1[r];
                 z[ob][r] = v > 0.f ? v : 0.f;
             }
-            if (ok && !ka->ablate) stg4(T.z + row * HG + 16 * ob + 4 * q, z[ob]);
+            if ((X || ka->direct) && ok && !ka->ablate) stg4(T.z + row * HG + 16 * ob + 4 * q, z[ob]);
         }
+        if (!(X || ka->direct) && !ka->ablate) store_slab<C::TH>(scr, z, T.z, HG, s * 16, R, lane);
         f4v x[C::TD];
         zero(x);
         tile_gemm<C::TD, C::TH, C::F_LD2>(g2s, 0, z, x, li, q);  // (pre-sigmoid)^T = G2 . z^T
-        if (ok && !ka->ablate) {
+        if (!(X || ka->direct) && !ka->ablate) {
+            // g, then t = g e + (1 - g) f in place, a, then aug = t + a in place: one live array
+#pragma unroll
+            for (int ob = 0; ob < C::TD; ++ob) {
+                const f4v c2 = lds4(c2s + 16 * ob + 4 * q);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) x[ob][r] = sigmoid_(x[ob][r] + c2[r]);
+            }
+            store_slab<C::TD>(scr, x, T.g, D, s * 16, R, lane);
+#pragma unroll
+            for (int ob = 0; ob < C::TD; ++ob) {
+                const f4v e = ef[ob], f = ef[C::TD + ob];  // this lane's columns of e and f
+#pragma unroll
+                for (int r = 0; r < 4; ++r) x[ob][r] = x[ob][r] * e[r] + (1.0f - x[ob][r]) * f[r];
+            }
+            store_slab<C::TD>(scr, x, T.t, T.ld_t, s * 16, R, lane);
+            if (T.table) {
+                store_slab<C::TD>(scr, a, T.a, T.ld_t, s * 16, R, lane);
+#pragma unroll
+                for (int ob = 0; ob < C::TD; ++ob)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) x[ob][r] = x[ob][r] + a[ob][r];
+            }
+            if (T.aug) store_slab<C::TD>(scr, x, T.aug, D, s * 16, R, lane);
+        }
+        if ((X || ka->direct) && ok && !ka->ablate) {
 #pragma unroll
             for (int ob = 0; ob < C::TD; ++ob) {
                 const int col = 16 * ob + 4 * q;
@@ -306,7 +367,7 @@ template <int D, int HG, bool X>
 __global__ __launch_bounds__(kGateThreads) void gate_bwd_kernel(GateArgs) {
     using C = GateCfg<D, HG>;
     constexpr int NX = HG / 32;  // split: k-steps of the dEF GEMM
-    __shared__ __attribute__((aligned(16))) float lds[X ? C::XB_BYTES / 4 : C::B_LDS];
+    __shared__ __attribute__((aligned(16))) float lds[X ? C::XB_BYTES / 4 : C::B_LDS + kGateWaves * kSlabScratch];
     const KArg(GateArgs)* ka = (const KArg(GateArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
     int bidx;
     const KArg(GateTower)& T = ka->tw[gate_tower(ka, bidx)];
@@ -379,8 +440,10 @@ __global__ __launch_bounds__(kGateThreads) void gate_bwd_kernel(GateArgs) {
                     const float dg = d[t][r] * ef[t][r] - d[t][r] * ef[C::TD + t][r];
                     dq[t][r] = dg * (1.0f - g[t][r]) * g[t][r];
                 }
-                if (ok && !ka->ablate) stg4(T.dq + row * D + 16 * t + 4 * q, dq[t]);
+                if ((X || ka->direct) && ok && !ka->ablate) stg4(T.dq + row * D + 16 * t + 4 * q, dq[t]);
             }
+            if (!(X || ka->direct) && !ka->ablate)
+                store_slab<C::TD>(lds + C::B_LDS + wave * kSlabScratch, dq, T.dq, D, s * 16, R, lane);
             zero(dz);
             tile_gemm<C::TH, C::TD, C::B_LD1>(g2t, 0, dq, dz, li, q);  // dz^T = G2^T . dq^T
         }
@@ -388,8 +451,10 @@ __global__ __launch_bounds__(kGateThreads) void gate_bwd_kernel(GateArgs) {
         for (int ob = 0; ob < C::TH; ++ob) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) dz[ob][r] = zr[ob][r] > 0.f ? dz[ob][r] : 0.f;
-            if (ok && !ka->ablate) stg4(T.dz + row * HG + 16 * ob + 4 * q, dz[ob]);
+            if ((X || ka->direct) && ok && !ka->ablate) stg4(T.dz + row * HG + 16 * ob + 4 * q, dz[ob]);
         }
+        if (!(X || ka->direct) && !ka->ablate)
+            store_slab<C::TH>(lds + C::B_LDS + wave * kSlabScratch, dz, T.dz, HG, s * 16, R, lane);
         // dEF^T = G1^T . dz^T + [dT g | dT (1 - g)], in two halves (e part, f part)
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
@@ -397,15 +462,17 @@ __global__ __launch_bounds__(kGateThreads) void gate_bwd_kernel(GateArgs) {
             zero(de);
             if constexpr (X) tile_gemm_x<C::TD, NX, 2 * D>(img, half * C::TD, dz, de, li, q);
             else tile_gemm<C::TD, C::TH, C::B_LD2>(g1t, half * C::TD, dz, de, li, q);
-            if (ok && !ka->ablate) {
 #pragma unroll
-                for (int ob = 0; ob < C::TD; ++ob) {
+            for (int ob = 0; ob < C::TD; ++ob)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        de[ob][r] += half == 0 ? d[ob][r] * g[ob][r] : d[ob][r] * (1.0f - g[ob][r]);
-                    stg4(T.dEF + row * 2 * D + half * D + 16 * ob + 4 * q, de[ob]);
-                }
+                for (int r = 0; r < 4; ++r)
+                    de[ob][r] += half == 0 ? d[ob][r] * g[ob][r] : d[ob][r] * (1.0f - g[ob][r]);
+            if ((X || ka->direct) && ok && !ka->ablate) {
+#pragma unroll
+                for (int ob = 0; ob < C::TD; ++ob) stg4(T.dEF + row * 2 * D + half * D + 16 * ob + 4 * q, de[ob]);
             }
+            if (!(X || ka->direct) && !ka->ablate)
+                store_slab<C::TD>(lds + C::B_LDS + wave * kSlabScratch, de, T.dEF + half * D, 2 * D, s * 16, R, lane);
         }
     }
 }
@@ -460,7 +527,9 @@ bool gate_fused_supported(int D, int HG) { return D == HG && (D == 32 || D == 64
 
 int launch_gate(GateArgs& a, bool backward, hipStream_t s) {
     static const bool ablate = std::getenv("TTAMM_GATE_ABLATE") != nullptr;
+    static const bool direct = std::getenv("TTAMM_GATE_DIRECT_STORES") != nullptr;
     a.ablate = ablate ? 1 : 0;
+    a.direct = direct ? 1 : 0;
     TTAMM_REQUIRE(a.count >= 1 && a.count <= 2 && gate_fused_supported(a.D, a.HG), "fused gate: unsupported shape");
     for (int i = 0; i < a.count; ++i) TTAMM_REQUIRE(a.tw[i].R > 0, "fused gate: empty tower");
     switch (a.D) {

@@ -169,6 +169,7 @@ struct GateArgs {
     int count;
     int D, HG;
     int ablate;  // developer timing ablation (TTAMM_GATE_ABLATE=1: no output stores); set by launch_gate
+    int direct;  // TTAMM_GATE_DIRECT_STORES=1: stores from the MFMA layout (16 rows x 64 B each); set by launch_gate
 };
 bool gate_fused_supported(int D, int HG);
 int launch_gate(GateArgs& a, bool backward, hipStream_t s);
