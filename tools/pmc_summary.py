@@ -68,8 +68,9 @@ def main() -> None:
             "fetch_bytes_per_launch": round(sum(f) / len(f) * 1024 * 2),
             "write_bytes_per_launch": round(sum(w) / len(w) * 1024),
         }
-    entry = {"tag": tag, "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE / --pmc SQ_INSTS_VALU SQ_WAVES "
-             "SQ_INSTS_SALU, one pass each, bench.py --steps 40 --warmup 3; bytes = FETCH_SIZE*1024*2 + "
+    entry = {"tag": tag, "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE / --pmc SQ_INSTS_VALU "
+             "SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_WAVES SQ_INSTS_SALU, one pass "
+             "each, bench.py --steps 40 --warmup 3; bytes = FETCH_SIZE*1024*2 + "
              "WRITE_SIZE*1024 (MI355X_MICROARCH.md HBM); kernel times from rocprofv3 --kernel-trace --stats of "
              "the default bench command", "kernels": kernels}
 
