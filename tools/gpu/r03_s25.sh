@@ -1,0 +1,15 @@
+# Round 3 session 25: SQ counters of the C3 retrieval kernel (what bounds retrieval_x_kernel)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS --output-format csv -d gpurun_out/pmc_retr -o run -- python3 tools/bench_retrieval.py --queries 16384 > gpurun_out/pmc_retr.txt 2>&1 || { echo PMC_FAIL; tail -5 gpurun_out/pmc_retr.txt; exit 1; }
+find gpurun_out/pmc_retr -name "*counter_collection.csv" -exec cp {} gpurun_out/pmc_retr_sq.csv \;
+rm -rf gpurun_out/pmc_retr
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_WAVES SQ_BUSY_CYCLES --output-format csv -d gpurun_out/pmc_retr2 -o run -- python3 tools/bench_retrieval.py --queries 16384 > gpurun_out/pmc_retr2.txt 2>&1 || { echo PMC2_FAIL; tail -5 gpurun_out/pmc_retr2.txt; exit 1; }
+find gpurun_out/pmc_retr2 -name "*counter_collection.csv" -exec cp {} gpurun_out/pmc_retr_sq2.csv \;
+rm -rf gpurun_out/pmc_retr2
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/stats_r -o run -- python3 tools/bench_retrieval.py > gpurun_out/stats_retr.json 2> gpurun_out/stats_retr.err || { echo STATS_FAIL; exit 1; }
+find gpurun_out/stats_r -name "*kernel_stats.csv" -exec cp {} gpurun_out/stats_retr_kernel_stats.csv \;
+rm -rf gpurun_out/stats_r
+head -5 gpurun_out/stats_retr_kernel_stats.csv | cut -c1-160
