@@ -340,6 +340,7 @@ struct RetrievalArgs {
     int* buf_i;
     float* part_s;        // per-partition top-k [nq, parts, k]
     int* part_i;
+    int ablate;           // timing experiments only (TTAMM_RETRIEVAL_ABLATE): 1 no filter, 2 no MFMA, 4 no staging
 };
 size_t retrieval_workspace_bytes(int64_t nq, int64_t ni, int dim, int k);
 int launch_normalize_rows(float* x, int64_t n, int dim, int64_t ld, hipStream_t s);

@@ -81,24 +81,15 @@ __device__ void wave_bitonic_sort(float (&s)[J], int (&id)[J]) {
     }
 }
 
-__device__ __forceinline__ bool is_blocked(const int64_t* __restrict__ vals, int64_t lo, int64_t hi, int64_t item) {
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        const int64_t v = vals[mid];
-        if (v == item) return true;
-        if (v < item)
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    return false;
-}
-
-// Sort query q's buffered candidates, keep the best `keep`, update its threshold.
-__device__ void compact_query(float* __restrict__ bs, int* __restrict__ bi, int* cnt, float* tau, int q, int k,
-                              float* out_s, int* out_i, int out_k) {
+// Sort query q's buffered candidates, keep the best k, update its threshold.  With a blocked
+// list (bval[blo, bhi), sorted; the split kernel defers the blocked test to here) candidates on
+// it are dropped first: the wave loads the list 64 values at a time and every lane compares its
+// four candidates against each value (one load round trip per 64 blocked items, instead of a
+// dependent binary search per inserted candidate).
+__device__ int compact_core(float* __restrict__ bs, int* __restrict__ bi, int q, int n, int k, float* out_s,
+                             int* out_i, int out_k, const int64_t* __restrict__ bval, int64_t blo, int64_t bhi,
+                             float& tau_out) {
     const int lane = threadIdx.x & 63;
-    const int n = cnt[q];
     float s[4];
     int id[4];
 #pragma unroll
@@ -106,6 +97,30 @@ __device__ void compact_query(float* __restrict__ bs, int* __restrict__ bi, int*
         const int e = lane * 4 + j;
         s[j] = e < n ? bs[q * kRCap + e] : -INFINITY;
         id[j] = e < n ? bi[q * kRCap + e] : -1;
+    }
+    if (bhi > blo) {
+        bool drop[4] = {false, false, false, false};
+        for (int64_t c0 = blo; c0 < bhi; c0 += 64) {
+            const int64_t v = c0 + lane < bhi ? bval[c0 + lane] : int64_t(-1);
+            const int m = bhi - c0 < 64 ? (int)(bhi - c0) : 64;
+            const int vlo = (int)(uint32_t)v, vhi = (int)(v >> 32);
+            for (int i = 0; i < m; ++i) {
+                const int64_t b = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(vhi, i) << 32) |
+                                            (uint32_t)__builtin_amdgcn_readlane(vlo, i));
+#pragma unroll
+                for (int j = 0; j < 4; ++j) drop[j] |= id[j] >= 0 && (int64_t)id[j] == b;
+            }
+        }
+        int kept = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (drop[j]) {
+                s[j] = -INFINITY;  // sorts after every kept candidate (id -1 last among ties)
+                id[j] = -1;
+            }
+            kept += __popcll(__ballot(lane * 4 + j < n && !drop[j]));
+        }
+        n = kept;
     }
     wave_bitonic_sort<4>(s, id);
 #pragma unroll
@@ -115,13 +130,28 @@ __device__ void compact_query(float* __restrict__ bs, int* __restrict__ bi, int*
             bs[q * kRCap + e] = s[j];
             bi[q * kRCap + e] = id[j];
         }
-        if (e == k - 1) tau[q] = e < n ? s[j] : -INFINITY;
         if (out_s && e < out_k) {
             out_s[e] = e < n ? s[j] : -INFINITY;
             out_i[e] = e < n ? id[j] : -1;
         }
     }
-    if (lane == 0) cnt[q] = n < k ? n : k;
+    // the k-th best (element k - 1 = lane (k-1)/4, slot (k-1)%4) to every lane
+    const int jk = (k - 1) & 3;
+    const float sk = jk == 0 ? s[0] : jk == 1 ? s[1] : jk == 2 ? s[2] : s[3];
+    const float kth = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sk), (k - 1) >> 2));
+    tau_out = k <= n ? kth : -INFINITY;
+    return n < k ? n : k;
+}
+
+__device__ void compact_query(float* __restrict__ bs, int* __restrict__ bi, int* cnt, float* tau, int q, int k,
+                              float* out_s, int* out_i, int out_k, const int64_t* __restrict__ bval = nullptr,
+                              int64_t blo = 0, int64_t bhi = 0) {
+    float t;
+    const int nc = compact_core(bs, bi, q, cnt[q], k, out_s, out_i, out_k, bval, blo, bhi, t);
+    if ((threadIdx.x & 63) == 0) {
+        cnt[q] = nc;
+        tau[q] = t;
+    }
 }
 
 // IT items per tile: wave (qw, iw) scores queries [32 qw, 32 qw + 32) against items
@@ -158,11 +188,6 @@ __global__ __launch_bounds__(256) void retrieval_partial_kernel(RetrievalArgs A)
     const int myq = qw * 32 + (lane & 31);
     const int64_t gq = q0 + myq;
     const bool qvalid = gq < A.nq;
-    int64_t blo = 0, bhi = 0;
-    if (A.boff && qvalid) {
-        blo = A.boff[gq];
-        bhi = A.boff[gq + 1];
-    }
     const float* qb = Qs + myq * LD + h * Dh;
     float4 pf[PF];
     auto load_tile = [&](int64_t t0) {
@@ -188,7 +213,7 @@ __global__ __launch_bounds__(256) void retrieval_partial_kernel(RetrievalArgs A)
     }
     for (int64_t t0 = i_begin; t0 < i_end; t0 += IT) {
         __syncthreads();  // tile t0 is in LDS; thresholds and counts are current
-        if (t0 + IT < i_end) load_tile(t0 + IT);
+        if (t0 + IT < i_end && !(A.ablate & 4)) load_tile(t0 + IT);
         const float my_tau = tau[myq];
         f32x16 acc[MT];
 #pragma unroll
@@ -226,7 +251,7 @@ __global__ __launch_bounds__(256) void retrieval_partial_kernel(RetrievalArgs A)
                 for (int r = 0; r < 16; ++r) {
                     const int64_t item = t0 + iw * (IT / 2) + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                     const float sc = acc[m][r];
-                    if (item < i_end && sc >= my_tau && !(bhi > blo && is_blocked(A.bval, blo, bhi, item))) {
+                    if (item < i_end && sc >= my_tau) {  // blocked items are dropped at compaction
                         const int slot = atomicAdd(&cnt[myq], 1);
                         bs[myq * kRCap + slot] = sc;  // slot < kRCap: cnt <= kRCap - IT before the tile
                         bi[myq * kRCap + slot] = (int)item;
@@ -235,7 +260,11 @@ __global__ __launch_bounds__(256) void retrieval_partial_kernel(RetrievalArgs A)
         }
         __syncthreads();  // all scores of the tile are in; Xs is free
         for (int q = w; q < kRQ; q += 4)
-            if (cnt[q] > kRCap - IT) compact_query(bs, bi, cnt, tau, q, A.k, nullptr, nullptr, 0);
+            if (cnt[q] > kRCap - IT) {
+                const bool bl = A.boff && q0 + q < A.nq;
+                compact_query(bs, bi, cnt, tau, q, A.k, nullptr, nullptr, 0, A.bval, bl ? A.boff[q0 + q] : 0,
+                              bl ? A.boff[q0 + q + 1] : 0);
+            }
         if (t0 + IT < i_end) store_tile();
     }
     __syncthreads();
@@ -244,7 +273,8 @@ __global__ __launch_bounds__(256) void retrieval_partial_kernel(RetrievalArgs A)
         if (g >= A.nq) continue;
         float* os = A.part_s + (g * A.parts + blockIdx.y) * A.k;
         int* oi = A.part_i + (g * A.parts + blockIdx.y) * A.k;
-        compact_query(bs, bi, cnt, tau, q, A.k, os, oi, A.k);
+        const bool bl = A.boff != nullptr;
+        compact_query(bs, bi, cnt, tau, q, A.k, os, oi, A.k, A.bval, bl ? A.boff[g] : 0, bl ? A.boff[g + 1] : 0);
     }
 }
 
@@ -357,7 +387,7 @@ __global__ __launch_bounds__(kXThreads) void retrieval_x_kernel(RetrievalArgs A)
     }
     for (int64_t t0 = i_begin; t0 < i_end; t0 += IT) {
         __syncthreads();  // tile t0 is in LDS buffer `buf`; thresholds and counts are current
-        if (t0 + IT < i_end) load_tile(t0 + IT);
+        if (t0 + IT < i_end && !(A.ablate & 4)) load_tile(t0 + IT);
         const float my_tau = tau[myq];
         const unsigned char* base = lds + buf * BUF;
         f32x16 acc[MT];
@@ -367,6 +397,7 @@ __global__ __launch_bounds__(kXThreads) void retrieval_x_kernel(RetrievalArgs A)
             for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
+            if (A.ablate & 2) break;
 #pragma unroll
             for (int m = 0; m < MT; ++m) {
                 bf16x8r af[3];
@@ -382,38 +413,62 @@ __global__ __launch_bounds__(kXThreads) void retrieval_x_kernel(RetrievalArgs A)
                 acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], qf[0][ks], acc[m], 0, 0, 0);
             }
         }
-        float mx = -INFINITY;  // the per-score filter only when some score can pass
+        // hierarchical filter: a wave enters a 32-item group only when one of its lanes has a
+        // score >= tau there, then tests that group's scores one by one (steady state: one or
+        // two passing scores per wave and tile, so most groups are skipped after one compare)
+        float mm[MT];
 #pragma unroll
-        for (int m = 0; m < MT; ++m)
+        for (int m = 0; m < MT; ++m) {
+            mm[m] = acc[m][0];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, acc[m][r]);
-        if (qvalid && mx >= my_tau) {
+            for (int r = 1; r < 16; ++r) mm[m] = fmaxf(mm[m], acc[m][r]);
+        }
+        const bool full = t0 + IT <= i_end;
+        if (!(A.ablate & 1) && qvalid) {
 #pragma unroll
-            for (int m = 0; m < MT; ++m)
+            for (int m = 0; m < MT; ++m) {
+                if (mm[m] >= my_tau) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int64_t item = t0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const float sc = acc[m][r];
-                    if (item < i_end && sc >= my_tau && !(bhi > blo && is_blocked(A.bval, blo, bhi, item))) {
-                        const int slot = atomicAdd(&cnt[myq], 1);
-                        bs[myq * kRCap + slot] = sc;  // slot < kRCap: cnt <= kRCap - IT before the tile
-                        bi[myq * kRCap + slot] = (int)item;
+                    for (int r = 0; r < 16; ++r) {
+                        const float sc = acc[m][r];
+                        if (sc >= my_tau) {
+                            const int64_t item = t0 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                            if (full || item < i_end) {  // blocked items are dropped at compaction
+                                const int slot = atomicAdd(&cnt[myq], 1);
+                                bs[myq * kRCap + slot] = sc;  // slot < kRCap: cnt <= kRCap - IT before the tile
+                                bi[myq * kRCap + slot] = (int)item;
+                            }
+                        }
                     }
                 }
+            }
         }
-        __syncthreads();  // all scores of the tile are in; the other buffer is free
-        for (int q = w; q < kXQ; q += kXThreads / 64)
-            if (cnt[q] > kRCap - IT) compact_query(bs, bi, cnt, tau, q, A.k, nullptr, nullptr, 0);
-        if (t0 + IT < i_end) store_tile(buf ^ 1);
+        // compaction of this wave's own 32 queries (their candidates come only from this wave's
+        // lanes, so no block barrier): one LDS read per lane and a ballot, then only the buffers
+        // near capacity are sorted, in ascending q.  The other LDS buffer is already free: every
+        // wave finished reading it before this tile's barrier.
+        __threadfence_block();  // this wave's candidate stores before its own compaction loads
+        {
+            uint64_t need = __ballot(lane < 32 && cnt[w * 32 + lane] > kRCap - IT);
+            while (need) {
+                const int j = __builtin_ctzll(need);
+                need &= need - 1;
+                compact_query(bs, bi, cnt, tau, w * 32 + j, A.k, nullptr, nullptr, 0, A.bval, __shfl(blo, j, 64),
+                              __shfl(bhi, j, 64));
+            }
+        }
+        if (t0 + IT < i_end && !(A.ablate & 4)) store_tile(buf ^ 1);
         buf ^= 1;
     }
-    __syncthreads();
-    for (int q = w; q < kXQ; q += kXThreads / 64) {
+    __syncthreads();  // an empty partition skips the loop: counts and thresholds were set by waves 0-3
+    for (int j = 0; j < 32; ++j) {  // this wave's queries: their buffers are written only by it
+        const int q = w * 32 + j;
         const int64_t g = q0 + q;
+        const int64_t qlo = __shfl(blo, j, 64), qhi = __shfl(bhi, j, 64);
         if (g >= A.nq) continue;
         float* os = A.part_s + (g * A.parts + blockIdx.y) * A.k;
         int* oi = A.part_i + (g * A.parts + blockIdx.y) * A.k;
-        compact_query(bs, bi, cnt, tau, q, A.k, os, oi, A.k);
+        compact_query(bs, bi, cnt, tau, q, A.k, os, oi, A.k, A.bval, qlo, qhi);
     }
 }
 
@@ -704,6 +759,7 @@ int launch_retrieval_topk(const float* Q, int64_t nq, int64_t ldq, const float* 
     A.boff = boff;
     A.bval = bval;
     A.k = k;
+    if (const char* e = std::getenv("TTAMM_RETRIEVAL_ABLATE")) A.ablate = std::atoi(e);
     const int qb = retrieval_qb(dim);
     A.parts = pick_parts(nq, ni, k, qb);
     A.items_per_part = ni > 0 ? ((ni + A.parts - 1) / A.parts + 127) / 128 * 128 : 0;
