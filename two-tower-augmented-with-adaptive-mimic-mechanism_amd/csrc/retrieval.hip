@@ -500,7 +500,12 @@ __global__ __launch_bounds__(64) void retrieval_merge_kernel(RetrievalArgs A, fl
 
 int pick_parts(int64_t nq, int64_t ni, int k, int qb = kRQ) {
     const int64_t qtiles = (nq + qb - 1) / qb;
-    int64_t parts = (2048 + qtiles - 1) / qtiles;  // aim for >= 2048 blocks (8 per CU)
+    // the fp32 kernel: >= 2048 blocks (8 per CU).  The split kernel holds one block per CU (144 KB
+    // of LDS): one block per CU is enough, and every extra partition costs each query another
+    // k ln(items / (parts k)) candidate insertions and their compactions
+    const int64_t target = qb == kXQ ? 256 : 2048;
+    int64_t parts = (target + qtiles - 1) / qtiles;
+    if (const char* e = std::getenv("TTAMM_RETRIEVAL_PARTS")) parts = std::atoi(e);  // sweeps only
     const int64_t by_items = (ni + 4 * kRI - 1) / (4 * kRI);  // >= 4 tiles per partition
     if (parts > by_items) parts = by_items;
     const int64_t by_merge = (64 * kMergeJ) / k;
