@@ -10,8 +10,8 @@
 // Four waves: (query half, item half) of each 64-item tile.  Scores come from fp32 MFMA
 // 32x32x2 with items as M and queries as N, so every lane holds ONE query and 16 items of the
 // tile.  A lane appends (score, id) to its query's candidate buffer only when the score reaches
-// the query's running threshold (the k-th best so far) and the item is not blocked; a wave
-// compacts a query's buffer (bitonic sort in registers, keep k) before it could overflow.
+// the query's running threshold (the k-th best so far); a wave compacts a query's buffer
+// (blocked items dropped, bitonic sort in registers, keep k) before it could overflow.
 // D <= 128 runs the same scheme on split-bf16 MFMA (retrieval_x_kernel: fp32-level scores at
 // 2.6x the fp32 MFMA rate; TTAMM_RETRIEVAL_FP32=1 keeps the fp32 kernel for comparison).
 // Pass 2 (retrieval_merge_kernel): one wave per query merges the partitions' top-k lists.
