@@ -4,6 +4,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4|c5|tiny]
                     [--negatives sampled|in-batch] [--neg N]
 
+--gpus N > 1 without WORLD_SIZE in the environment starts the N ranks itself (a child
+`torch.distributed.run --nproc-per-node N`, rendezvous on 127.0.0.1) and prints rank 0's line;
+under an external launcher (WORLD_SIZE set) it runs as one of the ranks.
+
 Workload (BASELINE.json configs[1], "C2"): 2M items x 200K users, 96-dim towers, feature
 MLP 605 -> 192 -> 96 (ReLU, dropout 0.15), gated fusion, adaptive mimic on, batch 8192,
 5 sampled negatives per positive (the reference's semantics), AdamW
@@ -286,6 +290,44 @@ def wgrad_problems(c: dict, rows: dict) -> list[tuple[int, int, int]]:
     return out
 
 
+def launch_command(argv: list[str], gpus: int, port: int) -> list[str]:
+    """The torch.distributed.run command that starts `gpus` ranks of this script (one process
+    per GPU, rendezvous on 127.0.0.1), forwarding the caller's arguments unchanged."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(argv: list[str], gpus: int) -> int:
+    """`bench.py --gpus N` without a launcher: start the N ranks as a child torch.distributed.run
+    (this process never touches the GPU), relay rank 0's JSON line and check it covers N GPUs."""
+    import subprocess
+
+    proc = subprocess.run(launch_command(argv, gpus, free_port()), stdout=subprocess.PIPE, text=True)
+    line = None
+    for ln in proc.stdout.splitlines():
+        if ln.startswith("{") and '"metric"' in ln:
+            line = ln
+        else:
+            print(ln, flush=True)
+    if proc.returncode != 0 or line is None:
+        print(f"bench.py: the {gpus}-rank run failed (exit {proc.returncode})", file=sys.stderr)
+        return proc.returncode or 1
+    out = json.loads(line)
+    if out.get("n_gpus") != gpus:
+        print(f"bench.py: the {gpus}-rank run reported n_gpus={out.get('n_gpus')}", file=sys.stderr)
+        return 1
+    print(line, flush=True)
+    return 0
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -324,8 +366,13 @@ def main() -> None:
     ap.add_argument("--neg", type=int, default=None,
                     help="sampled negatives per positive (default: 5 sampled, 0 on top of in-batch)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no external launcher: this process only spawns the ranks (no GPU call before this point)
+        sys.exit(self_launch(sys.argv[1:], args.gpus))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None

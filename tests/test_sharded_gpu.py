@@ -192,6 +192,27 @@ def test_bench_two_ranks_one_gpu_gloo():
     assert out["final_loss"] == out["final_loss"]  # finite, not NaN
 
 
+def test_bench_gpus_two_self_launches():
+    """`bench.py --gpus 2` with no external launcher starts the two ranks itself (a child
+    torch.distributed.run) and relays rank 0's line, which must say n_gpus = 2."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, str(root / "bench.py"), "--gpus", "2", "--config", "tiny", "--dist-backend", "gloo",
+           "--no-cpu-baseline", "--steps", "3", "--warmup", "1"]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=root, env=env)
+    assert res.returncode == 0, res.stderr[-3000:]
+    line = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1
+    out = json.loads(line[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 2 * 1024 and out["value"] > 0
+
+
 def test_sharded_epoch_routes_pairs_to_user_owners():
     """ttamm.sharded.epoch_program: every rank reads its own slice of the interaction stream
     (any users); each batch's pairs go to their users' owners by all-to-all and the routed

@@ -251,3 +251,41 @@ def test_max_norm_renormalises_looked_up_rows():
         assert changed.any(), n  # the renorm did act
         assert (tsd[n].cpu().norm(dim=1)[changed] <= 0.05 * (1 + 1e-6)).all(), n
         assert rel_err(tsd[n].cpu(), osd[n]) <= 1e-6, n
+
+
+def test_ragged_batches_full_short_full():
+    """A short batch between full ones (the epoch's last batch is short, training.py:1382
+    drop_last=False; here in the middle, so a full batch follows it on the same workspace).
+    Every step must be counted (steps_applied; the prologue's completion counter sits at a
+    batch-size-independent offset) and the tables / optimizer state must match the oracle."""
+    import ttamm
+    from gpu_helpers import ttamm_model_from, ttamm_optimizers
+    from helpers import LOSS_WEIGHTS
+
+    shape = Shape(dropout=0.0)
+    prob = make_problem(shape, steps=3)
+    b = 13
+    users, pos, neg, um, im = prob.batches[1]
+    prob.batches[1] = (users[:b], pos[:b], neg[:b], [m[:b] for m in um], [m[: b * (1 + shape.N)] for m in im])
+    om, oo, ores = run_oracle(prob)
+    tm = ttamm_model_from(prob)
+    to = ttamm_optimizers(tm)
+    eng = ttamm.FusedTrainStep(tm, to, negatives_per_positive=shape.N, positives=prob.positives,
+                               user_features=prob.user_features.cuda(), item_features=prob.item_features.cuda(),
+                               loss_weights=LOSS_WEIGHTS, max_batch=shape.B)
+    for k, (u, p, n, a, c) in enumerate(prob.batches):
+        eng.step(u.cuda(), p.cuda(), n.cuda().reshape(-1),
+                 keep_masks={"user": [m.cuda() for m in a], "item": [m.cuda() for m in c]})
+        torch.cuda.synchronize()
+        assert int(eng.steps_applied.item()) == k + 1, f"step {k} not counted"
+        got = eng.last_losses()["total"]
+        assert abs(got - ores[k].total) <= 1e-5 * abs(ores[k].total), (k, got, ores[k].total)
+    eng.finish()
+    osd, tsd = om.state_dict(), tm.state_dict()
+    for n in osd:
+        d = (tsd[n].cpu() - osd[n]).abs().max().item()
+        assert d <= 1e-3 * 1e-3 * 50, f"{n}: max abs diff {d:.3e}"
+    ost, tst = named_optimizer_state(om, oo), named_optimizer_state(tm, to)
+    for n in ost:
+        assert rel_err(tst[n]["exp_avg"], ost[n]["exp_avg"]) <= 1e-4, n
+        assert float(tst[n]["step"]) == float(ost[n]["step"]) == 3.0, n

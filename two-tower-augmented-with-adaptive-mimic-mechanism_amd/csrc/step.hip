@@ -251,6 +251,9 @@ void plan_scratch(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
     }
     if (A.user.id.max_norm > 0.0) ws.user.renorm_mark = ar.take<int32_t>(A.user.id.rows);
     if (A.item.id.max_norm > 0.0) ws.item.renorm_mark = ar.take<int32_t>(A.item.id.rows);
+    // step_prologue_kernel's completion counter: its last block resets it, so it must sit at a
+    // batch-size-independent offset (a short last batch must find it zero, not old activations)
+    ws.prologue_done = ar.take<uint32_t>(1);
 }
 
 void plan_coalesce(Arena& ar, CoalesceWs& co, int64_t R) {
@@ -355,7 +358,6 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         tower(A.item, ws.item, B * (1 + N), false, B);
     ws.score_blocks = score_blocks(B, D);
     ws.partials = ar.take<float>((size_t)ws.score_blocks * 3);
-    ws.prologue_done = ar.take<uint32_t>(1);
     if (A.hp.grad_clip_norm > 0.0) {
         ws.clip_on = true;
         // [tables' total (sharded: all-reduced)] + both towers' row partials + the dense partials
