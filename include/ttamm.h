@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 20
+#define TTAMM_ABI_VERSION 22
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -215,7 +215,20 @@ typedef struct ttamm_hparams {
                               optimizers, ||g|| over all parameters (clip_grad_norm_).  One-process
                               step with dense ID tables only (torch raises on the sparse
                               gradients of sparse ID tables); 0 = off */
+    /* the dense group's optimizer (training.py:1311-1333): TTAMM_DENSE_ADAM = torch.optim.Adam /
+     * AdamW (decoupled_weight_decay), TTAMM_DENSE_SGD = torch.optim.SGD(lr, weight_decay, momentum)
+     * (sgd.py _single_tensor_sgd).  SGD keeps its momentum buffer in each dense tensor's exp_avg
+     * (exp_avg_sq may alias it); with momentum == 0 both may alias the parameter itself.  The
+     * deferred table replay is AdamW-only: SGD sweeps the dense-group tables eagerly (no sweep at
+     * all when momentum == weight_decay == 0: untouched rows do not move). */
+    int32_t dense_optimizer;
+    double momentum, dampening;
+    int32_t nesterov;
+    int32_t sgd_first_step; /* 1: the momentum buffers do not exist yet (torch: buf = grad.clone()) */
 } ttamm_hparams;
+
+#define TTAMM_DENSE_ADAM 0
+#define TTAMM_DENSE_SGD 1
 
 /* One batch of the training loop (training.py:726-736). */
 typedef struct ttamm_batch {
@@ -517,6 +530,19 @@ int ttamm_sparse_adam_rows(float* weight, float* exp_avg, float* exp_avg_sq, int
 int ttamm_adamw_dense(float* param, float* exp_avg, float* exp_avg_sq, const float* grad, int64_t n,
                       double lr, double beta1, double beta2, double eps, double weight_decay,
                       int32_t decoupled, int64_t step, void* stream);
+
+/* In-batch negatives as one op (ttamm's in-batch mode, BASELINE configs C2 / C4; the scoring it
+ * extends is training.py:770-798, its definition oracle/cpu_reference.py train_step(in_batch=True)):
+ *   S = users . positives^T [batch, n_positives], label 1 at (b, row_base + b), 0 elsewhere;
+ *   d_users = dS . positives, d_positives = dS^T . users with dS = (sigmoid(S) - Y) * inv_count;
+ *   *loss_sum = sum over S of the BCE-with-logits terms (fp64 on the device).
+ * Nothing batch x n_positives is stored (inbatch_x_kernel, split-bf16 MFMA).  In a row-sharded step
+ * n_positives is the all-gathered global batch and row_base the rank's first global position. */
+size_t ttamm_inbatch_workspace_size(int64_t batch, int64_t n_positives, int32_t dim);
+int ttamm_inbatch_bce(const float* users, int64_t batch, int64_t ldu, const float* positives,
+                      int64_t n_positives, int64_t ldp, int32_t dim, int64_t row_base, float inv_count,
+                      float* d_users, int64_t ld_du, float* d_positives, int64_t ld_dp, double* loss_sum,
+                      void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

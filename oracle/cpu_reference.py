@@ -291,12 +291,21 @@ def parameter_groups(model: OracleModel) -> tuple[list, list]:
 
 
 def build_optimizers(model: OracleModel, *, lr: float = 1e-3, weight_decay: float = 0.01, betas=(0.9, 0.999),
-                     optimizer: str = "adamw") -> list[torch.optim.Optimizer]:
+                     optimizer: str = "adamw", momentum: float = 0.0) -> list[torch.optim.Optimizer]:
+    """training.py:1311-1350: the dense group under Adam / AdamW / SGD(momentum) by
+    ``training.optimizer`` (the reference passes no betas to the dense Adam / AdamW; ``betas``
+    here serves the parity tests' lr = 0 gradient export), the sparse ID tables under SparseAdam."""
     dense, sparse = parameter_groups(model)
     opts: list[torch.optim.Optimizer] = []
+    name = optimizer.lower()
     if dense:
-        cls = torch.optim.AdamW if optimizer == "adamw" else torch.optim.Adam
-        opts.append(cls(dense, lr=lr, weight_decay=weight_decay, betas=betas))
+        if name in ("adam", "adamw"):  # :1316-1323
+            cls = torch.optim.AdamW if name == "adamw" else torch.optim.Adam
+            opts.append(cls(dense, lr=lr, weight_decay=weight_decay, betas=betas))
+        elif name == "sgd":  # :1324-1330
+            opts.append(torch.optim.SGD(dense, lr=lr, weight_decay=weight_decay, momentum=float(momentum)))
+        else:
+            raise ValueError(f"Unsupported optimizer: {optimizer}")  # :1331-1332
     if sparse:
         opts.append(torch.optim.SparseAdam(sparse, lr=lr, betas=betas))
     return opts
@@ -445,6 +454,37 @@ def train_step(
         float(loss_i.item()) if loss_i is not None else 0.0,
         float(cal.item()) if cal is not None else 0.0,
     )
+
+
+def inbatch_bce_chunked(users: torch.Tensor, positives: torch.Tensor, *, row_base: int = 0,
+                        inv_count: float | None = None, chunk: int = 1024,
+                        dtype: torch.dtype = torch.float64) -> tuple[float, torch.Tensor, torch.Tensor]:
+    """The in-batch block of train_step(in_batch=True) above (ib = u @ p^T, label 1 at
+    (b, row_base + b); row_base = 0 and positives = p in one process, a rank's first global
+    position and the all-gathered positives in the row-sharded step) evaluated in ``dtype``,
+    ``chunk`` users at a time so a [8192 x 65536] score matrix is never held whole.  Returns
+    (sum of the BCEWithLogits terms, dL/dusers, dL/dpositives) for L = inv_count * that sum
+    (torch's BCE term max(x, 0) - x y + log1p(exp(-|x|)); dL/dS = (sigmoid(S) - Y) inv_count).
+    Runs on whatever device the inputs are on (test infrastructure)."""
+    u = users.to(dtype)
+    p = positives.to(dtype)
+    B, Bc = u.shape[0], p.shape[0]
+    if inv_count is None:
+        inv_count = 1.0 / (B * Bc)
+    loss = 0.0
+    du = torch.empty_like(u)
+    dp = torch.zeros_like(p)
+    for lo in range(0, B, chunk):
+        hi = min(B, lo + chunk)
+        s = u[lo:hi] @ p.t()
+        y = torch.zeros_like(s)
+        rows = torch.arange(hi - lo, device=s.device)
+        y[rows, row_base + lo + rows] = 1.0
+        loss += float((s.clamp_min(0) - s * y + torch.log1p(torch.exp(-s.abs()))).sum().item())
+        ds = (torch.sigmoid(s) - y) * inv_count
+        du[lo:hi] = ds @ p
+        dp += ds.t() @ u[lo:hi]
+    return loss, du, dp
 
 
 def train_one_epoch(model, batches: Iterable, optimizers, *, negatives_per_positive: int, num_items: int,

@@ -21,9 +21,14 @@ def ttamm_model_from(prob: Problem, device="cuda"):
     return model
 
 
-def ttamm_optimizers(model, *, lr=1e-3, betas=(0.9, 0.999), weight_decay=0.01):
+def ttamm_optimizers(model, *, lr=1e-3, betas=(0.9, 0.999), weight_decay=0.01, optimizer="adamw", momentum=0.0):
+    """training.py:1311-1350 on the ttamm model (the same construction as oracle.build_optimizers)."""
     dense, sparse = ttamm._collect_parameter_groups(model)
-    opts = [torch.optim.AdamW(dense, lr=lr or 1e-3, weight_decay=weight_decay, betas=betas)]
+    if optimizer == "sgd":
+        opts = [torch.optim.SGD(dense, lr=lr or 1e-3, weight_decay=weight_decay, momentum=momentum)]
+    else:
+        cls = torch.optim.AdamW if optimizer == "adamw" else torch.optim.Adam
+        opts = [cls(dense, lr=lr or 1e-3, weight_decay=weight_decay, betas=betas)]
     if sparse:
         opts.append(torch.optim.SparseAdam(sparse, lr=lr or 1e-3, betas=betas))
     set_lr(opts, lr)
@@ -31,13 +36,15 @@ def ttamm_optimizers(model, *, lr=1e-3, betas=(0.9, 0.999), weight_decay=0.01):
 
 
 def run_ttamm(prob: Problem, *, lr=1e-3, betas=(0.9, 0.999), weight_decay=0.01, steps=None, device="cuda",
-              gradient_clip_norm=None):
+              gradient_clip_norm=None, optimizer="adamw", momentum=0.0, deferred_adamw=True):
     model = ttamm_model_from(prob, device)
-    opts = ttamm_optimizers(model, lr=lr, betas=betas, weight_decay=weight_decay)
+    opts = ttamm_optimizers(model, lr=lr, betas=betas, weight_decay=weight_decay, optimizer=optimizer,
+                            momentum=momentum)
     eng = ttamm.FusedTrainStep(
         model, opts, negatives_per_positive=prob.shape.N, positives=prob.positives,
         user_features=prob.user_features.to(device), item_features=prob.item_features.to(device),
         loss_weights=LOSS_WEIGHTS, max_batch=prob.shape.B, gradient_clip_norm=gradient_clip_norm,
+        deferred_adamw=deferred_adamw,
     )
     losses = []
     for (users, pos, neg, um, im) in prob.batches[: steps or len(prob.batches)]:

@@ -125,9 +125,10 @@ def clone_model(model):
 
 
 def run_oracle(prob: Problem, *, lr=1e-3, betas=(0.9, 0.999), weight_decay=0.01, steps=None, model=None,
-               gradient_clip_norm=None):
+               gradient_clip_norm=None, optimizer="adamw", momentum=0.0):
     model = model if model is not None else clone_model(prob.model)
-    opts = ref.build_optimizers(model, lr=lr or 1e-3, betas=betas, weight_decay=weight_decay)
+    opts = ref.build_optimizers(model, lr=lr or 1e-3, betas=betas, weight_decay=weight_decay, optimizer=optimizer,
+                                momentum=momentum)
     set_lr(opts, lr)
     results = []
     for (users, pos, neg, um, im) in prob.batches[: steps or len(prob.batches)]:

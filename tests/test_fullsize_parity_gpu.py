@@ -2,7 +2,8 @@
 CPU oracle (oracle/cpu_reference.train_step, the reference's training.py:726-831 restated) on
 the same parameters, batch, injected negatives and dropout keep-masks, at
 
-  * C2            2M items x 200K users, D = 96, MLP 605 -> 192 -> 96, B = 8192, N = 5 sampled;
+  * C2            2M items x 200K users, D = 96, MLP 605 -> 192 -> 96, B = 8192, N = 5 sampled,
+                  and in-batch (8192 x 8192 logits, no sampled negatives);
   * the C4 shard  6.25M items x 25K users, D = 128, MLP 605 -> 256 -> 128, B = 8192, in-batch
                   negatives (8192 x 8192 logits);
   * C5            2M items x 200K users, D = 256, MLP 605 -> 512 -> 256, bf16 tower GEMMs, B = 8192,
@@ -91,12 +92,14 @@ def _mean_abs_diff(a: torch.Tensor, b: torch.Tensor, rows: int = 1 << 20) -> flo
     return tot / max(1, a.numel())
 
 
-def _one_step(cfg_name: str, *, seed: int, in_batch: bool):
+def _one_step(cfg_name: str, *, seed: int, in_batch: bool, num_neg: int | None = None):
     import bench
     import ttamm
     from oracle import cpu_reference as ref
 
     c = dict(bench.CONFIGS[cfg_name])
+    if num_neg is not None:
+        c["N"] = num_neg
     U, I, F, D, H, B, N = (c[k] for k in ("U", "I", "F", "D", "H", "B", "N"))
     dev = torch.device("cuda")
     _log(f"{cfg_name}: building inputs (U={U}, I={I}, D={D}, H={H}, B={B}, N={N}, in_batch={in_batch})")
@@ -225,6 +228,13 @@ def _compare(om, oopts, tm, topts, ores, tl, fp64_grads, *, tol: float, mean_tol
 def test_c2_one_step_matches_oracle():
     """BASELINE C2, sampled negatives (the reference's semantics), fp32, 1e-5."""
     out = _one_step("c2", seed=2024, in_batch=False)
+    _compare(*out, tol=1e-5, mean_tol=None, loss_tol=1e-5)
+
+
+def test_c2_inbatch_one_step_matches_oracle():
+    """BASELINE configs[1] as worded: C2 with in-batch negatives (8192 x 8192 logits, D = 96,
+    no sampled negatives — bench.py --negatives in-batch), fp32, 1e-5."""
+    out = _one_step("c2", seed=2025, in_batch=True, num_neg=0)
     _compare(*out, tol=1e-5, mean_tol=None, loss_tol=1e-5)
 
 

@@ -121,3 +121,24 @@ def test_normalize_l2_known_answer():
     assert y[2].tolist() == [0.0, -1.0]
     assert abs(float(y[3, 0]) - 2 ** -0.5) < 1e-7 and y[3, 0] == y[3, 1]
     assert x[0].tolist() == [3, 4]  # input not modified
+
+
+def test_chunked_inbatch_definition_equals_train_step_block():
+    """oracle.inbatch_bce_chunked (the definition the in-batch op tests use at full size) is the
+    in-batch block of train_step(in_batch=True): autograd of BCEWithLogits over u @ p^T."""
+    import torch
+    from oracle import cpu_reference as ref
+
+    g = torch.Generator().manual_seed(3)
+    u = (torch.randn((37, 12), generator=g) * 0.4).double().requires_grad_()
+    p = (torch.randn((37, 12), generator=g) * 0.4).double().requires_grad_()
+    s = u @ p.t()
+    loss = torch.nn.BCEWithLogitsLoss()(s.reshape(-1), torch.eye(37, dtype=s.dtype).reshape(-1))
+    loss.backward()
+    got_sum, du, dp = ref.inbatch_bce_chunked(u.detach(), p.detach(), chunk=10)
+    assert abs(got_sum / 37 ** 2 - float(loss)) <= 1e-12
+    assert torch.allclose(du, u.grad, rtol=0, atol=1e-14)
+    assert torch.allclose(dp, p.grad, rtol=0, atol=1e-14)
+    # a rank's block of a sharded batch: users 10..19 of the global batch score all 37 positives
+    _, du2, _ = ref.inbatch_bce_chunked(u.detach()[10:20], p.detach(), row_base=10, inv_count=1 / 37 ** 2)
+    assert torch.allclose(du2, u.grad[10:20], rtol=0, atol=1e-14)

@@ -267,3 +267,17 @@ TTAMM_API int ttamm_adamw_dense(float* param, float* exp_avg, float* exp_avg_sq,
     a.ad = make_adam_consts(lr, beta1, beta2, eps, weight_decay, decoupled, step);
     return launch_dense_adam(a, (hipStream_t)stream);
 }
+
+TTAMM_API size_t ttamm_inbatch_workspace_size(int64_t batch, int64_t n_positives, int32_t dim) {
+    if (batch <= 0 || n_positives <= 0 || dim <= 0) return 0;
+    return inbatch_standalone_workspace_bytes(batch, n_positives, dim);
+}
+
+TTAMM_API int ttamm_inbatch_bce(const float* users, int64_t batch, int64_t ldu, const float* positives,
+                                int64_t n_positives, int64_t ldp, int32_t dim, int64_t row_base, float inv_count,
+                                float* d_users, int64_t ld_du, float* d_positives, int64_t ld_dp, double* loss_sum,
+                                void* workspace, size_t workspace_bytes, void* stream) {
+    g_last_error.clear();
+    return inbatch_standalone(users, batch, ldu, positives, n_positives, ldp, dim, row_base, inv_count, d_users,
+                              ld_du, d_positives, ld_dp, loss_sum, workspace, workspace_bytes, (hipStream_t)stream);
+}

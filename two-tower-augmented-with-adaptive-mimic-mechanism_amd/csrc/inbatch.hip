@@ -439,6 +439,21 @@ __global__ void ib_reduce_kernel(InBatchArgs A) {
     }
 }
 
+// The BCE sum over the user-role blocks' partial sums, in block order (fp64 accumulation):
+// the standalone entry's loss (the fused step folds the parts into loss_finalize_kernel).
+__global__ void ib_loss_sum_kernel(const float* __restrict__ parts, int n, double* __restrict__ out) {
+    __shared__ double red[256];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) s += (double)parts[i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[0] = red[0];
+}
+
 }  // namespace
 
 void inbatch_plan(int64_t B, int64_t Bc, InBatchArgs& a) {
@@ -494,6 +509,34 @@ int launch_inbatch(InBatchArgs& a, hipStream_t s) {
     const int64_t total = (a.B + a.Bc) * a.D;
     hipLaunchKernelGGL(ib_reduce_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(total, 256), 8192)), dim3(256), 0, s,
                        a);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+size_t inbatch_standalone_workspace_bytes(int64_t B, int64_t Bc, int D) {
+    size_t su, sp, parts;
+    inbatch_workspace_floats(B, Bc, D, &su, &sp, &parts);
+    return sizeof(float) * (su + sp + parts);
+}
+
+int inbatch_standalone(const float* U, int64_t B, int64_t ldu, const float* P, int64_t Bc, int64_t ldp, int D,
+                       int64_t row_base, float inv_T, float* dU, int64_t ld_du, float* dP, int64_t ld_dp,
+                       double* loss_sum, void* ws, size_t ws_bytes, hipStream_t s) {
+    TTAMM_REQUIRE(U && P && dU && dP && loss_sum && ws, "inbatch_bce: null argument");
+    TTAMM_REQUIRE(B > 0 && Bc > 0 && D > 0 && ldu >= D && ldp >= D && ld_du >= D && ld_dp >= D,
+                  "inbatch_bce: bad shape");
+    TTAMM_REQUIRE(ws_bytes >= inbatch_standalone_workspace_bytes(B, Bc, D), "inbatch_bce: workspace too small");
+    InBatchArgs a{};
+    a.U = U, a.ldu = ldu, a.B = B, a.P = P, a.ldp = ldp, a.Bc = Bc, a.D = D;
+    a.row_base = row_base, a.inv_T = inv_T;
+    size_t su, sp, parts;
+    inbatch_workspace_floats(B, Bc, D, &su, &sp, &parts);
+    float* w = static_cast<float*>(ws);
+    a.slab_u = w, a.slab_p = w + su, a.loss_part = w + su + sp;
+    a.dU = dU, a.ld_du = ld_du, a.dP = dP, a.ld_dp = ld_dp;
+    const int rc = launch_inbatch(a, s);
+    if (rc != TTAMM_OK) return rc;
+    hipLaunchKernelGGL(ib_loss_sum_kernel, dim3(1), dim3(256), 0, s, a.loss_part, a.rblk_u * a.splits_u, loss_sum);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

@@ -321,6 +321,10 @@ struct InBatchArgs {
 void inbatch_plan(int64_t B, int64_t Bc, InBatchArgs& a);
 size_t inbatch_workspace_floats(int64_t B, int64_t Bc, int D, size_t* slab_u, size_t* slab_p, size_t* parts);
 int launch_inbatch(InBatchArgs& a, hipStream_t s);
+size_t inbatch_standalone_workspace_bytes(int64_t B, int64_t Bc, int D);
+int inbatch_standalone(const float* U, int64_t B, int64_t ldu, const float* P, int64_t Bc, int64_t ldp, int D,
+                       int64_t row_base, float inv_T, float* dU, int64_t ld_du, float* dP, int64_t ld_dp,
+                       double* loss_sum, void* ws, size_t ws_bytes, hipStream_t s);
 
 // ------------------------------------------------------------------------------------
 // Exact inner-product retrieval + top-k (retrieval.hip)
@@ -448,6 +452,13 @@ struct AdamConsts {
     float wd;        // weight_decay (Adam L2 form)
     int decoupled;
     int fast_g0;     // g = 0 updates with v_sqrt / v_rcp (ttamm.h TTAMM_G0_FAST)
+    // torch.optim.SGD instead (ttamm.h TTAMM_DENSE_SGD): m holds the momentum buffer, v aliases it
+    int sgd;
+    float sgd_neg_lr;  // -lr
+    float sgd_mom;     // momentum
+    float sgd_damp1;   // 1 - dampening
+    int sgd_first;     // no buffer yet: buf = grad
+    int sgd_nesterov;
 };
 struct SparseConsts {
     float w1;        // 1 - beta1
@@ -624,6 +635,8 @@ int launch_sparse_adam_rows(float* w, float* m, float* v, int dim, const int64_t
 float correctly_rounded_reciprocal(float c);  // RN(1/c), c > 0 normal
 AdamConsts make_adam_consts(double lr, double beta1, double beta2, double eps, double wd,
                             int decoupled, int64_t step);
+// torch.optim.SGD (training.py:1324-1330): first = the momentum buffers do not exist yet
+AdamConsts make_sgd_consts(double lr, double wd, double momentum, double dampening, int nesterov, int first);
 SparseConsts make_sparse_consts(double lr, double beta1, double beta2, double eps, int64_t step);
 
 // ------------------------------------------------------------------------------------

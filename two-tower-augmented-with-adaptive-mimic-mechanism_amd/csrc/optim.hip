@@ -17,6 +17,7 @@
 #include <climits>
 #include <cstdlib>
 #include <cmath>
+#include <cstring>
 
 #include "kernels.h"
 
@@ -61,14 +62,37 @@ __device__ __forceinline__ void adam_elem_t(float& p, float& m, float& v, float 
     }
 }
 
+// torch.optim.SGD single-tensor step (sgd.py _single_tensor_sgd; training.py:1324-1330):
+//   grad = grad.add(param, alpha=wd)                  ATen add: fmadd(param, wd, grad)
+//   buf  = grad.clone() (first step) | buf.mul_(momentum).add_(grad, alpha=1 - dampening)
+//   grad = grad.add(buf, alpha=momentum) (nesterov) | buf ;  param.add_(grad, alpha=-lr)
+// m is the momentum buffer; v aliases it (or, momentum == 0, both alias the parameter), so the
+// callers' three stores all write the value that belongs at that address.
+__device__ __forceinline__ void sgd_elem(float& p, float& m, float& v, float g, const AdamConsts& c) {
+    if (c.wd != 0.f) g = fmaf(p, c.wd, g);
+    if (c.sgd_mom != 0.f) {
+        const float buf = c.sgd_first ? g : fmaf(g, c.sgd_damp1, m * c.sgd_mom);
+        g = c.sgd_nesterov ? fmaf(buf, c.sgd_mom, g) : buf;
+        p = fmaf(g, c.sgd_neg_lr, p);
+        m = v = buf;
+    } else {
+        p = fmaf(g, c.sgd_neg_lr, p);
+        m = v = p;
+    }
+}
+
 __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, const AdamConsts& c) {
-    if (c.decoupled)
+    if (c.sgd)
+        sgd_elem(p, m, v, g, c);
+    else if (c.decoupled)
         adam_elem_t<true>(p, m, v, g, c);
     else
         adam_elem_t<false>(p, m, v, g, c);
 }
 __device__ __forceinline__ void adam_elem_g0(float& p, float& m, float& v, const AdamConsts& c) {
-    if (c.fast_g0) {
+    if (c.sgd) {
+        sgd_elem(p, m, v, 0.f, c);
+    } else if (c.fast_g0) {
         if (c.decoupled)
             adam_elem_t<true, true, true>(p, m, v, 0.f, c);
         else
@@ -1098,6 +1122,20 @@ AdamConsts make_adam_consts(double lr, double beta1, double beta2, double eps, d
     c.wd = (float)wd;
     c.decoupled = decoupled;
     c.fast_g0 = 0;
+    c.sgd = 0, c.sgd_neg_lr = 0.f, c.sgd_mom = 0.f, c.sgd_damp1 = 0.f, c.sgd_first = 0, c.sgd_nesterov = 0;
+    return c;
+}
+
+AdamConsts make_sgd_consts(double lr, double wd, double momentum, double dampening, int nesterov, int first) {
+    AdamConsts c;
+    std::memset(&c, 0, sizeof(c));
+    c.sgd = 1;
+    c.sgd_neg_lr = (float)(-lr);
+    c.wd = (float)wd;
+    c.sgd_mom = (float)momentum;
+    c.sgd_damp1 = (float)(1.0 - dampening);
+    c.sgd_first = first ? 1 : 0;
+    c.sgd_nesterov = nesterov ? 1 : 0;
     return c;
 }
 

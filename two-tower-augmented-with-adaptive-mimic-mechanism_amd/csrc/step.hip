@@ -1287,8 +1287,10 @@ int table_updates(const ttamm_tower* T[2], TowerWs* W[2], int n, int D, bool mim
         for (int k = 0; k < n; ++k) add_seg(sw, T[k]->mimic);
     for (int k = 0; k < n; ++k)
         if (T[k]->id.optimizer == TTAMM_OPT_DENSE) add_seg(sw, T[k]->id);
+    // SGD without momentum or weight decay leaves g = 0 rows where they are: no sweep
+    const bool sweep = !(ad.sgd && ad.sgd_mom == 0.f && ad.wd == 0.f);
     if (events && events[0]) TTAMM_HIP(hipEventRecord((hipEvent_t)events[0], s));
-    if ((rc = launch_dense_sweep(sw, s))) return rc;
+    if (sweep && (rc = launch_dense_sweep(sw, s))) return rc;
     if (events && events[1]) TTAMM_HIP(hipEventRecord((hipEvent_t)events[1], s));
     for (int k = 0; k < n; ++k) {
         const ttamm_tower& t = *T[k];
@@ -1407,6 +1409,7 @@ int deferred_of(const ttamm_step_args& A, Deferred& df) {
         }
     }
     if (with == 0) return TTAMM_OK;
+    TTAMM_REQUIRE(A.hp.dense_optimizer == TTAMM_DENSE_ADAM, "deferred table updates are Adam / AdamW only (SGD: eager)");
     TTAMM_REQUIRE(with == total, "deferred AdamW: every dense-group table needs last_step");
     TTAMM_REQUIRE(A.adam_history != nullptr && A.replay_slices >= 1 && A.history_capacity > A.replay_slices &&
                       A.history_capacity <= kMaxAdamHistory,
@@ -1489,6 +1492,8 @@ int validate_step(const ttamm_step_args& A) {
                       "Adaptive mimic requires user and item embedding dimensions to match.");
     }
     TTAMM_REQUIRE(A.hp.dense_step >= 1 && A.hp.sparse_step >= 1, "optimizer step counts must be >= 1");
+    TTAMM_REQUIRE(A.hp.dense_optimizer == TTAMM_DENSE_ADAM || A.hp.dense_optimizer == TTAMM_DENSE_SGD,
+                  "hp.dense_optimizer must be TTAMM_DENSE_ADAM or TTAMM_DENSE_SGD");
     for (const ttamm_tower* t : {&A.user, &A.item})
         if (t->id.max_norm > 0.0) {
             TTAMM_REQUIRE(t->id.optimizer == TTAMM_OPT_DENSE, "max_norm is not supported when using sparse embeddings.");
@@ -1580,8 +1585,11 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     const ttamm_tower* T[2] = {&A.user, &A.item};
     TowerWs* W[2] = {&U, &I};
     const ttamm_hparams& hp = A.hp;
-    AdamConsts ad = make_adam_consts(hp.lr, hp.beta1, hp.beta2, hp.eps, hp.weight_decay,
-                                     hp.decoupled_weight_decay, hp.dense_step);
+    AdamConsts ad = hp.dense_optimizer == TTAMM_DENSE_SGD
+                        ? make_sgd_consts(hp.lr, hp.weight_decay, hp.momentum, hp.dampening, hp.nesterov,
+                                          hp.sgd_first_step)
+                        : make_adam_consts(hp.lr, hp.beta1, hp.beta2, hp.eps, hp.weight_decay,
+                                           hp.decoupled_weight_decay, hp.dense_step);
     ad.fast_g0 = A.table_g0_math == TTAMM_G0_FAST ? 1 : 0;
     const SparseConsts sp = make_sparse_consts(hp.sparse_lr, hp.sparse_beta1, hp.sparse_beta2, hp.sparse_eps,
                                                hp.sparse_step);

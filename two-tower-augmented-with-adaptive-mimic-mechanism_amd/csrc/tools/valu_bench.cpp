@@ -38,6 +38,10 @@ __global__ __launch_bounds__(256) void valu_kernel(float* out, float a, float b)
             if (OP == 2) y[i] = y[i] * a2;       // v_pk_mul_f32
             if (OP == 3) x[i] = __builtin_amdgcn_sqrtf(x[i]);
             if (OP == 4) x[i] = __builtin_amdgcn_rcpf(x[i]);
+            if (OP == 6) asm volatile("v_mul_f32_e32 %0, %1, %0" : "+v"(x[i]) : "v"(a));
+            if (OP == 7) asm volatile("v_fmac_f32_e32 %0, %1, %2" : "+v"(x[i]) : "v"(a), "v"(b));
+            if (OP == 8) asm volatile("v_add_f32_e32 %0, %1, %0" : "+v"(x[i]) : "v"(b));
+            if (OP == 9) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(y[i]) : "v"(a2));
             if (OP == 5) {  // the replay's warm mix per element pair: 3 pk + 2 sqrt + 2 fma + 2 rcp + ...
                 x[i] = __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_sqrtf(x[i]), a, b));
             }
@@ -84,5 +88,9 @@ int main() {
     run<3>("v_sqrt_f32", 1, out, cus);
     run<4>("v_rcp_f32", 1, out, cus);
     run<5>("sqrt+fma+rcp (3 instr)", 3, out, cus);
+    run<6>("v_mul_f32_e32 (VOP2)", 1, out, cus);
+    run<7>("v_fmac_f32_e32 (VOP2)", 1, out, cus);
+    run<8>("v_add_f32_e32 (VOP2)", 1, out, cus);
+    run<9>("v_pk_mul_f32 (asm)", 1, out, cus);
     return 0;
 }

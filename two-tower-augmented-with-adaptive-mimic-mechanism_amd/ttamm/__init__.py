@@ -14,6 +14,7 @@ from .encoders import (
     build_id_embedding,
     build_tower_encoder,
 )
+from .inbatch import inbatch_bce
 from .retrieval import encode_item_embeddings, evaluate_model, prepare_faiss_resources
 from .samplers import PositivesCSR, sample_negative_items
 from .training import DotProductSimilarity, FusedTrainStep, _collect_parameter_groups, train_one_epoch
@@ -35,6 +36,7 @@ __all__ = [
     "build_tower_encoder",
     "encode_item_embeddings",
     "evaluate_model",
+    "inbatch_bce",
     "load_features",
     "load_interactions",
     "prepare_faiss_resources",

@@ -102,6 +102,11 @@ class HParams(ctypes.Structure):
         ("lambda_mimic_item", c_d),
         ("lambda_category_alignment", c_d),
         ("grad_clip_norm", c_d),
+        ("dense_optimizer", c_i32),
+        ("momentum", c_d),
+        ("dampening", c_d),
+        ("nesterov", c_i32),
+        ("sgd_first_step", c_i32),
     ]
 
 
@@ -171,8 +176,10 @@ class StepArgs(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 20  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 22  # ttamm.h TTAMM_ABI_VERSION
 G0_EXACT = 0  # ttamm.h TTAMM_G0_EXACT
+DENSE_ADAM = 0  # ttamm.h TTAMM_DENSE_ADAM
+DENSE_SGD = 1  # ttamm.h TTAMM_DENSE_SGD
 G0_FAST = 1  # ttamm.h TTAMM_G0_FAST
 
 # ttamm.h TTAMM_PHASE_*
@@ -258,6 +265,12 @@ SIGNATURES = {
     "ttamm_adamw_dense": (
         ctypes.c_int,
         [c_vp, c_vp, c_vp, c_vp, c_i64, c_d, c_d, c_d, c_d, c_d, c_i32, c_i64, c_vp],
+    ),
+    "ttamm_inbatch_workspace_size": (ctypes.c_size_t, [c_i64, c_i64, c_i32]),
+    "ttamm_inbatch_bce": (
+        ctypes.c_int,
+        [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_i32, c_i64, ctypes.c_float, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp,
+         ctypes.c_size_t, c_vp],
     ),
 }
 

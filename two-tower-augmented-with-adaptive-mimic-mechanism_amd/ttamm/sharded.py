@@ -557,6 +557,7 @@ class ShardedTrainStep(FusedTrainStep):
         a.timing_events[0] = a.timing_events[1] = None
         self._phase(_lib.PHASE_DENSE)
         self.steps_done += 1
+        self._register_sgd_buffers()
         # keep the step's device buffers alive until the stream has consumed them
         self._live = (route, back, bwd_in) + ib
 

@@ -156,17 +156,24 @@ class FusedTrainStep:
         for opt in optimizers:
             if isinstance(opt, torch.optim.SparseAdam):
                 sparse_opt = opt
-            elif isinstance(opt, (torch.optim.AdamW, torch.optim.Adam)):
+            elif isinstance(opt, (torch.optim.AdamW, torch.optim.Adam, torch.optim.SGD)):
                 dense_opt = opt
             else:
-                raise NotImplementedError(f"ttamm: optimizer {type(opt).__name__} is not implemented (Adam/AdamW + SparseAdam)")
+                raise NotImplementedError(
+                    f"ttamm: optimizer {type(opt).__name__} is not implemented (Adam / AdamW / SGD + SparseAdam)")
         self.dense_opt, self.sparse_opt = dense_opt, sparse_opt
+        # the dense group's optimizer (training.py:1311-1333): Adam / AdamW, or SGD with momentum
+        self.sgd = isinstance(dense_opt, torch.optim.SGD)
+        self._sgd_buffers: list[tuple[torch.Tensor, torch.Tensor]] = []  # (param, buffer) not yet in state
         dense_ids = {id(p) for g in (dense_opt.param_groups if dense_opt else []) for p in g["params"]}
         sparse_ids = {id(p) for g in (sparse_opt.param_groups if sparse_opt else []) for p in g["params"]}
+        self.decoupled = False
         if dense_opt is not None:
             g = _single_group(dense_opt)
             if g.get("amsgrad") or g.get("maximize"):
                 raise NotImplementedError("ttamm: amsgrad / maximize are not implemented")
+            if self.sgd and g.get("differentiable"):
+                raise NotImplementedError("ttamm: differentiable SGD is not implemented")
             self.decoupled = isinstance(dense_opt, torch.optim.AdamW) or bool(g.get("decoupled_weight_decay", False))
         if sparse_opt is not None and _single_group(sparse_opt).get("maximize"):
             raise NotImplementedError("ttamm: maximize is not implemented")
@@ -180,9 +187,12 @@ class FusedTrainStep:
         def dense_param(p: torch.Tensor) -> None:
             if id(p) not in dense_ids:
                 raise ValueError("ttamm: a trained parameter is missing from the dense optimizer")
-            st = _adam_state(dense_opt, p)
-            state[id(p)] = st
-            self._adam_steps.append(st)
+            if self.sgd:
+                state[id(p)] = self._sgd_state(dense_opt, p)
+            else:
+                st = _adam_state(dense_opt, p)
+                state[id(p)] = st
+                self._adam_steps.append(st)
             handled.add(id(p))
 
         self.towers = {}
@@ -314,7 +324,7 @@ class FusedTrainStep:
         # deferred exact AdamW(g = 0) on the dense-group tables (ttamm.h ttamm_table.last_step):
         # the rows are current to dense_step0 now
         self._deferred: list[torch.Tensor] = []
-        if deferred_adamw and self.dense_opt is not None:
+        if deferred_adamw and self.dense_opt is not None and not self.sgd:
             if not 1 <= replay_slices <= 255:
                 raise ValueError("ttamm: replay_slices must be in [1, 255]")
             tables = []
@@ -370,12 +380,37 @@ class FusedTrainStep:
         self._keep = getattr(self, "_keep", []) + [out]
         return out
 
+    def _sgd_state(self, opt: torch.optim.Optimizer, p: torch.Tensor) -> dict:
+        """The kernels' view of torch.optim.SGD's state (sgd.py): the momentum buffer as exp_avg
+        (exp_avg_sq aliases it), created by the first step as torch does (buf = grad.clone());
+        without momentum torch keeps no state and both alias the parameter (ttamm.h
+        TTAMM_DENSE_SGD)."""
+        if float(opt.param_groups[0]["momentum"]) == 0.0:
+            return {"exp_avg": p, "exp_avg_sq": p}
+        buf = opt.state[p].get("momentum_buffer")
+        if buf is None:
+            buf = torch.zeros_like(p, memory_format=torch.preserve_format)
+            self._sgd_buffers.append((p, buf))
+        elif buf.shape != p.shape or not buf.is_contiguous():
+            raise ValueError("ttamm: SGD momentum_buffer must be a contiguous tensor of the parameter's shape")
+        return {"exp_avg": buf, "exp_avg_sq": buf}
+
     def _configure(self, args: _lib.StepArgs) -> None:
         """Hook: descriptor fields that shape the workspace (set before it is sized)."""
 
     def _hparams(self) -> None:
         hp = self.args.hp
-        if self.dense_opt is not None:
+        if self.sgd:
+            g = self.dense_opt.param_groups[0]
+            hp.dense_optimizer = _lib.DENSE_SGD
+            hp.lr = float(g["lr"])
+            hp.weight_decay = float(g["weight_decay"])
+            hp.momentum = float(g["momentum"])
+            hp.dampening = float(g["dampening"])
+            hp.nesterov = 1 if g["nesterov"] else 0
+            # torch creates every momentum buffer at the first step that has gradients
+            hp.sgd_first_step = 1 if self._sgd_buffers else 0
+        elif self.dense_opt is not None:
             g = self.dense_opt.param_groups[0]
             hp.lr = float(g["lr"])
             hp.beta1, hp.beta2 = (float(b) for b in g["betas"])
@@ -410,6 +445,14 @@ class FusedTrainStep:
         self._hparams()
         _lib.check(self.lib.ttamm_train_step(ctypes.byref(a), _lib.stream_handle(self.device)))
         self.steps_done += 1
+        self._register_sgd_buffers()
+
+    def _register_sgd_buffers(self) -> None:
+        """After the first enqueued step: it wrote buf = grad into the SGD momentum buffers
+        (stream-ordered), so torch's optimizer state holds them from now on."""
+        for p, buf in self._sgd_buffers:
+            self.dense_opt.state[p]["momentum_buffer"] = buf
+        self._sgd_buffers = []
 
     def _bind_batch(self, users, pos_items, neg_items, keep_masks) -> bool:
         B = users.numel()
