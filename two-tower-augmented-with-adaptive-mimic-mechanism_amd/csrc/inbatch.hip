@@ -240,16 +240,18 @@ __device__ __forceinline__ f32x16 ibx_mfma6(const bf16x8_t a[3], const bf16x8_t 
     return c;
 }
 
-// MINB blocks per CU
-template <int DP, int MINB>
-__global__ __launch_bounds__(256, MINB) void inbatch_x_kernel(InBatchArgs A) {
+// MINB blocks per CU of NW waves (32 rows each); DBUF: two LDS tile buffers (one barrier per
+// tile, the next tile split and stored right after this one's MFMAs)
+template <int DP, int MINB, int NW, bool DBUF>
+__global__ __launch_bounds__(64 * NW, MINB) void inbatch_x_kernel(InBatchArgs A) {
+    constexpr int NT = 64 * NW;                      // threads
     constexpr int NB = DP / 32;                      // 32-wide output column blocks
     constexpr int KS = DP / 16;                      // k steps of product 1
     constexpr int TF4 = kIbTile * DP / 4;            // float4 per column tile
-    constexpr int LOADS = TF4 / 256;
-    static_assert(TF4 % 256 == 0, "whole staging rounds");
-    __shared__ __attribute__((aligned(16))) unsigned char tile[3 * kIbxPlane];
-    __shared__ float red[4];
+    constexpr int LOADS = TF4 / NT;
+    static_assert(TF4 % NT == 0, "whole staging rounds");
+    __shared__ __attribute__((aligned(16))) unsigned char tiles[DBUF ? 2 : 1][3 * kIbxPlane];
+    __shared__ float red[NW];
 
     int blk = blockIdx.x;
     const int nu = A.rblk_u * A.splits_u;
@@ -266,7 +268,7 @@ __global__ __launch_bounds__(256, MINB) void inbatch_x_kernel(InBatchArgs A) {
     const int D = A.D;
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, h = lane >> 5;
-    const int64_t r0 = (int64_t)rb * kIbRows + 32 * w;
+    const int64_t r0 = (int64_t)rb * (32 * NW) + 32 * w;
 
     // this lane's row fragments (B operand of product 1): R[r0 + li][16 s + 8 h + j], zero past D / nr
     bf16x8_t rf[KS][3];
@@ -291,30 +293,30 @@ __global__ __launch_bounds__(256, MINB) void inbatch_x_kernel(InBatchArgs A) {
     for (int n = 0; n < NB; ++n)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[n][r] = 0.f;
-    float bce = 0.f;
+    float bce = 0.f, bce_lin = 0.f, bce_log2 = 0.f;
 
     // column tile -> registers (zero past c_end / D, so masked rows contribute exact zeros)
     float4 st[LOADS];
     auto load = [&](int64_t c0) {
 #pragma unroll
         for (int it = 0; it < LOADS; ++it) {
-            const int lin = tid + it * 256;
+            const int lin = tid + it * NT;
             const int row = lin / (DP / 4), col = (lin - row * (DP / 4)) * 4;
             const int64_t gc = c0 + row;
             st[it] = (gc < c_end && col < D) ? *reinterpret_cast<const float4*>(C + gc * ldc + col)
                                              : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
-    auto store = [&]() {
+    auto store = [&](unsigned char* dst) {
 #pragma unroll
         for (int it = 0; it < LOADS; ++it) {
-            const int lin = tid + it * 256;
+            const int lin = tid + it * NT;
             const int row = lin / (DP / 4), c4 = lin - row * (DP / 4);
             const int o = ibx_off(row, c4 >> 1) + 8 * (c4 & 1);
             uint2 pl[3];
             ibx_split(st[it], pl);
 #pragma unroll
-            for (int q = 0; q < 3; ++q) *reinterpret_cast<uint2*>(tile + q * kIbxPlane + o) = pl[q];
+            for (int q = 0; q < 3; ++q) *reinterpret_cast<uint2*>(dst + q * kIbxPlane + o) = pl[q];
         }
     };
 
@@ -322,23 +324,37 @@ __global__ __launch_bounds__(256, MINB) void inbatch_x_kernel(InBatchArgs A) {
     // the next tile in flight in registers while this one is multiplied (narrow D); at D > 64 the
     // registers go to the operands and the second block of the CU hides the load instead
     constexpr bool PREFETCH = DP <= 64 || MINB == 1;
-    if (PREFETCH && ntiles > 0) load(c_begin);
+    if (DBUF) {  // tile 0 in buffer 0, tile 1 in flight in registers
+        if (ntiles > 0) {
+            load(c_begin);
+            store(tiles[0]);
+            if (ntiles > 1) load(c_begin + kIbTile);
+        }
+        __syncthreads();
+    } else if (PREFETCH && ntiles > 0) {
+        load(c_begin);
+    }
     // tr-read lane roles: 16-lane group g, lane 4q + p of the group
     const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
     const int64_t gr = r0 + li;
     for (int t = 0; t < ntiles; ++t) {
         const int64_t c0 = c_begin + (int64_t)t * kIbTile;
-        if (!PREFETCH) load(c0);
-        __syncthreads();  // every wave is done with the previous tile
-        store();
-        __syncthreads();
-        if (PREFETCH && t + 1 < ntiles) load(c0 + kIbTile);  // in flight during this tile's MFMAs
+        unsigned char* const tile = tiles[DBUF ? (t & 1) : 0];
+        if (!DBUF) {
+            if (!PREFETCH) load(c0);
+            __syncthreads();  // every wave is done with the previous tile
+            store(tile);
+            __syncthreads();
+            if (PREFETCH && t + 1 < ntiles) load(c0 + kIbTile);  // in flight during this tile's MFMAs
+        }
         // the label Y = 1 sits at tile column diag of this lane's row: user u's own positive is
         // column row_base + u (user role), positive i's user is row i - row_base (item role)
         const int64_t dl = role_u ? A.row_base + gr - c0 : gr - A.row_base - c0;
         const int diag = (dl >= 0 && dl < kIbTile) ? (int)dl : -1;
         const int cols_here = (int)min((int64_t)kIbTile, c_end - c0);
         const bool row_ok = gr < nr;
+        // wave-uniform: the whole 32 x 64 block is interior and label-free (most tiles)
+        const bool fast = cols_here == kIbTile && __builtin_amdgcn_ballot_w64(diag >= 0 || !row_ok) == 0;
 #pragma unroll
         for (int jc = 0; jc < 2; ++jc) {  // tile rows 32 jc .. 32 jc + 31
             // ---- product 1: S^T block [32 c x 32 u] --------------------------------------------------
@@ -355,20 +371,48 @@ __global__ __launch_bounds__(256, MINB) void inbatch_x_kernel(InBatchArgs A) {
             }
             // ---- dS^T in registers (lane: row u = r0 + li; register r: tile column c) -----------
             // hardware exp2 / log2 / rcp (<= 1-2 ulp): this elementwise pass, not the MFMAs, bounds
-            // the kernel with IEEE expf / logf / division
+            // the kernel with IEEE expf / logf / division.  Sigmoid and the ATen BCE term from one
+            // exp: t = exp(-|x|); for x >= 0 exp(-max(-x,0)) = 1 and exp(-x-max(-x,0)) = t, for x < 0
+            // the reverse.
+            if (fast) {
+                // every row and column in range, no label in this wave's block: y = 0, so the BCE
+                // term is max(x, 0) + ln(1 + t) (x + max(-x, 0) == max(x, 0) exactly), summed as
+                // two lane sums (the log2 terms scaled by ln 2 once at the end)
+                if (role_u) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int lc = 32 * jc + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const bool ok = row_ok && lc < cols_here;
-                const float y = lc == diag ? 1.0f : 0.0f;
-                const float x = s2[r];
-                // sigmoid and the ATen BCE term from one exp: t = exp(-|x|); for x >= 0
-                // exp(-max(-x,0)) = 1 and exp(-x-max(-x,0)) = t, for x < 0 the reverse
-                const float tx = __builtin_amdgcn_exp2f(-fabsf(x) * 1.4426950408889634f);
-                const float inv = __builtin_amdgcn_rcpf(1.0f + tx);
-                const float sg = x >= 0.f ? inv : tx * inv;
-                if (role_u && ok) bce += (1.0f - y) * x + fmaxf(-x, 0.f) + __builtin_amdgcn_logf(1.0f + tx) * 0.6931471805599453f;
-                s2[r] = ok ? (sg - y) * A.inv_T : 0.f;
+                    for (int r = 0; r < 16; ++r) {
+                        const float x = s2[r];
+                        const float tx = __builtin_amdgcn_exp2f(-fabsf(x) * 1.4426950408889634f);
+                        const float d1 = 1.0f + tx;
+                        const float inv = __builtin_amdgcn_rcpf(d1);
+                        const float sg = x >= 0.f ? inv : tx * inv;
+                        bce_lin += fmaxf(x, 0.f);
+                        bce_log2 += __builtin_amdgcn_logf(d1);
+                        s2[r] = sg * A.inv_T;
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const float x = s2[r];
+                        const float tx = __builtin_amdgcn_exp2f(-fabsf(x) * 1.4426950408889634f);
+                        const float inv = __builtin_amdgcn_rcpf(1.0f + tx);
+                        const float sg = x >= 0.f ? inv : tx * inv;
+                        s2[r] = sg * A.inv_T;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int lc = 32 * jc + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const bool ok = row_ok && lc < cols_here;
+                    const float y = lc == diag ? 1.0f : 0.0f;
+                    const float x = s2[r];
+                    const float tx = __builtin_amdgcn_exp2f(-fabsf(x) * 1.4426950408889634f);
+                    const float inv = __builtin_amdgcn_rcpf(1.0f + tx);
+                    const float sg = x >= 0.f ? inv : tx * inv;
+                    if (role_u && ok) bce += (1.0f - y) * x + fmaxf(-x, 0.f) + __builtin_amdgcn_logf(1.0f + tx) * 0.6931471805599453f;
+                    s2[r] = ok ? (sg - y) * A.inv_T : 0.f;
+                }
             }
             // ---- product 2: acc[n] (rows u, columns 32 n ..) += dS . tile ---------------------------
 #pragma unroll
@@ -401,6 +445,15 @@ __global__ __launch_bounds__(256, MINB) void inbatch_x_kernel(InBatchArgs A) {
                 }
             }
         }
+        if (DBUF) {
+            // tile t + 1 (landed in registers during this tile's MFMAs) into the other buffer, last
+            // read in tile t - 1 before that tile's barrier; tile t + 2 in flight
+            if (t + 1 < ntiles) {
+                store(tiles[(t + 1) & 1]);
+                if (t + 2 < ntiles) load(c0 + 2 * kIbTile);
+            }
+            __syncthreads();
+        }
     }
     // ---- partial rows -> this split's slab ------------------------------------------------------
     float* slab = role_u ? A.slab_u + (int64_t)sp * A.B * D : A.slab_p + (int64_t)sp * A.Bc * D;
@@ -414,10 +467,15 @@ __global__ __launch_bounds__(256, MINB) void inbatch_x_kernel(InBatchArgs A) {
             if (gr < nr && col < D) slab[gr * D + col] = acc[n][r];
         }
     if (role_u) {
-        bce = wave_sum(bce);
+        bce = wave_sum(bce + (bce_lin + bce_log2 * 0.6931471805599453f));
         if (lane == 0) red[w] = bce;
         __syncthreads();
-        if (tid == 0) A.loss_part[blk] = (red[0] + red[1]) + (red[2] + red[3]);
+        if (tid == 0) {
+            float sum = 0.f;
+#pragma unroll
+            for (int i = 0; i < NW; i += 2) sum += red[i] + red[i + 1];
+            A.loss_part[blk] = sum;
+        }
     }
 }
 
@@ -456,11 +514,25 @@ __global__ void ib_loss_sum_kernel(const float* __restrict__ parts, int n, doubl
 
 }  // namespace
 
+// Waves per block of the split-bf16 kernel: 4 (128 rows per block, two blocks per CU, one tile
+// buffer), or TTAMM_IB_WAVES=8 (256 rows, one block per CU, double-buffered: the column tile staged
+// once for twice the rows, but the tile prefetch registers push D = 128 into spills — 9.3 vs
+// 3.15 ms at the C4 rank shape, profiles/r04_inbatch_variants.txt); the fp32-MFMA kernel
+// (TTAMM_FP32_MFMA=exact) always uses 4.
+int inbatch_waves() {
+    const char* mf = std::getenv("TTAMM_FP32_MFMA");
+    if (mf && std::strcmp(mf, "exact") == 0) return 4;
+    const char* env = std::getenv("TTAMM_IB_WAVES");
+    return (env && std::atoi(env) == 8) ? 8 : 4;
+}
+
 void inbatch_plan(int64_t B, int64_t Bc, InBatchArgs& a) {
-    a.rblk_u = (int)ceil_div(B, kIbRows);
-    a.rblk_p = (int)ceil_div(Bc, kIbRows);
-    // ~4 blocks per CU over both roles: split the columns so each role has >= ~512 blocks
-    const int64_t want = 512;
+    const int rows = 32 * inbatch_waves();
+    a.rblk_u = (int)ceil_div(B, rows);
+    a.rblk_p = (int)ceil_div(Bc, rows);
+    // ~4 waves per SIMD over both roles: split the columns so each role has >= ~512 blocks of 4
+    // waves (>= ~256 of 8)
+    const int64_t want = rows == 128 ? 512 : 256;
     a.splits_u = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(Bc, kIbTile), ceil_div(want, a.rblk_u)));
     a.splits_p = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(B, kIbTile), ceil_div(want, a.rblk_p)));
     a.cols_u = ceil_div(ceil_div(Bc, a.splits_u), kIbTile) * kIbTile;
@@ -496,13 +568,22 @@ int launch_inbatch(InBatchArgs& a, hipStream_t s) {
             default: hipLaunchKernelGGL(inbatch_kernel<128>, dim3(blocks), dim3(256), 0, s, a); break;
         }
     } else {
-        switch (dp) {
-            case 32: hipLaunchKernelGGL((inbatch_x_kernel<32, 2>), dim3(blocks), dim3(256), 0, s, a); break;
-            case 64: hipLaunchKernelGGL((inbatch_x_kernel<64, 2>), dim3(blocks), dim3(256), 0, s, a); break;
-            case 96: hipLaunchKernelGGL((inbatch_x_kernel<96, 2>), dim3(blocks), dim3(256), 0, s, a); break;
-            // D = 128 at two blocks per CU spills ~20 registers and still beats one block per CU
-            // (C4: 0.41 vs 0.50 ms per launch)
-            default: hipLaunchKernelGGL((inbatch_x_kernel<128, 2>), dim3(blocks), dim3(256), 0, s, a); break;
+        if (inbatch_waves() == 8) {
+            switch (dp) {
+                case 32: hipLaunchKernelGGL((inbatch_x_kernel<32, 1, 8, true>), dim3(blocks), dim3(512), 0, s, a); break;
+                case 64: hipLaunchKernelGGL((inbatch_x_kernel<64, 1, 8, true>), dim3(blocks), dim3(512), 0, s, a); break;
+                case 96: hipLaunchKernelGGL((inbatch_x_kernel<96, 1, 8, true>), dim3(blocks), dim3(512), 0, s, a); break;
+                default: hipLaunchKernelGGL((inbatch_x_kernel<128, 1, 8, true>), dim3(blocks), dim3(512), 0, s, a); break;
+            }
+        } else {
+            switch (dp) {
+                case 32: hipLaunchKernelGGL((inbatch_x_kernel<32, 2, 4, false>), dim3(blocks), dim3(256), 0, s, a); break;
+                case 64: hipLaunchKernelGGL((inbatch_x_kernel<64, 2, 4, false>), dim3(blocks), dim3(256), 0, s, a); break;
+                case 96: hipLaunchKernelGGL((inbatch_x_kernel<96, 2, 4, false>), dim3(blocks), dim3(256), 0, s, a); break;
+                // D = 128 at two blocks per CU spills ~20 registers and still beats one block per CU
+                // (C4: 0.41 vs 0.50 ms per launch)
+                default: hipLaunchKernelGGL((inbatch_x_kernel<128, 2, 4, false>), dim3(blocks), dim3(256), 0, s, a); break;
+            }
         }
     }
     TTAMM_LAUNCH_CHECK();
