@@ -136,3 +136,25 @@ def test_fast_g0_math_close_to_exact():
         d = (fast[k].double() - exact[k].double()).abs().max().item()
         scale = exact[k].double().abs().max().item()
         assert d <= 1e-6 * max(scale, 1e-30), (k, d, scale)
+
+
+def test_fast_g0_drift_bounded_over_many_steps():
+    """The fast g = 0 arithmetic over a long horizon: 150 steps on a 4096-item table that a
+    32-row batch mostly misses, so most item rows take 100+ consecutive g = 0 updates (each a few
+    ulp from torch's IEEE step).  Bound: every parameter within 2 ulp of its magnitude per step
+    of the IEEE path (fast vs exact), and far below the parameters' own movement; the moments are
+    the same operations in both modes (only the parameters the forward reads differ)."""
+    steps = 150
+    prob = make_problem(Shape(U=64, I=4096, B=32, N=5), seed=5)
+    init = {k: v.detach().clone() for k, v in prob.model.state_dict().items()}
+    fast, _ = _run(prob, steps, deferred=True, slices=8, math="fast")
+    exact, _ = _run(prob, steps, deferred=True, slices=8, math="exact")
+    name = "adaptive_mimic.item_augmented.weight"
+    f, e = fast[name].double(), exact[name].double()
+    err = (f - e).abs().max().item()
+    ulp = torch.finfo(torch.float32).eps * e.abs().max().item()
+    moved = (e.cpu() - init[name].double()).abs().max().item()
+    print(f"\nfast vs exact after {steps} steps: max |diff| {err:.3e} = {err / ulp:.1f} ulp(max|p|); "
+          f"max movement {moved:.3e}")
+    assert err <= 2 * steps * ulp, (err, ulp)
+    assert err <= 1e-3 * moved, (err, moved)

@@ -178,3 +178,43 @@ def test_train_mode_dropout_runs_and_is_reproducible():
     a, b, c = grads(True), grads(True), grads(False)
     assert torch.equal(a, b)
     assert not torch.equal(a, c)
+
+
+def test_mse_target_gradient_matches_torch():
+    """ttamm's F.mse_loss (adaptive_mimic._mse) with a target that requires grad: both inputs get
+    F.mse_loss's gradients (the reference detaches the target; an undetached one is not dropped)."""
+    from ttamm.adaptive_mimic import _mse
+
+    torch.manual_seed(5)
+    x = torch.randn(40, 16, device="cuda", requires_grad=True)
+    y = torch.randn(40, 16, device="cuda", requires_grad=True)
+    _mse(x, y).backward()
+    x2, y2 = x.detach().clone().requires_grad_(True), y.detach().clone().requires_grad_(True)
+    torch.nn.functional.mse_loss(x2, y2).backward()
+    assert rel_err(x.grad, x2.grad) <= 1e-6 and rel_err(y.grad, y2.grad) <= 1e-6
+    y3 = y.detach().clone().requires_grad_(True)  # only the target requires grad
+    _mse(x.detach(), y3).backward()
+    assert rel_err(y3.grad, y2.grad) <= 1e-6
+
+
+def test_tower_forward_with_mimic_rows_under_autograd():
+    """encoders.tower_forward(..., mimic_table=) in train mode: the tower's training forward plus
+    table[idx] with the table's gradient (adaptive_mimic.py:88-95), not the eval kernel."""
+    from ttamm.encoders import tower_forward
+
+    shape = Shape(dropout=0.0)
+    prob = make_problem(shape, steps=1)
+    model = _ttamm_model(prob, shape)
+    model.train()
+    users, pos, _, _, _ = prob.batches[0]
+    table = model.adaptive_mimic.item_augmented.weight
+    feats = prob.item_features.cuda()[pos.cuda()]
+    out = tower_forward(model.item_encoder, pos.cuda(), features=feats, mimic_table=table)
+    assert out.grad_fn is not None
+    base = model.item_encoder({"indices": pos.cuda(), "features": feats})
+    assert rel_err(out, base + table[pos.cuda()]) <= 1e-6
+    w = torch.randn_like(out)
+    (out * w).sum().backward()
+    want = torch.zeros_like(table).index_add_(0, pos.cuda(), w)
+    assert rel_err(table.grad, want) <= 1e-6
+    assert model.item_encoder.embedding.weight.grad is not None

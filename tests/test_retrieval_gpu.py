@@ -195,3 +195,34 @@ def test_recall_at_20_cosine_model_matches_oracle():
                                       item_features=prob.item_features, user_features=prob.user_features,
                                       num_items=shape.I, k_values=[10, 20])
     assert sum(preds_dot[u] != preds_o[u] for u in preds_o) > 0
+
+
+def test_near_ties_split_vs_fp32_kernel(monkeypatch):
+    """The default split-bf16 scores keep 6 of the 9 bf16 partial products (dropped terms below
+    2^-24 relative), so they are close to, not equal to, faiss IndexFlatIP's fp32 inner products.
+    Deliberately near-tied items (each a copy of a base item perturbed by ~1e-6 relative): the
+    default kernel and the fp32-MFMA kernel (TTAMM_RETRIEVAL_FP32=1) both return scores within
+    1e-6 relative of the exact (fp64) ones, and wherever their top-k lists differ, the items
+    involved are within 2^-18 relative of each other's exact score (near ties, not errors)."""
+    g = torch.Generator().manual_seed(19)
+    nq, D, k, groups, copies = 200, 96, 40, 500, 8
+    base = torch.randn((groups, D), generator=g)
+    items = (base.repeat_interleave(copies, 0) * (1 + 1e-6 * torch.randn((groups * copies, D), generator=g)))
+    queries = torch.randn((nq, D), generator=g)
+    exact = queries.double() @ items.double().T
+    monkeypatch.delenv("TTAMM_RETRIEVAL_FP32", raising=False)
+    s_split, i_split = retrieve_topk(queries.cuda(), items.cuda(), k)
+    monkeypatch.setenv("TTAMM_RETRIEVAL_FP32", "1")
+    s_fp32, i_fp32 = retrieve_topk(queries.cuda(), items.cuda(), k)
+    monkeypatch.delenv("TTAMM_RETRIEVAL_FP32", raising=False)
+    for s, i in ((s_split, i_split), (s_fp32, i_fp32)):
+        got = exact.gather(1, i.cpu())
+        assert ((s.cpu().double() - got).abs() <= 1e-6 * got.abs().clamp_min(1.0)).all()
+    diff_rows = (i_split.cpu() != i_fp32.cpu()).any(dim=1)
+    kth = exact.topk(k, dim=1).values[:, -1:]
+    # every returned item of either kernel is at or within a near tie of the exact k-th score
+    for i in (i_split, i_fp32):
+        got = exact.gather(1, i.cpu())
+        assert (got >= kth - 2.0 ** -18 * kth.abs().clamp_min(1.0)).all()
+    print(f"\nnear ties: {int(diff_rows.sum())} of {nq} queries order their top-{k} differently "
+          "(split-bf16 vs fp32 MFMA)")

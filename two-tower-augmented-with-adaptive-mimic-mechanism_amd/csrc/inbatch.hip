@@ -479,6 +479,226 @@ __global__ __launch_bounds__(64 * NW, MINB) void inbatch_x_kernel(InBatchArgs A)
     }
 }
 
+// ---- software-pipelined variant (default): one wave per SIMD ---------------------------------------
+// The split kernel above at two waves per SIMD spills at D = 128 (the row fragments, 96 registers,
+// and the dR accumulators, 64, leave too little of a 256-register budget), and its VALU work (the
+// sigmoid / BCE pass and the dS splits) only overlaps the MFMAs across the two waves.  Here one
+// 256-thread block per CU (one wave per SIMD, up to 512 registers: no spills) runs each role in a
+// launch of its own (ROLE_U compile-time: the BCE terms only in the user role's code) and pipelines
+// a 64-column tile inside the wave, in one basic block per tile:
+//   S1 = P1(cols 0..31);  S2 = P1(cols 32..63)  ||  dS(S1);  P2(S1)  ||  dS(S2);  P2(S2)  ||  next tile -> LDS
+// so the 8-cycle-issue MFMAs of one product cover the elementwise VALU of the other half.  The
+// column tile is double buffered in LDS (one barrier per tile), the tile after next in flight in
+// registers.  Same roles, splits, slabs, operand images and arithmetic as inbatch_x_kernel.
+template <int DP, bool ROLE_U>
+__global__ __launch_bounds__(256, 1) void inbatch_p_kernel(InBatchArgs A) {
+    constexpr int NB = DP / 32;
+    constexpr int KS = DP / 16;
+    constexpr int TF4 = kIbTile * DP / 4;
+    constexpr int LOADS = TF4 / 256;
+    static_assert(TF4 % 256 == 0, "whole staging rounds");
+    __shared__ __attribute__((aligned(16))) unsigned char tiles[2][3 * kIbxPlane];
+    __shared__ float red[4];
+
+    const int blk = blockIdx.x;
+    const int splits = ROLE_U ? A.splits_u : A.splits_p;
+    const int rb = blk / splits, sp = blk - (blk / splits) * splits;
+    const float* R = ROLE_U ? A.U : A.P;
+    const int64_t ldr = ROLE_U ? A.ldu : A.ldp, nr = ROLE_U ? A.B : A.Bc;
+    const float* C = ROLE_U ? A.P : A.U;
+    const int64_t ldc = ROLE_U ? A.ldp : A.ldu, nc = ROLE_U ? A.Bc : A.B;
+    const int64_t per = ROLE_U ? A.cols_u : A.cols_p;
+    const int64_t c_begin = min(nc, (int64_t)sp * per), c_end = min(nc, c_begin + per);
+    const int D = A.D;
+    const float inv_T = A.inv_T;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, h = lane >> 5;
+    const int64_t r0 = (int64_t)rb * kIbRows + 32 * w;
+
+    bf16x8_t rf[KS][3];
+    {
+        const int64_t row = r0 + li;
+        const bool rok = row < nr;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int col = 16 * s + 8 * h;
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 a = (rok && col < D) ? *reinterpret_cast<const float4*>(R + row * ldr + col) : z;
+            const float4 b = (rok && col + 4 < D) ? *reinterpret_cast<const float4*>(R + row * ldr + col + 4) : z;
+            uint2 pa[3], pb[3];
+            ibx_split(a, pa);
+            ibx_split(b, pb);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) rf[s][q] = ibx_cat(pa[q], pb[q]);
+        }
+    }
+    f32x16 acc[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[n][r] = 0.f;
+    float bce = 0.f, bce_lin = 0.f, bce_log2 = 0.f;
+
+    float4 st[LOADS];
+    auto load = [&](int64_t c0) {
+#pragma unroll
+        for (int it = 0; it < LOADS; ++it) {
+            const int lin = tid + it * 256;
+            const int row = lin / (DP / 4), col = (lin - row * (DP / 4)) * 4;
+            const int64_t gc = c0 + row;
+            st[it] = (gc < c_end && col < D) ? *reinterpret_cast<const float4*>(C + gc * ldc + col)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store = [&](unsigned char* dst) {
+#pragma unroll
+        for (int it = 0; it < LOADS; ++it) {
+            const int lin = tid + it * 256;
+            const int row = lin / (DP / 4), c4 = lin - row * (DP / 4);
+            const int o = ibx_off(row, c4 >> 1) + 8 * (c4 & 1);
+            uint2 pl[3];
+            ibx_split(st[it], pl);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) *reinterpret_cast<uint2*>(dst + q * kIbxPlane + o) = pl[q];
+        }
+    };
+    const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+    const int64_t gr = r0 + li;
+    const bool row_ok = gr < nr;
+
+    // product 1: S^T block of tile rows 32 jc .. 32 jc + 31 x this wave's 32 rows
+    auto p1 = [&](const unsigned char* tile, int jc) {
+        f32x16 s2;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s2[r] = 0.f;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int o = ibx_off(32 * jc + li, 2 * s + h);
+            bf16x8_t a[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) a[q] = *reinterpret_cast<const bf16x8_t*>(tile + q * kIbxPlane + o);
+            s2 = ibx_mfma6(a, rf[s], s2);
+        }
+        return s2;
+    };
+    // dS^T in registers: the label-free interior form, or the general one (labels, edges)
+    auto ds_fast = [&](f32x16& s2) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float x = s2[r];
+            const float tx = __builtin_amdgcn_exp2f(-fabsf(x) * 1.4426950408889634f);
+            const float d1 = 1.0f + tx;
+            const float inv = __builtin_amdgcn_rcpf(d1);
+            const float sg = x >= 0.f ? inv : tx * inv;
+            if (ROLE_U) {
+                bce_lin += fmaxf(x, 0.f);
+                bce_log2 += __builtin_amdgcn_logf(d1);
+            }
+            s2[r] = sg * inv_T;
+        }
+    };
+    auto ds_general = [&](f32x16& s2, int jc, int diag, int cols_here) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int lc = 32 * jc + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const bool ok = row_ok && lc < cols_here;
+            const float y = lc == diag ? 1.0f : 0.0f;
+            const float x = s2[r];
+            const float tx = __builtin_amdgcn_exp2f(-fabsf(x) * 1.4426950408889634f);
+            const float inv = __builtin_amdgcn_rcpf(1.0f + tx);
+            const float sg = x >= 0.f ? inv : tx * inv;
+            if (ROLE_U && ok) bce += (1.0f - y) * x + fmaxf(-x, 0.f) + __builtin_amdgcn_logf(1.0f + tx) * 0.6931471805599453f;
+            s2[r] = ok ? (sg - y) * inv_T : 0.f;
+        }
+    };
+    // product 2: acc[n] += dS . tile rows 32 jc ..
+    auto p2 = [&](const unsigned char* tile, const f32x16& s2, int jc) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            bf16x8_t a[3];
+            {
+                const float4 x0 = make_float4(s2[8 * s + 0], s2[8 * s + 1], s2[8 * s + 2], s2[8 * s + 3]);
+                const float4 x1 = make_float4(s2[8 * s + 4], s2[8 * s + 5], s2[8 * s + 6], s2[8 * s + 7]);
+                uint2 pa[3], pb[3];
+                ibx_split(x0, pa);
+                ibx_split(x1, pb);
+#pragma unroll
+                for (int q = 0; q < 3; ++q) a[q] = ibx_cat(pa[q], pb[q]);
+            }
+            const int brow = 32 * jc + 16 * s + 4 * h + q4;
+#pragma unroll
+            for (int n = 0; n < NB; ++n) {
+                const int ch = 4 * n + 2 * (g & 1) + (p4 >> 1);
+                const int o0 = ibx_off(brow, ch) + 8 * (p4 & 1), o1 = ibx_off(brow + 8, ch) + 8 * (p4 & 1);
+                bf16x8_t b[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(tile + q * kIbxPlane + o0));
+                    const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(tile + q * kIbxPlane + o1));
+                    const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    b[q] = __builtin_bit_cast(bf16x8_t, v);
+                }
+                acc[n] = ibx_mfma6(a, b, acc[n]);
+            }
+        }
+    };
+
+    const int ntiles = c_end > c_begin ? (int)((c_end - c_begin + kIbTile - 1) / kIbTile) : 0;
+    if (ntiles > 0) {
+        load(c_begin);
+        store(tiles[0]);
+        if (ntiles > 1) load(c_begin + kIbTile);
+    }
+    __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+        const int64_t c0 = c_begin + (int64_t)t * kIbTile;
+        const unsigned char* const tile = tiles[t & 1];
+        unsigned char* const next = tiles[(t + 1) & 1];
+        const bool more = t + 1 < ntiles;
+        const int64_t dl = ROLE_U ? A.row_base + gr - c0 : gr - A.row_base - c0;
+        const int diag = (dl >= 0 && dl < kIbTile) ? (int)dl : -1;
+        const int cols_here = (int)min((int64_t)kIbTile, c_end - c0);
+        const bool fast = cols_here == kIbTile && __builtin_amdgcn_ballot_w64(diag >= 0 || !row_ok) == 0;
+        if (fast) {  // one basic block: the scheduler interleaves each product with the other half's VALU
+            f32x16 s_a = p1(tile, 0);
+            f32x16 s_b = p1(tile, 1);
+            ds_fast(s_a);
+            p2(tile, s_a, 0);
+            ds_fast(s_b);
+            p2(tile, s_b, 1);
+            if (more) store(next);
+        } else {
+            f32x16 s_a = p1(tile, 0);
+            f32x16 s_b = p1(tile, 1);
+            ds_general(s_a, 0, diag, cols_here);
+            p2(tile, s_a, 0);
+            ds_general(s_b, 1, diag, cols_here);
+            p2(tile, s_b, 1);
+            if (more) store(next);
+        }
+        // tile t + 1 is in the other buffer (last read in tile t - 1, before that tile's barrier);
+        // tile t + 2 in flight
+        if (t + 2 < ntiles) load(c0 + 2 * kIbTile);
+        __syncthreads();
+    }
+    float* slab = ROLE_U ? A.slab_u + (int64_t)sp * A.B * D : A.slab_p + (int64_t)sp * A.Bc * D;
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int lr = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int64_t grr = r0 + lr;
+            const int col = 32 * n + li;
+            if (grr < nr && col < D) slab[grr * D + col] = acc[n][r];
+        }
+    if (ROLE_U) {
+        bce = wave_sum(bce + (bce_lin + bce_log2 * 0.6931471805599453f));
+        if (lane == 0) red[w] = bce;
+        __syncthreads();
+        if (tid == 0) A.loss_part[blk] = (red[0] + red[1]) + (red[2] + red[3]);
+    }
+}
+
 // dU = sum of the user slabs, dP = sum of the item slabs, in split order.
 __global__ void ib_reduce_kernel(InBatchArgs A) {
     const int64_t nu = A.B * A.D, total = nu + A.Bc * A.D;
@@ -526,8 +746,17 @@ int inbatch_waves() {
     return (env && std::atoi(env) == 8) ? 8 : 4;
 }
 
+// TTAMM_IB_KERNEL=p: the software-pipelined one-wave-per-SIMD kernel (inbatch_p_kernel), one
+// launch per role
+bool inbatch_pipelined() {
+    const char* mf = std::getenv("TTAMM_FP32_MFMA");
+    if (mf && std::strcmp(mf, "exact") == 0) return false;
+    const char* env = std::getenv("TTAMM_IB_KERNEL");
+    return env && std::strcmp(env, "p") == 0;
+}
+
 void inbatch_plan(int64_t B, int64_t Bc, InBatchArgs& a) {
-    const int rows = 32 * inbatch_waves();
+    const int rows = inbatch_pipelined() ? kIbRows : 32 * inbatch_waves();
     a.rblk_u = (int)ceil_div(B, rows);
     a.rblk_p = (int)ceil_div(Bc, rows);
     // ~4 waves per SIMD over both roles: split the columns so each role has >= ~512 blocks of 4
@@ -568,7 +797,27 @@ int launch_inbatch(InBatchArgs& a, hipStream_t s) {
             default: hipLaunchKernelGGL(inbatch_kernel<128>, dim3(blocks), dim3(256), 0, s, a); break;
         }
     } else {
-        if (inbatch_waves() == 8) {
+        if (inbatch_pipelined()) {
+            const unsigned bu = (unsigned)(a.rblk_u * a.splits_u), bp = (unsigned)(a.rblk_p * a.splits_p);
+            switch (dp) {
+                case 32:
+                    hipLaunchKernelGGL((inbatch_p_kernel<32, true>), dim3(bu), dim3(256), 0, s, a);
+                    hipLaunchKernelGGL((inbatch_p_kernel<32, false>), dim3(bp), dim3(256), 0, s, a);
+                    break;
+                case 64:
+                    hipLaunchKernelGGL((inbatch_p_kernel<64, true>), dim3(bu), dim3(256), 0, s, a);
+                    hipLaunchKernelGGL((inbatch_p_kernel<64, false>), dim3(bp), dim3(256), 0, s, a);
+                    break;
+                case 96:
+                    hipLaunchKernelGGL((inbatch_p_kernel<96, true>), dim3(bu), dim3(256), 0, s, a);
+                    hipLaunchKernelGGL((inbatch_p_kernel<96, false>), dim3(bp), dim3(256), 0, s, a);
+                    break;
+                default:
+                    hipLaunchKernelGGL((inbatch_p_kernel<128, true>), dim3(bu), dim3(256), 0, s, a);
+                    hipLaunchKernelGGL((inbatch_p_kernel<128, false>), dim3(bp), dim3(256), 0, s, a);
+                    break;
+            }
+        } else if (inbatch_waves() == 8) {
             switch (dp) {
                 case 32: hipLaunchKernelGGL((inbatch_x_kernel<32, 1, 8, true>), dim3(blocks), dim3(512), 0, s, a); break;
                 case 64: hipLaunchKernelGGL((inbatch_x_kernel<64, 1, 8, true>), dim3(blocks), dim3(512), 0, s, a); break;

@@ -450,6 +450,10 @@ struct AdamConsts {
     float bc2_sqrt;  // sqrt(bias_correction2)
     float inv_bc2_sqrt;  // RN(1 / bc2_sqrt): the correctly rounded reciprocal (div_by_const)
     float wd;        // weight_decay (Adam L2 form)
+    // TTAMM_G0_FAST: the step folded into the reciprocal, r = rcp(sqrt(v) * fast_ibc + fast_eps)
+    // = neg_step / denom, so p = fma(m, r, p * decay) (lr = 0: fast_ibc = 0, fast_eps = +inf, r = 0)
+    float fast_ibc;  // RN(1 / (sqrt(bias_correction2) * neg_step))
+    float fast_eps;  // RN(eps / neg_step)
     int decoupled;
     int fast_g0;     // g = 0 updates with v_sqrt / v_rcp (ttamm.h TTAMM_G0_FAST)
     // torch.optim.SGD instead (ttamm.h TTAMM_DENSE_SGD): m holds the momentum buffer, v aliases it

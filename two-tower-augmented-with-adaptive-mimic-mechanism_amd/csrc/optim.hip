@@ -51,11 +51,13 @@ __device__ __forceinline__ void adam_elem_t(float& p, float& m, float& v, float 
     }
     if constexpr (FAST) {
         static_assert(G0, "fast arithmetic is for the g = 0 updates only");
-        // two fmas instead of mul + add pairs (the compiler kept them separate): the replay is
-        // VALU-bound, and this is ~25 % of its instructions.  m and v stay bit-exact (torch's
-        // operations); p moves by the same update term within an ulp or two.
-        const float denom = fmaf(__builtin_amdgcn_sqrtf(v), c.inv_bc2_sqrt, c.eps);
-        p = fmaf(c.neg_step, m * __builtin_amdgcn_rcpf(denom), p);
+        // the step folded into the reciprocal: r = neg_step / denom = rcp(sqrt(v) * fast_ibc +
+        // fast_eps), p = fma(m, r, p): one multiply fewer per element than m * rcp(denom) scaled
+        // by neg_step, and the denominator's fma pairs into v_pk_fma_f32 (replay_kernel).  The
+        // replay is VALU-issue-bound.  m and v stay bit-exact (torch's operations); p moves by the
+        // same update term within a few ulp.
+        const float d = fmaf(__builtin_amdgcn_sqrtf(v), c.fast_ibc, c.fast_eps);
+        p = fmaf(m, __builtin_amdgcn_rcpf(d), p);
     } else {
         const float denom = div_by_const(sqrtf(v), c.bc2_sqrt, c.inv_bc2_sqrt) + c.eps;
         p = p + c.neg_step * (m / denom);
@@ -605,9 +607,11 @@ __global__ void step_begin_kernel(const uint32_t* status, int64_t* applied, Adam
     if (hist) hist[step % cap] = c;
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 // The per-step constants a g = 0 replay reads (the AdamW fast path loads the first 24 B)
 struct ReplayConsts {
-    float decay, w1, b2, eps, neg_step, inv_bc2_sqrt, bc2_sqrt, wd, w2, pad0, pad1, pad2;
+    float decay, w1, b2, eps, neg_step, inv_bc2_sqrt, bc2_sqrt, wd, w2, fast_ibc, fast_eps, pad0;
 };
 
 // One thread per V float4s of a row (dim % (4 V) == 0: 4 V independent dependency chains per
@@ -629,7 +633,8 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
     const int cap = ka->cap;
     for (int i = threadIdx.x; i < 2 * cap; i += blockDim.x) {
         const AdamConsts& h = ka->hist[i < cap ? i : i - cap];
-        H2[i] = ReplayConsts{h.decay, h.w1, h.b2, h.eps, h.neg_step, h.inv_bc2_sqrt, h.bc2_sqrt, h.wd, h.w2, 0.f, 0.f, 0.f};
+        H2[i] = ReplayConsts{h.decay, h.w1, h.b2, h.eps, h.neg_step, h.inv_bc2_sqrt, h.bc2_sqrt, h.wd, h.w2,
+                             h.fast_ibc, h.fast_eps, 0.f};
     }
     __syncthreads();
     const int dim = S.dim;
@@ -680,10 +685,41 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
                 }
             }
         }
+        if constexpr (DECOUPLED && FAST) {
+            // adam_elem_t<true, true, true> on element pairs, written with 2-wide vectors so every
+            // multiply / fma issues as one v_pk_* for two elements (the denominator's fma included):
+            // the same IEEE operations per element, so the dense sweep's scalar form gives the same bits
+            for (; hc != hend; ++hc) {
+                const f32x2 decay = {hc->decay, hc->decay}, w1 = {hc->w1, hc->w1}, b2 = {hc->b2, hc->b2};
+                const f32x2 ibc = {hc->fast_ibc, hc->fast_ibc}, eps = {hc->fast_eps, hc->fast_eps};
+#pragma unroll
+                for (int i = 0; i < V; ++i) {
+#pragma unroll
+                    for (int half = 0; half < 2; ++half) {
+                        f32x2 P = half ? f32x2{p[i].z, p[i].w} : f32x2{p[i].x, p[i].y};
+                        f32x2 M = half ? f32x2{m[i].z, m[i].w} : f32x2{m[i].x, m[i].y};
+                        f32x2 Q = half ? f32x2{v[i].z, v[i].w} : f32x2{v[i].x, v[i].y};
+                        P = P * decay;
+                        M = __builtin_elementwise_fma(w1, -M, M);
+                        Q = Q * b2;
+                        const f32x2 S = {__builtin_amdgcn_sqrtf(Q.x), __builtin_amdgcn_sqrtf(Q.y)};
+                        const f32x2 Dn = __builtin_elementwise_fma(S, ibc, eps);
+                        const f32x2 R = {__builtin_amdgcn_rcpf(Dn.x), __builtin_amdgcn_rcpf(Dn.y)};
+                        P = __builtin_elementwise_fma(M, R, P);
+                        if (half) {
+                            p[i].z = P.x, p[i].w = P.y, m[i].z = M.x, m[i].w = M.y, v[i].z = Q.x, v[i].w = Q.y;
+                        } else {
+                            p[i].x = P.x, p[i].y = P.y, m[i].x = M.x, m[i].y = M.y, v[i].x = Q.x, v[i].y = Q.y;
+                        }
+                    }
+                }
+            }
+        }
         for (; hc != hend; ++hc) {
             AdamConsts c;
             c.decay = hc->decay, c.w1 = hc->w1, c.b2 = hc->b2, c.eps = hc->eps, c.neg_step = hc->neg_step;
             c.bc2_sqrt = hc->bc2_sqrt, c.inv_bc2_sqrt = hc->inv_bc2_sqrt, c.wd = hc->wd, c.w2 = hc->w2;
+            c.fast_ibc = hc->fast_ibc, c.fast_eps = hc->fast_eps;
             c.decoupled = DECOUPLED ? 1 : 0, c.fast_g0 = FAST ? 1 : 0;
 #pragma unroll
             for (int i = 0; i < V; ++i) {
@@ -724,6 +760,7 @@ __device__ __forceinline__ AdamConsts consts_at(H h) {
     AdamConsts c;
     c.decay = h->decay, c.w1 = h->w1, c.b2 = h->b2, c.eps = h->eps, c.neg_step = h->neg_step;
     c.bc2_sqrt = h->bc2_sqrt, c.inv_bc2_sqrt = h->inv_bc2_sqrt, c.wd = h->wd, c.w2 = h->w2;
+    c.fast_ibc = h->fast_ibc, c.fast_eps = h->fast_eps;
     c.decoupled = 0, c.fast_g0 = 0;
     return c;
 }
@@ -1119,6 +1156,14 @@ AdamConsts make_adam_consts(double lr, double beta1, double beta2, double eps, d
     c.neg_step = (float)(-(lr / bc1));
     c.bc2_sqrt = (float)std::pow(bc2, 0.5);
     c.inv_bc2_sqrt = correctly_rounded_reciprocal(c.bc2_sqrt);
+    const double ns = -(lr / bc1);
+    if (ns != 0.0) {
+        c.fast_ibc = (float)(1.0 / (std::sqrt(bc2) * ns));
+        c.fast_eps = (float)(eps / ns);
+    } else {  // lr = 0: r = rcp(+inf) = +0, p = fma(m, 0, p) = p (torch: p + (-0) * (m / denom))
+        c.fast_ibc = 0.f;
+        c.fast_eps = INFINITY;
+    }
     c.wd = (float)wd;
     c.decoupled = decoupled;
     c.fast_g0 = 0;

@@ -118,6 +118,7 @@ __global__ void step_prologue_kernel(StepPrologue) {
         c.decay = pa->c.decay, c.w1 = pa->c.w1, c.b2 = pa->c.b2, c.w2 = pa->c.w2, c.eps = pa->c.eps;
         c.neg_step = pa->c.neg_step, c.bc2_sqrt = pa->c.bc2_sqrt, c.inv_bc2_sqrt = pa->c.inv_bc2_sqrt;
         c.wd = pa->c.wd, c.decoupled = pa->c.decoupled, c.fast_g0 = pa->c.fast_g0;
+        c.fast_ibc = pa->c.fast_ibc, c.fast_eps = pa->c.fast_eps;
         pa->hist[pa->step % pa->cap] = c;
     }
 }

@@ -35,6 +35,8 @@ static AdamConsts consts_for(int64_t step) {
     c.neg_step = (float)(-lr / bc1);
     c.bc2_sqrt = (float)std::sqrt(bc2);
     c.inv_bc2_sqrt = 1.0f / c.bc2_sqrt;
+    c.fast_ibc = (float)(1.0 / (std::sqrt(bc2) * (double)c.neg_step));
+    c.fast_eps = (float)((double)c.eps / (double)c.neg_step);
     c.wd = (float)wd;
     c.decoupled = 1;
     c.fast_g0 = 1;

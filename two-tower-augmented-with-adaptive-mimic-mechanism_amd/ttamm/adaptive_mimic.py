@@ -89,11 +89,12 @@ class AdaptiveMimicMechanism(nn.Module):
 
 
 def _mse(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
-    """F.mse_loss(x, y), reduction 'mean' (y is detached by the callers, adaptive_mimic.py:66-67)."""
+    """F.mse_loss(x, y), reduction 'mean' (y is detached by the callers, adaptive_mimic.py:66-67;
+    a y that requires grad gets its gradient as in F.mse_loss)."""
     xs, ys = x.contiguous(), y.contiguous()
     if xs.shape != ys.shape:
         raise ValueError("ttamm: mse_loss input and target shapes differ")
-    if torch.is_grad_enabled() and xs.requires_grad:
+    if torch.is_grad_enabled() and (xs.requires_grad or ys.requires_grad):
         from .autograd import MSEFunction
 
         return MSEFunction.apply(xs.reshape(xs.shape[0], -1), ys.reshape(ys.shape[0], -1))

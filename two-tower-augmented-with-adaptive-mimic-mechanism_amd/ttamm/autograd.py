@@ -259,8 +259,8 @@ class ApplyAugFunction(torch.autograd.Function):
 
 
 class MSEFunction(torch.autograd.Function):
-    """F.mse_loss(x, target) (reduction 'mean'); the target gets no gradient (it is detached in
-    adaptive_mimic.py:66-67)."""
+    """F.mse_loss(x, target) (reduction 'mean').  The reference detaches the target
+    (adaptive_mimic.py:66-67); a target that requires grad gets -dx, as F.mse_loss gives it."""
 
     @staticmethod
     def forward(ctx, x: torch.Tensor, target: torch.Tensor):  # noqa: D401
@@ -279,4 +279,4 @@ class MSEFunction(torch.autograd.Function):
         # dx = 2 / numel * (x - target) * dL (idx = NULL: row r into row r)
         _lib.check(_lib.load().ttamm_scatter_add_rows(_ptr(dx), n, D, None, n, _ptr(x), D, _ptr(target), D, _ptr(dl),
                                                       2.0 / x.numel(), -1, _lib.stream_handle(x.device)))
-        return dx, None
+        return (dx if ctx.needs_input_grad[0] else None), (-dx if ctx.needs_input_grad[1] else None)

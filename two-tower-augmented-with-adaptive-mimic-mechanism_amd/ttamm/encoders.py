@@ -407,8 +407,9 @@ def tower_forward(
     mimic_table: torch.Tensor | None = None,
 ) -> torch.Tensor:
     """TowerEncoder.forward on the MI355X (encoders.py:221-255); optionally adds the mimic rows
-    (eval path only).  Under autograd (a parameter requires grad) or in train mode with dropout,
-    the training forward runs (ttamm/autograd.py: activations kept for the backward)."""
+    (AdaptiveMimicMechanism._apply_aug, adaptive_mimic.py:88-95).  Under autograd (a parameter
+    requires grad) or in train mode with dropout, the training forward runs (ttamm/autograd.py:
+    activations kept for the backward, the mimic rows added with their table gradient)."""
     _lib.require_rocm(indices, "TowerEncoder.forward")
     if indices.dtype != torch.long:
         raise ValueError("ttamm: indices must be torch.long")
@@ -420,8 +421,8 @@ def tower_forward(
     n = idx.numel()
     train = (torch.is_grad_enabled() and any(p.requires_grad for p in tower.parameters())) or \
         (tower.training and feature_layers(tower)[1] > 0)
-    if train and mimic_table is None:
-        from .autograd import tower_train_forward
+    if train:
+        from .autograd import ApplyAugFunction, tower_train_forward
 
         feats = None
         if use_features:
@@ -429,6 +430,10 @@ def tower_forward(
             if feats.shape[0] != n:
                 raise ValueError("ttamm: features must have one row per index")
         out = tower_train_forward(tower, idx, feats)
+        if mimic_table is not None:  # + table[idx] with the table's gradient (adaptive_mimic.py:88-95)
+            if mimic_table.shape[1] != out.shape[-1]:
+                raise ValueError("Adaptive mimic requires user and item embedding dimensions to match.")
+            out, _ = ApplyAugFunction.apply(mimic_table, idx, out.contiguous())
         return out.reshape(*indices.shape, out.shape[-1])
     out = torch.empty((n, tower.output_dim if use_features else tower.id_dim), dtype=torch.float32, device=idx.device)
     if not use_features and tower.fusion != "identity":
