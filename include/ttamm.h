@@ -430,11 +430,13 @@ int ttamm_epoch_batch(const int64_t* users, const int64_t* items, int64_t n, uin
  * [positives; negatives], keys = global request positions) and the pair routing of its epoch
  * driver (ids = users, payload = items) — replaces a host argsort / bincount
  * (torch.argsort(owner, stable=True), ttamm/sharded.py).  1 <= world <= 1024; every id >= 0;
- * scratch: device memory of ttamm_route_scratch_bytes(n0 + n1, world) bytes. */
+ * scratch: device memory of ttamm_route_scratch_bytes(n0 + n1, world) bytes.  counts[o * counts_ld]
+ * (counts_ld >= 1); with status != NULL and counts_ld >= 2, counts[o * counts_ld + 1] = *status —
+ * the (count, status word) rows of the sharded step's count all-to-all, written in the same launch. */
 size_t ttamm_route_scratch_bytes(int64_t n, int32_t world);
 int ttamm_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_t n1, const int64_t* payload,
                      int64_t key0, int64_t key1, int32_t world, int64_t* packed, int64_t* slot, int64_t* counts,
-                     void* scratch, size_t scratch_bytes, void* stream);
+                     int64_t counts_ld, const uint32_t* status, void* scratch, size_t scratch_bytes, void* stream);
 
 /* A HIP stream whose kernels run on `num_cus` compute units only, spread evenly over the device
  * (every (CUs / num_cus)-th CU, so every XCD keeps some): a ttamm_step_args.aux_stream for the

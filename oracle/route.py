@@ -14,9 +14,10 @@ import torch
 
 
 def route_rows(world: int, id0: torch.Tensor, id1: torch.Tensor | None = None, payload: torch.Tensor | None = None,
-               key0: int = 0, key1: int = 0, counts_out: torch.Tensor | None = None
-               ) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    """(packed [n, 2], slot [n], counts [world]) as ttamm_route_rows defines them."""
+               key0: int = 0, key1: int = 0, counts_out: torch.Tensor | None = None,
+               status: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """(packed [n, 2], slot [n], counts [world]) as ttamm_route_rows defines them; a [world, 2]
+    ``counts_out`` gets the counts in column 0 and, with ``status``, the status word in column 1."""
     ids = id0.reshape(-1).cpu() if id1 is None else torch.cat([id0.reshape(-1).cpu(), id1.reshape(-1).cpu()])
     n0 = id0.numel()
     n = ids.numel()
@@ -30,6 +31,11 @@ def route_rows(world: int, id0: torch.Tensor, id1: torch.Tensor | None = None, p
     counts = torch.bincount(owner, minlength=world)
     dev = id0.device
     if counts_out is not None:
-        counts_out.copy_(counts)
+        if counts_out.dim() == 2:
+            counts_out[:, 0].copy_(counts)
+            if status is not None:
+                counts_out[:, 1] = int(status.reshape(-1)[0])
+        else:
+            counts_out.copy_(counts)
         counts = counts_out
     return packed.to(dev), slot.to(dev), counts.to(dev)

@@ -103,10 +103,11 @@ TTAMM_API size_t ttamm_route_scratch_bytes(int64_t n, int32_t world) { return ro
 
 TTAMM_API int ttamm_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_t n1, const int64_t* payload,
                                int64_t key0, int64_t key1, int32_t world, int64_t* packed, int64_t* slot,
-                               int64_t* counts, void* scratch, size_t scratch_bytes, void* stream) {
+                               int64_t* counts, int64_t counts_ld, const uint32_t* status, void* scratch,
+                               size_t scratch_bytes, void* stream) {
     g_last_error.clear();
-    return launch_route_rows(id0, n0, id1, n1, payload, key0, key1, world, packed, slot, counts, scratch,
-                             scratch_bytes, (hipStream_t)stream);
+    return launch_route_rows(id0, n0, id1, n1, payload, key0, key1, world, packed, slot, counts, counts_ld, status,
+                             scratch, scratch_bytes, (hipStream_t)stream);
 }
 
 TTAMM_API int ttamm_stream_create_cu_limited(int32_t num_cus, void** stream) {

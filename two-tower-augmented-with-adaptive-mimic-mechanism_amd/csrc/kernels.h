@@ -93,7 +93,7 @@ int epoch_half_bits(int64_t n);
 size_t route_scratch_bytes(int64_t n, int world);
 int launch_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_t n1, const int64_t* payload,
                       int64_t key0, int64_t key1, int world, int64_t* packed, int64_t* slot, int64_t* counts,
-                      void* scratch, size_t scratch_bytes, hipStream_t s);
+                      int64_t counts_ld, const uint32_t* status, void* scratch, size_t scratch_bytes, hipStream_t s);
 void epoch_round_keys(uint64_t seed, int64_t epoch, uint32_t keys[4]);
 int launch_epoch_batch(const int64_t* users, const int64_t* items, int64_t n, uint64_t seed, int64_t epoch,
                        int shuffle, int64_t start, int64_t count, int64_t* out_users, int64_t* out_items,

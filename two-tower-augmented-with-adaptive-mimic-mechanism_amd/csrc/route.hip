@@ -49,13 +49,15 @@ __global__ __launch_bounds__(kRouteThreads) void route_count_kernel(RouteIn a, i
 }
 
 __global__ __launch_bounds__(kRouteThreads) void route_scan_kernel(int32_t* __restrict__ blk, int nb, int W,
-                                                                   int64_t* __restrict__ counts) {
+                                                                   int64_t* __restrict__ counts, int64_t ld,
+                                                                   const uint32_t* __restrict__ status) {
     extern __shared__ int64_t tot[];
     for (int o = threadIdx.x; o < W; o += kRouteThreads) {
         int64_t t = 0;
         for (int b = 0; b < nb; ++b) t += blk[(int64_t)b * W + o];
         tot[o] = t;
-        counts[o] = t;
+        counts[o * ld] = t;
+        if (status) counts[o * ld + 1] = (int64_t)*status;
     }
     __syncthreads();
     if (threadIdx.x == 0) {  // exclusive scan over owners (W <= 1024)
@@ -135,13 +137,16 @@ size_t route_scratch_bytes(int64_t n, int world) {
 
 int launch_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_t n1, const int64_t* payload,
                       int64_t key0, int64_t key1, int world, int64_t* packed, int64_t* slot, int64_t* counts,
-                      void* scratch, size_t scratch_bytes, hipStream_t s) {
+                      int64_t counts_ld, const uint32_t* status, void* scratch, size_t scratch_bytes, hipStream_t s) {
     TTAMM_REQUIRE(world >= 1 && world <= 1024, "route: world must be in [1, 1024]");
     TTAMM_REQUIRE(n0 >= 0 && n1 >= 0 && n0 + n1 < (int64_t(1) << 31), "route: bad sizes");
     TTAMM_REQUIRE(counts != nullptr, "route: counts missing");
+    TTAMM_REQUIRE(counts_ld >= 1 && (status == nullptr || counts_ld >= 2), "route: counts_ld must be >= 1 (>= 2 with status)");
     const int64_t n = n0 + n1;
-    if (n == 0) {
-        TTAMM_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * world, s));
+    if (n == 0) {  // zero counts (and the status column): the scan over no blocks
+        hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(kRouteThreads), sizeof(int64_t) * world, s,
+                           static_cast<int32_t*>(nullptr), 0, world, counts, counts_ld, status);
+        TTAMM_LAUNCH_CHECK();
         return TTAMM_OK;
     }
     TTAMM_REQUIRE((n0 == 0 || id0) && (n1 == 0 || id1) && packed && slot, "route: null pointer");
@@ -154,7 +159,7 @@ int launch_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_
     hipLaunchKernelGGL(route_count_kernel, dim3(nb), dim3(kRouteThreads), sizeof(int32_t) * world, s, a, blk);
     TTAMM_LAUNCH_CHECK();
     hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(kRouteThreads), sizeof(int64_t) * world, s, blk, nb, world,
-                       counts);
+                       counts, counts_ld, status);
     TTAMM_LAUNCH_CHECK();
     hipLaunchKernelGGL(route_scatter_kernel, dim3(nb), dim3(kRouteThreads),
                        sizeof(int32_t) * world * (1 + kRouteWaves), s, a, blk, bits, packed, slot);

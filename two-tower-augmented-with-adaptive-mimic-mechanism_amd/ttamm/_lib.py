@@ -214,7 +214,8 @@ SIGNATURES = {
     "ttamm_stream_create_cu_limited": (ctypes.c_int, [c_i32, ctypes.POINTER(c_vp)]),
     "ttamm_stream_destroy": (ctypes.c_int, [c_vp]),
     "ttamm_route_scratch_bytes": (ctypes.c_size_t, [c_i64, c_i32]),
-    "ttamm_route_rows": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp,
+    "ttamm_route_rows": (ctypes.c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64,
+                                        c_vp, c_vp,
                                         ctypes.c_size_t, c_vp]),
     "ttamm_epoch_batch": (ctypes.c_int, [c_vp, c_vp, c_i64, ctypes.c_uint64, c_i64, c_i32, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "ttamm_candidate_topk": (

@@ -3,9 +3,12 @@ the reference's evaluation: ``_encode_item_embeddings`` (training.py:613-643), t
 ``IndexFlatIP`` index (:645-679) and ``_evaluate_model``'s search + filter (:917-1043,
 :944-970).
 
-The item matrix stays in HBM; ``retrieve_topk`` runs ``ttamm_retrieval_topk`` (fp32 MFMA scores
-fused with a per-query top-k that skips each user's blocked train positives), so there is no
-per-user search call and no host round trip per user.
+The item matrix stays in HBM; ``retrieve_topk`` runs ``ttamm_retrieval_topk`` (fp32-accurate
+scores on the bf16 matrix cores — each operand split into three bf16 planes, six MFMA products
+per fp32 product, D <= 128; fp32 MFMA for wider rows or with TTAMM_RETRIEVAL_FP32=1 — fused with
+a per-query top-k that skips each user's blocked train positives), so there is no per-user search
+call and no host round trip per user.  Scores agree with faiss IndexFlatIP's fp32 inner products
+to ~1e-7 relative, not bit for bit: near-tied items can swap.
 """
 
 from __future__ import annotations

@@ -322,9 +322,12 @@ class Route:
 
 def device_route(lib: Any, world: int, id0: torch.Tensor, id1: torch.Tensor | None = None,
                  payload: torch.Tensor | None = None, key0: int = 0, key1: int = 0,
-                 counts_out: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+                 counts_out: torch.Tensor | None = None,
+                 status: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """ttamm_route_rows: ids [id0; id1] grouped by owner (id % world), stably.  Returns (packed
-    [n, 2] = (id // world, payload or key) in the grouped order, slot [n], counts [world])."""
+    [n, 2] = (id // world, payload or key) in the grouped order, slot [n], counts [world]).
+    ``counts_out`` may be a [world, 2] int64 buffer: column 0 gets the counts and, with ``status``
+    (the int32 status word), column 1 the status — the count all-to-all's send rows, one launch."""
     dev = id0.device
     n0 = id0.numel()
     n1 = id1.numel() if id1 is not None else 0
@@ -332,11 +335,12 @@ def device_route(lib: Any, world: int, id0: torch.Tensor, id1: torch.Tensor | No
     packed = torch.empty((n, 2), dtype=torch.long, device=dev)
     slot = torch.empty(n, dtype=torch.long, device=dev)
     counts = counts_out if counts_out is not None else torch.empty(world, dtype=torch.long, device=dev)
+    ld = counts.stride(0) if counts.dim() == 2 else 1
     scratch = torch.empty(max(1, int(lib.ttamm_route_scratch_bytes(n, world))), dtype=torch.uint8, device=dev)
     ptr = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None and t.numel() else None  # noqa: E731
     _lib.check(lib.ttamm_route_rows(ptr(id0), n0, ptr(id1), n1, ptr(payload), key0, key1, world, ptr(packed),
-                                    ptr(slot), ctypes.c_void_p(counts.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
-                                    scratch.numel(), _lib.stream_handle(dev)))
+                                    ptr(slot), ctypes.c_void_p(counts.data_ptr()), ld, ptr(status),
+                                    ctypes.c_void_p(scratch.data_ptr()), scratch.numel(), _lib.stream_handle(dev)))
     return packed, slot, counts
 
 
@@ -352,17 +356,15 @@ def route_requests(own: RowOwnership, router: Router, pos: torch.Tensor, negs: t
     step is poisoned (Route.peer_status) before any of them writes state."""
     W = own.world_size
     n = pos.numel() + negs.numel()
-    counts = torch.empty(W, dtype=torch.long, device=pos.device)
-    packed, slot, _ = router(W, pos, negs, None, key0, key1, counts_out=counts)
+    # rows 0..W-1: what this rank sends (count to owner d, its status word); rows W..2W-1: received
+    sr = torch.empty((2 * W, 2), dtype=torch.long, device=pos.device)
+    if status is None:
+        sr[:W, 1] = 0
+    packed, slot, _ = router(W, pos, negs, None, key0, key1, counts_out=sr[:W], status=status)
     if W == 1:
         return Route(slot, [n], [n], packed[:, 0].contiguous(), packed[:, 1].contiguous())
-    send = torch.zeros((W, 2), dtype=torch.long, device=pos.device)  # (count to d, my status)
-    send[:, 0] = counts
-    if status is not None:
-        send[:, 1] = status.to(torch.long)
-    recv = torch.empty_like(send)
-    yield AllToAll(send, [1] * W, [1] * W, out=recv)
-    c = torch.cat([send.reshape(-1), recv.reshape(-1)]).tolist()
+    yield AllToAll(sr[:W], [1] * W, [1] * W, out=sr[W:])
+    c = sr.reshape(-1).tolist()  # the one host synchronisation of the step
     sent, got_c = c[0:2 * W:2], c[2 * W::2]
     peers = 0
     for r, st in enumerate(c[2 * W + 1::2]):
