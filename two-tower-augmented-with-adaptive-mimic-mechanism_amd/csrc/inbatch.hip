@@ -490,6 +490,9 @@ __global__ __launch_bounds__(64 * NW, MINB) void inbatch_x_kernel(InBatchArgs A)
 // so the 8-cycle-issue MFMAs of one product cover the elementwise VALU of the other half.  The
 // column tile is double buffered in LDS (one barrier per tile), the tile after next in flight in
 // registers.  Same roles, splits, slabs, operand images and arithmetic as inbatch_x_kernel.
+#ifndef IB_VALU_PER_MFMA
+#define IB_VALU_PER_MFMA 5
+#endif
 template <int DP, bool ROLE_U>
 __global__ __launch_bounds__(256, 1) void inbatch_p_kernel(InBatchArgs A) {
     constexpr int NB = DP / 32;
@@ -582,21 +585,6 @@ __global__ __launch_bounds__(256, 1) void inbatch_p_kernel(InBatchArgs A) {
         return s2;
     };
     // dS^T in registers: the label-free interior form, or the general one (labels, edges)
-    auto ds_fast = [&](f32x16& s2) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float x = s2[r];
-            const float tx = __builtin_amdgcn_exp2f(-fabsf(x) * 1.4426950408889634f);
-            const float d1 = 1.0f + tx;
-            const float inv = __builtin_amdgcn_rcpf(d1);
-            const float sg = x >= 0.f ? inv : tx * inv;
-            if (ROLE_U) {
-                bce_lin += fmaxf(x, 0.f);
-                bce_log2 += __builtin_amdgcn_logf(d1);
-            }
-            s2[r] = sg * inv_T;
-        }
-    };
     auto ds_general = [&](f32x16& s2, int jc, int diag, int cols_here) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -643,6 +631,67 @@ __global__ __launch_bounds__(256, 1) void inbatch_p_kernel(InBatchArgs A) {
         }
     };
 
+    // one element of ds_fast (the interleaved form; same operations)
+    auto ds_fast_elem = [&](f32x16& s2, int r) {
+        const float x = s2[r];
+        const float tx = __builtin_amdgcn_exp2f(-fabsf(x) * 1.4426950408889634f);
+        const float d1 = 1.0f + tx;
+        const float inv = __builtin_amdgcn_rcpf(d1);
+        const float sg = x >= 0.f ? inv : tx * inv;
+        if (ROLE_U) {
+            bce_lin += fmaxf(x, 0.f);
+            bce_log2 += __builtin_amdgcn_logf(d1);
+        }
+        s2[r] = sg * inv_T;
+    };
+    // staging round i (of LOADS) of the next tile: its three planes into dst
+    auto store_part = [&](unsigned char* dst, int it) {
+        if (it >= LOADS) return;
+        const int lin = tid + it * 256;
+        const int row = lin / (DP / 4), c4 = lin - row * (DP / 4);
+        const int o = ibx_off(row, c4 >> 1) + 8 * (c4 & 1);
+        uint2 pl[3];
+        ibx_split(st[it], pl);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) *reinterpret_cast<uint2*>(dst + q * kIbxPlane + o) = pl[q];
+    };
+    // product 2 with side work f(i) after its i-th 6-MFMA group (i = 0 .. 2 NB - 1); the staging
+    // rounds past 2 NB (LOADS > 2 NB) run after the last group
+    auto split8 = [&](const f32x16& s2, int s, bf16x8_t a[3]) {
+        const float4 x0 = make_float4(s2[8 * s + 0], s2[8 * s + 1], s2[8 * s + 2], s2[8 * s + 3]);
+        const float4 x1 = make_float4(s2[8 * s + 4], s2[8 * s + 5], s2[8 * s + 6], s2[8 * s + 7]);
+        uint2 pa[3], pb[3];
+        ibx_split(x0, pa);
+        ibx_split(x1, pb);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) a[q] = ibx_cat(pa[q], pb[q]);
+    };
+    auto p2_il = [&](const unsigned char* tile, const f32x16& s2, int jc, auto&& f) {
+        bf16x8_t aa[2][3];
+        split8(s2, 0, aa[0]);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const bf16x8_t* a = aa[s];
+            const int brow = 32 * jc + 16 * s + 4 * h + q4;
+#pragma unroll
+            for (int n = 0; n < NB; ++n) {
+                const int ch = 4 * n + 2 * (g & 1) + (p4 >> 1);
+                const int o0 = ibx_off(brow, ch) + 8 * (p4 & 1), o1 = ibx_off(brow + 8, ch) + 8 * (p4 & 1);
+                bf16x8_t b[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(tile + q * kIbxPlane + o0));
+                    const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(tile + q * kIbxPlane + o1));
+                    const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    b[q] = __builtin_bit_cast(bf16x8_t, v);
+                }
+                acc[n] = ibx_mfma6(a, b, acc[n]);
+                if (s == 0 && n == 0) split8(s2, 1, aa[1]);  // the second half's planes under these MFMAs
+                f(s * NB + n);
+            }
+        }
+    };
+
     const int ntiles = c_end > c_begin ? (int)((c_end - c_begin + kIbTile - 1) / kIbTile) : 0;
     if (ntiles > 0) {
         load(c_begin);
@@ -659,14 +708,36 @@ __global__ __launch_bounds__(256, 1) void inbatch_p_kernel(InBatchArgs A) {
         const int diag = (dl >= 0 && dl < kIbTile) ? (int)dl : -1;
         const int cols_here = (int)min((int64_t)kIbTile, c_end - c0);
         const bool fast = cols_here == kIbTile && __builtin_amdgcn_ballot_w64(diag >= 0 || !row_ok) == 0;
-        if (fast) {  // one basic block: the scheduler interleaves each product with the other half's VALU
+        // tile t + 1 goes into the other buffer (last read in tile t - 1, before that tile's
+        // barrier; after the last tile the store is harmless), tile t + 2 into flight (masked to
+        // zeros past the split's columns) — unconditionally, so each body is one basic block
+        (void)more;
+        if (fast) {
+            // written in issue order: every MFMA group of one product carries a slice of the
+            // other half's elementwise work
             f32x16 s_a = p1(tile, 0);
-            f32x16 s_b = p1(tile, 1);
-            ds_fast(s_a);
-            p2(tile, s_a, 0);
-            ds_fast(s_b);
-            p2(tile, s_b, 1);
-            if (more) store(next);
+            f32x16 s_b;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s_b[r] = 0.f;
+            // S(cols 32..63) || dS(cols 0..31), two elements per k-step
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                const int o = ibx_off(32 + li, 2 * ks + h);
+                bf16x8_t a[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) a[q] = *reinterpret_cast<const bf16x8_t*>(tile + q * kIbxPlane + o);
+                s_b = ibx_mfma6(a, rf[ks], s_b);
+#pragma unroll
+                for (int e = (ks * 16) / KS; e < ((ks + 1) * 16) / KS; ++e) ds_fast_elem(s_a, e);
+            }
+            // dR += dS(cols 0..31) . tile || dS(cols 32..63), 16 / (2 NB) elements per 6-MFMA group
+            p2_il(tile, s_a, 0, [&](int i) {
+#pragma unroll
+                for (int e = (i * 16) / (2 * NB); e < ((i + 1) * 16) / (2 * NB); ++e) ds_fast_elem(s_b, e);
+            });
+            // dR += dS(cols 32..63) . tile || the next tile's planes into the other buffer
+            p2_il(tile, s_b, 1, [&](int i) { store_part(next, i); });
+            load(c0 + 2 * kIbTile);
         } else {
             f32x16 s_a = p1(tile, 0);
             f32x16 s_b = p1(tile, 1);
@@ -674,11 +745,9 @@ __global__ __launch_bounds__(256, 1) void inbatch_p_kernel(InBatchArgs A) {
             p2(tile, s_a, 0);
             ds_general(s_b, 1, diag, cols_here);
             p2(tile, s_b, 1);
-            if (more) store(next);
+            store(next);
+            load(c0 + 2 * kIbTile);
         }
-        // tile t + 1 is in the other buffer (last read in tile t - 1, before that tile's barrier);
-        // tile t + 2 in flight
-        if (t + 2 < ntiles) load(c0 + 2 * kIbTile);
         __syncthreads();
     }
     float* slab = ROLE_U ? A.slab_u + (int64_t)sp * A.B * D : A.slab_p + (int64_t)sp * A.Bc * D;
