@@ -32,3 +32,13 @@ python3 -c "
 import pstats
 p = pstats.Stats('gpurun_out/s7_emu.prof'); p.sort_stats('cumulative').print_stats(50)" > gpurun_out/s7_prof_cum.txt
 echo done
+for wt in 0 1; do
+  if [ $wt = 1 ]; then export TTAMM_GEMM_WIDE_TILES=1; else unset TTAMM_GEMM_WIDE_TILES; fi
+  timeout -k 10 400 python -u bench.py --no-cpu-baseline --negatives in-batch > gpurun_out/s7_c2ib_wt$wt.json 2> gpurun_out/s7_c2ib_wt$wt.err || { echo IB_BENCH_FAIL; tail -5 gpurun_out/s7_c2ib_wt$wt.err; exit 1; }
+  timeout -k 10 400 python -u bench.py --no-cpu-baseline --config c4 > gpurun_out/s7_c4_wt$wt.json 2> gpurun_out/s7_c4_wt$wt.err || { echo C4_FAIL; tail -5 gpurun_out/s7_c4_wt$wt.err; exit 1; }
+  python3 -c "
+import json
+for f in ('s7_c2ib_wt$wt','s7_c4_wt$wt'):
+    d=json.load(open('gpurun_out/'+f+'.json')); print(f, d['value'], d['ms_per_step'], [(k['kernel'][:30], k.get('ms_per_step')) for k in d['kernels']])"
+done
+unset TTAMM_GEMM_WIDE_TILES
