@@ -344,6 +344,9 @@ typedef struct ttamm_step_args {
      * floats; the step zeroes and fills them between the caller's all-reduces.              */
     float* cal_stats;
     float* cal_scatter;
+    /* element stride of item_rows and item_row_keys (0 = 1): the (local row, key) pairs of an
+     * owner's request all-to-all are read in place (stride 2), the step stages contiguous copies */
+    int64_t item_rows_ld;
 } ttamm_step_args;
 
 #define TTAMM_G0_EXACT 0

@@ -196,6 +196,7 @@ struct StageSeg {
     int64_t* out;
     int64_t n;
     int64_t rows;
+    int64_t ld;  // element stride of `in` (0 = 1)
 };
 constexpr int kMaxStageSegs = 3;
 struct StageArgs {

@@ -126,7 +126,7 @@ __global__ void stage_rows_kernel(StageArgs) {
     const int64_t n = S.n, rows = S.rows;
     bool bad = false;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t v = S.in[i];
+        const int64_t v = S.in[i * (S.ld ? S.ld : 1)];
         const bool ok = v >= 0 && v < rows;
         bad |= !ok;
         if (S.out) S.out[i] = ok ? v : 0;

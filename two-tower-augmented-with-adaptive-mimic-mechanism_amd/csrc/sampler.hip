@@ -85,7 +85,7 @@ __global__ void step_prologue_kernel(StepPrologue) {
         const KArg(StageSeg)& S = st->seg[y];
         bool bad = false;
         for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < S.n; i += (int64_t)gridDim.x * blockDim.x) {
-            const int64_t v = S.in[i];
+            const int64_t v = S.in[i * (S.ld ? S.ld : 1)];
             const bool ok = v >= 0 && v < S.rows;
             bad |= !ok;
             if (S.out) S.out[i] = ok ? v : 0;

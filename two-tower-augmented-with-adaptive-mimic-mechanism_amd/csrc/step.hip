@@ -16,6 +16,7 @@
 // item tower of a rank runs over the item rows it owns, for whoever requested them; the
 // host moves (t | a) and (dT | dA) rows between phases and all-reduces the gradient arena.
 #include <algorithm>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -89,6 +90,7 @@ struct StepWs {
     TowerWs user, item;
     float* partials = nullptr;
     uint32_t* prologue_done = nullptr;  // completion counter of step_prologue_kernel (zero between calls)
+    int64_t* keys_own = nullptr;        // sharded owner: staged request keys [item_rows_capacity]
     int score_blocks = 0;
     // in-batch negatives (ttamm_step_args.in_batch)
     bool ib_on = false;
@@ -352,8 +354,10 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
     ws.user.role = ROLE_USER;
     ws.item.role = ROLE_ITEM;
     tower(A.user, ws.user, B, false, B);
-    if (shard)
+    if (shard) {
         tower(A.item, ws.item, A.item_rows_capacity, true, 0);
+        ws.keys_own = ar.take<int64_t>(A.item_rows_capacity);
+    }
     else
         tower(A.item, ws.item, B * (1 + N), false, B);
     ws.score_blocks = score_blocks(B, D);
@@ -1559,7 +1563,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     if (shard) {
         I.R = A.n_item_rows;
         I.idx = I.fidx = I.idx_own;  // staged copy of A.item_rows
-        I.row_key = A.item_row_keys;
+        I.row_key = ws.keys_own;  // staged copy of A.item_row_keys (ITEM_FWD)
         I.t = A.item_fwd_out;
         I.a = mimic && A.item_fwd_out ? A.item_fwd_out + D : nullptr;
         I.t_ld = 2 * D;
@@ -1647,11 +1651,13 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         pa.c = ad;
         if ((rc = launch_step_prologue(st, pa, s))) return rc;
     }
-    if (shard && (ph & TTAMM_PHASE_ITEM_FWD) && I.R > 0) {  // owner: stage the requested local rows
+    if (shard && (ph & TTAMM_PHASE_ITEM_FWD) && I.R > 0) {
+        // owner: stage the requested local rows (range-checked) and their keys, contiguous
         StageArgs st;
         std::memset(&st, 0, sizeof(st));
         st.status = A.status;
-        st.seg[st.count++] = StageSeg{A.item_rows, I.idx_own, I.R, A.item.id.rows};
+        st.seg[st.count++] = StageSeg{A.item_rows, I.idx_own, I.R, A.item.id.rows, A.item_rows_ld};
+        st.seg[st.count++] = StageSeg{A.item_row_keys, ws.keys_own, I.R, INT64_MAX, A.item_rows_ld};
         if ((rc = launch_stage_rows(st, s))) return rc;
     }
     // ---- forward ----------------------------------------------------------------------------

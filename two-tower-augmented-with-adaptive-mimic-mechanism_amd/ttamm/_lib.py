@@ -173,6 +173,7 @@ class StepArgs(ctypes.Structure):
         ("item_slot", c_vp),
         ("cal_stats", c_vp),
         ("cal_scatter", c_vp),
+        ("item_rows_ld", c_i64),
     ]
 
 

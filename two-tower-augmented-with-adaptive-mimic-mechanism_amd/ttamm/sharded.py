@@ -361,8 +361,8 @@ def route_requests(own: RowOwnership, router: Router, pos: torch.Tensor, negs: t
     if status is None:
         sr[:W, 1] = 0
     packed, slot, _ = router(W, pos, negs, None, key0, key1, counts_out=sr[:W], status=status)
-    if W == 1:
-        return Route(slot, [n], [n], packed[:, 0].contiguous(), packed[:, 1].contiguous())
+    if W == 1:  # (local row, key) columns read in place by the step (ttamm_step_args.item_rows_ld)
+        return Route(slot, [n], [n], packed[:, 0], packed[:, 1])
     yield AllToAll(sr[:W], [1] * W, [1] * W, out=sr[W:])
     c = sr.reshape(-1).tolist()  # the one host synchronisation of the step
     sent, got_c = c[0:2 * W:2], c[2 * W::2]
@@ -371,7 +371,7 @@ def route_requests(own: RowOwnership, router: Router, pos: torch.Tensor, negs: t
         if r != own.rank:
             peers |= int(st)
     got = yield AllToAll(packed, sent, got_c)
-    return Route(slot, sent, got_c, got[:, 0].contiguous(), got[:, 1].contiguous(), int(c[1]), peers)
+    return Route(slot, sent, got_c, got[:, 0], got[:, 1], int(c[1]), peers)
 
 
 # ---------------------------------------------------------------------------------------
@@ -492,8 +492,11 @@ class ShardedTrainStep(FusedTrainStep):
         self.item_rows_seen += n
         if n > self.capacity:
             raise RuntimeError("ttamm: item requests exceed the sharded step's capacity")
+        if route.rows.stride(0) != route.keys.stride(0):
+            raise RuntimeError("ttamm: request rows and keys must share one stride")
         a.item_rows = route.rows.data_ptr()
         a.item_row_keys = route.keys.data_ptr()
+        a.item_rows_ld = route.rows.stride(0) if n > 0 else 1
         a.n_item_rows = n
         a.item_slot = route.slot.data_ptr()  # exchange buffers stay in owner-grouped order
         a.item_fwd_out = self.fwd_out.data_ptr()
