@@ -346,6 +346,9 @@ def main() -> None:
     ap.add_argument("--overlap-exchange", action="store_true",
                     help="row-sharded step: overlap the (t | a) all-to-all with a separate user-tower forward "
                          "instead of grouping the two towers' launches (ShardedTrainStep(group_towers=False))")
+    ap.add_argument("--no-look-ahead", action="store_true",
+                    help="row-sharded step: route each batch in its own step (a host synchronisation on the "
+                         "request counts every step) instead of one step ahead")
     ap.add_argument("--sharded-single", action="store_true",
                     help="developer: run the row-sharded step's phases at one GPU (W = 1, in-process exchange)")
     ap.add_argument("--emulate-world", type=int, default=0,
@@ -407,9 +410,24 @@ def main() -> None:
                  aux_cus=args.aux_cus, sharded_single=args.sharded_single,
                  group_towers=not args.overlap_exchange, emulate=emulate)
     eng = w.engine
+    # row-sharded step: each step routes the next batch ahead (look-ahead routing, its request
+    # counts reach the host during this step's backward); one process: the batch only
+    from ttamm.sharded import ShardedTrainStep
+
+    look_ahead = isinstance(eng, ShardedTrainStep) and not args.no_look_ahead
+    nxt = w.batch()
+
+    def step(**kw) -> None:
+        nonlocal nxt
+        u, p = nxt
+        nxt = w.batch()
+        if look_ahead:
+            eng.step(u, p, next_batch=nxt, **kw)
+        else:
+            eng.step(u, p, **kw)
+
     for _ in range(args.warmup):
-        u, p = w.batch()
-        eng.step(u, p)
+        step()
     eng.flush()  # the timed region starts with every table row current
     torch.cuda.synchronize()
 
@@ -432,8 +450,8 @@ def main() -> None:
     t0 = time.perf_counter()
     marks[0].record()
     for k in range(args.steps):
-        u, p = w.batch()  # ttamm_epoch_batch: the loader's gather runs inside the timed region
-        eng.step(u, p, timing_events=[e.cuda_event for e in evs[k]])
+        # the loader's gather of the next batch (ttamm_epoch_batch) runs inside the timed region
+        step(timing_events=[e.cuda_event for e in evs[k]])
     marks[1].record()
     # deferred AdamW: the g = 0 updates still owed to untouched rows are part of the K steps' work
     eng.flush()

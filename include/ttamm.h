@@ -519,11 +519,22 @@ int ttamm_mimic_augment(const float* table, int64_t table_rows, int32_t dim, con
 int ttamm_mse_loss(const float* input, const float* target, int64_t n, float* out, void* stream);
 
 /* sample_negative_items (samplers.py:11-85) on device: out[b, j] uniform in [0, num_items)
- * and not among user b's positives (CSR, sorted per user); up to 11 draws per slot, then
- * the TTAMM_STATUS_SAMPLER_EXHAUSTED bit is set in *status. */
+ * and not among user b's positives (CSR over user_rows users, sorted per user; a user id outside
+ * [0, user_rows) has no positives, as positives.get(user, set()) gives the reference); up to 11
+ * draws per slot, then the TTAMM_STATUS_SAMPLER_EXHAUSTED bit is set in *status.  The draws of slot
+ * j come from the Philox stream keyed by (seed, counter, slot_base + j): the fused step's sampler
+ * for a batch whose first slot is slot_base (row_base * num_neg in a row-sharded step). */
 int ttamm_sample_negatives(const int64_t* users, int64_t batch, int32_t num_neg, int64_t num_items,
-                           const int64_t* pos_offsets, const int64_t* pos_values, uint64_t seed,
-                           uint64_t counter, int64_t* out, uint32_t* status, void* stream);
+                           const int64_t* pos_offsets, const int64_t* pos_values, int64_t user_rows,
+                           uint64_t seed, uint64_t counter, int64_t slot_base, int64_t* out, uint32_t* status,
+                           void* stream);
+
+/* nn.Embedding's index check (encoders.py:222-223) without a lookup: sets
+ * TTAMM_STATUS_INDEX_OUT_OF_RANGE in *status when an id of ids0[0..n0) lies outside [0, rows0) or
+ * one of ids1[0..n1) outside [0, rows1) (ids1 may be NULL).  The row-sharded step's look-ahead
+ * checks the next batch with it before that batch's request counts are exchanged. */
+int ttamm_check_rows(const int64_t* ids0, int64_t n0, int64_t rows0, const int64_t* ids1, int64_t n1,
+                     int64_t rows1, uint32_t* status, void* stream);
 
 /* torch.optim.SparseAdam step on one table for already-coalesced rows
  * (_functional.py:24-84): rows[u] unique, grad [n_rows, dim]. */

@@ -89,9 +89,14 @@ def test_errors_map_to_reference_exceptions():
     with pytest.raises(ValueError):
         _lib.check(lib.ttamm_gather_rows(None, 10, 0, None, 5, None, 0, None))
     with pytest.raises(ValueError):
-        _lib.check(lib.ttamm_sample_negatives(None, 4, 0, 10, None, None, 0, 0, None, None, None))
+        _lib.check(lib.ttamm_sample_negatives(None, 4, 0, 10, None, None, 0, 0, 0, 0, None, None, None))
+    # (non-null placeholders: the argument checks fail before any device access)
     with pytest.raises(ValueError, match="num_items must be greater than one"):
-        _lib.check(lib.ttamm_sample_negatives(None, 4, 2, 1, None, None, 0, 0, None, None, None))
+        _lib.check(lib.ttamm_sample_negatives(8, 4, 2, 1, None, None, 0, 0, 0, 0, 8, 8, None))
+    with pytest.raises(ValueError, match="num_negatives"):
+        _lib.check(lib.ttamm_sample_negatives(8, 4, 0, 10, None, None, 0, 0, 0, 0, 8, 8, None))
+    with pytest.raises(ValueError):
+        _lib.check(lib.ttamm_check_rows(None, 4, 10, None, 0, 0, 8, None))
     with pytest.raises(ValueError):
         _lib.check(lib.ttamm_adamw_dense(None, None, None, None, 4, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1, 0, None))
     with pytest.raises(ValueError):

@@ -165,6 +165,45 @@ def test_sharded_three_steps_match_global_step(in_batch, group):
             assert d <= 5e-5, f"rank {own.rank} {k}: {d:.2e}"
 
 
+@pytest.mark.parametrize("W,in_batch,group", [(2, False, True), (3, True, True), (2, False, False), (8, False, True)],
+                         ids=["w2", "w3-in-batch", "w2-overlapped", "w8"])
+def test_look_ahead_routing_matches_global_step(W, in_batch, group):
+    """program(next_batch=...): each step draws the next step's negatives, groups its requests
+    and exchanges its counts after the forward exchange (look-ahead routing).  Three steps
+    against the one-process step over the global batches: the same losses and final state as
+    test_sharded_three_steps_match_global_step, and the look-ahead's draws are the ones the
+    one-process sampler makes (Philox keyed by global slot and step)."""
+    shape = Shape(N=2) if in_batch else Shape()
+    prob, batches, g, ranks = _setup(shape, W, lr=1e-3, betas=(0.9, 0.999), steps=3, in_batch=in_batch, group=group)
+    gm, gopts, geng = g
+    dev = [[((u // W).cuda(), p.cuda()) for (u, p) in per_rank] for per_rank in batches]
+    for s, per_rank in enumerate(batches):
+        users = torch.cat([u for u, _ in per_rank]).cuda()
+        pos = torch.cat([p for _, p in per_rank]).cuda()
+        geng.step(users, pos)
+        gl = geng.last_losses()
+        gneg = geng.neg_buffer.clone()
+        progs = [eng.program(*dev[s][r], next_batch=dev[s + 1][r] if s + 1 < len(batches) else None)
+                 for r, (own, m, o, eng) in enumerate(ranks)]
+        run_loopback(progs)
+        for r, (_, _, _, eng) in enumerate(ranks):
+            assert abs(eng.last_losses()["total"] - gl["total"]) <= 1e-5 * abs(gl["total"]), (s, r)
+            if s > 0:  # this step ran on the look-ahead's negatives
+                B, N = shape.B, shape.N
+                got = torch.from_numpy(eng._ahead_bufs[(s - 1) % 2][: B * N].cpu().numpy())
+                assert torch.equal(got, gneg[r * B * N:(r + 1) * B * N].cpu()), (s, r)
+    gavg = geng.finish()
+    ravg = run_loopback([eng.finish_program() for (_, _, _, eng) in ranks])
+    for r in range(W):
+        assert abs(ravg[r] - gavg) <= 1e-5 * abs(gavg)
+    gsd = gm.state_dict()
+    for own, m, _, _ in ranks:
+        for k, v in m.state_dict().items():
+            want = gsd[k][own.rank:: W] if k in TABLES else gsd[k]
+            d = (v - want).abs().max().item()
+            assert d <= 5e-5, f"rank {own.rank} {k}: {d:.2e}"
+
+
 def test_bench_two_ranks_one_gpu_gloo():
     """The real multi-process path (torch.distributed.run, TorchComm, ShardedTrainStep, bench
     timing) with 2 ranks on one GPU; gloo stages the exchanges through the host because RCCL

@@ -12,7 +12,8 @@ for v in x p; do
   done
 done
 TTAMM_IB_KERNEL=p timeout -k 10 600 python -u -m pytest tests/test_inbatch_op_gpu.py tests/test_inbatch_gpu.py -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/s7_ib_tests.log 2>&1; tail -3 gpurun_out/s7_ib_tests.log
-timeout -k 10 900 python -u -m pytest tests/test_deferred_gpu.py tests/test_module_autograd_gpu.py tests/test_retrieval_gpu.py tests/test_route_gpu.py tests/test_sharded_gpu.py -q -s -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/s7_tests.log 2>&1; grep -E "passed|failed|near ties|fast vs exact|Error" gpurun_out/s7_tests.log | tail -12
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q -s -p no:cacheprovider --timeout 600 --timeout-method thread > gpurun_out/s7_tests.log 2>&1; rc=$?; grep -E "passed|failed|near ties|fast vs exact|^FAILED|Error" gpurun_out/s7_tests.log | tail -25
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "suite rc=$rc"; exit $rc; fi
 timeout -k 10 120 ./two-tower-augmented-with-adaptive-mimic-mechanism_amd/build/replay_bench > gpurun_out/s7_replay_bench.txt 2>&1; cat gpurun_out/s7_replay_bench.txt | tail -8
 timeout -k 10 600 python -u bench.py --no-cpu-baseline > gpurun_out/s7_bench.json 2> gpurun_out/s7_bench.err || { echo BENCH_FAIL; tail -20 gpurun_out/s7_bench.err; exit 1; }
 python3 -c "

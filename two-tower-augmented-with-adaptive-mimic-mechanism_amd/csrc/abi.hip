@@ -243,10 +243,27 @@ TTAMM_API int ttamm_mse_loss(const float* input, const float* target, int64_t n,
 }
 
 TTAMM_API int ttamm_sample_negatives(const int64_t* users, int64_t batch, int32_t num_neg, int64_t num_items,
-                                     const int64_t* pos_offsets, const int64_t* pos_values, uint64_t seed,
-                                     uint64_t counter, int64_t* out, uint32_t* status, void* stream) {
-    return launch_sample_negatives(users, batch, num_neg, num_items, pos_offsets, pos_values, seed, counter, 0, out,
-                                   nullptr, status, (hipStream_t)stream);
+                                     const int64_t* pos_offsets, const int64_t* pos_values, int64_t user_rows,
+                                     uint64_t seed, uint64_t counter, int64_t slot_base, int64_t* out,
+                                     uint32_t* status, void* stream) {
+    g_last_error.clear();
+    if (batch < 0 || (batch > 0 && (!users || !out || !status)) || (pos_offsets && user_rows <= 0))
+        return fail(TTAMM_E_INVALID, "sample_negatives: bad arguments");
+    return launch_sample_negatives(users, batch, num_neg, num_items, pos_offsets, pos_values, user_rows, seed, counter,
+                                   slot_base, out, nullptr, status, (hipStream_t)stream);
+}
+
+TTAMM_API int ttamm_check_rows(const int64_t* ids0, int64_t n0, int64_t rows0, const int64_t* ids1, int64_t n1,
+                               int64_t rows1, uint32_t* status, void* stream) {
+    g_last_error.clear();
+    if (!status || n0 < 0 || n1 < 0 || (n0 > 0 && !ids0) || (n1 > 0 && !ids1))
+        return fail(TTAMM_E_INVALID, "check_rows: bad arguments");
+    StageArgs st;
+    std::memset(&st, 0, sizeof(st));
+    st.status = status;
+    if (n0 > 0) st.seg[st.count++] = StageSeg{ids0, nullptr, n0, rows0, 1};
+    if (n1 > 0) st.seg[st.count++] = StageSeg{ids1, nullptr, n1, rows1, 1};
+    return launch_stage_rows(st, (hipStream_t)stream);
 }
 
 TTAMM_API int ttamm_sparse_adam_rows(float* weight, float* exp_avg, float* exp_avg_sq, int32_t dim,

@@ -649,7 +649,7 @@ SparseConsts make_sparse_consts(double lr, double beta1, double beta2, double ep
 // ------------------------------------------------------------------------------------
 // slot_base: global index of this batch's first slot (row_base * num_neg) — the Philox stream key
 int launch_sample_negatives(const int64_t* users, int64_t batch, int num_neg, int64_t num_items,
-                            const int64_t* pos_offsets, const int64_t* pos_values, uint64_t seed,
+                            const int64_t* pos_offsets, const int64_t* pos_values, int64_t user_rows, uint64_t seed,
                             uint64_t counter, int64_t slot_base, int64_t* out, int64_t* out2, uint32_t* status,
                             hipStream_t s);  // out2: optional second copy
 

@@ -57,13 +57,16 @@ __device__ __forceinline__ void sample_slot(int64_t slot, int64_t u, uint64_t nu
 
 __global__ void sample_negatives_kernel(const int64_t* __restrict__ users, int64_t batch, int num_neg,
                                         uint64_t num_items, const int64_t* __restrict__ pos_offsets,
-                                        const int64_t* __restrict__ pos_values, uint32_t k0, uint32_t k1,
-                                        uint64_t counter, int64_t slot_base, int64_t* __restrict__ out,
+                                        const int64_t* __restrict__ pos_values, int64_t user_rows, uint32_t k0,
+                                        uint32_t k1, uint64_t counter, int64_t slot_base, int64_t* __restrict__ out,
                                         int64_t* __restrict__ out2, uint32_t* __restrict__ status) {
     const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (slot >= batch * num_neg) return;
-    sample_slot(slot, users[slot / num_neg], num_items, pos_offsets, pos_values, k0, k1, counter, slot_base, out, out2,
-                status);
+    const int64_t u = users[slot / num_neg];
+    // a user outside the CSR has no positives (the reference's positives.get(user, set()))
+    const bool known = u >= 0 && u < user_rows;
+    sample_slot(slot, known ? u : 0, num_items, known ? pos_offsets : nullptr, pos_values, k0, k1, counter, slot_base,
+                out, out2, status);
 }
 
 // The step's prologue in one launch (blockIdx.y < st.count: staging segment y, as
@@ -144,15 +147,16 @@ int launch_step_prologue(const StageArgs& st, const PrologueArgs& pa, hipStream_
 }
 
 int launch_sample_negatives(const int64_t* users, int64_t batch, int num_neg, int64_t num_items,
-                            const int64_t* pos_offsets, const int64_t* pos_values, uint64_t seed, uint64_t counter,
-                            int64_t slot_base, int64_t* out, int64_t* out2, uint32_t* status, hipStream_t s) {
+                            const int64_t* pos_offsets, const int64_t* pos_values, int64_t user_rows, uint64_t seed,
+                            uint64_t counter, int64_t slot_base, int64_t* out, int64_t* out2, uint32_t* status,
+                            hipStream_t s) {
     TTAMM_REQUIRE(num_neg > 0, "num_negatives must be greater than zero.");
     TTAMM_REQUIRE(num_items > 1, "num_items must be greater than one.");
     const int64_t slots = batch * num_neg;
     if (slots <= 0) return TTAMM_OK;
     hipLaunchKernelGGL(sample_negatives_kernel, dim3((unsigned)ceil_div(slots, 256)), dim3(256), 0, s, users, batch,
-                       num_neg, (uint64_t)num_items, pos_offsets, pos_values, (uint32_t)seed, (uint32_t)(seed >> 32),
-                       counter, slot_base, out, out2, status);
+                       num_neg, (uint64_t)num_items, pos_offsets, pos_values, pos_offsets ? user_rows : 0,
+                       (uint32_t)seed, (uint32_t)(seed >> 32), counter, slot_base, out, out2, status);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

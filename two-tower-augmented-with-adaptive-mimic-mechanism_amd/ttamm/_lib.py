@@ -253,8 +253,9 @@ SIGNATURES = {
     "ttamm_mse_loss": (ctypes.c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "ttamm_sample_negatives": (
         ctypes.c_int,
-        [c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp, c_vp],
+        [c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_i64, c_u64, c_u64, c_i64, c_vp, c_vp, c_vp],
     ),
+    "ttamm_check_rows": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "ttamm_coalesce_workspace_bytes": (ctypes.c_size_t, [c_i64, c_i64]),
     "ttamm_coalesce_rows": (
         ctypes.c_int,

@@ -111,7 +111,7 @@ def sample_negative_items(
     _lib.check(
         lib.ttamm_sample_negatives(
             users.data_ptr(), users.numel(), num_negatives, num_items, csr.offsets.data_ptr(), csr.values.data_ptr(),
-            draw_seed(), 0, out.data_ptr(), status.data_ptr(), _lib.stream_handle(device),
+            csr.offsets.numel() - 1, draw_seed(), 0, 0, out.data_ptr(), status.data_ptr(), _lib.stream_handle(device),
         )
     )
     if int(status.item()) & _lib.STATUS_SAMPLER_EXHAUSTED:

@@ -347,13 +347,25 @@ def device_route(lib: Any, world: int, id0: torch.Tensor, id1: torch.Tensor | No
 Router = Callable[..., "tuple[torch.Tensor, torch.Tensor, torch.Tensor]"]  # device_route minus lib
 
 
-def route_requests(own: RowOwnership, router: Router, pos: torch.Tensor, negs: torch.Tensor, key0: int,
-                   key1: int, status: torch.Tensor | None = None) -> Program:
-    """Program: send (local row, key) of every requested item ([pos; negs], keys key0 + j for
-    positives, key1 + j for negatives) to its owner.  Returns a Route.  One host sync (the
-    counts, which size the variable all-to-all); none at world size 1.  ``status`` (the rank's
-    device status word): rides along with the counts, so every rank learns whether any rank's
-    step is poisoned (Route.peer_status) before any of them writes state."""
+@dataclass
+class PendingRoute:
+    """route_start's result: the requests grouped by owner, the count rows exchanged, their copy
+    to the host in flight (``event`` marks it)."""
+
+    packed: torch.Tensor
+    slot: torch.Tensor
+    n: int
+    sr: torch.Tensor  # [2W, 2] (count, status) rows sent, then received
+    host: torch.Tensor | None  # pinned copy of sr (None: read sr itself)
+    event: Any  # torch.cuda.Event after the copy, or None
+
+
+def route_start(own: RowOwnership, router: Router, pos: torch.Tensor, negs: torch.Tensor, key0: int, key1: int,
+                status: torch.Tensor | None = None, host: torch.Tensor | None = None) -> Program:
+    """Program: group the requests [pos; negs] by owner (keys key0 + j for positives, key1 + j for
+    negatives) and exchange the per-owner counts with the rank's status word.  With a pinned
+    ``host`` buffer the counts are copied to it asynchronously (no host synchronisation here:
+    route_finish waits, so a look-ahead can start the copy a step early)."""
     W = own.world_size
     n = pos.numel() + negs.numel()
     # rows 0..W-1: what this rank sends (count to owner d, its status word); rows W..2W-1: received
@@ -361,22 +373,66 @@ def route_requests(own: RowOwnership, router: Router, pos: torch.Tensor, negs: t
     if status is None:
         sr[:W, 1] = 0
     packed, slot, _ = router(W, pos, negs, None, key0, key1, counts_out=sr[:W], status=status)
+    event = None
+    if W > 1:
+        yield AllToAll(sr[:W], [1] * W, [1] * W, out=sr[W:])
+        if host is not None and sr.device.type == "cuda":
+            host.copy_(sr, non_blocking=True)
+            event = torch.cuda.Event()
+            event.record()
+        else:
+            host = None
+    return PendingRoute(packed, slot, n, sr, host, event)
+
+
+def route_finish(own: RowOwnership, pend: PendingRoute) -> Program:
+    """Program: read the exchanged counts (the step's one host synchronisation, already done when
+    a look-ahead started it a step earlier) and send (local row, key) of every request to its owner.
+    Returns a Route.  The status words that rode with the counts tell every rank whether any rank's
+    step is poisoned (Route.peer_status) before any of them writes state."""
+    W = own.world_size
     if W == 1:  # (local row, key) columns read in place by the step (ttamm_step_args.item_rows_ld)
-        return Route(slot, [n], [n], packed[:, 0], packed[:, 1])
-    yield AllToAll(sr[:W], [1] * W, [1] * W, out=sr[W:])
-    c = sr.reshape(-1).tolist()  # the one host synchronisation of the step
+        return Route(pend.slot, [pend.n], [pend.n], pend.packed[:, 0], pend.packed[:, 1])
+    if pend.host is not None:
+        pend.event.synchronize()
+        c = pend.host.reshape(-1).tolist()
+    else:
+        c = pend.sr.reshape(-1).tolist()
     sent, got_c = c[0:2 * W:2], c[2 * W::2]
     peers = 0
     for r, st in enumerate(c[2 * W + 1::2]):
         if r != own.rank:
             peers |= int(st)
-    got = yield AllToAll(packed, sent, got_c)
-    return Route(slot, sent, got_c, got[:, 0], got[:, 1], int(c[1]), peers)
+    got = yield AllToAll(pend.packed, sent, got_c)
+    return Route(pend.slot, sent, got_c, got[:, 0], got[:, 1], int(c[1]), peers)
+
+
+def route_requests(own: RowOwnership, router: Router, pos: torch.Tensor, negs: torch.Tensor, key0: int,
+                   key1: int, status: torch.Tensor | None = None) -> Program:
+    """Program: send (local row, key) of every requested item ([pos; negs], keys key0 + j for
+    positives, key1 + j for negatives) to its owner.  Returns a Route.  One host sync (the
+    counts, which size the variable all-to-all); none at world size 1.  ``status`` (the rank's
+    device status word): rides along with the counts, so every rank learns whether any rank's
+    step is poisoned (Route.peer_status) before any of them writes state."""
+    pend = yield from route_start(own, router, pos, negs, key0, key1, status=status)
+    return (yield from route_finish(own, pend))
 
 
 # ---------------------------------------------------------------------------------------
 # the sharded step
 # ---------------------------------------------------------------------------------------
+@dataclass
+class _Ahead:
+    """The next step as a look-ahead prepared it: its batch (matched by identity), negatives,
+    status word and the request routing up to the exchanged counts."""
+
+    users: torch.Tensor
+    pos: torch.Tensor
+    negs: torch.Tensor
+    status: torch.Tensor
+    pending: PendingRoute
+
+
 class ShardedTrainStep(FusedTrainStep):
     """FusedTrainStep over a rank's shard.  ``model`` holds this rank's rows of the user / item
     ID and mimic tables (``RowOwnership.shard``) and a replica of the feature-encoder and gate
@@ -410,6 +466,12 @@ class ShardedTrainStep(FusedTrainStep):
         # first).  The grouped schedule launches each tower-wide kernel once per step.
         self.group_towers = bool(group_towers)
         self.item_rows_seen = 0  # item-tower rows this owner ran (bench roofline)
+        # look-ahead routing (program(next_batch=...)): the prepared next step, its buffers
+        self._ahead: _Ahead | None = None
+        self._ahead_bufs: list[torch.Tensor] | None = None
+        self._ahead_status: list[torch.Tensor] = []
+        self._ahead_host: torch.Tensor | None = None
+        self._ahead_flip = 0
         super().__init__(model, optimizers, num_items=num_items, **kw)
         self.router: Router = functools.partial(device_route, self.lib)
 
@@ -455,13 +517,24 @@ class ShardedTrainStep(FusedTrainStep):
     def program(self, users: torch.Tensor, pos_items: torch.Tensor, neg_items: torch.Tensor | None = None, *,
                 keep_masks: Mapping[str, Sequence[torch.Tensor]] | None = None,
                 timing_events: Sequence[Any] | None = None, row_base: int | None = None,
-                global_batch: int | None = None) -> Program:
+                global_batch: int | None = None,
+                next_batch: tuple[torch.Tensor, torch.Tensor] | None = None) -> Program:
         """One step as an SPMD program (yields collective requests).  ``timing_events``
         (hipEvent_t handles, pairs as in ttamm.h) bracket the owner's item-table maintenance
         and its item-tower first-layer GEMM.  By default every rank holds B interactions and
         rank r's are global positions [r B, (r + 1) B); ranks with different batch sizes pass
-        ``row_base`` (the sizes of the ranks before this one) and ``global_batch`` (the sum)."""
-        if not self._bind_batch(users, pos_items, neg_items, keep_masks):
+        ``row_base`` (the sizes of the ranks before this one) and ``global_batch`` (the sum).
+
+        ``next_batch`` = (users, positives) of the following step (default positions, sampled
+        negatives): its negatives are drawn, its requests grouped and its request counts
+        exchanged during this step, after the forward exchange, and their copy to the host runs
+        behind this step's backward — so the next step reads them without waiting (look-ahead
+        routing; the draws and ids are the ones that step would make itself)."""
+        ahead = self._ahead
+        self._ahead = None
+        use_ahead = (ahead is not None and ahead.users is users and ahead.pos is pos_items and neg_items is None
+                     and row_base is None and global_batch is None)
+        if not self._bind_batch(users, pos_items, ahead.negs if use_ahead else neg_items, keep_masks):
             raise ValueError("ttamm: empty batch in a sharded step (every rank must step)")
         a = self.args
         W, rank = self.own.world_size, self.own.rank
@@ -477,11 +550,19 @@ class ShardedTrainStep(FusedTrainStep):
         for i in range(nev):
             a.timing_events[i] = None
         self._hparams()
-        negs = neg_items.reshape(-1) if neg_items is not None else self.neg_buffer[: B * N]
+        if use_ahead:
+            negs = ahead.negs
+            self.status.bitwise_or_(ahead.status)  # what the look-ahead's checks and draws found
+        else:
+            negs = neg_items.reshape(-1) if neg_items is not None else self.neg_buffer[: B * N]
         self._phase(_lib.PHASE_SAMPLE)
         # ---- route the item requests [positives; negatives] to their owners -----------------
-        route = yield from route_requests(self.own, self.router, pos_items.reshape(-1), negs, base, Bg + base * N,
+        if use_ahead:
+            pend = ahead.pending
+        else:
+            pend = yield from route_start(self.own, self.router, pos_items.reshape(-1), negs, base, Bg + base * N,
                                           status=self.status)
+        route = yield from route_finish(self.own, pend)
         if route.peer_status and not route.own_status:
             # another rank's step is poisoned (an id outside its table, sampler exhaustion):
             # poison this rank's step too, before it writes any state, so every rank keeps the
@@ -521,6 +602,8 @@ class ShardedTrainStep(FusedTrainStep):
             a.timing_events[i] = None
         a.item_fwd_in = back.data_ptr()
         a.item_bwd_out = self.bwd_out.data_ptr()
+        if next_batch is not None and row_base is None and global_batch is None:
+            self._ahead = yield from self._look_ahead(*next_batch)
         ib = ()
         if self.in_batch:
             # ---- in-batch: every rank's augmented positives, then dP summed back to its rank ------
@@ -566,17 +649,57 @@ class ShardedTrainStep(FusedTrainStep):
         # keep the step's device buffers alive until the stream has consumed them
         self._live = (route, back, bwd_in) + ib
 
-    def step(self, users, pos_items, neg_items=None, *, keep_masks=None, timing_events=None) -> None:
+    def _look_ahead(self, users: torch.Tensor, pos: torch.Tensor) -> Program:
+        """Program: the next step's id checks, negatives and request routing up to the count
+        exchange (route_start with its host copy in flight).  Its status word starts as this
+        rank's (an earlier poison rides along as in the step's own exchange)."""
+        W, rank = self.own.world_size, self.own.rank
+        B, N = users.numel(), self.num_neg
+        if B == 0 or B > self.max_batch or users.dtype != torch.long or pos.dtype != torch.long or \
+                pos.numel() != B:
+            raise ValueError("ttamm: next_batch must be int64 (users, positives) of one size <= max_batch")
+        users0, pos0 = users, pos  # the next step's program finds its batch by identity
+        users, pos = users.reshape(-1), pos.reshape(-1)
+        dev = self.device
+        if self._ahead_bufs is None:
+            self._ahead_bufs = [torch.empty(self.max_batch * N, dtype=torch.long, device=dev) for _ in range(2)]
+            self._ahead_status = [torch.zeros(1, dtype=torch.int32, device=dev) for _ in range(2)]
+            self._ahead_host = (torch.empty((2 * W, 2), dtype=torch.long, pin_memory=True)
+                                if dev.type == "cuda" and W > 1 else None)
+        k = self._ahead_flip
+        self._ahead_flip ^= 1
+        status = self._ahead_status[k]
+        status.copy_(self.status)
+        stream = _lib.stream_handle(dev)
+        _lib.check(self.lib.ttamm_check_rows(users.data_ptr(), B, self.model.user_encoder.num_embeddings,
+                                             pos.data_ptr(), B, self.num_items, status.data_ptr(), stream))
+        negs = self._ahead_bufs[k][: B * N]
+        base, Bg = rank * B, W * B
+        if N > 0:
+            if self.csr is None:
+                raise ValueError("ttamm: positives are required to sample negatives")
+            _lib.check(self.lib.ttamm_sample_negatives(
+                users.data_ptr(), B, N, self.num_items, self.csr.offsets.data_ptr(), self.csr.values.data_ptr(),
+                self.csr.num_users, self.args.b.seed, self.steps_done + 1, base * N, negs.data_ptr(),
+                status.data_ptr(), stream))
+        pend = yield from route_start(self.own, self.router, pos, negs, base, Bg + base * N, status=status,
+                                      host=self._ahead_host)
+        return _Ahead(users0, pos0, negs, status, pend)
+
+    def step(self, users, pos_items, neg_items=None, *, keep_masks=None, timing_events=None,
+             next_batch=None) -> None:
         if self.comm is None:
             raise RuntimeError("ttamm: ShardedTrainStep.step needs comm= (e.g. TorchComm()); "
                                "use program() with run_loopback for in-process ranks")
-        self.comm.run(self.program(users, pos_items, neg_items, keep_masks=keep_masks, timing_events=timing_events))
+        self.comm.run(self.program(users, pos_items, neg_items, keep_masks=keep_masks, timing_events=timing_events,
+                                   next_batch=next_batch))
 
     def finish_program(self) -> Program:
         """Collective finish: global epoch loss (sum of the ranks' shares).  A status error on
         any rank (an out-of-range id, sampler exhaustion) raises on every rank, and every rank
         holds the state after the same last good step: the status words ride with each step's
         request counts, so a poisoned step is skipped by all ranks before any writes state."""
+        self._ahead = None  # a look-ahead no step consumed: its exchange ran on every rank, nothing to undo
         flags = torch.stack([(self.status & b) != 0 for b in (1, 2)]).reshape(-1).to(torch.float32)
         yield AllReduce(flags)
         self.status.bitwise_or_((flags[0] > 0).to(torch.int32) + 2 * (flags[1] > 0).to(torch.int32))
