@@ -24,6 +24,8 @@ for nb in 20 1000 5000; do
   python3 -c "import json; d=json.load(open('gpurun_out/s7_c3_b$nb.json')); print('C3 blocked=$nb', d['value'])"
 done
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --emulate-world 8 --steps 100 --warmup 3 > gpurun_out/s7_emu.json 2> gpurun_out/s7_emu.err || { echo EMU_FAIL; tail -20 gpurun_out/s7_emu.err; exit 1; }
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --emulate-world 8 --steps 100 --warmup 3 --no-look-ahead > gpurun_out/s7_emu_nola.json 2> gpurun_out/s7_emu_nola.err || { echo EMU2_FAIL; tail -20 gpurun_out/s7_emu_nola.err; exit 1; }
+python3 -c "import json; d=json.load(open('gpurun_out/s7_emu_nola.json')); print('emu8 no look-ahead', d['value'], d['ms_per_step'])"
 python3 -c "import json; d=json.load(open('gpurun_out/s7_emu.json')); print('emu8', d['value'], d['ms_per_step'])"
 timeout -k 10 300 python -u -m cProfile -o gpurun_out/s7_emu.prof bench.py --no-cpu-baseline --emulate-world 8 --steps 100 --warmup 3 > gpurun_out/s7_emu_prof.json 2> gpurun_out/s7_emu_prof.err || { echo PROF_FAIL; tail -20 gpurun_out/s7_emu_prof.err; exit 1; }
 python3 -c "
