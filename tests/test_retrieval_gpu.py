@@ -55,6 +55,31 @@ def test_topk_bit_exact_on_exact_scores(nq, ni, D, k):
     assert torch.equal(s.cpu().double(), torch.from_numpy(want_s))
 
 
+@pytest.mark.parametrize("D", [96, 256])
+def test_topk_long_blocked_lists(D):
+    """Blocked lists from 0 to thousands of items per query (a heavy user's history; past the
+    kernel's one-scan limit the candidates take a lower-bound search), some covering the query's
+    whole exact top: bit-exact against the restatement."""
+    nq, ni, k = 96, 6000, 40
+    g = torch.Generator().manual_seed(D)
+    items = torch.randint(-3, 4, (ni, D), generator=g).float()
+    queries = torch.randint(-2, 3, (nq, D), generator=g).float()
+    exact = queries.double() @ items.double().T
+    lens = [0, 1, 63, 64, 65, 200, 1000, 4999, 5990] * (nq // 9) + [3000] * (nq % 9)
+    blocked = []
+    for q, n in enumerate(lens):
+        if q % 3 == 0:  # the query's best n items blocked: the answer lies past them
+            top = torch.sort(-exact[q], stable=True).indices[:n]
+            blocked.append(set(top.tolist()))
+        else:
+            blocked.append(set(torch.randperm(ni, generator=g)[:n].tolist()))
+    want_s, want_i = _oracle_topk(items.numpy(), queries.numpy(), k, blocked)
+    boff, bval = blocked_csr(range(nq), dict(enumerate(blocked)), torch.device("cuda"))
+    s, i = retrieve_topk(queries.cuda(), items.cuda(), k, blocked_offsets=boff, blocked_values=bval)
+    assert torch.equal(i.cpu(), torch.from_numpy(want_i))
+    assert torch.equal(s.cpu().double(), torch.from_numpy(want_s))
+
+
 def test_topk_matches_faiss_restatement_without_blocking():
     g = torch.Generator().manual_seed(3)
     items = torch.randint(-3, 4, (3000, 96), generator=g).float()

@@ -34,9 +34,12 @@ def _model(cfg, shape: Shape, U: int, I: int, state: dict):
     return m
 
 
-def _opts(model, lr, betas):
+def _opts(model, lr, betas, sgd: bool = False):
     dense, sparse = ttamm._collect_parameter_groups(model)
-    opts = [torch.optim.AdamW(dense, lr=1e-3, weight_decay=0.01, betas=betas)]
+    if sgd:  # torch.optim.SGD with momentum, dampening, coupled L2 (training.py:1311-1333's other choice)
+        opts = [torch.optim.SGD(dense, lr=1e-3, momentum=0.9, dampening=0.1, weight_decay=0.01)]
+    else:
+        opts = [torch.optim.AdamW(dense, lr=1e-3, weight_decay=0.01, betas=betas)]
     if sparse:
         opts.append(torch.optim.SparseAdam(sparse, lr=1e-3, betas=betas))
     for o in opts:
@@ -68,7 +71,8 @@ def _categories(I: int, C: int = 4, major_share: float = 0.4, seed: int = 9) -> 
     return cats
 
 
-def _run(shape: Shape, W: int, *, lr: float, betas, steps: int, clip: float | None, cal: bool = False):
+def _run(shape: Shape, W: int, *, lr: float, betas, steps: int, clip: float | None, cal: bool = False,
+         sgd: bool = False):
     prob = make_problem(shape, seed=77)
     lw = CAL_WEIGHTS if cal else LOSS_WEIGHTS
     cat_kw = dict(item_category_tensor=_categories(shape.I).cuda(), major_category_id=0) if cal else {}
@@ -88,7 +92,7 @@ def _run(shape: Shape, W: int, *, lr: float, betas, steps: int, clip: float | No
             per_rank.append((users, pos))
         batches.append(per_rank)
     gm = _model(shape.tower_cfg(), shape, shape.U, shape.I, state)
-    gopts = _opts(gm, lr, betas)
+    gopts = _opts(gm, lr, betas, sgd)
     geng = ttamm.FusedTrainStep(gm, gopts, negatives_per_positive=shape.N, positives=prob.positives,
                                 user_features=prob.user_features.cuda(), item_features=prob.item_features.cuda(),
                                 loss_weights=lw, max_batch=W * shape.B, seed=SEED, gradient_clip_norm=clip,
@@ -98,7 +102,7 @@ def _run(shape: Shape, W: int, *, lr: float, betas, steps: int, clip: float | No
         own = RowOwnership(W, r)
         st = {k: (own.shard(v) if k in TABLES else v.clone()) for k, v in state.items()}
         m = _model(_shard_cfg(shape, own), shape, own.local_count(shape.U), own.local_count(shape.I), st)
-        opts = _opts(m, lr, betas)
+        opts = _opts(m, lr, betas, sgd)
         local_pos = {u // W: prob.positives[u] for u in range(r, shape.U, W)}
         eng = ShardedTrainStep(m, opts, world_size=W, rank=r, num_items=shape.I, negatives_per_positive=shape.N,
                                positives=local_pos, user_features=own.shard(prob.user_features).cuda(),
@@ -173,6 +177,28 @@ def test_sharded_options_three_steps_match_global_step(W, shape, clip, cal):
         init = make_problem(shape, seed=77).model.state_dict()
         for n in ("user_encoder.embedding.weight", "item_encoder.embedding.weight"):
             assert torch.equal(m.state_dict()[n][shape.padding_idx // W].cpu(), init[n][shape.padding_idx]), n
+
+
+@pytest.mark.parametrize("W,shape,clip", [(2, Shape(), None), (3, Shape(sparse=False, max_norm=0.05), 0.05)],
+                         ids=["sparse-w2", "dense-clip-w3"])
+def test_sharded_sgd_three_steps_match_global_step(W, shape, clip):
+    """The dense group under SGD (momentum buffers written by the first step, then damped): every
+    rank's replicated dense parameters and its table shard follow the global step's."""
+    (gm, gopts), ranks, gl, rl = _run(shape, W, lr=0.05, betas=(0.9, 0.999), steps=3, clip=clip, sgd=True)
+    for s in range(3):
+        assert abs(rl[s][0]["total"] - gl[s]["total"]) <= 1e-5 * abs(gl[s]["total"])
+    gsd = gm.state_dict()
+    gstate = named_optimizer_state(gm, gopts)
+    for own, m, opts, _ in ranks:
+        for k, v in m.state_dict().items():
+            want = gsd[k][own.rank:: W] if k in TABLES else gsd[k]
+            d = (v - want).abs().max().item()
+            assert d <= 5e-5, f"rank {own.rank} {k}: {d:.2e}"
+        for name, st in named_optimizer_state(m, opts).items():
+            if "momentum_buffer" in st:
+                want = gstate[name]["momentum_buffer"]
+                want = want[own.rank:: W] if name in TABLES else want
+                assert rel_err(st["momentum_buffer"], want) <= 1e-4, (own.rank, name)
 
 
 def test_sharded_clipping_needs_grouped_schedule():

@@ -19,6 +19,8 @@
 #include <cmath>
 #include <cstring>
 
+#include <type_traits>
+
 #include "kernels.h"
 
 #pragma clang fp contract(off)
@@ -613,6 +615,21 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 struct ReplayConsts {
     float decay, w1, b2, eps, neg_step, inv_bc2_sqrt, bc2_sqrt, wd, w2, fast_ibc, fast_eps, pad0;
 };
+// The fast decoupled replay's constants as element pairs (each value twice), read as whole 64-bit
+// operands by the packed loop.  Built from one float, the compiler broadcast it into both halves
+// of a v_pk_* with op_sel, and picked a destination pair whose low register was that broadcast
+// source (v_pk_fma_f32 v[48:49], v[54:55], v[48:49], v[48:49] op_sel_hi:[1,0,1]); run beside the
+// feature MLP's GEMMs on the main stream, that replay gave run-to-run different parameters
+// (tools/diag/deferred_c2.py, profiles/r04_replay_pk_overlap.txt).  With pair operands the halves
+// of every packed instruction read only their own lane.
+struct ReplayPairs {
+    f32x2 decay, w1, b2, ibc, eps;
+    float pad0, pad1;
+};
+static_assert(sizeof(ReplayPairs) == sizeof(ReplayConsts), "one LDS ring size for both layouts");
+
+__device__ __forceinline__ float lo_of(float x) { return x; }
+__device__ __forceinline__ float lo_of(f32x2 x) { return x.x; }
 
 // One thread per V float4s of a row (dim % (4 V) == 0: 4 V independent dependency chains per
 // thread sharing each step's constants, at float4 columns q and q + dim / (4 V)); blockIdx.y =
@@ -623,18 +640,25 @@ struct ReplayConsts {
 // run one trip count.
 template <bool DECOUPLED, bool FAST, int V>
 __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
+    constexpr bool PKL = DECOUPLED && FAST;  // the packed-pair loop
+    using HC = typename std::conditional<PKL, ReplayPairs, ReplayConsts>::type;
     const KArg(ReplayArgs)* ka = (const KArg(ReplayArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
     const KArg(ReplaySeg)& S = ka->seg[blockIdx.y];
     if (step_poisoned(ka->status)) return;
     // the history ring unrolled twice in LDS (2 cap entries, sized at launch: ~6 KB by default),
     // so a row's steps l+1 .. target are consecutive entries from (l + 1) % cap — no wrap test
     // and no address arithmetic beyond a pointer increment in the VALU-bound loop
-    extern __shared__ ReplayConsts H2[];
+    extern __shared__ __attribute__((aligned(16))) unsigned char replay_lds[];
+    HC* H2 = reinterpret_cast<HC*>(replay_lds);
     const int cap = ka->cap;
     for (int i = threadIdx.x; i < 2 * cap; i += blockDim.x) {
         const AdamConsts& h = ka->hist[i < cap ? i : i - cap];
-        H2[i] = ReplayConsts{h.decay, h.w1, h.b2, h.eps, h.neg_step, h.inv_bc2_sqrt, h.bc2_sqrt, h.wd, h.w2,
-                             h.fast_ibc, h.fast_eps, 0.f};
+        if constexpr (PKL)
+            H2[i] = ReplayPairs{f32x2{h.decay, h.decay}, f32x2{h.w1, h.w1}, f32x2{h.b2, h.b2},
+                                f32x2{h.fast_ibc, h.fast_ibc}, f32x2{h.fast_eps, h.fast_eps}, 0.f, 0.f};
+        else
+            H2[i] = ReplayConsts{h.decay, h.w1, h.b2, h.eps, h.neg_step, h.inv_bc2_sqrt, h.bc2_sqrt, h.wd, h.w2,
+                                 h.fast_ibc, h.fast_eps, 0.f};
     }
     __syncthreads();
     const int dim = S.dim;
@@ -664,8 +688,8 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
             m[i] = *reinterpret_cast<const float4*>(S.m + oi);
             v[i] = *reinterpret_cast<const float4*>(S.v + oi);
         }
-        const ReplayConsts* hc = H2 + (l + 1) % cap;
-        const ReplayConsts* const hend = hc + (target - l);
+        const HC* hc = H2 + (l + 1) % cap;
+        const HC* const hend = hc + (target - l);
         // A cold row (first moment +0.0: never given a gradient) stays cold under g = 0 (m = fma(w1,
         // -0, 0) = +0), and its update term neg_step * (0 * r) is -0.0, which leaves p * decay
         // unchanged for every p — so its replay is p *= decay, v *= b2 per step, bit for bit what
@@ -677,7 +701,7 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
             mbits |= __float_as_uint(m[i].x) | __float_as_uint(m[i].y) | __float_as_uint(m[i].z) | __float_as_uint(m[i].w);
         if (DECOUPLED && mbits == 0u) {
             for (; hc != hend; ++hc) {
-                const float decay = hc->decay, b2 = hc->b2;
+                const float decay = lo_of(hc->decay), b2 = lo_of(hc->b2);
 #pragma unroll
                 for (int i = 0; i < V; ++i) {
                     p[i].x = p[i].x * decay, p[i].y = p[i].y * decay, p[i].z = p[i].z * decay, p[i].w = p[i].w * decay;
@@ -685,13 +709,12 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
                 }
             }
         }
-        if constexpr (DECOUPLED && FAST) {
+        if constexpr (PKL) {
             // adam_elem_t<true, true, true> on element pairs, written with 2-wide vectors so every
             // multiply / fma issues as one v_pk_* for two elements (the denominator's fma included):
             // the same IEEE operations per element, so the dense sweep's scalar form gives the same bits
             for (; hc != hend; ++hc) {
-                const f32x2 decay = {hc->decay, hc->decay}, w1 = {hc->w1, hc->w1}, b2 = {hc->b2, hc->b2};
-                const f32x2 ibc = {hc->fast_ibc, hc->fast_ibc}, eps = {hc->fast_eps, hc->fast_eps};
+                const f32x2 decay = hc->decay, w1 = hc->w1, b2 = hc->b2, ibc = hc->ibc, eps = hc->eps;
 #pragma unroll
                 for (int i = 0; i < V; ++i) {
 #pragma unroll
@@ -702,8 +725,8 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
                         P = P * decay;
                         M = __builtin_elementwise_fma(w1, -M, M);
                         Q = Q * b2;
-                        const f32x2 S = {__builtin_amdgcn_sqrtf(Q.x), __builtin_amdgcn_sqrtf(Q.y)};
-                        const f32x2 Dn = __builtin_elementwise_fma(S, ibc, eps);
+                        const f32x2 Sq = {__builtin_amdgcn_sqrtf(Q.x), __builtin_amdgcn_sqrtf(Q.y)};
+                        const f32x2 Dn = __builtin_elementwise_fma(Sq, ibc, eps);
                         const f32x2 R = {__builtin_amdgcn_rcpf(Dn.x), __builtin_amdgcn_rcpf(Dn.y)};
                         P = __builtin_elementwise_fma(M, R, P);
                         if (half) {
@@ -714,19 +737,20 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
                     }
                 }
             }
-        }
-        for (; hc != hend; ++hc) {
-            AdamConsts c;
-            c.decay = hc->decay, c.w1 = hc->w1, c.b2 = hc->b2, c.eps = hc->eps, c.neg_step = hc->neg_step;
-            c.bc2_sqrt = hc->bc2_sqrt, c.inv_bc2_sqrt = hc->inv_bc2_sqrt, c.wd = hc->wd, c.w2 = hc->w2;
-            c.fast_ibc = hc->fast_ibc, c.fast_eps = hc->fast_eps;
-            c.decoupled = DECOUPLED ? 1 : 0, c.fast_g0 = FAST ? 1 : 0;
+        } else {
+            for (; hc != hend; ++hc) {
+                AdamConsts c;
+                c.decay = hc->decay, c.w1 = hc->w1, c.b2 = hc->b2, c.eps = hc->eps, c.neg_step = hc->neg_step;
+                c.bc2_sqrt = hc->bc2_sqrt, c.inv_bc2_sqrt = hc->inv_bc2_sqrt, c.wd = hc->wd, c.w2 = hc->w2;
+                c.fast_ibc = hc->fast_ibc, c.fast_eps = hc->fast_eps;
+                c.decoupled = DECOUPLED ? 1 : 0, c.fast_g0 = FAST ? 1 : 0;
 #pragma unroll
-            for (int i = 0; i < V; ++i) {
-                adam_elem_t<DECOUPLED, true, FAST>(p[i].x, m[i].x, v[i].x, 0.f, c);
-                adam_elem_t<DECOUPLED, true, FAST>(p[i].y, m[i].y, v[i].y, 0.f, c);
-                adam_elem_t<DECOUPLED, true, FAST>(p[i].z, m[i].z, v[i].z, 0.f, c);
-                adam_elem_t<DECOUPLED, true, FAST>(p[i].w, m[i].w, v[i].w, 0.f, c);
+                for (int i = 0; i < V; ++i) {
+                    adam_elem_t<DECOUPLED, true, FAST>(p[i].x, m[i].x, v[i].x, 0.f, c);
+                    adam_elem_t<DECOUPLED, true, FAST>(p[i].y, m[i].y, v[i].y, 0.f, c);
+                    adam_elem_t<DECOUPLED, true, FAST>(p[i].z, m[i].z, v[i].z, 0.f, c);
+                    adam_elem_t<DECOUPLED, true, FAST>(p[i].w, m[i].w, v[i].w, 0.f, c);
+                }
             }
         }
 #pragma unroll

@@ -31,6 +31,7 @@ constexpr int kRQ = 64;      // queries per block
 constexpr int kRI = 64;      // items per tile
 constexpr int kRCap = 256;   // candidate slots per query: k + kRI <= kRCap
 constexpr int kMergeJ = 8;   // merge: up to 64 * 8 = 512 candidates per query
+constexpr int kLinearBlocked = 64;  // blocked lists up to this long: one wave-wide scan
 
 __device__ __forceinline__ bool better(float sa, int ia, float sb, int ib) {
     return sa > sb || (sa == sb && (unsigned)ia < (unsigned)ib);
@@ -85,7 +86,8 @@ __device__ void wave_bitonic_sort(float (&s)[J], int (&id)[J]) {
 // list (bval[blo, bhi), sorted; the split kernel defers the blocked test to here) candidates on
 // it are dropped first: the wave loads the list 64 values at a time and every lane compares its
 // four candidates against each value (one load round trip per 64 blocked items, instead of a
-// dependent binary search per inserted candidate).
+// dependent binary search per inserted candidate); lists longer than kLinearBlocked take one
+// lower-bound search per candidate instead (cost log n, not n / 64 x 64).
 __device__ int compact_core(float* __restrict__ bs, int* __restrict__ bi, int q, int n, int k, float* out_s,
                              int* out_i, int out_k, const int64_t* __restrict__ bval, int64_t blo, int64_t bhi,
                              float& tau_out) {
@@ -98,7 +100,35 @@ __device__ int compact_core(float* __restrict__ bs, int* __restrict__ bi, int q,
         s[j] = e < n ? bs[q * kRCap + e] : -INFINITY;
         id[j] = e < n ? bi[q * kRCap + e] : -1;
     }
-    if (bhi > blo) {
+    if (bhi - blo > kLinearBlocked) {
+        // a long list (a heavy user's history): a branchless lower bound per candidate, the four
+        // searches of a lane interleaved — log2(n) rounds of four independent L2-resident loads
+        // instead of n / 64 rounds of 64 compares per candidate.  The trip count depends on n
+        // only, so the wave stays converged.
+        int64_t base[4];
+        const int64_t cnt = bhi - blo;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) base[j] = blo;
+        for (int64_t len = cnt; len > 1;) {
+            const int64_t half = len >> 1;
+            int64_t b[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = bval[base[j] + half];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) base[j] = b[j] <= (int64_t)id[j] ? base[j] + half : base[j];
+            len -= half;
+        }
+        int kept = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (id[j] >= 0 && bval[base[j]] == (int64_t)id[j]) {
+                s[j] = -INFINITY;
+                id[j] = -1;
+            }
+            kept += __popcll(__ballot(lane * 4 + j < n && id[j] >= 0));
+        }
+        n = kept;
+    } else if (bhi > blo) {
         bool drop[4] = {false, false, false, false};
         for (int64_t c0 = blo; c0 < bhi; c0 += 64) {
             const int64_t v = c0 + lane < bhi ? bval[c0 + lane] : int64_t(-1);
