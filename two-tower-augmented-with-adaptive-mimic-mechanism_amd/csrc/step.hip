@@ -726,9 +726,13 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
 
 // ---- backward ------------------------------------------------------------------------------
 // wg_events (optional, 2 events): around the wide weight-gradient GEMM launch (bench)
+// part BWD_GATE: the fusion's backward (dEF, the ID rows' gradient with it); BWD_MLP: the feature
+// MLP's dgrad chain and every weight gradient
+enum { BWD_GATE = 1, BWD_MLP = 2, BWD_ALL = 3 };
 int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s, int ntowers,
-                   void* const* wg_events = nullptr) {
+                   void* const* wg_events = nullptr, int part = BWD_ALL) {
     int rc;
+    if (part & BWD_GATE) {
     // gate: dq, dz, dEF
     GateArgs ga;
     const bool fused_gate = gate_group(T, W, ntowers, D, false, ga);
@@ -797,6 +801,8 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
     }
     if ((rc = b1.run(s))) return rc;
     if ((rc = b2.run(s))) return rc;
+    }
+    if (!(part & BWD_MLP)) return TTAMM_OK;
     // MLP dgrad chain (layers L-1 .. 1)
     int maxL = 0;
     for (int k = 0; k < ntowers; ++k)
@@ -1109,24 +1115,27 @@ int tower_prepare(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred& 
 // Fork / join events of the aux stream, one set per host thread and device (reused across
 // steps: a wait binds to the record that precedes it).  [0] fork, [1] rows current (before the
 // fusion), [2] rows grouped (before the table updates), [3] main stream at the table updates
-// (the late slice's start).
-int aux_events(hipEvent_t ev[4]) {
+// (the late slice's start), [4] main stream after the fusion backward (the row updates' start
+// on the aux stream), [5] aux stream after the row updates (joined at the step's end).
+constexpr int kAuxEvents = 6;
+int aux_events(hipEvent_t ev[kAuxEvents]) {
     struct Set {
         int dev;
-        hipEvent_t e[4];
+        hipEvent_t e[kAuxEvents];
     };
     thread_local std::vector<Set> cache;
     int dev = 0;
     TTAMM_HIP(hipGetDevice(&dev));
     for (const Set& p : cache)
         if (p.dev == dev) {
-            for (int i = 0; i < 4; ++i) ev[i] = p.e[i];
+            for (int i = 0; i < kAuxEvents; ++i) ev[i] = p.e[i];
             return TTAMM_OK;
         }
-    Set p{dev, {nullptr, nullptr, nullptr, nullptr}};
-    for (int i = 0; i < 4; ++i) TTAMM_HIP(hipEventCreateWithFlags(&p.e[i], hipEventDisableTiming));
+    Set p;
+    p.dev = dev;
+    for (int i = 0; i < kAuxEvents; ++i) TTAMM_HIP(hipEventCreateWithFlags(&p.e[i], hipEventDisableTiming));
     cache.push_back(p);
-    for (int i = 0; i < 4; ++i) ev[i] = p.e[i];
+    for (int i = 0; i < kAuxEvents; ++i) ev[i] = p.e[i];
     return TTAMM_OK;
 }
 
@@ -1159,7 +1168,7 @@ int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_b
     }
     // The MLP launches are enqueued first: the prologue is a dozen small launches whose
     // host-side enqueue would otherwise hold the GEMMs back behind the host.
-    hipEvent_t ev[4];
+    hipEvent_t ev[kAuxEvents];
     if ((rc = aux_events(ev))) return rc;
     // bf16 towers: the prologue starts after the first layer's GEMM (its one-block-per-CU tiles
     // otherwise wait for CUs behind the catch-up replay); fp32 towers: at once
@@ -1190,7 +1199,7 @@ int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_b
 // the row updates need the grouping (prepare part B), possibly still running on the aux stream
 int join_grouping(hipStream_t s, hipStream_t aux) {
     if (aux == nullptr || aux == s) return TTAMM_OK;
-    hipEvent_t ev[4];
+    hipEvent_t ev[kAuxEvents];
     int rc;
     if ((rc = aux_events(ev))) return rc;
     TTAMM_HIP(hipStreamWaitEvent(s, ev[2], 0));
@@ -1271,7 +1280,7 @@ int table_updates(const ttamm_tower* T[2], TowerWs* W[2], int n, int D, bool mim
         // the previous step's slice (target step - 1, as in prepare_forward), started on the aux
         // stream now: the catch-up and the grouping before it on that stream, the row updates
         // beside it (the rows they touch are current to step - 1, so the slice skips them)
-        hipEvent_t ev[4];
+        hipEvent_t ev[kAuxEvents];
         if ((rc = aux_events(ev))) return rc;
         TTAMM_HIP(hipEventRecord(ev[3], s));
         TTAMM_HIP(hipStreamWaitEvent(aux, ev[3], 0));
@@ -1800,10 +1809,32 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         }
         if (!shard) {
             // ---- the whole backward + optimizers in one process --------------------------------
-            if ((rc = tower_backward(T, W, D, s, 2, A.timing_events + 6))) return rc;
-            if (ws.clip_on && (rc = clip_coefficient(T, W, D, mimic, sp, ad, df, A, ws, s, aux))) return rc;
-            if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, s, aux, ws.clip_coef))) return rc;
-            return dense_update(T, W, ad, A.status, s, ws.clip_coef);
+            // With the aux stream (no clipping: the table updates would wait for the global norm)
+            // the touched-row updates run there once the fusion backward has formed the ID and
+            // mimic rows' gradients, beside the MLP's dgrad chain and weight gradients (memory-
+            // bound row traffic under MFMA-bound GEMMs); the step's end joins them, so the next
+            // step's ID-row gather reads the updated rows.  TTAMM_ROWS_MAIN=1: on the main stream.
+            static const bool rows_main = std::getenv("TTAMM_ROWS_MAIN") != nullptr;
+            const bool rows_aux = !ws.clip_on && !rows_main && aux != nullptr && aux != s && overlapped(T, 2, df, s, aux);
+            if (!rows_aux) {
+                if ((rc = tower_backward(T, W, D, s, 2, A.timing_events + 6))) return rc;
+                if (ws.clip_on && (rc = clip_coefficient(T, W, D, mimic, sp, ad, df, A, ws, s, aux))) return rc;
+                if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, s, aux, ws.clip_coef)))
+                    return rc;
+                return dense_update(T, W, ad, A.status, s, ws.clip_coef);
+            }
+            hipEvent_t ev[kAuxEvents];
+            if ((rc = aux_events(ev))) return rc;
+            if ((rc = tower_backward(T, W, D, s, 2, nullptr, BWD_GATE))) return rc;
+            TTAMM_HIP(hipEventRecord(ev[4], s));
+            TTAMM_HIP(hipStreamWaitEvent(aux, ev[4], 0));
+            // on the aux stream: the grouping before it there already, so no join
+            if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, aux, aux))) return rc;
+            TTAMM_HIP(hipEventRecord(ev[5], aux));
+            if ((rc = tower_backward(T, W, D, s, 2, A.timing_events + 6, BWD_MLP))) return rc;
+            if ((rc = dense_update(T, W, ad, A.status, s))) return rc;
+            TTAMM_HIP(hipStreamWaitEvent(s, ev[5], 0));
+            return TTAMM_OK;
         }
         if (ph & TTAMM_PHASE_USER) {
             if ((rc = tower_backward(T, W, D, s, 1))) return rc;

@@ -223,11 +223,11 @@ class MirrorComm:
         W, me = self.world, self.rank
         if isinstance(req, AllToAll):
             chunks = list(torch.split(req.send, req.send_splits))
-            got = torch.cat([chunks[(2 * me - s) % W] for s in range(W)])
-            if got.shape[0] != sum(req.recv_splits):
+            parts = [chunks[(2 * me - s) % W] for s in range(W)]
+            if sum(p.shape[0] for p in parts) != sum(req.recv_splits):
                 raise RuntimeError("mirror: recv splits do not match the mirrored sends")
-            if req.out is not None:
-                got = req.out.copy_(got)
+            # one pass into the receive buffer, as an all-to-all writes it
+            got = torch.cat(parts, out=req.out) if req.out is not None else torch.cat(parts)
             return (None, got) if req.async_op else got
         if isinstance(req, Wait):
             return req.handle[1]
