@@ -1112,27 +1112,30 @@ int tower_prepare(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred& 
     return tower_prepare_b(t, w, s);
 }
 
-// Fork / join events of the aux stream, one set per host thread and device (reused across
-// steps: a wait binds to the record that precedes it).  [0] fork, [1] rows current (before the
+// Fork / join events of the aux stream, one set per host thread, device and aux stream (reused
+// across steps: a wait binds to the record that precedes it; per aux stream, so the engines of
+// in-process ranks — each with its own aux stream — never wait on one another's records).  [0] fork, [1] rows current (before the
 // fusion), [2] rows grouped (before the table updates), [3] main stream at the table updates
 // (the late slice's start), [4] main stream after the fusion backward (the row updates' start
 // on the aux stream), [5] aux stream after the row updates (joined at the step's end).
 constexpr int kAuxEvents = 6;
-int aux_events(hipEvent_t ev[kAuxEvents]) {
+int aux_events(hipEvent_t ev[kAuxEvents], hipStream_t aux) {
     struct Set {
         int dev;
+        hipStream_t aux;
         hipEvent_t e[kAuxEvents];
     };
     thread_local std::vector<Set> cache;
     int dev = 0;
     TTAMM_HIP(hipGetDevice(&dev));
     for (const Set& p : cache)
-        if (p.dev == dev) {
+        if (p.dev == dev && p.aux == aux) {
             for (int i = 0; i < kAuxEvents; ++i) ev[i] = p.e[i];
             return TTAMM_OK;
         }
     Set p;
     p.dev = dev;
+    p.aux = aux;
     for (int i = 0; i < kAuxEvents; ++i) TTAMM_HIP(hipEventCreateWithFlags(&p.e[i], hipEventDisableTiming));
     cache.push_back(p);
     for (int i = 0; i < kAuxEvents; ++i) ev[i] = p.e[i];
@@ -1169,7 +1172,7 @@ int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_b
     // The MLP launches are enqueued first: the prologue is a dozen small launches whose
     // host-side enqueue would otherwise hold the GEMMs back behind the host.
     hipEvent_t ev[kAuxEvents];
-    if ((rc = aux_events(ev))) return rc;
+    if ((rc = aux_events(ev, aux))) return rc;
     // bf16 towers: the prologue starts after the first layer's GEMM (its one-block-per-CU tiles
     // otherwise wait for CUs behind the catch-up replay); fp32 towers: at once
     const bool late_fork = T[0]->matmul_bf16 && std::getenv("TTAMM_EARLY_FORK") == nullptr;
@@ -1201,7 +1204,7 @@ int join_grouping(hipStream_t s, hipStream_t aux) {
     if (aux == nullptr || aux == s) return TTAMM_OK;
     hipEvent_t ev[kAuxEvents];
     int rc;
-    if ((rc = aux_events(ev))) return rc;
+    if ((rc = aux_events(ev, aux))) return rc;
     TTAMM_HIP(hipStreamWaitEvent(s, ev[2], 0));
     return TTAMM_OK;
 }
@@ -1281,7 +1284,7 @@ int table_updates(const ttamm_tower* T[2], TowerWs* W[2], int n, int D, bool mim
         // stream now: the catch-up and the grouping before it on that stream, the row updates
         // beside it (the rows they touch are current to step - 1, so the slice skips them)
         hipEvent_t ev[kAuxEvents];
-        if ((rc = aux_events(ev))) return rc;
+        if ((rc = aux_events(ev, aux))) return rc;
         TTAMM_HIP(hipEventRecord(ev[3], s));
         TTAMM_HIP(hipStreamWaitEvent(aux, ev[3], 0));
         if ((rc = replay_slice(T, n, mimic, df, df.step - 1, 2, events, aux))) return rc;
@@ -1824,7 +1827,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
                 return dense_update(T, W, ad, A.status, s, ws.clip_coef);
             }
             hipEvent_t ev[kAuxEvents];
-            if ((rc = aux_events(ev))) return rc;
+            if ((rc = aux_events(ev, aux))) return rc;
             if ((rc = tower_backward(T, W, D, s, 2, nullptr, BWD_GATE))) return rc;
             TTAMM_HIP(hipEventRecord(ev[4], s));
             TTAMM_HIP(hipStreamWaitEvent(aux, ev[4], 0));
@@ -1843,17 +1846,32 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     }
     // ---- grouped: both towers' backward and table updates ------------------------------------
     if (ph & TTAMM_PHASE_TOWERS_BWD) {
-        if (I.R > 0) {
-            if ((rc = tower_backward(T, W, D, s, 2, A.timing_events + 6))) return rc;
+        static const bool rows_main = std::getenv("TTAMM_ROWS_MAIN") != nullptr;
+        if (I.R > 0 && !ws.clip_on && !rows_main && aux != nullptr && aux != s && overlapped(T, 2, df, s, aux)) {
+            // as in one process: the touched-row updates on the aux stream beside the MLP backward,
+            // joined before this phase ends (the caller's all-reduce and DENSE follow)
+            hipEvent_t ev[kAuxEvents];
+            if ((rc = aux_events(ev, aux))) return rc;
+            if ((rc = tower_backward(T, W, D, s, 2, nullptr, BWD_GATE))) return rc;
+            TTAMM_HIP(hipEventRecord(ev[4], s));
+            TTAMM_HIP(hipStreamWaitEvent(aux, ev[4], 0));
+            if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, aux, aux))) return rc;
+            TTAMM_HIP(hipEventRecord(ev[5], aux));
+            if ((rc = tower_backward(T, W, D, s, 2, A.timing_events + 6, BWD_MLP))) return rc;
+            TTAMM_HIP(hipStreamWaitEvent(s, ev[5], 0));
         } else {
-            if ((rc = tower_backward(T, W, D, s, 1))) return rc;
-            const size_t n = tower_grad_floats(A.item);
-            if (n) TTAMM_HIP(hipMemsetAsync(I.gw[0] ? I.gw[0] : I.ggw[0], 0, n * sizeof(float), s));
-        }
-        if (ws.clip_on) {  // the table updates wait for the global norm (TABLES, after the all-reduce)
-            if ((rc = clip_table_share(T, W, D, mimic, sp, ad, df, A, ws, s, aux))) return rc;
-        } else if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, s, aux))) {
-            return rc;
+            if (I.R > 0) {
+                if ((rc = tower_backward(T, W, D, s, 2, A.timing_events + 6))) return rc;
+            } else {
+                if ((rc = tower_backward(T, W, D, s, 1))) return rc;
+                const size_t n = tower_grad_floats(A.item);
+                if (n) TTAMM_HIP(hipMemsetAsync(I.gw[0] ? I.gw[0] : I.ggw[0], 0, n * sizeof(float), s));
+            }
+            if (ws.clip_on) {  // the table updates wait for the global norm (TABLES, after the all-reduce)
+                if ((rc = clip_table_share(T, W, D, mimic, sp, ad, df, A, ws, s, aux))) return rc;
+            } else if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, s, aux))) {
+                return rc;
+            }
         }
     }
     // ---- sharded clipping: the deferred table updates, scaled by clip_grad_norm_'s coefficient --
