@@ -515,12 +515,13 @@ bool gate_group(const ttamm_tower* const* T, TowerWs* const* W, int ntowers, int
 }
 
 // ---- forward -------------------------------------------------------------------------------
-// part FWD_MLP: ID-row gather + feature encoder; FWD_FUSION: gate / combine (reads the mimic rows)
-enum { FWD_MLP = 1, FWD_FUSION = 2, FWD_ALL = 3 };
+// part FWD_GATHER: ID-row renorm + gather; FWD_FEAT: feature encoder; FWD_FUSION: gate / combine
+// (reads the mimic rows)
+enum { FWD_GATHER = 1, FWD_FUSION = 2, FWD_FEAT = 4, FWD_MLP = FWD_GATHER | FWD_FEAT, FWD_ALL = 7 };
 int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt, int D, bool mimic, hipStream_t s,
                   int ntowers, void* const* l0_events = nullptr, int part = FWD_ALL, hipEvent_t after_l0 = nullptr) {
     int rc;
-    if (part & FWD_MLP) {
+    if (part & FWD_GATHER) {
         // ID rows -> e (ef[:, :D] when gated): both towers' gathers in one launch
         GatherSegs gs;
         gs.count = 0;
@@ -547,14 +548,21 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
             float* dst = uses_ef(t) ? w.ef : w.e;
             const int64_t ld = uses_ef(t) ? efw(t) : t.id.dim;
             gs.seg[gs.count++] = GatherSeg{t.id.weight, t.id.rows, t.id.dim, w.idx, w.R, dst, ld};
+        }
+        if ((rc = launch_gather_rows_segs(gs, s))) return rc;
+    }
+    if (part & FWD_FEAT) {
+        for (int k = 0; k < ntowers; ++k) {
+            const ttamm_tower& t = *T[k];
+            TowerWs& w = *W[k];
             if (t.fusion != TTAMM_FUSION_IDENTITY && t.n_linear == 0 && w.R > 0) {
                 // identity feature encoder (encoders.py:114-119): f = the feature row
+                const int64_t ld = uses_ef(t) ? efw(t) : t.id.dim;
                 float* fdst = uses_ef(t) ? w.ef + t.id.dim : w.f;
                 if ((rc = launch_add_rows(t.features, t.feat_ld, nullptr, 0, w.R, fo_dim(t), fdst, ld, s, w.fidx)))
                     return rc;
             }
         }
-        if ((rc = launch_gather_rows_segs(gs, s))) return rc;
         // feature encoder layers
         int maxL = 0;
         for (int k = 0; k < ntowers; ++k)
@@ -1176,9 +1184,16 @@ int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_b
     // bf16 towers: the prologue starts after the first layer's GEMM (its one-block-per-CU tiles
     // otherwise wait for CUs behind the catch-up replay); fp32 towers: at once
     const bool late_fork = T[0]->matmul_bf16 && std::getenv("TTAMM_EARLY_FORK") == nullptr;
+    // fp32 towers: the ID-row gather also runs on the aux stream (ahead of the catch-up), beside the
+    // first-layer GEMM, which reads only the feature rows; the fusion joins it with the catch-up
+    static const bool gather_main = std::getenv("TTAMM_GATHER_MAIN") != nullptr;
+    const bool gather_aux = !late_fork && !gather_main;
     if (!late_fork) TTAMM_HIP(hipEventRecord(ev[0], s));
-    if ((rc = tower_forward(T, W, bt, D, mimic, s, n, l0_events, FWD_MLP, late_fork ? ev[0] : nullptr))) return rc;
+    if ((rc = tower_forward(T, W, bt, D, mimic, s, n, l0_events, gather_aux ? FWD_FEAT : FWD_MLP,
+                            late_fork ? ev[0] : nullptr)))
+        return rc;
     TTAMM_HIP(hipStreamWaitEvent(aux, ev[0], 0));
+    if (gather_aux && (rc = tower_forward(T, W, bt, D, mimic, aux, n, nullptr, FWD_GATHER))) return rc;
     if ((rc = towers_prepare_a(T, W, n, mimic, df, aux, cu_ev(0)))) return rc;
     TTAMM_HIP(hipEventRecord(ev[1], aux));
     // the fusion is enqueued before the grouping's dozen launches: enqueued after them, the host
