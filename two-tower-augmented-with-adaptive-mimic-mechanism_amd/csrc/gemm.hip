@@ -1592,10 +1592,16 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
     }
     int rc;
     const bool timed = ev && ev[0] && ev[1] && wide.count > 0;
+    // The narrow launch (latency-bound: many short splits) first, then the wide one (MFMA-bound),
+    // which the aux stream's memory-bound row updates then run beside: C2 0.660 -> 0.652 ms,
+    // the emulated 8-rank C2 0.804 -> 0.769 ms (profiles/r04_wgrad_order_s22.txt).
+    // TTAMM_WGRAD_WIDE_FIRST=1: the old order.
+    static const bool narrow_first = std::getenv("TTAMM_WGRAD_WIDE_FIRST") == nullptr;
+    if (narrow_first && (rc = flush(narrow, false))) return rc;
     if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)ev[0], s));
     if ((rc = flush(wide, true))) return rc;
     if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)ev[1], s));
-    if ((rc = flush(narrow, false))) return rc;
+    if (!narrow_first && (rc = flush(narrow, false))) return rc;
     if (total > 0) {
         hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, s, wb, total);
         TTAMM_LAUNCH_CHECK();
