@@ -485,7 +485,9 @@ def main() -> None:
     exact_mfma = os.environ.get("TTAMM_FP32_MFMA") == "exact"
     mfma_peak = MFMA_BF16_PEAK_TFLOPS if bf16 else MFMA_FP32_PEAK_TFLOPS
     split_ceiling = None if (bf16 or exact_mfma) else MFMA_BF16_PEAK_TFLOPS / 6.0  # six bf16 MFMAs per product
-    traffic = load_traffic(args.config) or {}
+    # PMC entry: the config's own, or "<config>_inbatch" when in-batch negatives replace its sampled ones
+    tkey = args.config + ("_inbatch" if in_batch and CONFIGS[args.config].get("negatives", "sampled") != "in-batch" else "")
+    traffic = load_traffic(tkey) or {}
     # tower rows of one step: users B; items B (1 + N) (one process) or the owner's requested rows
     if not sharded:
         item_rows = B * (1 + N)

@@ -83,6 +83,14 @@ def main() -> None:
     tf = flops / (ms * 1e-3) / 1e12
     cpu = (cpu_baseline(items[: ni].cpu().numpy(), queries[: args.cpu_queries].cpu().numpy(), k)
            if args.cpu_queries > 0 else None)
+    # HBM bytes per launch of the scan kernel from the committed rocprofv3 PMC passes
+    # (profiles/pmc_traffic.json "c3", tools/gpu/pmc_c3.sh), at the default C3 shape only
+    traffic = None
+    if (nq, ni, D, k, nb) == (65536, 2_000_000, 96, 80, 20):
+        try:
+            traffic = json.loads((ROOT / "profiles" / "pmc_traffic.json").read_text())["c3"]["retrieval_bytes_per_launch"]
+        except (OSError, ValueError, KeyError):
+            traffic = None
     print(json.dumps({
         "metric": "C3 exact-IP retrieval top-K (queries/s)",
         "value": round(nq / (ms * 1e-3), 1),
@@ -94,7 +102,8 @@ def main() -> None:
                       "achieved": round(tf, 2), "peak": round(SPLIT_BF16_CEILING_TFLOPS, 1), "unit": "TFLOP/s",
                       "frac": round(tf / SPLIT_BF16_CEILING_TFLOPS, 4),
                       "peak_basis": "dense bf16 MFMA peak / 6 (six bf16 products per fp32 product)",
-                      "vs_fp32_mfma_peak": round(tf / MFMA_FP32_PEAK_TFLOPS, 4), "algorithmic_flops": flops}
+                      "vs_fp32_mfma_peak": round(tf / MFMA_FP32_PEAK_TFLOPS, 4), "algorithmic_flops": flops,
+                      "traffic": traffic}
                      if split else
                      {"bound": "mfma", "kernel": "retrieval_partial_kernel + retrieval_merge_kernel (fp32 MFMA)",
                       "achieved": round(tf, 2), "peak": MFMA_FP32_PEAK_TFLOPS, "unit": "TFLOP/s",

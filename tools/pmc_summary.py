@@ -57,7 +57,7 @@ def main() -> None:
 
     import bench as B  # the config's shapes
 
-    c = B.CONFIGS[config]
+    c = B.CONFIGS[config.split("_")[0]]  # "c2_inbatch": c2's shapes (bench.py --negatives in-batch)
     kernels = {}
     for k in sorted(set(fetch) | set(write)):
         f = fetch.get(k, [0.0])
