@@ -669,11 +669,12 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
 //   K-major operand:  [16 k][mn] bf16, row stride = 64 or 192 (mod 256) bytes — fragments are
 //                     two ds_read_b64_tr_b16 (hardware transpose: lane i of a 16-lane group gets
 //                     column i of a 4 x 16 block), conflict-free per 32-lane half.
-template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KMAJ_, bool B_KMAJ_, int KT_ = 16>
+template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KMAJ_, bool B_KMAJ_, int KT_ = 16, int AD_ = 2>
 struct XCfg {
     static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_;
     static constexpr bool A_KMAJ = A_KMAJ_, B_KMAJ = B_KMAJ_;
     static constexpr int KT = KT_;     // k per tile: 16 (three planes) or 32 (bf16, one plane)
+    static constexpr int AD = AD_;     // 16-k tiles: A register sets (3: A loads two k-tiles ahead)
     static constexpr int RB = KT * 2;  // MN-major row bytes
     static constexpr int TM = BM / WAVES_M, TN = BN / WAVES_N, I = TM / 32, J = TN / 32;
     static constexpr int A_F4 = BM * KT / 4, B_F4 = BN * KT / 4;
@@ -836,11 +837,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
     // 16-k tiles: two register sets (the tile two ahead in flight); 32-k tiles (bf16): one set
     // (the register budget), loaded at a step's start and written after its MFMAs
     constexpr bool XDEEP = KT == 16;
-    float4 ra[XDEEP ? 2 : 1][CX::A_LOADS], rb[XDEEP ? 2 : 1][CX::B_LOADS];
+    // A3: A in three register sets, loaded two k-tiles ahead (B, L2-resident weights or dY, one)
+    constexpr bool A3 = XDEEP && CX::AD == 3;
+    float4 ra[XDEEP ? (A3 ? 3 : 2) : 1][CX::A_LOADS], rb[XDEEP ? 2 : 1][CX::B_LOADS];
 
     auto mainloop = [&](auto fast_tag) {
         constexpr bool FAST = decltype(fast_tag)::value;
-        auto load_tile = [&](auto S, int k0) {
+        auto load_a = [&](auto S, int k0) {
             constexpr int R = decltype(S)::value;
 #pragma unroll
             for (int it = 0; it < CX::A_LOADS; ++it) {
@@ -853,6 +856,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
                     ra[R][it] = FAST ? *reinterpret_cast<const float4*>(rp + m0 + a_c[it]) : raw4(rp, m0 + a_c[it], P.lda);
                 }
             }
+        };
+        auto load_b = [&](auto S, int k0) {
+            constexpr int R = decltype(S)::value;
 #pragma unroll
             for (int it = 0; it < CX::B_LOADS; ++it) {
                 const int lin = tid + it * kThreads;
@@ -868,9 +874,14 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
                 }
             }
         };
-        // staged item q (A loads first, then B loads) of register set S -> its planes in buffer Buf
-        auto store_item = [&](auto S, auto Buf, int q, int k0) {
-            constexpr int R = decltype(S)::value;
+        auto load_tile = [&](auto S, int k0) {
+            load_a(S, k0);
+            load_b(S, k0);
+        };
+        // staged item q (A loads first, then B loads) of register sets SA (A) / SB (B) -> its
+        // planes in buffer Buf
+        auto store_item2 = [&](auto SA, auto SB, auto Buf, int q, int k0) {
+            constexpr int RA = decltype(SA)::value, RB = decltype(SB)::value;
             unsigned char* Ap = lds + decltype(Buf)::value * CX::buf_bytes(PL);
             unsigned char* Bp = Ap + PL * CX::A_PLANE;
             float4 v;
@@ -880,11 +891,11 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
             if (q < CX::A_LOADS) {
                 const int it = q;
                 if (!AK) {
-                    v = FAST ? ra[R][it] : mask4(ra[R][it], k0 + a_c[it], k_end, P.lda, -1, a_ok[it]);
+                    v = FAST ? ra[RA][it] : mask4(ra[RA][it], k0 + a_c[it], k_end, P.lda, -1, a_ok[it]);
                     off = mn_off<CX::RB>(a_r[it], a_c[it]);
                 } else {
-                    v = FAST ? ra[R][it]
-                             : mask4(ra[R][it], m0 + a_c[it], P.a_cols, P.lda, P.a_ones_col, k0 + a_r[it] < k_end);
+                    v = FAST ? ra[RA][it]
+                             : mask4(ra[RA][it], m0 + a_c[it], P.a_cols, P.lda, P.a_ones_col, k0 + a_r[it] < k_end);
                     off = a_r[it] * CX::SA + a_c[it] * 2;
                 }
                 base = Ap;
@@ -895,11 +906,11 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
                 if (CX::B_F4 % kThreads && lin >= CX::B_F4) return;  // partial last round (BN = 96)
                 if (!BKM) {
                     const int n = n0 + lin / (KT / 4), c = k0 + (lin % (KT / 4)) * 4;
-                    v = FAST ? rb[R][it] : mask4(rb[R][it], c, k_end, P.ldb, -1, n < N);
+                    v = FAST ? rb[RB][it] : mask4(rb[RB][it], c, k_end, P.ldb, -1, n < N);
                     off = mn_off<CX::RB>(lin / (KT / 4), (lin % (KT / 4)) * 4);
                 } else {
                     const int kr = lin / (BN / 4), nc = (lin % (BN / 4)) * 4;
-                    v = FAST ? rb[R][it] : mask4(rb[R][it], n0 + nc, N, P.ldb, -1, k0 + kr < k_end);
+                    v = FAST ? rb[RB][it] : mask4(rb[RB][it], n0 + nc, N, P.ldb, -1, k0 + kr < k_end);
                     off = kr * CX::SB + nc * 2;
                 }
                 base = Bp;
@@ -910,6 +921,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
 #pragma unroll
             for (int pl = 0; pl < PL; ++pl) *reinterpret_cast<uint2*>(base + pl * plane + off) = w[pl];
         };
+        auto store_item = [&](auto S, auto Buf, int q, int k0) { store_item2(S, S, Buf, q, k0); };
         constexpr int NITEMS = CX::A_LOADS + CX::B_LOADS;
         auto store_tile = [&](auto S, auto Buf, int k0) {
 #pragma unroll
@@ -918,7 +930,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
         // multiply the k-tile in buffer Buf; the split + LDS writes of the next k-tile (register
         // set S -> buffer NB) are spread between the MFMA groups so the vector work issues in the
         // matrix pipe's shadow
-        auto compute = [&](auto Buf, auto S, auto NB, int k0n) {
+        auto compute2 = [&](auto Buf, auto SA, auto SB, auto NB, int k0n) {
             const unsigned char* Ap = lds + decltype(Buf)::value * CX::buf_bytes(PL);
             const unsigned char* Bp = Ap + PL * CX::A_PLANE;
             constexpr int NP = I * J, KS = KT / 16, NSLOT = KS * NP;
@@ -950,12 +962,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
                         const int slot = ks * NP + pq;
 #pragma unroll
                         for (int q = (slot * NITEMS) / NSLOT; q < ((slot + 1) * NITEMS) / NSLOT; ++q)
-                            store_item(S, NB, q, k0n);
+                            store_item2(SA, SB, NB, q, k0n);
                     }
 #endif
                 }
             }
         };
+        auto compute = [&](auto Buf, auto S, auto NB, int k0n) { compute2(Buf, S, S, NB, k0n); };
         using S0 = std::integral_constant<int, 0>;
         using S1 = std::integral_constant<int, 1>;
         const int nk = k_end > k_begin ? (k_end - k_begin + KT - 1) / KT : 0;
@@ -983,6 +996,44 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
                 sstep(S1{}, S0{}, kt + 1);
             }
             if (kt < nk) sstep(S0{}, S1{}, kt);
+        } else if constexpr (A3) {
+            // k-tile kt (i = kt mod 6): LDS buffer i & 1; A register set i mod 3, B set i & 1.  Step
+            // kt loads A of kt + 3 into the A set tile kt left and B of kt + 2 into the B set tile kt
+            // left (both already in LDS), multiplies kt while splitting kt + 1 (A set (i + 1) mod 3,
+            // B set (i + 1) & 1) into the other buffer: A two k-tiles ahead, B one.
+            using S2 = std::integral_constant<int, 2>;
+            load_tile(S0{}, kof(0));
+            store_tile(S0{}, S0{}, kof(0));
+            load_tile(S1{}, kof(1));
+            load_a(S2{}, kof(2));
+            __syncthreads();
+            auto step3 = [&](auto I6, int kt) {
+                constexpr int i = decltype(I6)::value;
+                using Buf = std::integral_constant<int, i & 1>;
+                using NB = std::integral_constant<int, (i + 1) & 1>;
+                using LA = std::integral_constant<int, i % 3>;
+                using SA = std::integral_constant<int, (i + 1) % 3>;
+#if TTAMM_X_ABLATE != 3
+                load_a(LA{}, kof(kt + 3));
+                load_b(Buf{}, kof(kt + 2));
+#endif
+                compute2(Buf{}, SA{}, NB{}, NB{}, kof(kt + 1));
+                __syncthreads();
+            };
+            int kt = 0;
+            for (; kt + 5 < nk; kt += 6) {
+                step3(std::integral_constant<int, 0>{}, kt);
+                step3(std::integral_constant<int, 1>{}, kt + 1);
+                step3(std::integral_constant<int, 2>{}, kt + 2);
+                step3(std::integral_constant<int, 3>{}, kt + 3);
+                step3(std::integral_constant<int, 4>{}, kt + 4);
+                step3(std::integral_constant<int, 5>{}, kt + 5);
+            }
+            if (kt < nk) step3(std::integral_constant<int, 0>{}, kt);
+            if (kt + 1 < nk) step3(std::integral_constant<int, 1>{}, kt + 1);
+            if (kt + 2 < nk) step3(std::integral_constant<int, 2>{}, kt + 2);
+            if (kt + 3 < nk) step3(std::integral_constant<int, 3>{}, kt + 3);
+            if (kt + 4 < nk) step3(std::integral_constant<int, 4>{}, kt + 4);
         } else {
             load_tile(S0{}, kof(0));
             store_tile(S0{}, S0{}, kof(0));
@@ -1342,10 +1393,20 @@ int dispatch_epi_x(GemmBatch& b, hipStream_t s) {
 }
 // three planes on 16-k tiles (fp32 towers), or one plane on 32-k tiles (bf16 towers: twice the
 // MFMAs per barrier, the same LDS footprint)
+// fp32 towers, forward (weights MN-major): the A operand two k-tiles ahead (three register sets)
+// unless TTAMM_GEMM_ADEEP=2.  Alone the layer-1 forward runs 3 % slower that way (105 -> 108 us,
+// one spilled register), in the step beside the aux stream's gather and catch-up 6 % faster
+// (129 -> 122 us; C2 0.650 -> 0.641-0.644 ms, profiles/r04_gemm_adeep_s29.txt).  dgrad (K-major
+// weights, six k-tiles at C2) keeps two sets.
 template <int BM, int BN, int WM, int WN, bool AK, bool BK>
 int dispatch_x(GemmBatch& b, hipStream_t s) {
-    return b.p[0].bf16 ? dispatch_epi_x<XCfg<BM, BN, WM, WN, AK, BK, 32>, 1>(b, s)
-                       : dispatch_epi_x<XCfg<BM, BN, WM, WN, AK, BK, 16>, 3>(b, s);
+    static const bool adeep2 = [] {
+        const char* e = std::getenv("TTAMM_GEMM_ADEEP");
+        return e && e[0] == '2';
+    }();
+    if (b.p[0].bf16) return dispatch_epi_x<XCfg<BM, BN, WM, WN, AK, BK, 32>, 1>(b, s);
+    if (adeep2 || AK || BK) return dispatch_epi_x<XCfg<BM, BN, WM, WN, AK, BK, 16>, 3>(b, s);
+    return dispatch_epi_x<XCfg<BM, BN, WM, WN, AK, BK, 16, 3>, 3>(b, s);
 }
 
 // Matrix-core path of the fp32 / bf16 GEMMs: the split-bf16 kernel (default), or with
@@ -1460,6 +1521,8 @@ using WgradWide = Cfg<128, 192, 2, 2, true, true>;
 using WgradNarrow = Cfg<128, 96, 4, 1, true, true>;
 using WgradWideX = XCfg<128, 192, 2, 2, true, true>;
 using WgradNarrowX = XCfg<128, 96, 4, 1, true, true>;
+// the narrow launch's X two k-tiles ahead (178 registers; the wide one would spill 38)
+using WgradNarrowXA3 = XCfg<128, 96, 4, 1, true, true, 16, 3>;
 using WgradWideX32 = XCfg<128, 192, 2, 2, true, true, 32>;
 using WgradNarrowX32 = XCfg<128, 96, 4, 1, true, true, 32>;
 int wgrad_slots(bool wide, bool exact) {
@@ -1524,6 +1587,15 @@ size_t wgrad_slab_floats(int R, int M, int N, int rps) {
     return (size_t)splits * M * (N + 1);
 }
 
+// TTAMM_WGRAD_ADEEP=3: the narrow weight-gradient launch's X operand two k-tiles ahead
+static bool wgrad_a3() {
+    static const bool on = [] {
+        const char* e = std::getenv("TTAMM_WGRAD_ADEEP");
+        return e && e[0] == '3';
+    }();
+    return on;
+}
+
 // Weight gradients as C = X^T dY (M = n_in + 1 incl. the ones column, N = m_out, K = rows),
 // both operands K-major; one launch per tile configuration, then one fixed-order reduce.
 int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
@@ -1538,7 +1610,8 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
         if (!exact)
             rc = is_wide ? (bf ? launch_one_x<WgradWideX32, EPI_STORE, 1>(g, s) : launch_one_x<WgradWideX, EPI_STORE, 3>(g, s))
                          : (bf ? launch_one_x<WgradNarrowX32, EPI_STORE, 1>(g, s)
-                               : launch_one_x<WgradNarrowX, EPI_STORE, 3>(g, s));
+                               : wgrad_a3() ? launch_one_x<WgradNarrowXA3, EPI_STORE, 3>(g, s)
+                                            : launch_one_x<WgradNarrowX, EPI_STORE, 3>(g, s));
         else
             rc = is_wide ? (bf ? launch_one<WgradWide, EPI_STORE, true>(g, s) : launch_one<WgradWide, EPI_STORE, false>(g, s))
                          : (bf ? launch_one<WgradNarrow, EPI_STORE, true>(g, s)
