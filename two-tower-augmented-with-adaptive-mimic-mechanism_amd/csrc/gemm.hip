@@ -1494,11 +1494,14 @@ int launch_gemm(GemmBatch& b, hipStream_t s) {
         maxN = p.N > maxN ? p.N : maxN;
     }
     // wide outputs take 128 x 192 tiles unless that leaves most of the chip idle (in-batch steps
-    // have R = 2B rows: C2 in-batch layer 1 is 128 such tiles for 256 CUs); then 128 x 96 tiles,
-    // twice the blocks for a second read of the A rows (TTAMM_GEMM_WIDE_TILES=1 keeps 128 x 192)
+    // have R = 2B rows: C2 in-batch layer 1 is 128 such tiles for 256 CUs), or for dgrad; then
+    // 128 x 96 tiles, twice the blocks for a second read of the A rows (TTAMM_GEMM_WIDE_TILES=1
+    // keeps 128 x 192)
     int64_t wide_tiles = 0;
     for (int i = 0; i < b.count; ++i) wide_tiles += ceil_div(b.p[i].M, 128) * ceil_div(b.p[i].N, 192);
-    const bool narrow_tiles = wide_tiles < 300 && std::getenv("TTAMM_GEMM_WIDE_TILES") == nullptr;
+    // dgrad (K-major weights, K = one layer's width: six k-tiles at C2) is latency-bound: twice the
+    // blocks on 128 x 96 tiles hide more of it (C2 0.638 -> 0.630-0.635 ms, profiles/r04_dgrad_tiles_s31.txt)
+    const bool narrow_tiles = (wide_tiles < 300 || bkn) && std::getenv("TTAMM_GEMM_WIDE_TILES") == nullptr;
     if (!exact_mfma()) {
         if (maxN > 96 && !narrow_tiles) {
             if (bkn) return dispatch_x<128, 192, 2, 2, false, true>(b, s);
