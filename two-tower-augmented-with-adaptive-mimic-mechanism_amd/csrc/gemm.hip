@@ -1590,6 +1590,11 @@ size_t wgrad_slab_floats(int R, int M, int N, int rps) {
     return (size_t)splits * M * (N + 1);
 }
 
+int wgrad_class(int m_out) {
+    static const bool all_narrow = std::getenv("TTAMM_WGRAD_ALL_NARROW") != nullptr;
+    return m_out > 96 && !all_narrow ? 1 : 0;
+}
+
 // TTAMM_WGRAD_ADEEP=3: the narrow weight-gradient launch's X operand two k-tiles ahead
 static bool wgrad_a3() {
     static const bool on = [] {

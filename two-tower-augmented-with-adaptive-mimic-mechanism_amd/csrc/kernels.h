@@ -132,7 +132,9 @@ struct WgradShape {
     int M, N;   // out features, in features
 };
 // tile class of a weight gradient: m_out > 96 runs on the wide tile configuration
-inline int wgrad_class(int m_out) { return m_out > 96 ? 1 : 0; }
+// weight-gradient tile class: 1 = wide (128 x 192 tiles, m_out > 96), 0 = narrow (128 x 96);
+// TTAMM_WGRAD_ALL_NARROW=1 (developer switch) puts every problem in the narrow class
+int wgrad_class(int m_out);
 // rows per split-K chunk for each class ([0] narrow, [1] wide) of a step's weight gradients
 void wgrad_rows_per_split(const WgradShape* shapes, int n, int rps[2]);
 size_t wgrad_slab_floats(int R, int M, int N, int rows_per_split);
