@@ -362,6 +362,9 @@ def main() -> None:
     ap.add_argument("--exact-table-math", action="store_true",
                     help="IEEE sqrt / division for the g = 0 table AdamW updates (bit-identical to torch) "
                          "instead of v_sqrt / v_rcp")
+    ap.add_argument("--kernel-events", choices=["every-step", "none"], default="every-step",
+                    help="none: no per-kernel HIP event pairs in the timed steps (the roofline entries "
+                         "then have no live launch durations; a measurement of the events' own cost)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the step's index-only prologue on the main stream (no aux stream)")
     ap.add_argument("--negatives", choices=["sampled", "in-batch"], default=None,
@@ -451,7 +454,10 @@ def main() -> None:
     marks[0].record()
     for k in range(args.steps):
         # the loader's gather of the next batch (ttamm_epoch_batch) runs inside the timed region
-        step(timing_events=[e.cuda_event for e in evs[k]])
+        if args.kernel_events == "none":
+            step()
+        else:
+            step(timing_events=[e.cuda_event for e in evs[k]])
     marks[1].record()
     # deferred AdamW: the g = 0 updates still owed to untouched rows are part of the K steps' work
     eng.flush()
