@@ -227,6 +227,9 @@ __device__ __forceinline__ bool step_poisoned(const uint32_t* status) {
 int launch_combine(const float* e, int64_t ld_e, const float* f, int64_t ld_f, const float* table,
                    int64_t table_rows, const int64_t* idx, int64_t n, int dim, float* t, float* a, int64_t ld_ta, float* aug,
                    hipStream_t s);
+// generic gated fusion: g = sigmoid(x) in place, t = g e + (1 - g) f, a = table[idx], aug = t + a
+int launch_gate_mix(float* g, const float* ef, const float* table, const int64_t* idx, int64_t n, int dim, float* t,
+                    float* a, int64_t ld_ta, float* aug, hipStream_t s);
 int launch_pad_rows(const float* src, int64_t rows, int cols, int64_t ld_src, float* dst, int ld_dst,
                     hipStream_t s);
 // the same over up to two segments in one launch (the two towers)

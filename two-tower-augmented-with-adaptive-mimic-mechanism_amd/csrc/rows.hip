@@ -700,6 +700,51 @@ int launch_pad_rows_segs(const PadSegs& p, hipStream_t s) {
     return TTAMM_OK;
 }
 
+// The gated fusion's output pass for the generic (two-GEMM) gate: x = the second gate GEMM's
+// pre-activation (bias added, stored in g by an EPI_STORE launch), then per element
+// g = sigmoid(x) (in place), t = g e + (1 - g) f, a = table[idx], aug = t + a (aug may be null:
+// the sharded item owner) — gemm.hip's EPI_GATE_OUT epilogue as a streaming kernel, whose
+// per-row operand loads and four output streams left the GEMM waiting on memory (C5: 187 us,
+// 75 % of its wave-cycles waiting, profiles/r04_s41_c5_sq_counters.txt).  As a pass of its own:
+// C5 1.576 -> 1.566 ms/step, C4 0.958 -> 0.952 (profiles/r04_s42_gate_mix.txt).
+__global__ void gate_mix_kernel(float* __restrict__ g, const float* __restrict__ ef, const float* __restrict__ table,
+                                const int64_t* __restrict__ idx, int64_t n, int dim, float* __restrict__ t,
+                                float* __restrict__ a, int64_t ld_ta, float* __restrict__ aug) {
+    const int d4 = dim / 4;
+    const int64_t total = n * d4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t row = i / d4;
+        const int c = (int)(i - row * d4) * 4;
+        const float4 x = ld4(g + row * dim + c);
+        const float* efr = ef + row * 2 * dim;
+        const float4 ev = ld4(efr + c), fv = ld4(efr + dim + c);
+        const float4 av = table ? ld4(table + idx[row] * (int64_t)dim + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float xs[4] = {x.x, x.y, x.z, x.w}, e4[4] = {ev.x, ev.y, ev.z, ev.w}, f4[4] = {fv.x, fv.y, fv.z, fv.w};
+        const float a4[4] = {av.x, av.y, av.z, av.w};
+        float gg[4], tt[4], uu[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            gg[e] = 1.0f / (1.0f + __expf(-xs[e]));
+            tt[e] = gg[e] * e4[e] + (1.0f - gg[e]) * f4[e];
+            uu[e] = table ? tt[e] + a4[e] : tt[e];
+        }
+        st4(g + row * dim + c, make_float4(gg[0], gg[1], gg[2], gg[3]));
+        st4(t + row * ld_ta + c, make_float4(tt[0], tt[1], tt[2], tt[3]));
+        if (table) st4(a + row * ld_ta + c, av);
+        if (aug) st4(aug + row * dim + c, make_float4(uu[0], uu[1], uu[2], uu[3]));
+    }
+}
+
+int launch_gate_mix(float* g, const float* ef, const float* table, const int64_t* idx, int64_t n, int dim, float* t,
+                    float* a, int64_t ld_ta, float* aug, hipStream_t s) {
+    TTAMM_REQUIRE(dim % 4 == 0 && ld_ta % 4 == 0, "gate mix: dim and ld must be multiples of 4");
+    if (n <= 0) return TTAMM_OK;
+    hipLaunchKernelGGL(gate_mix_kernel, dim3(grid_for(n * (dim / 4))), dim3(256), 0, s, g, ef, table, idx, n, dim, t, a,
+                       ld_ta, aug);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
 int launch_combine(const float* e, int64_t ld_e, const float* f, int64_t ld_f, const float* table,
                    int64_t table_rows, const int64_t* idx, int64_t n, int dim, float* t, float* a, int64_t ld_ta, float* aug,
                    hipStream_t s) {

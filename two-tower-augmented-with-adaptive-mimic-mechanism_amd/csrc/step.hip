@@ -517,6 +517,12 @@ bool gate_group(const ttamm_tower* const* T, TowerWs* const* W, int ntowers, int
 // ---- forward -------------------------------------------------------------------------------
 // part FWD_GATHER: ID-row renorm + gather; FWD_FEAT: feature encoder; FWD_FUSION: gate / combine
 // (reads the mimic rows)
+// TTAMM_GATE_OUT_EPILOGUE=1: the generic gate's sigmoid mix / mimic augment in the second gate
+// GEMM's epilogue (EPI_GATE_OUT) instead of gate_mix_kernel after an EPI_STORE launch
+bool gate_out_epilogue() {
+    static const bool on = std::getenv("TTAMM_GATE_OUT_EPILOGUE") != nullptr;
+    return on;
+}
 enum { FWD_GATHER = 1, FWD_FUSION = 2, FWD_FEAT = 4, FWD_MLP = FWD_GATHER | FWD_FEAT, FWD_ALL = 7 };
 int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt, int D, bool mimic, hipStream_t s,
                   int ntowers, void* const* l0_events = nullptr, int part = FWD_ALL, hipEvent_t after_l0 = nullptr) {
@@ -699,18 +705,24 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
             q.N = D;
             q.K = Hg;
             q.bias = t.gate[1].bias;
-            q.epi = EPI_GATE_OUT;
-            q.C = w.aug;
-            q.ldc = D;
-            q.aux0 = w.ef;
-            q.ld_aux0 = 2 * D;
-            q.out1 = w.g;
-            q.out2 = w.t;
-            q.out3 = w.a;
-            q.table = table;
-            q.idx = w.idx;
-            q.ld_out = D;
-            q.ld_out2 = w.t_ld;
+            if (gate_out_epilogue()) {  // TTAMM_GATE_OUT_EPILOGUE=1: the mix in the GEMM's epilogue
+                q.epi = EPI_GATE_OUT;
+                q.C = w.aug;
+                q.ldc = D;
+                q.aux0 = w.ef;
+                q.ld_aux0 = 2 * D;
+                q.out1 = w.g;
+                q.out2 = w.t;
+                q.out3 = w.a;
+                q.table = table;
+                q.idx = w.idx;
+                q.ld_out = D;
+                q.ld_out2 = w.t_ld;
+            } else {  // the pre-activation into g; gate_mix_kernel below (rows.hip)
+                q.epi = EPI_STORE;
+                q.C = w.g;
+                q.ldc = D;
+            }
             g2.add(q);
         } else {
             if ((rc = launch_combine(w.e, D, t.fusion == TTAMM_FUSION_SUM ? w.f : nullptr, D, table, t.mimic.rows, w.idx,
@@ -720,6 +732,15 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
     }
     if ((rc = g1.run(s))) return rc;
     if ((rc = g2.run(s))) return rc;
+    if (!gate_out_epilogue() && !fused_gate) {
+        for (int k = 0; k < ntowers; ++k) {
+            const ttamm_tower& t = *T[k];
+            TowerWs& w = *W[k];
+            if (t.fusion != TTAMM_FUSION_GATED) continue;
+            if ((rc = launch_gate_mix(w.g, w.ef, mimic ? t.mimic.weight : nullptr, w.idx, w.R, D, w.t, w.a, w.t_ld, w.aug, s)))
+                return rc;
+        }
+    }
     if ((rc = gc.run(s))) return rc;
     for (int k = 0; k < ntowers; ++k) {  // concat: a = A[idx], aug = t + a (in place on t)
         const ttamm_tower& t = *T[k];
