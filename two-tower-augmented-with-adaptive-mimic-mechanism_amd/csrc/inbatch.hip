@@ -828,9 +828,15 @@ void inbatch_plan(int64_t B, int64_t Bc, InBatchArgs& a) {
     const int rows = inbatch_pipelined() ? kIbRows : 32 * inbatch_waves();
     a.rblk_u = (int)ceil_div(B, rows);
     a.rblk_p = (int)ceil_div(Bc, rows);
-    // ~4 waves per SIMD over both roles: split the columns so each role has >= ~512 blocks of 4
-    // waves (>= ~256 of 8)
-    const int64_t want = rows == 128 ? 512 : 256;
+    // ~256 blocks per role (one resident round over both roles at two blocks per CU, each block
+    // twice the columns of the former 512: C4 0.952 -> 0.924 ms/step, C2 in-batch 0.658 -> 0.625,
+    // the C4 rank-of-8 shape unchanged, profiles/r04_s43_inbatch_blocks.txt); developer knob
+    // TTAMM_IB_BLOCKS = blocks per role
+    static const int64_t want_env = [] {
+        const char* e = std::getenv("TTAMM_IB_BLOCKS");
+        return e ? (int64_t)std::atoi(e) : (int64_t)0;
+    }();
+    const int64_t want = want_env > 0 ? want_env : 256;
     a.splits_u = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(Bc, kIbTile), ceil_div(want, a.rblk_u)));
     a.splits_p = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(B, kIbTile), ceil_div(want, a.rblk_p)));
     a.cols_u = ceil_div(ceil_div(Bc, a.splits_u), kIbTile) * kIbTile;
