@@ -362,6 +362,9 @@ def main() -> None:
     ap.add_argument("--exact-table-math", action="store_true",
                     help="IEEE sqrt / division for the g = 0 table AdamW updates (bit-identical to torch) "
                          "instead of v_sqrt / v_rcp")
+    ap.add_argument("--no-exact-line", dest="exact_line", action="store_false",
+                    help="skip the exact_table_math sub-line (K more steps with the drop-in default's "
+                         "bit-exact g = 0 table arithmetic)")
     ap.add_argument("--kernel-events", choices=["every-step", "none"], default="every-step",
                     help="none: no per-kernel HIP event pairs in the timed steps (the roofline entries "
                          "then have no live launch durations; a measurement of the events' own cost)")
@@ -470,6 +473,36 @@ def main() -> None:
         t = torch.tensor([elapsed], device=device if args.dist_backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    exact_line = None
+    if args.exact_line and not args.eager_adamw and not args.exact_table_math and hasattr(eng, "args"):
+        # the drop-in default's table arithmetic (ttamm.FusedTrainStep(table_adamw_math="exact"),
+        # IEEE sqrt / division, bit-identical to torch's AdamW): the same step, K more steps + the
+        # flush, timed the same way.  Every row is current here (the flush above), so the switch
+        # applies from the next step on.
+        from ttamm import _lib as ttamm_lib
+
+        eng.args.table_g0_math = ttamm_lib.G0_EXACT
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        eng.flush()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        ex_elapsed = time.perf_counter() - t1
+        if dist is not None:
+            t = torch.tensor([ex_elapsed], device=device if args.dist_backend == "nccl" else "cpu", dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ex_elapsed = float(t.item())
+        eng.args.table_g0_math = ttamm_lib.G0_FAST
+        exact_line = {"value": round(args.steps * c["B"] * world / ex_elapsed, 1), "unit": "interactions/s",
+                      "ms_per_step": round(ex_elapsed / args.steps * 1e3, 4), "steps": args.steps,
+                      "note": "table_adamw_math='exact' (the ttamm.FusedTrainStep / train_one_epoch default: IEEE "
+                              "sqrt and division in the g = 0 table AdamW, bit-identical to torch): the same "
+                              "workload, K steps + the closing flush, right after the main timed region"}
     loss = eng.finish()
     steps_only_ms = marks[0].elapsed_time(marks[1]) / args.steps
     flush_ms = marks[1].elapsed_time(marks[2])
@@ -491,8 +524,12 @@ def main() -> None:
     exact_mfma = os.environ.get("TTAMM_FP32_MFMA") == "exact"
     mfma_peak = MFMA_BF16_PEAK_TFLOPS if bf16 else MFMA_FP32_PEAK_TFLOPS
     split_ceiling = None if (bf16 or exact_mfma) else MFMA_BF16_PEAK_TFLOPS / 6.0  # six bf16 MFMAs per product
-    # PMC entry: the config's own, or "<config>_inbatch" when in-batch negatives replace its sampled ones
+    # PMC entry: the config's own, or "<config>_inbatch" when in-batch negatives replace its sampled ones;
+    # the sharded shapes of a W-rank step carry their own passes ("<key>_w<W>"): a 1-GPU pass never
+    # stands in for a launch of another shape (no entry -> traffic null)
     tkey = args.config + ("_inbatch" if in_batch and CONFIGS[args.config].get("negatives", "sampled") != "in-batch" else "")
+    if shard_world > 1 or args.sharded_single:
+        tkey += f"_w{shard_world}"
     traffic = load_traffic(tkey) or {}
     # tower rows of one step: users B; items B (1 + N) (one process) or the owner's requested rows
     if not sharded:
@@ -510,8 +547,9 @@ def main() -> None:
     def mfma_entry(name: str, flops: float, ms: float, ceiling: float | None, traffic_key: str,
                    alg_bytes: float | None = None) -> dict:
         """peak = the roof of the MFMA the kernel runs on: the split-bf16 kernels' own ceiling (the
-        bf16 dense peak / 6 bf16 MFMAs per fp32 product, / 8 for the in-batch kernel, which forms S
-        twice), the bf16 peak for bf16 towers, the fp32 MFMA peak for TTAMM_FP32_MFMA=exact; the
+        bf16 dense peak / 6 bf16 MFMAs per fp32 product; work a kernel repeats, such as the in-batch
+        kernel's second formation of S, counts against it, not as a lower roof), the bf16 peak for
+        bf16 towers, the fp32 MFMA peak for TTAMM_FP32_MFMA=exact; the
         fp32 MFMA peak (what an fp32 GEMM could reach on the fp32 instruction) is kept beside it."""
         tf = flops / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
         peak = ceiling or mfma_peak
@@ -544,11 +582,14 @@ def main() -> None:
     if in_batch:
         Bg = B * shard_world if sharded else B
         ib_flops = 6.0 * B * Bg * D  # S = U P^T, dU = dS P, dP = dS^T U (S recomputed: not counted)
-        # S is formed twice (user and item roles): 8 B Bg D executed flops
-        kernels.append(mfma_entry(
+        # priced against the full split-bf16 ceiling: the kernel forms S twice (user and item roles,
+        # 8 B Bg D executed flops), and that second formation is overhead of this kernel, not a lower roof
+        ent = mfma_entry(
             f"inbatch_x_kernel (S = U P^T [{B} x {Bg}] + BCE + dU + dP), {impl}" if not exact_mfma else
             f"inbatch_kernel (S = U P^T [{B} x {Bg}] + BCE + dU + dP, fp32 MFMA 32x32x2)",
-            ib_flops, pair_ms(4), split_ceiling * 6.0 / 8.0 if split_ceiling else None, "inbatch_bytes_per_launch"))
+            ib_flops, pair_ms(4), split_ceiling, "inbatch_bytes_per_launch")
+        ent["executed_flops_per_launch"] = 8.0 * B * Bg * D
+        kernels.append(ent)
     deferred = not args.eager_adamw
     slice_ms, cu_user_ms, cu_item_ms = pair_ms(0), pair_ms(8), pair_ms(10)
     if deferred:
@@ -640,6 +681,8 @@ def main() -> None:
                              "every deferred table row current (part of the K steps' work)"},
         "cpu_baseline": None,
     }
+    if exact_line is not None:
+        out["exact_table_math"] = exact_line
     if emulate:
         out["emulated_world"] = shard_world
         out["config"]["parallelism"] = (f"EMULATED rank 0 of {shard_world}: row-sharded step with mirrored ranks "

@@ -124,6 +124,8 @@ extern "C" {
 #define TTAMM_STATUS_SAMPLER_EXHAUSTED 1u    /* samplers.py:78-81 -> RuntimeError            */
 #define TTAMM_STATUS_INDEX_OUT_OF_RANGE 2u   /* a batch id < 0 or >= table rows -> IndexError
                                                 (nn.Embedding, encoders.py:222-223)         */
+#define TTAMM_STATUS_LOOKAHEAD_MISMATCH 4u   /* row-sharded step called with a batch other than the
+                                                one its look-ahead prepared -> ValueError   */
 
 /* ---------------------------------------------------------------------------------- */
 /* Parameter descriptors                                                               */
@@ -219,8 +221,10 @@ typedef struct ttamm_hparams {
      * AdamW (decoupled_weight_decay), TTAMM_DENSE_SGD = torch.optim.SGD(lr, weight_decay, momentum)
      * (sgd.py _single_tensor_sgd).  SGD keeps its momentum buffer in each dense tensor's exp_avg
      * (exp_avg_sq may alias it); with momentum == 0 both may alias the parameter itself.  The
-     * deferred table replay is AdamW-only: SGD sweeps the dense-group tables eagerly (no sweep at
-     * all when momentum == weight_decay == 0: untouched rows do not move). */
+     * deferred table replay covers SGD too: an untouched row's g = 0 step (p wd decay through the
+     * momentum buffer) is replayed from the history ring with each step's SGD constants, bit for
+     * bit the eager sweep's operations (no sweep at all when momentum == weight_decay == 0:
+     * untouched rows do not move). */
     int32_t dense_optimizer;
     double momentum, dampening;
     int32_t nesterov;

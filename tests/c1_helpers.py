@@ -47,11 +47,12 @@ class C1:
     major: int
 
 
-@lru_cache(maxsize=1)
-def load_c1() -> C1:
+@lru_cache(maxsize=2)
+def load_c1(variant: str = "c1") -> C1:
+    """The fixture: "c1" (tests/golden/c1, 1,600 users) or "c1_large" (20,000 users)."""
     import make_c1_fixture as fx
 
-    data, train, val, test, cats, major = fx.prepare()
+    data, train, val, test, cats, major = fx.prepare(fx.OUT_LARGE if variant == "c1_large" else fx.OUT)
     tp = {int(u): set(map(int, g["item_idx"].tolist())) for u, g in train.groupby("user_idx")}
     return C1(data.num_users, data.num_items, torch.tensor(train[["user_idx", "item_idx"]].to_numpy(), dtype=torch.long),
               [(int(u), int(i)) for u, i in val[["user_idx", "item_idx"]].to_numpy()], data.user_positive_items, tp,

@@ -17,7 +17,8 @@ Then it runs the oracle's restatement of the reference's data preparation
 (oracle/data_prep.py) and records a summary (counts, feature checksums) in c1_expected.json;
 tests/test_c1_cpu.py checks the preparation still reproduces it.
 
-    python tests/golden/make_c1_fixture.py
+    python tests/golden/make_c1_fixture.py            # tests/golden/c1
+    python tests/golden/make_c1_fixture.py --large    # tests/golden/c1_large (20,000 users)
 """
 
 from __future__ import annotations
@@ -56,7 +57,15 @@ DATA_CONFIG = {
 }
 
 
-def generate(rng: np.random.Generator) -> tuple[pd.DataFrame, pd.DataFrame]:
+# The large variant (tests/golden/c1_large): the same schema and planted structure at 20,000 users
+# (one validation pair each, so Recall@20's +-0.002 is 40 users, not 3), 6-14 interactions per
+# user and 12-character user ids so the three training epochs and the committed CSVs stay small
+LARGE = {"n_users": 20_000, "n_items": 4_000, "inter": (5, 11), "seed": 20261018, "id_len": 12}
+
+
+def generate(rng: np.random.Generator, n_users: int = N_USERS, n_items: int = N_ITEMS,
+             inter: tuple[int, int] = (8, 31), id_len: int = 28) -> tuple[pd.DataFrame, pd.DataFrame]:
+    N_ITEMS, N_USERS = n_items, n_users  # noqa: N806 (module defaults = the C1 fixture)
     cluster_names = [f"Cluster {c:02d} Studies" for c in range(N_CLUSTERS)]
     item_cluster = rng.integers(0, N_CLUSTERS, N_ITEMS)
     books = []
@@ -85,9 +94,9 @@ def generate(rng: np.random.Generator) -> tuple[pd.DataFrame, pd.DataFrame]:
     rows = []
     t0 = 1_600_000_000_000
     for u in range(N_USERS):
-        uid = "".join(rng.choice(list("ABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789"), size=28))
+        uid = "".join(rng.choice(list("ABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789"), size=id_len))
         fav = rng.choice(N_CLUSTERS, size=int(rng.integers(1, 3)), replace=False)
-        n = int(rng.integers(8, 31))
+        n = int(rng.integers(*inter))
         picked: set[int] = set()
         while len(picked) < n:
             if rng.random() < 0.85:
@@ -140,15 +149,24 @@ def summary(prepared) -> dict:
     }
 
 
-def main() -> None:
-    OUT.mkdir(parents=True, exist_ok=True)
-    books, users = generate(np.random.default_rng(20251114))
-    books.to_csv(OUT / "books_c1.csv.gz", index=False, compression={"method": "gzip", "mtime": 0})
-    users.to_csv(OUT / "users_c1.csv.gz", index=False, compression={"method": "gzip", "mtime": 0})
-    s = summary(prepare())
-    (OUT / "c1_expected.json").write_text(json.dumps(s, indent=1) + "\n")
+OUT_LARGE = HERE / "c1_large"
+
+
+def main(argv: list[str]) -> None:
+    large = "--large" in argv
+    out = OUT_LARGE if large else OUT
+    out.mkdir(parents=True, exist_ok=True)
+    if large:
+        books, users = generate(np.random.default_rng(LARGE["seed"]), LARGE["n_users"], LARGE["n_items"],
+                                LARGE["inter"], LARGE["id_len"])
+    else:
+        books, users = generate(np.random.default_rng(20251114))
+    books.to_csv(out / "books_c1.csv.gz", index=False, compression={"method": "gzip", "mtime": 0})
+    users.to_csv(out / "users_c1.csv.gz", index=False, compression={"method": "gzip", "mtime": 0})
+    s = summary(prepare(out))
+    (out / "c1_expected.json").write_text(json.dumps(s, indent=1) + "\n")
     print(json.dumps(s))
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

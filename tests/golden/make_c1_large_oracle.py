@@ -1,0 +1,91 @@
+"""The oracle's Recall@20 on the large C1-schema fixture (tests/golden/c1_large, 20,000 users), and
+the oracle's own spread under summation-order-only changes.
+
+Trains the CPU restatement (oracle/cpu_reference.py) for EPOCHS epochs exactly as
+tests/test_c1_gpu.py trains ttamm (same init, DataLoader order, injected negatives and dropout
+masks: tests/c1_helpers.py) and evaluates Recall@20 with the restated _evaluate_model (exact-IP
+branch, cosine).  Variants that change only fp32 summation order:
+
+  threads8   8 intra-op threads (the default run; its Recall@20 is the test's reference value)
+  threads1   1 thread (other GEMM blocking in the CPU BLAS)
+  splitk2    8 threads, the first feature layer's K = 605 reduction split in two halves summed
+             (the reordering of ttamm's reverted split-K layer 1, round 4)
+
+Writes tests/golden/c1_large/oracle_recall.json (Recall@5/10/20 per variant, epoch means, and
+the largest pairwise Recall@20 difference among the variants = the oracle's own spread).
+
+    python tests/golden/make_c1_large_oracle.py     (~5 minutes on 8 cores)
+"""
+
+from __future__ import annotations
+
+import json
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+HERE = Path(__file__).resolve().parent
+ROOT = HERE.parents[1]
+sys.path[:0] = [str(ROOT / "tests"), str(ROOT)]
+
+from c1_helpers import K_VALUES, load_c1, train_oracle  # noqa: E402
+from oracle import cpu_reference as ref  # noqa: E402
+
+EPOCHS = 3
+
+
+def _splitk_linear(orig):
+    def lin(layer, x, bf16):
+        k = layer.in_features
+        if bf16 or k < 512:
+            return orig(layer, x, bf16)
+        h = k // 2
+        w = layer.weight
+        return x[:, :h] @ w[:, :h].t() + x[:, h:] @ w[:, h:].t() + layer.bias
+    return lin
+
+
+def run(variant: str, c1) -> dict:
+    orig = ref._linear
+    torch.set_num_threads(1 if variant == "threads1" else 8)
+    if variant == "splitk2":
+        ref._linear = _splitk_linear(orig)
+    try:
+        t0 = time.time()
+        model, epochs, _ = train_oracle(c1, EPOCHS)
+        secs = time.time() - t0
+    finally:
+        ref._linear = orig
+    torch.set_num_threads(8)
+    preds, truth = ref.evaluate_model(model, train_positive_map=c1.train_positive_map, val_pairs=c1.val_pairs,
+                                      item_features=c1.item_features, user_features=c1.user_features,
+                                      num_items=c1.num_items, k_values=K_VALUES, faiss_search_k=max(K_VALUES) * 4,
+                                      normalize=True)
+    m = ref.ranking_metrics(preds, truth, K_VALUES)
+    out = {"recall": {str(k): float(m.recall[k]) for k in K_VALUES}, "epoch_means": epochs,
+           "train_seconds": round(secs, 1)}
+    print(variant, json.dumps(out), flush=True)
+    return out
+
+
+def main() -> None:
+    c1 = load_c1("c1_large")
+    res = {v: run(v, c1) for v in ("threads8", "threads1", "splitk2")}
+    r20 = [r["recall"]["20"] for r in res.values()]
+    doc = {
+        "fixture": "tests/golden/c1_large (make_c1_fixture.py --large)",
+        "epochs": EPOCHS,
+        "val_users": len(c1.val_pairs),
+        "variants": res,
+        "reference_recall20": res["threads8"]["recall"]["20"],
+        "oracle_spread_recall20": max(r20) - min(r20),
+        "torch": torch.__version__,
+    }
+    (HERE / "c1_large" / "oracle_recall.json").write_text(json.dumps(doc, indent=1) + "\n")
+    print(json.dumps(doc))
+
+
+if __name__ == "__main__":
+    main()

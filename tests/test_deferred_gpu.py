@@ -3,7 +3,7 @@ against the eager per-step sweep: after any number of steps and a flush, every p
 every optimizer moment is BIT-identical (the deferred path replays the same fp32 operations
 with the same per-step constants).  Covered: rows lagging up to replay_slices steps, the
 history ring wrapping, a learning-rate change mid-run (per-step constants), a mid-run flush,
-a dense-optimized ID table, and the C2 shapes."""
+a dense-optimized ID table, the C2 shapes, and torch.optim.SGD in the dense group."""
 
 from __future__ import annotations
 
@@ -22,14 +22,17 @@ ROOT = Path(__file__).resolve().parents[1]
 
 
 def _engine(prob, *, deferred: bool, slices: int, sparse: bool = True, overlap: bool = True, math: str = "fast",
-            aux_cus=None):
+            aux_cus=None, sgd: dict | None = None):
     from gpu_helpers import ttamm_model_from
 
     model = ttamm_model_from(prob)
     dense, sp = ttamm._collect_parameter_groups(model)
     if not sparse:  # every table in the AdamW group (the reference's sparse=False configuration)
         dense, sp = dense + sp, []
-    opts = [torch.optim.AdamW(dense, lr=1e-3, weight_decay=0.01)]
+    if sgd is not None:  # optimizer: sgd (training.py:1324-1330)
+        opts = [torch.optim.SGD(dense, lr=1e-3, weight_decay=0.01, **sgd)]
+    else:
+        opts = [torch.optim.AdamW(dense, lr=1e-3, weight_decay=0.01)]
     if sp:
         opts.append(torch.optim.SparseAdam(sp, lr=1e-3))
     eng = ttamm.FusedTrainStep(model, opts, negatives_per_positive=prob.shape.N, positives=prob.positives,
@@ -51,9 +54,9 @@ def _state(model, opts):
 
 
 def _run(prob, steps, *, deferred, slices, sparse=True, flush_at=None, lr_change_at=None, overlap=True, math="fast",
-         aux_cus=None):
+         aux_cus=None, sgd=None):
     model, opts, eng = _engine(prob, deferred=deferred, slices=slices, sparse=sparse, overlap=overlap, math=math,
-                               aux_cus=aux_cus)
+                               aux_cus=aux_cus, sgd=sgd)
     gen = torch.Generator().manual_seed(3)
     losses = []
     for k in range(steps):
@@ -78,6 +81,25 @@ def test_deferred_equals_eager_bitwise(slices, steps, sparse, math):
     eager, le = _run(prob, steps, deferred=False, slices=slices, sparse=sparse, lr_change_at=steps // 2, math=math)
     lazy, ll = _run(prob, steps, deferred=True, slices=slices, sparse=sparse, lr_change_at=steps // 2,
                     flush_at=steps // 3, math=math)
+    assert le == ll
+    assert eager.keys() == lazy.keys()
+    for k in eager:
+        assert torch.equal(eager[k], lazy[k]), k
+
+
+@pytest.mark.parametrize("sgd", [dict(momentum=0.9), dict(momentum=0.9, nesterov=True),
+                                 dict(momentum=0.8, dampening=0.1), dict(momentum=0.0)],
+                         ids=["momentum", "nesterov", "dampening", "no-momentum"])
+@pytest.mark.parametrize("slices,steps,sparse", [(3, 13, True), (5, 17, False)])
+def test_deferred_sgd_equals_eager_bitwise(sgd, slices, steps, sparse):
+    """optimizer: sgd (training.py:1324-1330): the g = 0 steps of untouched table rows (weight decay
+    through the momentum buffer) replayed from the history ring equal the eager per-step sweep bit
+    for bit, with lagging rows, a mid-run lr change, a mid-run flush and (dampening) the first
+    step's buf = grad."""
+    prob = make_problem(Shape(), seed=21)
+    eager, le = _run(prob, steps, deferred=False, slices=slices, sparse=sparse, lr_change_at=steps // 2, sgd=sgd)
+    lazy, ll = _run(prob, steps, deferred=True, slices=slices, sparse=sparse, lr_change_at=steps // 2,
+                    flush_at=steps // 3, sgd=sgd)
     assert le == ll
     assert eager.keys() == lazy.keys()
     for k in eager:

@@ -103,8 +103,9 @@ def test_adam_coupled_l2_matches_oracle(steps, deferred):
     assert (m.abs().sum(dim=1) > 0).all()
 
 
-def test_sgd_deferred_request_is_eager():
-    """FusedTrainStep(deferred_adamw=True) with SGD sweeps eagerly (the replay is Adam-only)."""
+def test_sgd_deferred_creates_momentum_buffers():
+    """FusedTrainStep(deferred_adamw=True) with SGD defers the g = 0 table steps too (the replay's
+    sgd_elem path), and the first step still creates torch's momentum buffers in place."""
     import ttamm
     from gpu_helpers import ttamm_model_from, ttamm_optimizers
     from helpers import LOSS_WEIGHTS
@@ -115,7 +116,7 @@ def test_sgd_deferred_request_is_eager():
     eng = ttamm.FusedTrainStep(tm, opts, negatives_per_positive=prob.shape.N, positives=prob.positives,
                                user_features=prob.user_features.cuda(), item_features=prob.item_features.cuda(),
                                loss_weights=LOSS_WEIGHTS, max_batch=prob.shape.B, deferred_adamw=True)
-    assert eng._deferred == []
+    assert len(eng._deferred) == 2  # both mimic tables carry last_step
     assert "momentum_buffer" not in opts[0].state.get(tm.adaptive_mimic.item_augmented.weight, {})
     u, p, n, um, im = prob.batches[0]
     eng.step(u.cuda(), p.cuda(), n.cuda().reshape(-1), keep_masks={"user": [x.cuda() for x in um],

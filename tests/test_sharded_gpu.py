@@ -409,3 +409,107 @@ def test_sharded_poisoned_step_is_skipped_by_every_rank():
         for n in st:
             assert float(st[n]["step"]) == float(st2[n]["step"]) == 1.0, (own.rank, n)
             assert torch.equal(st[n]["exp_avg"], st2[n]["exp_avg"]), (own.rank, n)
+
+
+def _owned_batches(prob, shape: Shape, W: int, steps: int, seed: int = 9):
+    gen = torch.Generator().manual_seed(seed)
+    out = []
+    for _ in range(steps):
+        per = []
+        for r in range(W):
+            owned = torch.arange(r, shape.U, W)
+            users = owned[torch.randint(0, owned.numel(), (shape.B,), generator=gen)]
+            pos = torch.tensor([sorted(prob.positives[int(u)])[0] for u in users], dtype=torch.long)
+            per.append(((users // W).cuda(), pos.cuda()))
+        out.append(per)
+    return out
+
+
+def _catching(prog, kinds=(IndexError, RuntimeError, ValueError)):
+    try:
+        return (yield from prog)
+    except kinds as e:
+        return e
+
+
+@pytest.mark.parametrize("W", [2, 3])
+def test_look_ahead_poison_in_next_batch_skipped_by_every_rank(W):
+    """A bad user id in ONE rank's next_batch (step 2's batch, checked and routed by step 1's
+    look-ahead): every rank skips step 2 and 3 (the look-ahead's status rides with the counts it
+    exchanges), finish raises IndexError on every rank, and every rank holds exactly the state
+    after step 1."""
+    shape = Shape()
+    prob, ranks = _ranks_only(shape, W, max_batch=shape.B)
+    steps = _owned_batches(prob, shape, W, 3)
+    bad = steps[1][W - 1][0].clone()
+    bad[3] = 10 ** 6  # not a row of the last rank's user shard
+    steps[1][W - 1] = (bad, steps[1][W - 1][1])
+    for s, per in enumerate(steps):
+        nxt = steps[s + 1] if s + 1 < len(steps) else None
+        run_loopback([eng.program(u, p, next_batch=nxt[r] if nxt else None)
+                      for r, ((_, _, _, eng), (u, p)) in enumerate(zip(ranks, per))])
+    res = run_loopback([_catching(eng.finish_program()) for (_, _, _, eng) in ranks])
+    assert all(isinstance(x, IndexError) for x in res), res
+
+    prob2, ref = _ranks_only(shape, W, max_batch=shape.B)
+    run_loopback([eng.program(u, p) for (_, _, _, eng), (u, p) in zip(ref, steps[0])])
+    run_loopback([eng.finish_program() for (_, _, _, eng) in ref])
+    for (own, m, opts, _), (_, m2, opts2, _) in zip(ranks, ref):
+        for (k, v), (_, v2) in zip(m.state_dict().items(), m2.state_dict().items()):
+            assert torch.equal(v, v2), (own.rank, k)
+
+
+def test_look_ahead_batch_copy_is_used_and_other_batch_raises_on_every_rank():
+    """A prepared look-ahead is consumed by every rank (its count exchange already ran on all of
+    them), so the collective sequence never diverges.  (a) A rank handed a COPY of the prepared
+    batch (equal values, another tensor) steps normally: the same state as identity-passing
+    ranks.  (b) A rank handed ANOTHER batch skips that step (nothing written) and finish raises
+    ValueError on every rank instead of one rank hanging the others."""
+    W, shape = 2, Shape()
+    prob, ranks = _ranks_only(shape, W, max_batch=shape.B)
+    prob_b, twin = _ranks_only(shape, W, max_batch=shape.B)
+    steps = _owned_batches(prob, shape, W, 2)
+    # (a) rank 1 gets a copy at step 2
+    for s, per in enumerate(steps):
+        nxt = steps[s + 1] if s + 1 < len(steps) else None
+        progs = []
+        for r, ((_, _, _, eng), (u, p)) in enumerate(zip(ranks, per)):
+            if s == 1 and r == 1:
+                u, p = u.clone(), p.clone()
+            progs.append(eng.program(u, p, next_batch=nxt[r] if nxt else None))
+        run_loopback(progs)
+        run_loopback([eng.program(u, p, next_batch=nxt[r] if nxt else None)
+                      for r, ((_, _, _, eng), (u, p)) in enumerate(zip(twin, per))])
+    la = run_loopback([eng.finish_program() for (_, _, _, eng) in ranks])
+    lb = run_loopback([eng.finish_program() for (_, _, _, eng) in twin])
+    assert la == lb
+    for (_, m, _, _), (_, m2, _, _) in zip(ranks, twin):
+        for (k, v), (_, v2) in zip(m.state_dict().items(), m2.state_dict().items()):
+            assert torch.equal(v, v2), k
+    # (b) rank 0 gets a different batch at step 2
+    prob_c, bad = _ranks_only(shape, W, max_batch=shape.B)
+    other = _owned_batches(prob, shape, W, 1, seed=123)[0]
+    for s, per in enumerate(steps):
+        nxt = steps[s + 1] if s + 1 < len(steps) else None
+        progs = []
+        for r, ((_, _, _, eng), (u, p)) in enumerate(zip(bad, per)):
+            if s == 1 and r == 0:
+                u, p = other[0]
+            progs.append(eng.program(u, p, next_batch=nxt[r] if nxt else None))
+        run_loopback(progs)
+    res = run_loopback([_catching(eng.finish_program()) for (_, _, _, eng) in bad])
+    assert all(isinstance(x, ValueError) and "look-ahead" in str(x) for x in res), res
+
+
+def test_look_ahead_rejects_bad_next_batch_before_any_collective():
+    """A malformed next_batch raises ValueError at the top of program(), before the step's first
+    collective, on the rank that got it (not halfway through the step, after the forward
+    exchange, with the peers blocked in the next collective)."""
+    W, shape = 2, Shape()
+    prob, ranks = _ranks_only(shape, W, max_batch=shape.B)
+    steps = _owned_batches(prob, shape, W, 1)
+    eng = ranks[0][3]
+    u, p = steps[0][0]
+    prog = eng.program(u, p, next_batch=(u.to(torch.int32), p))
+    with pytest.raises(ValueError, match="next_batch"):
+        next(prog)

@@ -932,6 +932,9 @@ int inbatch_standalone(const float* U, int64_t B, int64_t ldu, const float* P, i
     TTAMM_REQUIRE(U && P && dU && dP && loss_sum && ws, "inbatch_bce: null argument");
     TTAMM_REQUIRE(B > 0 && Bc > 0 && D > 0 && ldu >= D && ldp >= D && ld_du >= D && ld_dp >= D,
                   "inbatch_bce: bad shape");
+    TTAMM_REQUIRE(row_base >= 0 && row_base + B <= Bc,
+                  "inbatch_bce: row_base must place the B users' labels inside the Bc columns (0 <= row_base, "
+                  "row_base + B <= Bc)");
     TTAMM_REQUIRE(ws_bytes >= inbatch_standalone_workspace_bytes(B, Bc, D), "inbatch_bce: workspace too small");
     InBatchArgs a{};
     a.U = U, a.ldu = ldu, a.B = B, a.P = P, a.ldp = ldp, a.Bc = Bc, a.D = D;

@@ -218,7 +218,8 @@ int launch_scatter_add_rows(float* dst, int64_t dst_rows, int dim, const int64_t
                             int64_t skip_row, hipStream_t s);
 
 // Status bits that stop every later step (ttamm.h TTAMM_STATUS_*).
-constexpr uint32_t kStatusPoison = TTAMM_STATUS_SAMPLER_EXHAUSTED | TTAMM_STATUS_INDEX_OUT_OF_RANGE;
+constexpr uint32_t kStatusPoison =
+    TTAMM_STATUS_SAMPLER_EXHAUSTED | TTAMM_STATUS_INDEX_OUT_OF_RANGE | TTAMM_STATUS_LOOKAHEAD_MISMATCH;
 __device__ __forceinline__ bool step_poisoned(const uint32_t* status) {
     return status != nullptr && (*status & kStatusPoison) != 0u;
 }
@@ -551,6 +552,7 @@ struct ReplayArgs {
                       // row update may have moved a row past target)
     int decoupled;    // AdamW (decoupled weight decay) vs Adam (L2): the optimizer's, every step
     int fast_g0;      // TTAMM_G0_FAST arithmetic
+    int sgd;          // torch.optim.SGD (ttamm.h TTAMM_DENSE_SGD): sgd_elem(g = 0) per step
     const uint32_t* status;  // poisoned: no write (null for the flush)
 };
 // ev (optional, 2 hipEvent_t): recorded around the replay kernel itself (not the stamp)

@@ -875,6 +875,73 @@ __global__ __launch_bounds__(256) void replay_s_kernel(ReplayArgs) {
     }
 }
 
+// The deferred SGD(g = 0) replay (torch.optim.SGD in the dense group, training.py:1324-1330): an
+// untouched row's step is p' = p + lr-scaled momentum of its own decay term,
+//     g = p wd;  buf = fma(g, 1 - dampening, buf momentum) (buf = g on a first step);
+//     p = fma(nesterov ? fma(buf, momentum, g) : buf, -lr, p)
+// — linear in (p, buf), no transcendentals.  Each replayed step applies sgd_elem(g = 0) with that
+// step's constants from the history ring (AdamConsts: sgd_neg_lr, sgd_mom, sgd_damp1, sgd_first,
+// sgd_nesterov, wd), exactly the operations the eager sweep applies, so deferred == eager bit for
+// bit.  momentum == 0: m and v alias the parameter (no state), the stores write p three times.
+// Constants are read per lane from the ring in global memory (L1/L2-resident, a few dozen bytes a
+// step); the loop is a handful of FMAs per element-step, so it is HBM-bound like the row traffic.
+template <int V>
+__global__ __launch_bounds__(256) void replay_sgd_kernel(ReplayArgs) {
+    const KArg(ReplayArgs)* ka = (const KArg(ReplayArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
+    const KArg(ReplaySeg)& S = ka->seg[blockIdx.y];
+    if (step_poisoned(ka->status)) return;
+    const AdamConsts* hist = ka->hist;
+    const int cap = ka->cap;
+    const int dim = S.dim;
+    const uint32_t per_row = (uint32_t)(dim >> 2) / V;
+    const int32_t target = ka->target;
+    const bool by_list = S.list_rows != nullptr;
+    const uint32_t nrows = by_list ? (uint32_t)S.list_cnt[0] : (uint32_t)(S.row_hi - S.row_lo);
+    const uint32_t total = nrows * per_row;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+        const uint32_t r = e / per_row, q = e - r * per_row;
+        int64_t row;
+        int32_t l;
+        if (by_list) {
+            row = S.list_rows[r];
+            l = target - S.list_lag[r];
+        } else {
+            row = S.row_lo + r;
+            l = S.last[row];
+            if (l >= target) continue;
+        }
+        const int64_t o = row * dim + 4 * (int64_t)q;
+        float4 p[V], m[V], v[V];
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const int64_t oi = o + (int64_t)(4 * per_row) * i;
+            p[i] = *reinterpret_cast<const float4*>(S.p + oi);
+            m[i] = *reinterpret_cast<const float4*>(S.m + oi);
+            v[i] = *reinterpret_cast<const float4*>(S.v + oi);
+        }
+        int j = (l + 1) % cap;
+        for (int32_t k = l; k < target; ++k) {
+            AdamConsts c = hist[j];
+            c.sgd = 1;
+            j = j + 1 == cap ? 0 : j + 1;
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                sgd_elem(p[i].x, m[i].x, v[i].x, 0.f, c);
+                sgd_elem(p[i].y, m[i].y, v[i].y, 0.f, c);
+                sgd_elem(p[i].z, m[i].z, v[i].z, 0.f, c);
+                sgd_elem(p[i].w, m[i].w, v[i].w, 0.f, c);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const int64_t oi = o + (int64_t)(4 * per_row) * i;
+            *reinterpret_cast<float4*>(S.p + oi) = p[i];
+            *reinterpret_cast<float4*>(S.m + oi) = m[i];
+            *reinterpret_cast<float4*>(S.v + oi) = v[i];
+        }
+    }
+}
+
 // row ranges only: last[row] = target (stamp 1) or max(last[row], target) (stamp 2) after the
 // replay (list segments were stamped by their build)
 __global__ void stamp_kernel(ReplayArgs) {
@@ -1358,6 +1425,10 @@ static void launch_replay_v(const ReplayArgs& a, dim3 grid, size_t lds, hipStrea
         const char* e = getenv("TTAMM_REPLAY_SCALAR");
         return e && e[0] == '1';
     }();
+    if (a.sgd) {
+        hipLaunchKernelGGL((replay_sgd_kernel<V>), grid, dim3(256), 0, s, a);
+        return;
+    }
     if (scalar) {
         if (a.fast_g0) {
             if (a.decoupled) hipLaunchKernelGGL((replay_s_kernel<true, true, V>), grid, dim3(256), 0, s, a);

@@ -122,6 +122,8 @@ __global__ void step_prologue_kernel(StepPrologue) {
         c.neg_step = pa->c.neg_step, c.bc2_sqrt = pa->c.bc2_sqrt, c.inv_bc2_sqrt = pa->c.inv_bc2_sqrt;
         c.wd = pa->c.wd, c.decoupled = pa->c.decoupled, c.fast_g0 = pa->c.fast_g0;
         c.fast_ibc = pa->c.fast_ibc, c.fast_eps = pa->c.fast_eps;
+        c.sgd = pa->c.sgd, c.sgd_neg_lr = pa->c.sgd_neg_lr, c.sgd_mom = pa->c.sgd_mom;  // deferred SGD replay
+        c.sgd_damp1 = pa->c.sgd_damp1, c.sgd_first = pa->c.sgd_first, c.sgd_nesterov = pa->c.sgd_nesterov;
         pa->hist[pa->step % pa->cap] = c;
     }
 }

@@ -973,6 +973,7 @@ struct Deferred {
     int32_t step = 0;  // the dense step this call executes
     int decoupled = 1;
     int fast = 0;  // TTAMM_G0_FAST arithmetic for the g = 0 updates
+    int sgd = 0;   // torch.optim.SGD dense group: the g = 0 replay is sgd_elem's (replay_sgd_kernel)
     const uint32_t* status = nullptr;  // poisoned: the step writes nothing
     // one-process step with the aux stream: the rolling slice runs there (replay_slice_aux)
     // instead of at the end of the main stream's step
@@ -1015,6 +1016,7 @@ int replay_slice(const ttamm_tower* const* T, int n, bool mimic, const Deferred&
     ra.hist = df.hist;
     ra.cap = df.cap;
     ra.decoupled = df.decoupled;
+    ra.sgd = df.sgd;
     ra.fast_g0 = df.fast;
     ra.status = df.status;
     ra.target = target;
@@ -1057,6 +1059,7 @@ int tower_prepare_a(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred
     ra.hist = df.hist;
     ra.cap = df.cap;
     ra.decoupled = df.decoupled;
+    ra.sgd = df.sgd;
     ra.fast_g0 = df.fast;
     ra.status = df.status;
     ra.target = df.step - 1;
@@ -1089,6 +1092,7 @@ int towers_prepare_a(const ttamm_tower* const* T, TowerWs* const* W, int n, bool
     ra.hist = df.hist;
     ra.cap = df.cap;
     ra.decoupled = df.decoupled;
+    ra.sgd = df.sgd;
     ra.fast_g0 = df.fast;
     ra.status = df.status;
     ra.target = df.step - 1;
@@ -1461,7 +1465,6 @@ int deferred_of(const ttamm_step_args& A, Deferred& df) {
         }
     }
     if (with == 0) return TTAMM_OK;
-    TTAMM_REQUIRE(A.hp.dense_optimizer == TTAMM_DENSE_ADAM, "deferred table updates are Adam / AdamW only (SGD: eager)");
     TTAMM_REQUIRE(with == total, "deferred AdamW: every dense-group table needs last_step");
     TTAMM_REQUIRE(A.adam_history != nullptr && A.replay_slices >= 1 && A.history_capacity > A.replay_slices &&
                       A.history_capacity <= kMaxAdamHistory,
@@ -1474,6 +1477,7 @@ int deferred_of(const ttamm_step_args& A, Deferred& df) {
     df.step = (int32_t)A.hp.dense_step;
     df.decoupled = A.hp.decoupled_weight_decay ? 1 : 0;
     df.fast = A.table_g0_math == TTAMM_G0_FAST ? 1 : 0;
+    df.sgd = A.hp.dense_optimizer == TTAMM_DENSE_SGD ? 1 : 0;
     return TTAMM_OK;
 }
 
@@ -1966,6 +1970,7 @@ int flush_tables(const ttamm_step_args& A, hipStream_t s) {
     ra.hist = df.hist;
     ra.cap = df.cap;
     ra.decoupled = df.decoupled;
+    ra.sgd = df.sgd;
     ra.fast_g0 = df.fast;
     ra.target = df.step;
     ra.stamp = 1;

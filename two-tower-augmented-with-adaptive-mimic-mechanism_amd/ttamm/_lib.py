@@ -24,7 +24,8 @@ ACT_RELU, ACT_GELU, ACT_TANH, ACT_SELU = 0, 1, 2, 3  # ttamm.h TTAMM_ACT_*
 OPT_SPARSE_ADAM, OPT_DENSE = 0, 1
 STATUS_SAMPLER_EXHAUSTED = 1
 STATUS_INDEX_OUT_OF_RANGE = 2
-STATUS_POISON = STATUS_SAMPLER_EXHAUSTED | STATUS_INDEX_OUT_OF_RANGE  # bits that stop every later step
+STATUS_LOOKAHEAD_MISMATCH = 4  # row-sharded step: a batch other than the prepared look-ahead's
+STATUS_POISON = STATUS_SAMPLER_EXHAUSTED | STATUS_INDEX_OUT_OF_RANGE | STATUS_LOOKAHEAD_MISMATCH  # bits that stop every later step
 
 _NATIVE_DIR = Path(__file__).resolve().parent / "_native"
 LIB_PATH = _NATIVE_DIR / "libttamm.so"

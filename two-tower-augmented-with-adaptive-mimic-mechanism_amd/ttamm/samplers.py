@@ -55,9 +55,14 @@ _csr_cache: dict[tuple, PositivesCSR] = {}
 
 
 def positives_csr(positives, *, device: torch.device, num_users: int | None = None) -> PositivesCSR:
+    """The device CSR of a dict[user] -> set(items), cached per mapping.  The key holds the user
+    count and the total positive count, so a caller that grows (or shrinks) a user's set in place
+    gets a rebuilt CSR; an in-place edit that keeps both counts (one item swapped for another)
+    needs a fresh mapping or an explicit PositivesCSR."""
     if isinstance(positives, PositivesCSR):
         return positives
-    key = (id(positives), len(positives), str(device))
+    total = sum(len(items) for items in positives.values())
+    key = (id(positives), len(positives), total, str(device))
     hit = _csr_cache.get(key)
     if hit is None or (num_users is not None and hit.num_users < num_users):
         hit = PositivesCSR.from_mapping(positives, device=device, num_users=num_users)

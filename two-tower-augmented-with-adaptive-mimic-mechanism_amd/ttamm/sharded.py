@@ -532,8 +532,20 @@ class ShardedTrainStep(FusedTrainStep):
         routing; the draws and ids are the ones that step would make itself)."""
         ahead = self._ahead
         self._ahead = None
-        use_ahead = (ahead is not None and ahead.users is users and ahead.pos is pos_items and neg_items is None
-                     and row_base is None and global_batch is None)
+        if next_batch is not None and row_base is None and global_batch is None:
+            self._check_next_batch(*next_batch)  # before this step's first collective
+        mismatch = False
+        if ahead is not None:
+            # A prepared look-ahead already exchanged this step's request counts on EVERY rank, so
+            # every rank consumes it (the same collective sequence everywhere, whatever this call
+            # passes).  A call with another batch is a caller error: this rank's step is then
+            # skipped (status bit, no state written) and finish() raises on every rank.
+            same = (ahead.users is users and ahead.pos is pos_items) or (
+                users.shape == ahead.users.shape and pos_items.shape == ahead.pos.shape
+                and torch.equal(users, ahead.users) and torch.equal(pos_items, ahead.pos))
+            mismatch = not same or neg_items is not None or row_base is not None or global_batch is not None
+            users, pos_items, neg_items, row_base, global_batch = ahead.users, ahead.pos, None, None, None
+        use_ahead = ahead is not None
         if not self._bind_batch(users, pos_items, ahead.negs if use_ahead else neg_items, keep_masks):
             raise ValueError("ttamm: empty batch in a sharded step (every rank must step)")
         a = self.args
@@ -553,6 +565,8 @@ class ShardedTrainStep(FusedTrainStep):
         if use_ahead:
             negs = ahead.negs
             self.status.bitwise_or_(ahead.status)  # what the look-ahead's checks and draws found
+            if mismatch:
+                self.status.bitwise_or_(_lib.STATUS_LOOKAHEAD_MISMATCH)
         else:
             negs = neg_items.reshape(-1) if neg_items is not None else self.neg_buffer[: B * N]
         self._phase(_lib.PHASE_SAMPLE)
@@ -649,15 +663,21 @@ class ShardedTrainStep(FusedTrainStep):
         # keep the step's device buffers alive until the stream has consumed them
         self._live = (route, back, bwd_in) + ib
 
-    def _look_ahead(self, users: torch.Tensor, pos: torch.Tensor) -> Program:
-        """Program: the next step's id checks, negatives and request routing up to the count
-        exchange (route_start with its host copy in flight).  Its status word starts as this
-        rank's (an earlier poison rides along as in the step's own exchange)."""
-        W, rank = self.own.world_size, self.own.rank
-        B, N = users.numel(), self.num_neg
+    def _check_next_batch(self, users: torch.Tensor, pos: torch.Tensor) -> None:
+        B = users.numel()
         if B == 0 or B > self.max_batch or users.dtype != torch.long or pos.dtype != torch.long or \
                 pos.numel() != B:
             raise ValueError("ttamm: next_batch must be int64 (users, positives) of one size <= max_batch")
+        if self.num_neg > 0 and self.csr is None:
+            raise ValueError("ttamm: positives are required to sample negatives")
+
+    def _look_ahead(self, users: torch.Tensor, pos: torch.Tensor) -> Program:
+        """Program: the next step's id checks, negatives and request routing up to the count
+        exchange (route_start with its host copy in flight).  Its status word starts as this
+        rank's (an earlier poison rides along as in the step's own exchange).  The batch was
+        validated before the step's first collective (_check_next_batch)."""
+        W, rank = self.own.world_size, self.own.rank
+        B, N = users.numel(), self.num_neg
         users0, pos0 = users, pos  # the next step's program finds its batch by identity
         users, pos = users.reshape(-1), pos.reshape(-1)
         dev = self.device
@@ -676,8 +696,6 @@ class ShardedTrainStep(FusedTrainStep):
         negs = self._ahead_bufs[k][: B * N]
         base, Bg = rank * B, W * B
         if N > 0:
-            if self.csr is None:
-                raise ValueError("ttamm: positives are required to sample negatives")
             _lib.check(self.lib.ttamm_sample_negatives(
                 users.data_ptr(), B, N, self.num_items, self.csr.offsets.data_ptr(), self.csr.values.data_ptr(),
                 self.csr.num_users, self.args.b.seed, self.steps_done + 1, base * N, negs.data_ptr(),
@@ -700,9 +718,11 @@ class ShardedTrainStep(FusedTrainStep):
         holds the state after the same last good step: the status words ride with each step's
         request counts, so a poisoned step is skipped by all ranks before any writes state."""
         self._ahead = None  # a look-ahead no step consumed: its exchange ran on every rank, nothing to undo
-        flags = torch.stack([(self.status & b) != 0 for b in (1, 2)]).reshape(-1).to(torch.float32)
+        bits = (_lib.STATUS_SAMPLER_EXHAUSTED, _lib.STATUS_INDEX_OUT_OF_RANGE, _lib.STATUS_LOOKAHEAD_MISMATCH)
+        flags = torch.stack([(self.status & b) != 0 for b in bits]).reshape(-1).to(torch.float32)
         yield AllReduce(flags)
-        self.status.bitwise_or_((flags[0] > 0).to(torch.int32) + 2 * (flags[1] > 0).to(torch.int32))
+        for i, b in enumerate(bits):
+            self.status.bitwise_or_((flags[i] > 0).to(torch.int32) * b)
         yield AllReduce(self.loss_accum)
         return FusedTrainStep.finish(self)
 

@@ -104,6 +104,10 @@ def _pad_features(features: torch.Tensor | None) -> torch.Tensor | None:
     return padded[:, :width]
 
 
+def _dense_params(opt: torch.optim.Optimizer) -> list[torch.Tensor]:
+    return [p for g in opt.param_groups for p in g["params"]]
+
+
 class FusedTrainStep:
     """Owns the native step descriptor and workspace for one (model, optimizers) pair."""
 
@@ -324,7 +328,10 @@ class FusedTrainStep:
         # deferred exact AdamW(g = 0) on the dense-group tables (ttamm.h ttamm_table.last_step):
         # the rows are current to dense_step0 now
         self._deferred: list[torch.Tensor] = []
-        if deferred_adamw and self.dense_opt is not None and not self.sgd:
+        if deferred_adamw and self.dense_opt is not None and not (
+                self.sgd and float(self.dense_opt.param_groups[0]["momentum"]) == 0.0
+                and float(self.dense_opt.param_groups[0]["weight_decay"]) == 0.0):
+            # (plain SGD without momentum or weight decay leaves g = 0 rows unchanged: nothing to defer)
             if not 1 <= replay_slices <= 255:
                 raise ValueError("ttamm: replay_slices must be in [1, 255]")
             tables = []
@@ -408,8 +415,20 @@ class FusedTrainStep:
             hp.momentum = float(g["momentum"])
             hp.dampening = float(g["dampening"])
             hp.nesterov = 1 if g["nesterov"] else 0
-            # torch creates every momentum buffer at the first step that has gradients
-            hp.sgd_first_step = 1 if self._sgd_buffers else 0
+            # torch creates a momentum buffer at its parameter's first step (buf = grad.clone()),
+            # later buf = momentum buf + (1 - dampening) grad.  With dampening == 0 (the reference
+            # never sets it) a zero buffer's normal update IS grad, so buffers created here start at
+            # zero and no first-step flag is needed; with dampening the flag is one per step, so a
+            # state where some buffers exist and others do not cannot be stepped exactly
+            if self._sgd_buffers and hp.dampening != 0.0:
+                created = {id(p) for p, _ in self._sgd_buffers}
+                if any(id(p) not in created for p in _dense_params(self.dense_opt)):
+                    raise NotImplementedError(
+                        "ttamm: SGD with dampening and momentum buffers for only some parameters (a partly "
+                        "initialised optimizer state) is not implemented")
+                hp.sgd_first_step = 1
+            else:
+                hp.sgd_first_step = 0
         elif self.dense_opt is not None:
             g = self.dense_opt.param_groups[0]
             hp.lr = float(g["lr"])
@@ -529,6 +548,9 @@ class FusedTrainStep:
             st["step"].fill_(float(self.dense_step0 + self.steps_done))
         for st in self._sparse_steps:
             st["step"] = self.sparse_step0 + self.steps_done
+        if status & _lib.STATUS_LOOKAHEAD_MISMATCH:
+            raise ValueError("ttamm: a row-sharded step was called with a batch other than the one its look-ahead "
+                             "(next_batch=) prepared; that step was skipped on the rank that got it")
         if status & _lib.STATUS_INDEX_OUT_OF_RANGE:
             raise IndexError("index out of range in self")
         if status & _lib.STATUS_SAMPLER_EXHAUSTED:
