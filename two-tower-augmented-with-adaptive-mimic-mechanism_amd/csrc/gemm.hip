@@ -717,6 +717,14 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 // x -> (hi, mid, lo) bf16 quadruples, 8 bytes each
 template <int PL>
 __device__ __forceinline__ void split_bf16(float4 v, uint2 out[PL]) {
+#if TTAMM_X_ABLATE == 4  // developer ablation 4: no split arithmetic (the raw bits as planes)
+    out[0] = uint2{__float_as_uint(v.x), __float_as_uint(v.y)};
+    if constexpr (PL == 3) {
+        out[1] = uint2{__float_as_uint(v.z), __float_as_uint(v.w)};
+        out[2] = out[0];
+    }
+    return;
+#endif
     const f32x4e x = {v.x, v.y, v.z, v.w};
     const bf16x4 h = __builtin_convertvector(x, bf16x4);
     out[0] = __builtin_bit_cast(uint2, h);
@@ -834,6 +842,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
         for (int j = 0; j < J; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    // weight gradients with b_colsum: the blocks of M-tile 0 sum the dY values they stage (the
+    // bias gradient, written to C row M after the main loop)
+    constexpr bool CSUM = AK && BKM;
+    const bool colsum = CSUM && P.b_colsum && tm == 0;
+    float4 bsum[CSUM ? CX::B_LOADS : 1];
+#pragma unroll
+    for (int it = 0; it < (CSUM ? CX::B_LOADS : 1); ++it) bsum[it] = make_float4(0.f, 0.f, 0.f, 0.f);
     // 16-k tiles: two register sets (the tile two ahead in flight); 32-k tiles (bf16): one set
     // (the register budget), loaded at a step's start and written after its MFMAs
     constexpr bool XDEEP = KT == 16;
@@ -880,7 +895,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
         };
         // staged item q (A loads first, then B loads) of register sets SA (A) / SB (B) -> its
         // planes in buffer Buf
-        auto store_item2 = [&](auto SA, auto SB, auto Buf, int q, int k0) {
+        // fresh: the k-tile is not a clamped repeat of the last one (kof) — its B values are summed once
+        auto store_item2 = [&](auto SA, auto SB, auto Buf, int q, int k0, bool fresh) {
             constexpr int RA = decltype(SA)::value, RB = decltype(SB)::value;
             unsigned char* Ap = lds + decltype(Buf)::value * CX::buf_bytes(PL);
             unsigned char* Bp = Ap + PL * CX::A_PLANE;
@@ -912,6 +928,17 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
                     const int kr = lin / (BN / 4), nc = (lin % (BN / 4)) * 4;
                     v = FAST ? rb[RB][it] : mask4(rb[RB][it], n0 + nc, N, P.ldb, -1, k0 + kr < k_end);
                     off = kr * CX::SB + nc * 2;
+                    if constexpr (CSUM) {
+                        if (colsum && fresh) {
+                            float4 u = v;
+                            if constexpr (PL == 1) {  // bf16 towers: the bias gradient sums bf16(dY)
+                                const f32x4e x = {v.x, v.y, v.z, v.w};
+                                const f32x4e r = __builtin_convertvector(__builtin_convertvector(x, bf16x4), f32x4e);
+                                u = make_float4(r[0], r[1], r[2], r[3]);
+                            }
+                            bsum[it].x += u.x, bsum[it].y += u.y, bsum[it].z += u.z, bsum[it].w += u.w;
+                        }
+                    }
                 }
                 base = Bp;
                 plane = CX::B_PLANE;
@@ -921,16 +948,16 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
 #pragma unroll
             for (int pl = 0; pl < PL; ++pl) *reinterpret_cast<uint2*>(base + pl * plane + off) = w[pl];
         };
-        auto store_item = [&](auto S, auto Buf, int q, int k0) { store_item2(S, S, Buf, q, k0); };
+        auto store_item = [&](auto S, auto Buf, int q, int k0, bool fresh) { store_item2(S, S, Buf, q, k0, fresh); };
         constexpr int NITEMS = CX::A_LOADS + CX::B_LOADS;
-        auto store_tile = [&](auto S, auto Buf, int k0) {
+        auto store_tile = [&](auto S, auto Buf, int k0, bool fresh) {
 #pragma unroll
-            for (int q = 0; q < NITEMS; ++q) store_item(S, Buf, q, k0);
+            for (int q = 0; q < NITEMS; ++q) store_item(S, Buf, q, k0, fresh);
         };
         // multiply the k-tile in buffer Buf; the split + LDS writes of the next k-tile (register
         // set S -> buffer NB) are spread between the MFMA groups so the vector work issues in the
         // matrix pipe's shadow
-        auto compute2 = [&](auto Buf, auto SA, auto SB, auto NB, int k0n) {
+        auto compute2 = [&](auto Buf, auto SA, auto SB, auto NB, int k0n, bool fresh) {
             const unsigned char* Ap = lds + decltype(Buf)::value * CX::buf_bytes(PL);
             const unsigned char* Bp = Ap + PL * CX::A_PLANE;
             constexpr int NP = I * J, KS = KT / 16, NSLOT = KS * NP;
@@ -962,13 +989,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
                         const int slot = ks * NP + pq;
 #pragma unroll
                         for (int q = (slot * NITEMS) / NSLOT; q < ((slot + 1) * NITEMS) / NSLOT; ++q)
-                            store_item2(SA, SB, NB, q, k0n);
+                            store_item2(SA, SB, NB, q, k0n, fresh);
                     }
 #endif
                 }
             }
         };
-        auto compute = [&](auto Buf, auto S, auto NB, int k0n) { compute2(Buf, S, S, NB, k0n); };
+        auto compute = [&](auto Buf, auto S, auto NB, int k0n, bool fresh) { compute2(Buf, S, S, NB, k0n, fresh); };
         using S0 = std::integral_constant<int, 0>;
         using S1 = std::integral_constant<int, 1>;
         const int nk = k_end > k_begin ? (k_end - k_begin + KT - 1) / KT : 0;
@@ -978,15 +1005,15 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
         auto kof = [&](int kt) { return k_begin + min(kt, nk - 1) * KT; };
         if constexpr (!XDEEP) {
             load_tile(S0{}, kof(0));
-            store_tile(S0{}, S0{}, kof(0));
+            store_tile(S0{}, S0{}, kof(0), true);
             __syncthreads();
             auto sstep = [&](auto Buf, auto NB, int kt) {
 #if TTAMM_X_ABLATE != 3
                 load_tile(S0{}, kof(kt + 1));
 #endif
-                compute(Buf, S0{}, NB, kof(kt + 1));
+                compute(Buf, S0{}, NB, kof(kt + 1), kt + 1 < nk);
 #if TTAMM_X_ABLATE != 3
-                store_tile(S0{}, NB, kof(kt + 1));
+                store_tile(S0{}, NB, kof(kt + 1), kt + 1 < nk);
 #endif
                 __syncthreads();
             };
@@ -1003,7 +1030,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
             // B set (i + 1) & 1) into the other buffer: A two k-tiles ahead, B one.
             using S2 = std::integral_constant<int, 2>;
             load_tile(S0{}, kof(0));
-            store_tile(S0{}, S0{}, kof(0));
+            store_tile(S0{}, S0{}, kof(0), true);
             load_tile(S1{}, kof(1));
             load_a(S2{}, kof(2));
             __syncthreads();
@@ -1017,7 +1044,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
                 load_a(LA{}, kof(kt + 3));
                 load_b(Buf{}, kof(kt + 2));
 #endif
-                compute2(Buf{}, SA{}, NB{}, NB{}, kof(kt + 1));
+                compute2(Buf{}, SA{}, NB{}, NB{}, kof(kt + 1), kt + 1 < nk);
                 __syncthreads();
             };
             int kt = 0;
@@ -1036,7 +1063,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
             if (kt + 4 < nk) step3(std::integral_constant<int, 4>{}, kt + 4);
         } else {
             load_tile(S0{}, kof(0));
-            store_tile(S0{}, S0{}, kof(0));
+            store_tile(S0{}, S0{}, kof(0), true);
             load_tile(S1{}, kof(1));
             __syncthreads();
             // k-tile kt: register set kt & 1, LDS buffer kt & 1.  Prefetch kt + 2 into the set tile
@@ -1046,7 +1073,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
 #if TTAMM_X_ABLATE != 3  // developer ablation 3: no k-loop traffic (MFMA + LDS reads only)
                 load_tile(Bf, kof(kt + 2));
 #endif
-                compute(Bf, NB, NB, kof(kt + 1));
+                compute(Bf, NB, NB, kof(kt + 1), kt + 1 < nk);
                 __syncthreads();
             };
             int kt = 0;
@@ -1059,6 +1086,31 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
     };
     if (fast) mainloop(std::true_type{});
     else mainloop(std::false_type{});
+
+    if constexpr (CSUM) {
+        // bias gradient of this split: the column sums of dY, reduced over the k rows of a tile in a
+        // fixed order (every (k row, column) slot of the staging map belongs to one thread) and
+        // written to row M of the split's slab
+        static_assert(KT * BN * 4 <= CX::lds_bytes(PL), "column-sum scratch fits the staging LDS");
+        if (colsum) {
+            float* red = reinterpret_cast<float*>(lds);
+            __syncthreads();
+#pragma unroll
+            for (int it = 0; it < CX::B_LOADS; ++it) {
+                const int lin = tid + it * kThreads;
+                if (CX::B_F4 % kThreads && lin >= CX::B_F4) continue;
+                const int kr = lin / (BN / 4), nc = (lin % (BN / 4)) * 4;
+                *reinterpret_cast<float4*>(red + kr * BN + nc) = bsum[it];
+            }
+            __syncthreads();
+            for (int c = tid; c < BN; c += kThreads) {
+                float acc_s = 0.f;
+                for (int kr = 0; kr < KT; ++kr) acc_s += red[kr * BN + c];
+                if (n0 + c < N) P.C[(int64_t)split * P.slab_stride + (int64_t)M * P.ldc + n0 + c] = acc_s;
+            }
+            __syncthreads();
+        }
+    }
 
     // ---- epilogue through LDS, in row slices (as gemm_kernel) ---------------------------------
     float* Cs = reinterpret_cast<float*>(lds);
@@ -1408,6 +1460,35 @@ int dispatch_x(GemmBatch& b, hipStream_t s) {
     if (adeep2 || AK || BK) return dispatch_epi_x<XCfg<BM, BN, WM, WN, AK, BK, 16>, 3>(b, s);
     return dispatch_epi_x<XCfg<BM, BN, WM, WN, AK, BK, 16, 3>, 3>(b, s);
 }
+// Output tile width of a forward / dgrad launch: the width with the least padded output columns
+// over the batch (ties: the first listed).  Layer widths that are multiples of 128 but not of 192
+// (C4's 128 / 256, C5's 256 / 512) lost a third of the MFMA work to 128 x 192 tiles.  Latency-
+// bound launches (dgrad, or few 128-row tiles) take the narrow set, which keeps more blocks.
+int pick_tile_n(const GemmBatch& b, bool narrow, bool bf16) {
+    static const bool legacy = [] {
+        const char* e = std::getenv("TTAMM_GEMM_TILES");
+        return e && std::strcmp(e, "legacy") == 0;
+    }();
+    int maxN = 0;
+    for (int i = 0; i < b.count; ++i) maxN = b.p[i].N > maxN ? b.p[i].N : maxN;
+    if (maxN <= 96) return 96;
+    if (legacy) return narrow ? 96 : 192;
+    // (128 x 256 tiles were built and measured: the bf16 kernel spills 200-350 B of scratch per
+    // thread at two waves per SIMD; two 128-wide tiles cover 256 with no padding)
+    (void)bf16;
+    static const int kNarrow[] = {96, 128};
+    static const int kWide[] = {192, 128, 96};
+    const int* c = narrow ? kNarrow : kWide;
+    const int nc = narrow ? 2 : 3;
+    int best = c[0];
+    int64_t best_cols = -1;
+    for (int j = 0; j < nc; ++j) {
+        int64_t cols = 0;
+        for (int i = 0; i < b.count; ++i) cols += ceil_div(b.p[i].M, 128) * ceil_div(b.p[i].N, c[j]) * c[j];
+        if (best_cols < 0 || cols < best_cols) best_cols = cols, best = c[j];
+    }
+    return best;
+}
 
 // Matrix-core path of the fp32 / bf16 GEMMs: the split-bf16 kernel (default), or with
 // TTAMM_FP32_MFMA=exact the v_mfma_f32_32x32x2_f32 kernel (exact fp32 products; bf16 towers
@@ -1503,12 +1584,17 @@ int launch_gemm(GemmBatch& b, hipStream_t s) {
     // blocks on 128 x 96 tiles hide more of it (C2 0.638 -> 0.630-0.635 ms, profiles/r04_dgrad_tiles_s31.txt)
     const bool narrow_tiles = (wide_tiles < 300 || bkn) && std::getenv("TTAMM_GEMM_WIDE_TILES") == nullptr;
     if (!exact_mfma()) {
-        if (maxN > 96 && !narrow_tiles) {
-            if (bkn) return dispatch_x<128, 192, 2, 2, false, true>(b, s);
-            return dispatch_x<128, 192, 2, 2, false, false>(b, s);
+        switch (pick_tile_n(b, narrow_tiles, b.p[0].bf16 != 0)) {
+            case 192:
+                if (bkn) return dispatch_x<128, 192, 2, 2, false, true>(b, s);
+                return dispatch_x<128, 192, 2, 2, false, false>(b, s);
+            case 128:
+                if (bkn) return dispatch_x<128, 128, 2, 2, false, true>(b, s);
+                return dispatch_x<128, 128, 2, 2, false, false>(b, s);
+            default:
+                if (bkn) return dispatch_x<128, 96, 4, 1, false, true>(b, s);
+                return dispatch_x<128, 96, 4, 1, false, false>(b, s);
         }
-        if (bkn) return dispatch_x<128, 96, 4, 1, false, true>(b, s);
-        return dispatch_x<128, 96, 4, 1, false, false>(b, s);
     }
     if (maxN > 96) {
         if (bkn) return dispatch_epi<Cfg<128, 192, 2, 2, false, true>>(b, s);
@@ -1528,19 +1614,27 @@ using WgradNarrowX = XCfg<128, 96, 4, 1, true, true>;
 using WgradNarrowXA3 = XCfg<128, 96, 4, 1, true, true, 16, 3>;
 using WgradWideX32 = XCfg<128, 192, 2, 2, true, true, 32>;
 using WgradNarrowX32 = XCfg<128, 96, 4, 1, true, true, 32>;
-int wgrad_slots(bool wide, bool exact) {
-    static int cached[2][2] = {{0, 0}, {0, 0}};
-    if (cached[exact][wide]) return cached[exact][wide];
+using Wgrad128X = XCfg<128, 128, 2, 2, true, true>;
+using Wgrad128X32 = XCfg<128, 128, 2, 2, true, true, 32>;
+// resident blocks of a weight-gradient class's launch configuration (fp32 split kernels; the
+// exact fp32-MFMA kernels have two classes)
+int wgrad_slots(int cls, bool exact) {
+    static int cached[2][kWgradClasses] = {};
+    if (exact) cls = cls == 0 ? 0 : 1;
+    if (cached[exact][cls]) return cached[exact][cls];
     int dev = 0, cus = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* k = exact ? (wide ? (const void*)gemm_kernel<WgradWide, EPI_STORE, false>
-                                  : (const void*)gemm_kernel<WgradNarrow, EPI_STORE, false>)
-                          : (wide ? (const void*)gemm_x_kernel<WgradWideX, EPI_STORE, 3>
-                                  : (const void*)gemm_x_kernel<WgradNarrowX, EPI_STORE, 3>);
+    const void* k = exact ? (cls ? (const void*)gemm_kernel<WgradWide, EPI_STORE, false>
+                                 : (const void*)gemm_kernel<WgradNarrow, EPI_STORE, false>)
+                          : cls == 0 ? (const void*)gemm_x_kernel<WgradNarrowX, EPI_STORE, 3>
+                          : cls == 1 ? (const void*)gemm_x_kernel<WgradWideX, EPI_STORE, 3>
+                                     : (const void*)gemm_x_kernel<Wgrad128X, EPI_STORE, 3>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kThreads, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-    cached[exact][wide] = cus * per_cu;
-    return cached[exact][wide];
+    cached[exact][cls] = cus * per_cu;
+    return cached[exact][cls];
 }
+// output tile width of a class: 96, 192, 128, and class 3 (multiples of 256) on 128-wide tiles
+constexpr int kWgradTileN[kWgradClasses] = {96, 192, 128, 128};
 }  // namespace
 
 // Rows per split-K chunk of a step's weight gradients, chosen per tile class (the wide and the
@@ -1549,19 +1643,20 @@ int wgrad_slots(bool wide, bool exact) {
 // a block), plus the fixed-order reduce over the slabs (splits x M x (N + 1) floats written and
 // read at HBM speed).  Narrow gradients (M <= 96) are latency-bound per k-tile, so they want
 // many short splits; wide ones fill the chip with few.
-void wgrad_rows_per_split(const WgradShape* shapes, int n, int rps[2]) {
+void wgrad_rows_per_split(const WgradShape* shapes, int n, int rps[kWgradClasses]) {
     // developer / test override (tests/test_step_parity_gpu.py covers splits past 512 rows)
     if (const char* e = std::getenv("TTAMM_WGRAD_ROWS_PER_SPLIT")) {
         const int v = std::atoi(e);
         if (v >= BK && v <= kWgradMaxRowsPerSplit && v % BK == 0) {
-            rps[0] = rps[1] = v;
+            for (int c = 0; c < kWgradClasses; ++c) rps[c] = v;
             return;
         }
     }
     const bool exact = exact_mfma();
-    const double us_per_row[2] = {0.11, 0.14};  // block time per split row (MI355X, C2 shapes)
+    // block time per split row (MI355X; 96 / 192 measured at C2, 128 / 256 scaled by tile width)
+    const double us_per_row[kWgradClasses] = {0.11, 0.14, 0.12, 0.12};
     const double hbm_us_per_byte = 1.0 / 5.0e6;  // ~5 TB/s
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < kWgradClasses; ++c) {
         int best = 512;
         double best_cost = -1.0;
         for (int r = 128; r <= kWgradMaxRowsPerSplit; r += 32) {
@@ -1570,11 +1665,11 @@ void wgrad_rows_per_split(const WgradShape* shapes, int n, int rps[2]) {
             for (int i = 0; i < n; ++i) {
                 if (shapes[i].R <= 0 || wgrad_class(shapes[i].M) != c) continue;
                 const int64_t splits = ceil_div(shapes[i].R, r);
-                tiles += ceil_div(shapes[i].N + 1, 128) * ceil_div(shapes[i].M, c ? 192 : 96) * splits;
+                tiles += ceil_div(shapes[i].N + 1, 128) * ceil_div(shapes[i].M, kWgradTileN[c]) * splits;
                 slab_bytes += 2.0 * 4.0 * (double)splits * shapes[i].M * (shapes[i].N + 1);
             }
             if (tiles == 0) break;
-            const double cost = (double)ceil_div(tiles, wgrad_slots(c == 1, exact)) * r * us_per_row[c] +
+            const double cost = (double)ceil_div(tiles, wgrad_slots(c, exact)) * r * us_per_row[c] +
                                 slab_bytes * hbm_us_per_byte;
             if (best_cost < 0.0 || cost < best_cost) {
                 best_cost = cost;
@@ -1592,7 +1687,18 @@ size_t wgrad_slab_floats(int R, int M, int N, int rps) {
 
 int wgrad_class(int m_out) {
     static const bool all_narrow = std::getenv("TTAMM_WGRAD_ALL_NARROW") != nullptr;
-    return m_out > 96 && !all_narrow ? 1 : 0;
+    static const bool legacy = [] {
+        const char* e = std::getenv("TTAMM_GEMM_TILES");
+        return e && std::strcmp(e, "legacy") == 0;
+    }();
+    if (all_narrow || m_out <= 96) return 0;
+    if (legacy) return 1;
+    auto pad = [&](int bn) { return ceil_div(m_out, bn) * bn; };
+    int best = 1;  // 192
+    int64_t bp = pad(192);
+    if (pad(256) < bp) best = 3, bp = pad(256);
+    if (pad(128) < bp) best = 2, bp = pad(128);
+    return best;
 }
 
 // TTAMM_WGRAD_ADEEP=3: the narrow weight-gradient launch's X operand two k-tiles ahead
@@ -1607,24 +1713,33 @@ static bool wgrad_a3() {
 // Weight gradients as C = X^T dY (M = n_in + 1 incl. the ones column, N = m_out, K = rows),
 // both operands K-major; one launch per tile configuration, then one fixed-order reduce.
 int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
-    GemmBatch wide, narrow;  // m_out > 96 / <= 96
-    std::memset(&wide, 0, sizeof(wide));
-    std::memset(&narrow, 0, sizeof(narrow));
+    // one launch per tile configuration: class 0 (128 x 96), 1 (128 x 192), 2 and 3 (128 x 128; a
+    // 128 x 256 bf16 tile spilled 132 B of scratch per thread)
+    GemmBatch g[kWgradClasses];
+    std::memset(g, 0, sizeof(g));
     const bool bf = wb.count > 0 && wb.p[0].bf16;
     const bool exact = exact_mfma();
-    auto flush = [&](GemmBatch& g, bool is_wide) -> int {
-        if (g.count == 0) return TTAMM_OK;
+    auto cfg_of = [&](int cls) {
+        if (exact) return cls == 0 ? 0 : 1;  // the fp32-MFMA kernels: narrow / wide
+        return cls == 3 ? 2 : cls;
+    };
+    auto flush = [&](GemmBatch& b, int cfg) -> int {
+        if (b.count == 0) return TTAMM_OK;
         int rc;
-        if (!exact)
-            rc = is_wide ? (bf ? launch_one_x<WgradWideX32, EPI_STORE, 1>(g, s) : launch_one_x<WgradWideX, EPI_STORE, 3>(g, s))
-                         : (bf ? launch_one_x<WgradNarrowX32, EPI_STORE, 1>(g, s)
-                               : wgrad_a3() ? launch_one_x<WgradNarrowXA3, EPI_STORE, 3>(g, s)
-                                            : launch_one_x<WgradNarrowX, EPI_STORE, 3>(g, s));
-        else
-            rc = is_wide ? (bf ? launch_one<WgradWide, EPI_STORE, true>(g, s) : launch_one<WgradWide, EPI_STORE, false>(g, s))
-                         : (bf ? launch_one<WgradNarrow, EPI_STORE, true>(g, s)
-                               : launch_one<WgradNarrow, EPI_STORE, false>(g, s));
-        std::memset(&g, 0, sizeof(g));
+        if (exact) {
+            rc = cfg ? (bf ? launch_one<WgradWide, EPI_STORE, true>(b, s) : launch_one<WgradWide, EPI_STORE, false>(b, s))
+                     : (bf ? launch_one<WgradNarrow, EPI_STORE, true>(b, s) : launch_one<WgradNarrow, EPI_STORE, false>(b, s));
+        } else if (bf) {
+            rc = cfg == 0   ? launch_one_x<WgradNarrowX32, EPI_STORE, 1>(b, s)
+                 : cfg == 1 ? launch_one_x<WgradWideX32, EPI_STORE, 1>(b, s)
+                            : launch_one_x<Wgrad128X32, EPI_STORE, 1>(b, s);
+        } else {
+            rc = cfg == 0   ? (wgrad_a3() ? launch_one_x<WgradNarrowXA3, EPI_STORE, 3>(b, s)
+                                          : launch_one_x<WgradNarrowX, EPI_STORE, 3>(b, s))
+                 : cfg == 1 ? launch_one_x<WgradWideX, EPI_STORE, 3>(b, s)
+                            : launch_one_x<Wgrad128X, EPI_STORE, 3>(b, s);
+        }
+        std::memset(&b, 0, sizeof(b));
         return rc;
     };
     int64_t total = 0;
@@ -1648,11 +1763,14 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
         p.lda = w.ld_x;
         p.a_kmaj = 1;
         p.a_cols = w.N;
-        p.a_ones_col = w.N;
         p.B = w.dY;
         p.ldb = w.ld_dy;
         p.b_kn = 1;
-        p.M = w.N + 1;
+        // split kernels: the bias gradient as column sums of dY in the M-tile-0 blocks (b_colsum),
+        // so M = n_in; the fp32-MFMA kernels keep the implicit ones column (M = n_in + 1)
+        p.b_colsum = exact ? 0 : 1;
+        p.a_ones_col = exact ? w.N : -1;
+        p.M = exact ? w.N + 1 : w.N;
         p.N = w.M;
         p.K = w.R;
         p.k_split = w.rows_per_split;
@@ -1663,26 +1781,28 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
         p.keep_prob = 1.f;
         p.inv_keep = 1.f;
         p.bf16 = w.bf16;
-        const bool is_wide = wgrad_class(w.M) == 1;
-        GemmBatch& g = is_wide ? wide : narrow;
-        if (g.count == kMaxGemmProblems) {
-            const int rc = flush(g, is_wide);
+        const int cfg = cfg_of(wgrad_class(w.M));
+        if (g[cfg].count == kMaxGemmProblems) {
+            const int rc = flush(g[cfg], cfg);
             if (rc) return rc;
         }
-        g.p[g.count++] = p;
+        g[cfg].p[g[cfg].count++] = p;
     }
     int rc;
-    const bool timed = ev && ev[0] && ev[1] && wide.count > 0;
-    // The narrow launch (latency-bound: many short splits) first, then the wide one (MFMA-bound),
+    bool any_wide = false;
+    for (int c = 1; c < kWgradClasses; ++c) any_wide = any_wide || g[c].count > 0;
+    const bool timed = ev && ev[0] && ev[1] && any_wide;
+    // The narrow launch (latency-bound: many short splits) first, then the wide ones (MFMA-bound),
     // which the aux stream's memory-bound row updates then run beside: C2 0.660 -> 0.652 ms,
     // the emulated 8-rank C2 0.804 -> 0.769 ms (profiles/r04_wgrad_order_s22.txt).
     // TTAMM_WGRAD_WIDE_FIRST=1: the old order.
     static const bool narrow_first = std::getenv("TTAMM_WGRAD_WIDE_FIRST") == nullptr;
-    if (narrow_first && (rc = flush(narrow, false))) return rc;
+    if (narrow_first && (rc = flush(g[0], 0))) return rc;
     if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)ev[0], s));
-    if ((rc = flush(wide, true))) return rc;
+    for (int c = 1; c < kWgradClasses; ++c)
+        if ((rc = flush(g[c], c))) return rc;
     if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)ev[1], s));
-    if (!narrow_first && (rc = flush(narrow, false))) return rc;
+    if (!narrow_first && (rc = flush(g[0], 0))) return rc;
     if (total > 0) {
         hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, s, wb, total);
         TTAMM_LAUNCH_CHECK();

@@ -59,6 +59,11 @@ struct GemmProblem {
     int a_kmaj;
     int a_cols;          // valid columns of X (m < a_cols)
     int a_ones_col;      // column of implicit ones (bias gradient), -1 = none
+    // K-major B (weight gradient, split kernel): the blocks of M-tile 0 also sum B over their k
+    // rows (bf16-rounded when bf16) and write the column sums to C row M of their split's slab —
+    // the bias gradient without an implicit ones column (which cost a whole extra M-tile when
+    // n_in is a multiple of the tile height: 512 + 1 = five 128-row tiles)
+    int b_colsum;
     // split-K over rows: each split writes its own slab at C + split * slab_stride
     int k_split;
     int64_t slab_stride;
@@ -131,14 +136,16 @@ struct WgradShape {
     int64_t R;  // rows
     int M, N;   // out features, in features
 };
-// tile class of a weight gradient: m_out > 96 runs on the wide tile configuration
-// weight-gradient tile class: 1 = wide (128 x 192 tiles, m_out > 96), 0 = narrow (128 x 96);
-// TTAMM_WGRAD_ALL_NARROW=1 (developer switch) puts every problem in the narrow class
+// weight-gradient tile class (the output tile width over m_out, the least padding):
+// 0 = 128 x 96 (m_out <= 96), 1 = 128 x 192, 2 = 128 x 128, 3 = multiples of 256 (on 128 x 128
+// tiles, their own split size); TTAMM_WGRAD_ALL_NARROW=1 (developer switch) puts every problem in
+// class 0
+constexpr int kWgradClasses = 4;
 int wgrad_class(int m_out);
-// rows per split-K chunk for each class ([0] narrow, [1] wide) of a step's weight gradients
-void wgrad_rows_per_split(const WgradShape* shapes, int n, int rps[2]);
+// rows per split-K chunk for each class of a step's weight gradients
+void wgrad_rows_per_split(const WgradShape* shapes, int n, int rps[kWgradClasses]);
 size_t wgrad_slab_floats(int R, int M, int N, int rows_per_split);
-// ev (optional, 2 hipEvent_t): recorded around the wide tile class's GEMM launch
+// ev (optional, 2 hipEvent_t): recorded around the launches of every class but the narrow one
 int launch_wgrad(WgradBatch& batch, hipStream_t s, void* const* ev = nullptr);
 
 // ------------------------------------------------------------------------------------

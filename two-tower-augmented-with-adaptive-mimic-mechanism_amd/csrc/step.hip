@@ -83,7 +83,7 @@ struct TowerWs {
     float* piece_a = nullptr;
     float* wpad = nullptr;  // first feature layer weight, in_features padded to a multiple of 4
     uint16_t* w16 = nullptr;  // bf16 towers with bf16 feature rows: the weight rounded, padded to % 8
-    int wgrad_rps[2] = {512, 512};  // split-K rows of the weight gradients, per tile class (wgrad_class)
+    int wgrad_rps[kWgradClasses] = {512, 512, 512, 512};  // split-K rows of the weight gradients, per tile class
 };
 
 struct StepWs {
@@ -281,9 +281,9 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         WgradShape shapes[2 * (TTAMM_MAX_LINEAR + 2)];
         int n = wgrad_shapes(A.user, B, shapes);
         n += wgrad_shapes(A.item, shard ? A.item_rows_capacity : B * (1 + N), shapes + n);
-        int rps[2];
+        int rps[kWgradClasses];
         wgrad_rows_per_split(shapes, n, rps);
-        for (int c = 0; c < 2; ++c) ws.user.wgrad_rps[c] = ws.item.wgrad_rps[c] = rps[c];
+        for (int c = 0; c < kWgradClasses; ++c) ws.user.wgrad_rps[c] = ws.item.wgrad_rps[c] = rps[c];
     }
     // ext_io: the item tower's t / a / dT / dA live in the caller's exchange buffers
     auto tower = [&](const ttamm_tower& T, TowerWs& w, int64_t R, bool ext_io, int64_t dA_rows) {
@@ -2101,10 +2101,9 @@ void plan_tower_train(Arena& ar, const ttamm_tower& T, int64_t n, TowerWs& w) {
     }
     WgradShape shapes[TTAMM_MAX_LINEAR + 2];
     const int ns = wgrad_shapes(T, n, shapes);
-    int rps[2] = {512, 512};
+    int rps[kWgradClasses] = {512, 512, 512, 512};
     if (ns) wgrad_rows_per_split(shapes, ns, rps);
-    w.wgrad_rps[0] = rps[0];
-    w.wgrad_rps[1] = rps[1];
+    for (int c = 0; c < kWgradClasses; ++c) w.wgrad_rps[c] = rps[c];
     if (T.fusion != TTAMM_FUSION_IDENTITY) {
         for (int l = 0; l < T.n_linear; ++l) {
             const ttamm_linear& L = T.linear[l];

@@ -197,7 +197,7 @@ int main() {
         w.dY = dY, w.ld_dy = H, w.X = X, w.x_idx = idx, w.ld_x = F, w.R = R, w.M = H, w.N = F - 3;
         w.grad_w = gw, w.grad_b = gb, w.slab = slab;
         const WgradShape sh{w.R, w.M, w.N};
-        int rps[2];
+        int rps[kWgradClasses];
         wgrad_rows_per_split(&sh, 1, rps);
         w.rows_per_split = rps[wgrad_class(w.M)];
         wb.p[0] = w, wb.count = 1;
@@ -210,7 +210,7 @@ int main() {
         w.dY = dF, w.ld_dy = D, w.X = Hb, w.ld_x = H, w.R = R, w.M = D, w.N = H;
         w.grad_w = gw, w.grad_b = gb, w.slab = slab;
         const WgradShape sh{w.R, w.M, w.N};
-        int rps[2];
+        int rps[kWgradClasses];
         wgrad_rows_per_split(&sh, 1, rps);
         w.rows_per_split = rps[wgrad_class(w.M)];
         wb.p[0] = w, wb.count = 1;

@@ -162,7 +162,7 @@ int main(int argc, char** argv) {
         w.dY = dy, w.ld_dy = ldy, w.X = x, w.x_idx = xi, w.ld_x = ldx, w.R = R, w.M = M, w.N = N;
         w.grad_w = gw, w.grad_b = gb, w.slab = slab, w.bf16 = 1;
         const WgradShape sh{w.R, w.M, w.N};
-        int rps[2];
+        int rps[kWgradClasses];
         wgrad_rows_per_split(&sh, 1, rps);
         w.rows_per_split = rps[wgrad_class(w.M)];
         wb.p[0] = w, wb.count = 1;
