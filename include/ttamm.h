@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 22
+#define TTAMM_ABI_VERSION 23
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -196,6 +196,14 @@ typedef struct ttamm_tower {
      * GEMM then streams bf16 operands (same values, half the bytes) on bf16 MFMA. */
     const uint16_t* features_bf16;
     int64_t feat_bf16_ld;
+    /* fp32 towers, optional: the feature rows pre-split into bf16 planes (ttamm_to_planes),
+     * [id.rows, feat_planes_ld] uint16 with row r's k-tile t (features 16 t .. 16 t + 15) at
+     * 48 t: hi[16], mid[16], lo[16] (hi + mid + lo == the fp32 value exactly), feat_planes_ld >=
+     * 48 ceil(feat_dim / 16).  The first feature layer's forward GEMM and its weight gradient then
+     * stage these planes instead of splitting the fp32 rows in every k-tile (same products, same
+     * bits). */
+    const uint16_t* features_planes;
+    int64_t feat_planes_ld;
 } ttamm_tower;
 
 /* Optimizer hyper-parameters for one step, as the Python floats torch holds (double).
@@ -414,6 +422,13 @@ int ttamm_candidate_topk(const float* queries, int64_t n_queries, int64_t ldq, c
  * bf16 feature copy of a matmul_bf16 tower (ttamm_tower.features_bf16). */
 int ttamm_to_bf16(const float* src, int64_t rows, int32_t cols, int64_t ld_src, uint16_t* dst, int64_t ld_dst,
                   void* stream);
+
+/* The bf16 planes of fp32 rows (ttamm_tower.features_planes): for c < cols, x = src[r, c],
+ * hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid) (round to nearest even, every
+ * difference exact) at dst[r * ld_dst + 48 (c / 16) + {0, 16, 32} + c % 16]; zero for
+ * cols <= c < 16 ceil(cols / 16).  ld_dst >= 48 ceil(cols / 16), a multiple of 8. */
+int ttamm_to_planes(const float* src, int64_t rows, int32_t cols, int64_t ld_src, uint16_t* dst, int64_t ld_dst,
+                    void* stream);
 
 /* DataLoader(InteractionDataset(train_df), batch_size, shuffle, drop_last=False)
  * (datasets.py:12-45, training.py:260-264) over pairs resident in HBM: writes positions

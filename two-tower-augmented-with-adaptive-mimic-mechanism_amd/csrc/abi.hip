@@ -91,6 +91,12 @@ TTAMM_API int ttamm_to_bf16(const float* src, int64_t rows, int32_t cols, int64_
     return launch_to_bf16(src, rows, cols, ld_src, dst, ld_dst, (hipStream_t)stream);
 }
 
+TTAMM_API int ttamm_to_planes(const float* src, int64_t rows, int32_t cols, int64_t ld_src, uint16_t* dst,
+                              int64_t ld_dst, void* stream) {
+    g_last_error.clear();
+    return launch_to_planes(src, rows, cols, ld_src, dst, ld_dst, (hipStream_t)stream);
+}
+
 TTAMM_API int ttamm_epoch_batch(const int64_t* users, const int64_t* items, int64_t n, uint64_t seed, int64_t epoch,
                                 int32_t shuffle, int64_t start, int64_t count, int64_t* out_users, int64_t* out_items,
                                 void* stream) {

@@ -669,15 +669,20 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
 //   K-major operand:  [16 k][mn] bf16, row stride = 64 or 192 (mod 256) bytes — fragments are
 //                     two ds_read_b64_tr_b16 (hardware transpose: lane i of a 16-lane group gets
 //                     column i of a 4 x 16 block), conflict-free per 32-lane half.
-template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KMAJ_, bool B_KMAJ_, int KT_ = 16, int AD_ = 2>
+template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KMAJ_, bool B_KMAJ_, int KT_ = 16, int AD_ = 2,
+          bool APL_ = false>
 struct XCfg {
     static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_;
     static constexpr bool A_KMAJ = A_KMAJ_, B_KMAJ = B_KMAJ_;
     static constexpr int KT = KT_;     // k per tile: 16 (three planes) or 32 (bf16, one plane)
     static constexpr int AD = AD_;     // 16-k tiles: A register sets (3: A loads two k-tiles ahead)
+    // A pre-split in memory (GemmProblem::A3p: [row][k / 16][hi, mid, lo][16] bf16, the feature rows
+    // split once): staged as 16-B pieces of the three planes, no split arithmetic in the loop
+    static constexpr bool APL = APL_;
     static constexpr int RB = KT * 2;  // MN-major row bytes
     static constexpr int TM = BM / WAVES_M, TN = BN / WAVES_N, I = TM / 32, J = TN / 32;
-    static constexpr int A_F4 = BM * KT / 4, B_F4 = BN * KT / 4;
+    static constexpr int A_F4 = APL ? BM * KT * 6 / 16 : BM * KT / 4, B_F4 = BN * KT / 4;
+    static_assert(!APL || KT == 16, "A planes: 16-k tiles (one 96-byte chunk per row and k-tile)");
     static constexpr int A_LOADS = (A_F4 + kThreads - 1) / kThreads;
     static constexpr int B_LOADS = (B_F4 + kThreads - 1) / kThreads;
     static constexpr int kmaj_stride(int mn) {
@@ -713,6 +718,9 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 #ifndef TTAMM_X_ABLATE
 #define TTAMM_X_ABLATE 0
+#endif
+#ifndef TTAMM_BF16_DEEP
+#define TTAMM_BF16_DEEP 1
 #endif
 // x -> (hi, mid, lo) bf16 quadruples, 8 bytes each
 template <int PL>
@@ -802,10 +810,35 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
     const float* a_rp[CX::A_LOADS];
     bool a_ok[CX::A_LOADS];
     int a_r[CX::A_LOADS], a_c[CX::A_LOADS];
+    // A planes: piece lin of a k-tile = (row, plane, 8-k half) — MN-major: row lin / 6, then
+    // (plane, half) = lin % 6; K-major: k row lin / 48, 16-column chunk (lin % 48) / 6, then
+    // (plane, half).  a_c holds the piece's element offset inside the row's planes, relative to the
+    // k-tile's (MN-major) or the M-tile's (K-major) first chunk; a_rp the row (MN-major)
+    const uint16_t* ap_rp[CX::APL ? CX::A_LOADS : 1];
+    int ap_lds[CX::APL ? CX::A_LOADS : 1];  // byte offset in the buffer's A planes
 #pragma unroll
     for (int it = 0; it < CX::A_LOADS; ++it) {
         const int lin = tid + it * kThreads;
-        if (!AK) {
+        if constexpr (CX::APL) {
+            const int ph = AK ? (lin % 48) % 6 : lin % 6, pl = ph >> 1, hf = ph & 1;
+            if (!AK) {
+                a_r[it] = lin / 6;
+                a_c[it] = pl * 16 + hf * 8;
+                const int gm = m0 + a_r[it];
+                a_ok[it] = gm < M;
+                const int gmc = min(gm, M - 1);
+                ap_rp[it] = P.A3p + (P.a_idx ? P.a_idx[gmc] : (int64_t)gmc) * P.lda3;
+                ap_lds[it] = pl * CX::A_PLANE + mn_off<CX::RB>(a_r[it], hf * 8);
+            } else {
+                const int ch = (lin % 48) / 6, last = (P.a_cols + 15) / 16 - 1 - (m0 >> 4);
+                a_r[it] = lin / 48;
+                a_c[it] = min(ch, last) * 48 + pl * 16 + hf * 8;  // loads stay inside the row's planes
+                a_ok[it] = ch <= last;  // chunks past the row's planes: zero
+                ap_rp[it] = P.A3p;
+                ap_lds[it] = pl * CX::A_PLANE + a_r[it] * CX::SA + (ch * 16 + hf * 8) * 2;
+            }
+            a_rp[it] = nullptr;
+        } else if (!AK) {
             a_r[it] = lin / (KT / 4);
             a_c[it] = (lin % (KT / 4)) * 4;
             const int gm = m0 + a_r[it];
@@ -849,9 +882,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
     float4 bsum[CSUM ? CX::B_LOADS : 1];
 #pragma unroll
     for (int it = 0; it < (CSUM ? CX::B_LOADS : 1); ++it) bsum[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-    // 16-k tiles: two register sets (the tile two ahead in flight); 32-k tiles (bf16): one set
-    // (the register budget), loaded at a step's start and written after its MFMAs
-    constexpr bool XDEEP = KT == 16;
+    // 16-k tiles, and 32-k tiles (bf16) with at most four 32 x 32 accumulators per wave (128 x 128,
+    // 128 x 96 tiles): two register sets, the k-tile two ahead in flight while the next one is
+    // written to LDS between the current tile's MFMAs.  32-k tiles with more accumulators (128 x 192)
+    // keep one set (the register budget), loaded at a step's start and written after its MFMAs —
+    // one k-tile of MFMAs (8-12 per wave) cannot hide an HBM load, which left C5's bf16 GEMMs
+    // latency-bound (build with -DTTAMM_BF16_DEEP=0 for one set everywhere)
+    constexpr bool XDEEP = KT == 16 || (I * J <= 4 && TTAMM_BF16_DEEP);
     // A3: A in three register sets, loaded two k-tiles ahead (B, L2-resident weights or dY, one)
     constexpr bool A3 = XDEEP && CX::AD == 3;
     float4 ra[XDEEP ? (A3 ? 3 : 2) : 1][CX::A_LOADS], rb[XDEEP ? 2 : 1][CX::B_LOADS];
@@ -862,6 +899,18 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
             constexpr int R = decltype(S)::value;
 #pragma unroll
             for (int it = 0; it < CX::A_LOADS; ++it) {
+                if constexpr (CX::APL) {
+                    // one 16-B piece: MN-major, k-tile k0 / 16 of the row; K-major, k row k0 + a_r
+                    // (clamped), chunks from the M-tile's first; masked when the tile is written
+                    if (!AK) {
+                        ra[R][it] = *reinterpret_cast<const float4*>(ap_rp[it] + (k0 >> 4) * 48 + a_c[it]);
+                    } else {
+                        const int k = FAST ? k0 + a_r[it] : min(k0 + a_r[it], k_end - 1);
+                        const uint16_t* rp = P.A3p + kidx[k - k_begin] * P.lda3 + (m0 >> 4) * 48;
+                        ra[R][it] = *reinterpret_cast<const float4*>(rp + a_c[it]);
+                    }
+                    continue;
+                }
                 if (!AK) {
                     ra[R][it] = FAST ? *reinterpret_cast<const float4*>(a_rp[it] + k0 + a_c[it])
                                      : raw4(a_rp[it], k0 + a_c[it], P.lda);
@@ -906,6 +955,18 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
             int plane;
             if (q < CX::A_LOADS) {
                 const int it = q;
+                if constexpr (CX::APL) {
+                    // a pre-split piece: straight into its plane (rows past M / k rows past the split
+                    // and chunks past the row's planes are zero)
+                    unsigned char* Ap2 = lds + decltype(Buf)::value * CX::buf_bytes(PL);
+                    const bool ok = AK ? (a_ok[it] && (FAST || k0 + a_r[it] < k_end)) : (FAST || a_ok[it]);
+                    // a value select per component (a select of the two float4 objects compiled to a
+                    // select of their addresses: both spilled to scratch)
+                    const float4 r = ra[RA][it];
+                    const float4 v = make_float4(ok ? r.x : 0.f, ok ? r.y : 0.f, ok ? r.z : 0.f, ok ? r.w : 0.f);
+                    *reinterpret_cast<float4*>(Ap2 + ap_lds[it]) = v;
+                    return;
+                }
                 if (!AK) {
                     v = FAST ? ra[RA][it] : mask4(ra[RA][it], k0 + a_c[it], k_end, P.lda, -1, a_ok[it]);
                     off = mn_off<CX::RB>(a_r[it], a_c[it]);
@@ -1363,6 +1424,26 @@ __global__ void to_bf16_kernel(const float* __restrict__ src, int64_t rows, int 
     }
 }
 
+// fp32 rows -> bf16 planes: thread = 4 consecutive columns of a row; hi / mid / lo exactly as
+// split_bf16 forms them in the GEMM's staging (so a pre-split operand multiplies bit-identically)
+__global__ void to_planes_kernel(const float* __restrict__ src, int64_t rows, int cols, int64_t ld_src,
+                                 uint16_t* __restrict__ dst, int64_t ld_dst, int kc) {
+    const int64_t per_row = (int64_t)kc * 4;  // 4-column groups
+    const int64_t total = rows * per_row;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / per_row;
+        const int g = (int)(i - r * per_row), c0 = 4 * g;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = c0 + e < cols ? src[r * ld_src + c0 + e] : 0.f;
+        uint2 w[3];
+        split_bf16<3>(make_float4(v[0], v[1], v[2], v[3]), w);
+        uint16_t* o = dst + r * ld_dst + (c0 >> 4) * 48 + (c0 & 15);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<uint2*>(o + 16 * pl) = w[pl];
+    }
+}
+
 // grad_w[m_out][n_in] = sum_s slab[s][n_in][m_out] ; grad_b[m_out] = sum_s slab[s][N_in][m_out]
 __global__ void wgrad_reduce_kernel(WgradBatch batch, int64_t total) {
     const KArg(WgradBatch)* kb = (const KArg(WgradBatch)*)(__builtin_amdgcn_kernarg_segment_ptr());
@@ -1557,6 +1638,29 @@ int launch_to_bf16(const float* src, int64_t rows, int cols, int64_t ld_src, uin
     return TTAMM_OK;
 }
 
+int launch_to_planes(const float* src, int64_t rows, int cols, int64_t ld_src, uint16_t* dst, int64_t ld_dst,
+                     hipStream_t s) {
+    const int kc = (int)ceil_div(cols, 16);
+    TTAMM_REQUIRE(rows >= 0 && cols >= 0 && ld_src >= cols && ld_dst >= 48 * (int64_t)kc && ld_dst % 8 == 0 &&
+                      (uintptr_t)dst % 16 == 0,
+                  "to_planes: bad shape (ld_dst >= 48 ceil(cols / 16), a multiple of 8, 16-byte aligned)");
+    if (rows == 0 || kc == 0) return TTAMM_OK;
+    int64_t blocks = ceil_div(rows * kc * 4, 256);
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(to_planes_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, rows, cols, ld_src, dst, ld_dst, kc);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
+
+// the first feature layer on pre-split feature rows (GemmProblem::A3p): EPI_HIDDEN / EPI_STORE
+template <int BN, int WM, int WN>
+int dispatch_x_planes(GemmBatch& b, hipStream_t s) {
+    using CX = XCfg<128, BN, WM, WN, false, false, 16, 3, true>;
+    if (b.p[0].epi == EPI_HIDDEN) return launch_one_x<CX, EPI_HIDDEN, 3>(b, s);
+    if (b.p[0].epi == EPI_STORE) return launch_one_x<CX, EPI_STORE, 3>(b, s);
+    return fail(TTAMM_E_INVALID, "gemm: pre-split A planes take EPI_HIDDEN / EPI_STORE");
+}
+
 int launch_gemm(GemmBatch& b, hipStream_t s) {
     if (b.count == 0) return TTAMM_OK;
     if (b.p[0].A16) return launch_gemm_bf16(b, s);
@@ -1583,6 +1687,19 @@ int launch_gemm(GemmBatch& b, hipStream_t s) {
     // dgrad (K-major weights, K = one layer's width: six k-tiles at C2) is latency-bound: twice the
     // blocks on 128 x 96 tiles hide more of it (C2 0.638 -> 0.630-0.635 ms, profiles/r04_dgrad_tiles_s31.txt)
     const bool narrow_tiles = (wide_tiles < 300 || bkn) && std::getenv("TTAMM_GEMM_WIDE_TILES") == nullptr;
+    bool planes = b.p[0].A3p != nullptr && !exact_mfma() && !b.p[0].bf16 && !bkn;
+    for (int i = 0; i < b.count; ++i) {
+        const GemmProblem& p = b.p[i];
+        planes = planes && p.A3p != nullptr && p.lda3 % 8 == 0 && (uintptr_t)p.A3p % 16 == 0 &&
+                 p.lda3 >= 48 * ceil_div(p.K, 16);
+    }
+    if (planes) {
+        switch (pick_tile_n(b, narrow_tiles, false)) {
+            case 192: return dispatch_x_planes<192, 2, 2>(b, s);
+            case 128: return dispatch_x_planes<128, 2, 2>(b, s);
+            default: return dispatch_x_planes<96, 4, 1>(b, s);
+        }
+    }
     if (!exact_mfma()) {
         switch (pick_tile_n(b, narrow_tiles, b.p[0].bf16 != 0)) {
             case 192:
@@ -1616,6 +1733,10 @@ using WgradWideX32 = XCfg<128, 192, 2, 2, true, true, 32>;
 using WgradNarrowX32 = XCfg<128, 96, 4, 1, true, true, 32>;
 using Wgrad128X = XCfg<128, 128, 2, 2, true, true>;
 using Wgrad128X32 = XCfg<128, 128, 2, 2, true, true, 32>;
+// X pre-split into planes (the first feature layer's weight gradient, fp32 towers)
+using WgradNarrowXP = XCfg<128, 96, 4, 1, true, true, 16, 2, true>;
+using WgradWideXP = XCfg<128, 192, 2, 2, true, true, 16, 2, true>;
+using Wgrad128XP = XCfg<128, 128, 2, 2, true, true, 16, 2, true>;
 // resident blocks of a weight-gradient class's launch configuration (fp32 split kernels; the
 // exact fp32-MFMA kernels have two classes)
 int wgrad_slots(int cls, bool exact) {
@@ -1715,18 +1836,23 @@ static bool wgrad_a3() {
 int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
     // one launch per tile configuration: class 0 (128 x 96), 1 (128 x 192), 2 and 3 (128 x 128; a
     // 128 x 256 bf16 tile spilled 132 B of scratch per thread)
-    GemmBatch g[kWgradClasses];
+    GemmBatch g[kWgradClasses], gp[kWgradClasses];  // gp: X pre-split into planes
     std::memset(g, 0, sizeof(g));
+    std::memset(gp, 0, sizeof(gp));
     const bool bf = wb.count > 0 && wb.p[0].bf16;
     const bool exact = exact_mfma();
     auto cfg_of = [&](int cls) {
         if (exact) return cls == 0 ? 0 : 1;  // the fp32-MFMA kernels: narrow / wide
         return cls == 3 ? 2 : cls;
     };
-    auto flush = [&](GemmBatch& b, int cfg) -> int {
+    auto flush = [&](GemmBatch& b, int cfg, bool planes = false) -> int {
         if (b.count == 0) return TTAMM_OK;
         int rc;
-        if (exact) {
+        if (planes) {
+            rc = cfg == 0   ? launch_one_x<WgradNarrowXP, EPI_STORE, 3>(b, s)
+                 : cfg == 1 ? launch_one_x<WgradWideXP, EPI_STORE, 3>(b, s)
+                            : launch_one_x<Wgrad128XP, EPI_STORE, 3>(b, s);
+        } else if (exact) {
             rc = cfg ? (bf ? launch_one<WgradWide, EPI_STORE, true>(b, s) : launch_one<WgradWide, EPI_STORE, false>(b, s))
                      : (bf ? launch_one<WgradNarrow, EPI_STORE, true>(b, s) : launch_one<WgradNarrow, EPI_STORE, false>(b, s));
         } else if (bf) {
@@ -1782,27 +1908,34 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
         p.inv_keep = 1.f;
         p.bf16 = w.bf16;
         const int cfg = cfg_of(wgrad_class(w.M));
-        if (g[cfg].count == kMaxGemmProblems) {
-            const int rc = flush(g[cfg], cfg);
+        const bool planes = w.X3p != nullptr && !exact && !bf && w.ld_x3 % 8 == 0 && (uintptr_t)w.X3p % 16 == 0 &&
+                            w.ld_x3 >= 48 * ceil_div(w.N, 16);
+        if (planes) {
+            p.A3p = w.X3p;
+            p.lda3 = w.ld_x3;
+        }
+        GemmBatch& gb = planes ? gp[cfg] : g[cfg];
+        if (gb.count == kMaxGemmProblems) {
+            const int rc = flush(gb, cfg, planes);
             if (rc) return rc;
         }
-        g[cfg].p[g[cfg].count++] = p;
+        gb.p[gb.count++] = p;
     }
     int rc;
     bool any_wide = false;
-    for (int c = 1; c < kWgradClasses; ++c) any_wide = any_wide || g[c].count > 0;
+    for (int c = 1; c < kWgradClasses; ++c) any_wide = any_wide || g[c].count > 0 || gp[c].count > 0;
     const bool timed = ev && ev[0] && ev[1] && any_wide;
     // The narrow launch (latency-bound: many short splits) first, then the wide ones (MFMA-bound),
     // which the aux stream's memory-bound row updates then run beside: C2 0.660 -> 0.652 ms,
     // the emulated 8-rank C2 0.804 -> 0.769 ms (profiles/r04_wgrad_order_s22.txt).
     // TTAMM_WGRAD_WIDE_FIRST=1: the old order.
     static const bool narrow_first = std::getenv("TTAMM_WGRAD_WIDE_FIRST") == nullptr;
-    if (narrow_first && (rc = flush(g[0], 0))) return rc;
+    if (narrow_first && ((rc = flush(g[0], 0)) || (rc = flush(gp[0], 0, true)))) return rc;
     if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)ev[0], s));
     for (int c = 1; c < kWgradClasses; ++c)
-        if ((rc = flush(g[c], c))) return rc;
+        if ((rc = flush(gp[c], c, true)) || (rc = flush(g[c], c))) return rc;
     if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)ev[1], s));
-    if (!narrow_first && (rc = flush(g[0], 0))) return rc;
+    if (!narrow_first && ((rc = flush(g[0], 0)) || (rc = flush(gp[0], 0, true)))) return rc;
     if (total > 0) {
         hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, s, wb, total);
         TTAMM_LAUNCH_CHECK();

@@ -75,6 +75,11 @@ struct GemmProblem {
     // (multiples of 8), K a multiple of 8.  Same epilogues as the fp32 kernel.
     const uint16_t* A16;
     const uint16_t* B16;
+    // A pre-split into bf16 planes (split kernel, fp32 towers): row r's k-tile t (16 k) is the 96 B
+    // at A3p + r * lda3 + 48 t: hi[16], mid[16], lo[16] with hi + mid + lo == the fp32 value; A keeps
+    // pointing at the fp32 rows (the exact-MFMA path reads those).  lda3 in uint16 elements.
+    const uint16_t* A3p;
+    int64_t lda3;
     // feature-MLP activation (EPI_HIDDEN / EPI_DGRAD_HIDDEN; ttamm.h TTAMM_ACT_*, 0 = ReLU).  A
     // non-ReLU EPI_HIDDEN also writes the pre-activation to `pre` [M, ldc] and, when it draws its
     // dropout decisions, the keep bytes to `mask_out` [M, N]; its EPI_DGRAD_HIDDEN reads the
@@ -106,6 +111,9 @@ int launch_epoch_batch(const int64_t* users, const int64_t* items, int64_t n, ui
 // fp32 -> bf16 (round to nearest even) rows, zero-filled from `cols` to ld_dst
 int launch_to_bf16(const float* src, int64_t rows, int cols, int64_t ld_src, uint16_t* dst, int64_t ld_dst,
                    hipStream_t s);
+// fp32 rows -> [rows][ceil(cols / 16)][hi, mid, lo][16] bf16 planes (ttamm.h ttamm_to_planes)
+int launch_to_planes(const float* src, int64_t rows, int cols, int64_t ld_src, uint16_t* dst, int64_t ld_dst,
+                     hipStream_t s);
 
 // Weight-gradient GEMM (split-K over rows) + fixed-order reduce.
 //   dW[m, n] = sum_r dY[r, m] * X[r, n] ;  db[m] = sum_r dY[r, m]
@@ -115,6 +123,8 @@ struct WgradProblem {
     const float* X;
     const int64_t* x_idx;  // gather rows of X (features) or null
     int64_t ld_x;
+    const uint16_t* X3p;   // X pre-split into bf16 planes (GemmProblem::A3p layout) or null
+    int64_t ld_x3;
     int R, M, N;           // rows, out features, in features
     float* grad_w;         // [M, N]
     float* grad_b;         // [M] (may be null)

@@ -158,6 +158,11 @@ int validate_tower(const ttamm_tower& T, const char* name, int D, bool training)
             TTAMM_REQUIRE(T.matmul_bf16 && T.feat_bf16_ld % 8 == 0 && T.feat_bf16_ld >= round8(T.feat_dim) &&
                               (uintptr_t)T.features_bf16 % 16 == 0,
                           n + ": bf16 feature rows need matmul_bf16, 16-byte aligned rows of >= round8(F) elements");
+        if (T.features_planes)
+            TTAMM_REQUIRE(!T.matmul_bf16 && T.feat_planes_ld % 8 == 0 &&
+                              T.feat_planes_ld >= 48 * ceil_div(T.feat_dim, 16) && (uintptr_t)T.features_planes % 16 == 0,
+                          n + ": feature planes need fp32 GEMMs and 16-byte aligned rows of >= 48 ceil(F / 16) "
+                              "elements (a multiple of 8)");
         for (int l = 0; l < T.n_linear; ++l) {
             const ttamm_linear& L = T.linear[l];
             TTAMM_REQUIRE(L.weight && L.bias, n + ": linear parameters missing");
@@ -616,6 +621,12 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
                 // width so every k-tile is whole (fast GEMM path)
                 if (l == 0 && w.wpad && t.feat_ld >= round4(L.in_features)) p.K = round4(L.in_features);
                 if (l == 0 && w.w16) p.K = round8(L.in_features);  // both operands zero beyond F
+                // pre-split feature rows (ttamm_tower.features_planes): zero beyond F up to whole
+                // 16-k chunks, so K may run to the padded width
+                if (l == 0 && t.features_planes && !t.matmul_bf16 && p.K <= 16 * (t.feat_planes_ld / 48)) {
+                    p.A3p = t.features_planes;
+                    p.lda3 = t.feat_planes_ld;
+                }
                 p.bias = L.bias;
                 if (l + 1 < t.n_linear) {
                     p.epi = EPI_HIDDEN;
@@ -946,6 +957,10 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
                 p.X = t.features;
                 p.x_idx = w.fidx;
                 p.ld_x = t.feat_ld;
+                if (t.features_planes && !t.matmul_bf16) {
+                    p.X3p = t.features_planes;
+                    p.ld_x3 = t.feat_planes_ld;
+                }
             } else {
                 p.X = w.hid[l - 1];
                 p.ld_x = t.linear[l - 1].out_features;

@@ -82,6 +82,8 @@ class Tower(ctypes.Structure):
         ("matmul_bf16", c_i32),
         ("features_bf16", c_vp),
         ("feat_bf16_ld", c_i64),
+        ("features_planes", c_vp),
+        ("feat_planes_ld", c_i64),
     ]
 
 
@@ -178,7 +180,7 @@ class StepArgs(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 22  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 23  # ttamm.h TTAMM_ABI_VERSION
 G0_EXACT = 0  # ttamm.h TTAMM_G0_EXACT
 DENSE_ADAM = 0  # ttamm.h TTAMM_DENSE_ADAM
 DENSE_SGD = 1  # ttamm.h TTAMM_DENSE_SGD
@@ -213,6 +215,7 @@ SIGNATURES = {
     "ttamm_retrieval_topk_workspace_size": (ctypes.c_size_t, [c_i64, c_i64, c_i32, c_i32]),
     "ttamm_normalize_rows": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i64, c_vp]),
     "ttamm_to_bf16": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i64, c_vp, c_i64, c_vp]),
+    "ttamm_to_planes": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i64, c_vp, c_i64, c_vp]),
     "ttamm_stream_create_cu_limited": (ctypes.c_int, [c_i32, ctypes.POINTER(c_vp)]),
     "ttamm_stream_destroy": (ctypes.c_int, [c_vp]),
     "ttamm_route_scratch_bytes": (ctypes.c_size_t, [c_i64, c_i32]),

@@ -108,6 +108,17 @@ def _dense_params(opt: torch.optim.Optimizer) -> list[torch.Tensor]:
     return [p for g in opt.param_groups for p in g["params"]]
 
 
+def feature_planes_enabled() -> bool:
+    """TTAMM_FEATURE_PLANES=1: fp32 towers keep their feature rows pre-split into bf16 planes
+    (1.5x the fp32 rows' bytes in HBM) for the first layer's forward and weight gradient, instead
+    of splitting them inside the GEMMs (same results, bit for bit).  Off by default: measured at C2
+    the forward GEMM reads 1.5x the gathered bytes and ran 126 -> 135 us, the weight gradient
+    103 -> 99 us, the step 0.656 -> 0.664 ms (profiles/r05_s7_feature_planes.txt)."""
+    import os
+
+    return os.environ.get("TTAMM_FEATURE_PLANES", "0") == "1"
+
+
 class FusedTrainStep:
     """Owns the native step descriptor and workspace for one (model, optimizers) pair."""
 
@@ -262,6 +273,13 @@ class FusedTrainStep:
                 f16 = self._bf16_copy(feats)
                 desc.features_bf16 = f16.data_ptr()
                 desc.feat_bf16_ld = f16.stride(0)
+            elif feats is not None and feature_planes_enabled():
+                # fp32 towers: the feature rows split once into their bf16 hi / mid / lo planes (the
+                # split every split-bf16 GEMM of the step forms), so the first layer's forward and
+                # weight gradient stage them instead of splitting in every k-tile (same bits)
+                fp = self._planes_copy(feats)
+                desc.features_planes = fp.data_ptr()
+                desc.feat_planes_ld = fp.stride(0)
             setattr(args, name, desc)
         args.mimic_enabled = 1 if mimic is not None else 0
         args.in_batch = 1 if self.in_batch else 0
@@ -384,6 +402,16 @@ class FusedTrainStep:
         lib = _lib.load()
         _lib.check(lib.ttamm_to_bf16(feats.data_ptr(), rows, width, feats.stride(0), out.data_ptr(), ld,
                                      _lib.stream_handle(feats.device)))
+        self._keep = getattr(self, "_keep", []) + [out]
+        return out
+
+    def _planes_copy(self, feats: torch.Tensor) -> torch.Tensor:
+        rows, width = feats.shape
+        ld = 48 * ((width + 15) // 16)
+        out = torch.empty((rows, ld), dtype=torch.int16, device=feats.device)
+        lib = _lib.load()
+        _lib.check(lib.ttamm_to_planes(feats.data_ptr(), rows, width, feats.stride(0), out.data_ptr(), ld,
+                                       _lib.stream_handle(feats.device)))
         self._keep = getattr(self, "_keep", []) + [out]
         return out
 
