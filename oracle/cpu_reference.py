@@ -222,8 +222,16 @@ def tower_forward(tower: OracleTower, idx: torch.Tensor, feats: torch.Tensor | N
     if tower.fusion == "concat":
         return _linear(tower.projection, torch.cat([e, f], dim=-1), bf16)  # :242-244
     g1, _, g2, _ = tower.adaptive_mimic.gate_network  # Linear, ReLU, Linear, Sigmoid (:157-162)
-    gate = torch.sigmoid(_linear(g2, torch.relu(_linear(g1, torch.cat([e, f], dim=-1), bf16)), bf16))  # :164-168
+    ef = torch.cat([e, f], dim=-1)
+    pre = _linear(g1, ef, bf16)
+    hidden = torch.relu(pre) if GATE_HIDDEN_HOOK is None else GATE_HIDDEN_HOOK(tower, ef, pre)
+    gate = torch.sigmoid(_linear(g2, hidden, bf16))  # :164-168
     return gate * e + (1.0 - gate) * f
+
+
+# Test hook (tests/test_fullsize_parity_gpu.py, fp32 ReLU kinks): when set, the gate's hidden
+# activation is GATE_HIDDEN_HOOK(tower, [e | f], pre-activation) instead of relu(pre-activation).
+GATE_HIDDEN_HOOK = None
 
 
 def gather_aug(table: nn.Embedding, idx: torch.Tensor, reference: torch.Tensor):

@@ -165,27 +165,97 @@ def _one_step(cfg_name: str, *, seed: int, in_batch: bool, num_neg: int | None =
     _log(f"{cfg_name}: oracle step took {time.perf_counter() - t0:.1f} s; comparing")
     state32 = {k: v.clone() for k, v in state.items()}
 
-    def fp64_grads() -> dict[str, torch.Tensor]:
-        """The same oracle step in float64 (every parameter, feature row and loss double)."""
+    def fp64_grads(make_hook=None) -> dict[str, torch.Tensor]:
+        """The same oracle step in float64 (every parameter, feature row and loss double);
+        make_hook(m64) -> the gate hidden-layer hook of that run (oracle GATE_HIDDEN_HOOK)."""
         _log(f"{cfg_name}: float64 oracle step")
         m64 = ref.build_model(tcfg, num_users=U, num_items=I, user_feature_dim=F, item_feature_dim=F, mimic=True)
         m64.load_state_dict(state32)
         m64 = m64.double()
+        ref.GATE_HIDDEN_HOOK = make_hook(m64) if make_hook is not None else None
         o64 = ref.build_optimizers(m64, lr=1e-3, betas=(0.0, 0.999), weight_decay=0.01)
         for o in o64:
             for g in o.param_groups:
                 g["lr"] = 0.0
-        ref.train_step(m64, o64, users, pos, neg, user_features=DeviceRows(user_features, torch.float64),
-                       item_features=DeviceRows(item_features, torch.float64), loss_weights=LOSS_WEIGHTS,
-                       user_keep_masks=um, item_keep_masks=im, in_batch=in_batch)
+        try:
+            ref.train_step(m64, o64, users, pos, neg, user_features=DeviceRows(user_features, torch.float64),
+                           item_features=DeviceRows(item_features, torch.float64), loss_weights=LOSS_WEIGHTS,
+                           user_keep_masks=um, item_keep_masks=im, in_batch=in_batch)
+        finally:
+            ref.GATE_HIDDEN_HOOK = None
         return _grads(m64, o64)
 
+    fp64_grads.ids = {"user_encoder": [users], "item_encoder": [pos] + ([neg.reshape(-1)] if N and not in_batch else [])}
     return om, oopts, tm, topts, ores, tl, fp64_grads
 
 
 def _grads(model, opts) -> dict[str, torch.Tensor]:
     by_id = {id(p): n for n, p in model.named_parameters()}
     return {by_id[id(p)]: st["exp_avg"] for opt in opts for p, st in opt.state.items()}
+
+
+U32 = 2.0 ** -24  # fp32 unit round-off
+
+
+def _kink_resolved_grads(tg: dict, g64: dict, fp64_grads, tol: float) -> tuple[dict | None, list]:
+    """The exact gradient of the step with the gate's fp32-ambiguous ReLU kinks resolved as ttamm's
+    fp32 arithmetic resolved them.
+
+    A gate hidden unit whose float64 pre-activation is within the fp32 dot-product error bound
+    (K u sum|x_k w_k| + |b|, any summation order) may land on either side of the ReLU in fp32: the
+    reference's own fp32 arithmetic under another BLAS blocking would flip it too, and the flip
+    moves that row's whole gradient by the unit's term (the r05 fused D = 128 gate: one unit of
+    8192 x 128 at C4).  Candidates come from the float64 step; the ones ttamm flipped are those on
+    rows whose ID-row gradient differs from float64 by more than tol / 4; the float64 step is then
+    re-run with exactly those units flipped, and every tensor is compared against that."""
+    cand: list[tuple[str, int, int, int]] = []  # (tower, call, row, unit)
+
+    def recorder(m64):
+        calls: dict[str, int] = {}
+        names = {id(m64.user_encoder): "user_encoder", id(m64.item_encoder): "item_encoder"}
+
+        def hook(tower, ef, pre):
+            name = names[id(tower)]
+            c = calls.get(name, 0)
+            calls[name] = c + 1
+            g1 = tower.adaptive_mimic.gate_network[0]
+            with torch.no_grad():
+                bound = ef.shape[-1] * U32 * (ef.abs() @ g1.weight.abs().t() + g1.bias.abs())
+                rows, units = torch.nonzero(pre.abs() <= bound, as_tuple=True)
+            cand.extend((name, c, int(r), int(u)) for r, u in zip(rows.tolist(), units.tolist()))
+            return torch.relu(pre)
+        return hook
+
+    fp64_grads(recorder)
+    flips = []
+    for name, c, r, u in cand:
+        emb = f"{name}.embedding.weight"
+        row = int(fp64_grads.ids[name][c][r])
+        den = _max_abs(g64[emb])
+        if _max_abs(tg[emb][row:row + 1], g64[emb][row:row + 1]) / den > tol / 4:
+            flips.append((name, c, r, u))
+    _log(f"ReLU kinks within the fp32 bound: {len(cand)}; flipped by ttamm (ID row differs): {flips}")
+    if not flips:
+        return None, flips
+
+    def flipper(m64):
+        calls: dict[str, int] = {}
+        names = {id(m64.user_encoder): "user_encoder", id(m64.item_encoder): "item_encoder"}
+
+        def hook(tower, ef, pre):
+            name = names[id(tower)]
+            c = calls.get(name, 0)
+            calls[name] = c + 1
+            out = torch.relu(pre)
+            for n, cc, r, u in flips:
+                if n == name and cc == c:  # the other side of the kink: active <-> inactive
+                    keep = torch.zeros_like(pre, dtype=torch.bool)
+                    keep[r, u] = True
+                    out = torch.where(keep, pre if float(pre[r, u]) <= 0.0 else torch.zeros_like(pre), out)
+            return out
+        return hook
+
+    return fp64_grads(flipper), flips
 
 
 def _compare(om, oopts, tm, topts, ores, tl, fp64_grads, *, tol: float, mean_tol: float | None,
@@ -197,6 +267,7 @@ def _compare(om, oopts, tm, topts, ores, tl, fp64_grads, *, tol: float, mean_tol
     assert set(og) == set(tg)
     report = {}
     g64 = None
+    g64k = None  # float64 with ttamm's resolution of fp32-ambiguous gate ReLU kinks (computed once)
     for name in sorted(og):
         den = _max_abs(og[name])
         num = _max_abs(tg[name], og[name])
@@ -209,6 +280,17 @@ def _compare(om, oopts, tm, topts, ores, tl, fp64_grads, *, tol: float, mean_tol
             ours = _max_abs(tg[name], g64[name]) / d64
             theirs = _max_abs(og[name], g64[name]) / d64
             _log(f"{name}: ttamm vs fp32 oracle {err:.2e}; vs float64: ttamm {ours:.2e}, fp32 oracle {theirs:.2e}")
+            if ours > tol and ours > theirs:
+                if g64k is None:
+                    g64k, flips = _kink_resolved_grads(tg, g64, fp64_grads, tol)
+                    assert g64k is not None, f"{name}: rel err {err:.3e} (vs float64 {ours:.3e}), no ReLU kink explains it"
+                    for n2 in og:  # every tensor, against the kink-resolved exact step (the same rule)
+                        dk = _max_abs(g64k[n2])
+                        e2 = _max_abs(tg[n2], g64k[n2]) / dk
+                        t2 = _max_abs(og[n2], g64[n2]) / _max_abs(g64[n2])
+                        _log(f"  kink-resolved float64: {n2} {e2:.2e} (fp32 oracle vs float64 {t2:.2e})")
+                        assert e2 <= tol or e2 <= t2, f"{n2}: rel err {e2:.3e} against the kink-resolved float64 step"
+                ours = _max_abs(tg[name], g64k[name]) / _max_abs(g64k[name])
             assert ours <= tol or ours <= theirs, f"{name}: rel err {err:.3e} (vs float64 {ours:.3e} > {theirs:.3e})"
             report[name] = ours
             continue

@@ -147,20 +147,26 @@ def test_bf16_step_gradients_match_bf16_oracle(shape):
     assert far > 5e-4 and far > 4 * near, (far, near)
 
 
-# Fused gate kernel (csrc/gate.hip: fp32 towers with D == Hg in {32, 64, 96}) and the generic
+# Fused gate kernel (csrc/gate.hip: fp32 towers with D == Hg in {32, 64, 96, 128}) and the generic
 # two-GEMM gate path (TTAMM_GENERIC_GATE=1), both against the oracle at the fp32 tolerance.
 # Row counts are not multiples of the kernel's 16-row slabs (user rows = B, item rows = B(1+N)).
+# D = 128 (C4's width) runs the 4-wave variant with G2 read from global memory and the backward's
+# two matrices staged one after the other; "d128-rounds" has more 16-row slabs than the grid has
+# waves (the backward's per-round staging runs twice in both towers).
 GATE_SHAPES = [
     Shape(U=64, I=256, F=40, H=48, D=32, B=45, N=5, hidden_dims=(48,)),
     Shape(U=64, I=512, F=70, H=64, D=64, B=40, N=4, hidden_dims=(64,)),
     Shape(U=96, I=768, F=605, H=192, D=96, B=37, N=5, hidden_dims=(192,)),
     Shape(U=64, I=256, F=40, H=48, D=32, B=32, N=5, hidden_dims=(48,), mimic=False),
     Shape(U=64, I=256, F=40, H=48, D=32, B=32, N=5, hidden_dims=(48,), sparse=False),
+    Shape(U=64, I=512, F=40, H=64, D=128, B=45, N=5, hidden_dims=(64,)),
+    Shape(U=2500, I=24000, F=40, H=64, D=128, B=2000, N=8, hidden_dims=(64,)),
 ]
 
 
 @pytest.mark.parametrize("generic", [False, True], ids=["fused", "generic"])
-@pytest.mark.parametrize("shape", GATE_SHAPES, ids=["d32", "d64", "d96-c2dims", "d32-nomimic", "d32-dense-id"])
+@pytest.mark.parametrize("shape", GATE_SHAPES,
+                         ids=["d32", "d64", "d96-c2dims", "d32-nomimic", "d32-dense-id", "d128", "d128-rounds"])
 def test_gate_paths_match_oracle(shape, generic, monkeypatch):
     from gpu_helpers import run_ttamm
 

@@ -82,11 +82,14 @@ def main() -> None:
         k = max(l1, key=lambda n: kernels[n]["hbm_bytes_per_launch"])
         entry["l1_forward_gemm_kernel"] = k
         entry["l1_forward_gemm_bytes_per_launch"] = kernels[k]["hbm_bytes_per_launch"]
-    # the wide weight-gradient launch (XCfg<128, 192, ..., true, true, ...>, EPI_STORE = 0)
-    wg = [k for k in kernels if k.startswith("gemm_x_kernel<XCfg<128, 192, 2, 2, true, true")]
+    # the wide weight-gradient launch: the split-K launch (XCfg<..., true, true, ...>, EPI_STORE = 0)
+    # moving the most bytes (round 5: its tile width follows the layer widths, gemm.hip pick_tile_n)
+    wg = [k for k in kernels if k.startswith("gemm_x_kernel<XCfg<") and ", true, true, " in k and
+          k.split(">, ")[-1].startswith("0, ")]
     if wg:
-        entry["wgrad_wide_kernel"] = wg[0]
-        entry["wgrad_wide_bytes_per_launch"] = kernels[wg[0]]["hbm_bytes_per_launch"]
+        k = max(wg, key=lambda n: kernels[n]["hbm_bytes_per_launch"])
+        entry["wgrad_wide_kernel"] = k
+        entry["wgrad_wide_bytes_per_launch"] = kernels[k]["hbm_bytes_per_launch"]
     ib = [k for k in kernels if k.startswith("inbatch")]
     if ib:
         k = max(ib, key=lambda n: kernels[n]["hbm_bytes_per_launch"])

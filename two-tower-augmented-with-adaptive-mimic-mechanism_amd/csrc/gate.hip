@@ -32,10 +32,16 @@ namespace ttamm {
 namespace {
 
 typedef float f4v __attribute__((ext_vector_type(4)));
-// 512 threads: 2 waves per SIMD with up to 256 VGPRs each — a wave keeps its slab's rows, the
-// next slab's prefetched rows and the MFMA operands of both chained GEMMs in registers
-constexpr int kGateWaves = 8;
-constexpr int kGateThreads = 64 * kGateWaves;
+// D <= 96: 512 threads, 2 waves per SIMD with up to 256 VGPRs each — a wave keeps its slab's
+// rows, the next slab's prefetched rows and the MFMA operands of both chained GEMMs in registers.
+// D = 128: the fp32 G1 (or G1^T) alone fills 133 KB of LDS, so the narrower matrix (G2, D x Hg)
+// is read from global memory (L2-resident: 64 KB read by every wave) and a block is 4 waves, one
+// per SIMD with the whole register file (VGPRs + AGPRs), one block per CU.
+template <int D>
+struct GateWaves {
+    static constexpr int NW = D >= 128 ? 4 : 8;
+    static constexpr int THREADS = 64 * NW;
+};
 
 __device__ __forceinline__ f4v ldg4(const float* p) { return *reinterpret_cast<const f4v*>(p); }
 __device__ __forceinline__ f4v lds4(const float* p) { return *reinterpret_cast<const f4v*>(p); }
@@ -65,6 +71,32 @@ __device__ __forceinline__ void tile_gemm(const float* w_lds, int ob0, const f4v
             for (int ob = 0; ob < NO; ++ob)
                 acc[ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[cur][ob][r], b[t][r], acc[ob], 0, 0, 0);
         // keep the scheduler from hoisting every k-tile's LDS reads to the top (register spills)
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// tile_gemm with W read from global memory (row-major, leading dimension ld; L2-resident), the
+// fragments of k-tile t + 1 in flight during k-tile t's MFMAs
+template <int NO, int NK, int ld>
+__device__ __forceinline__ void tile_gemm_g(const float* W, int ob0, const f4v (&b)[NK], f4v (&acc)[NO], int li,
+                                            int q) {
+    f4v w[2][NO];
+    const float* base = W + (int64_t)(16 * ob0 + li) * ld + 4 * q;
+#pragma unroll
+    for (int ob = 0; ob < NO; ++ob) w[0][ob] = *reinterpret_cast<const f4v*>(base + 16 * ob * ld);
+#pragma unroll
+    for (int t = 0; t < NK; ++t) {
+        const int cur = t & 1;
+        if (t + 1 < NK) {
+#pragma unroll
+            for (int ob = 0; ob < NO; ++ob)
+                w[cur ^ 1][ob] = *reinterpret_cast<const f4v*>(base + 16 * ob * ld + 16 * (t + 1));
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int ob = 0; ob < NO; ++ob)
+                acc[ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[cur][ob][r], b[t][r], acc[ob], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -164,12 +196,14 @@ __device__ __forceinline__ void load_row(f4v (&v)[N], const float* base, int64_t
 // instruction at NO = 6) instead of 16 rows x 64 B.  The direct form of these stores bounded the
 // gate kernels (their time without any output store: 64 -> 42 us forward, 65 -> 49 us backward,
 // profiles/r03_c2_gate_store_ablation_s22.txt).
-constexpr int kSlabScratch = 8 * (96 + 4);  // floats per wave: eight rows of up to 96 + 4 pad
+// floats per wave: eight rows of up to max(D, Hg) + 4 pad
+template <int D>
+constexpr int slab_scratch() { return 8 * ((D < 96 ? 96 : D) + 4); }
 template <int NO>
 __device__ __forceinline__ void store_slab(float* scr, const f4v (&v)[NO], float* out, int64_t ld, int64_t row0,
                                            int64_t R, int lane) {
     constexpr int W = 16 * NO, LDW = W + 4, C4 = W / 4, PER = 8 * C4 / 64;
-    static_assert(8 * LDW <= kSlabScratch && (8 * C4) % 64 == 0, "slab scratch");
+    static_assert((8 * C4) % 64 == 0, "slab scratch");
     const int li = lane & 15, q = lane >> 4;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -194,20 +228,26 @@ __device__ __forceinline__ void store_slab(float* scr, const f4v (&v)[NO], float
 template <int D, int HG>
 struct GateCfg {
     static constexpr int TD = D / 16, TH = HG / 16, TE = 2 * D / 16;  // 16-feature tiles
-    // forward LDS: G1 [HG][2D] and G2 [D][HG] as stored, rows padded by 4 floats, then c1, c2
+    static constexpr int NW = GateWaves<D>::NW;
+    // GG: G2 (forward) / G2^T (backward) read from global memory instead of LDS
+    static constexpr bool GG = D >= 128;
+    static constexpr int SCR = slab_scratch<(D > HG ? D : HG)>();  // floats of slab scratch per wave
+    // forward LDS: G1 [HG][2D] and (!GG) G2 [D][HG] as stored, rows padded by 4 floats, then c1, c2
     static constexpr int F_LD1 = 2 * D + 4, F_LD2 = HG + 4;
-    static constexpr int F_LDS = HG * F_LD1 + D * F_LD2 + HG + D;
-    // backward LDS: G2^T [HG][D] and G1^T [2D][HG]
+    static constexpr int F_LDS = HG * F_LD1 + (GG ? 0 : D * F_LD2) + HG + D;
+    // backward LDS: G2^T [HG][D], then G1^T [2D][HG] (GG: one at a time, G1^T over G2^T)
     static constexpr int B_LD1 = D + 4, B_LD2 = HG + 4;
-    static constexpr int B_LDS = HG * B_LD1 + 2 * D * B_LD2;
+    static constexpr int B_G1T = GG ? 0 : HG * B_LD1;  // offset of G1^T
+    static constexpr int B_LDS = B_G1T + 2 * D * B_LD2;
     static_assert(D % 16 == 0 && HG % 16 == 0, "16-feature tiles");
-    static_assert(F_LDS * 4 <= 163840 && B_LDS * 4 <= 163840, "the gate matrices must fit one CU's LDS");
+    static_assert((F_LDS + NW * SCR) * 4 <= 163840 && (B_LDS + NW * SCR) * 4 <= 163840,
+                  "the gate matrices must fit one CU's LDS");
     // split-bf16: G1 (forward, [HG] rows x 2D k) / G1^T (backward, [2D] rows x HG k) as three bf16
     // planes, 2 B x 3 per weight; G2 / G2^T stay fp32 (the 16x16x4 f32 GEMM)
     static constexpr int X1_BYTES = 3 * 2 * (2 * D) * HG;
     static constexpr int XF_BYTES = X1_BYTES + 4 * (D * F_LD2 + HG + D);
     static constexpr int XB_BYTES = X1_BYTES + 4 * (HG * B_LD1);
-    static constexpr bool X_OK = (2 * D) % 32 == 0 && HG % 32 == 0 && XF_BYTES <= 163840 && XB_BYTES <= 163840;
+    static constexpr bool X_OK = !GG && (2 * D) % 32 == 0 && HG % 32 == 0 && XF_BYTES <= 163840 && XB_BYTES <= 163840;
 };
 
 // this block's tower and its index among the tower's blocks
@@ -221,26 +261,27 @@ __device__ __forceinline__ int gate_tower(const KArg(GateArgs) * ka, int& bidx) 
 }
 
 template <int D, int HG, bool X>
-__global__ __launch_bounds__(kGateThreads) void gate_fwd_kernel(GateArgs) {
+__global__ __launch_bounds__(GateWaves<D>::THREADS) void gate_fwd_kernel(GateArgs) {
     using C = GateCfg<D, HG>;
+    constexpr int NW = C::NW, NT = 64 * NW;
     constexpr int NX = (2 * D) / 32;  // split: k-steps of the first GEMM
     // !X: each wave's slab-store scratch after the matrices (store_slab)
-    __shared__ __attribute__((aligned(16))) float lds[X ? C::XF_BYTES / 4 : C::F_LDS + kGateWaves * kSlabScratch];
+    __shared__ __attribute__((aligned(16))) float lds[X ? C::XF_BYTES / 4 : C::F_LDS + NW * C::SCR];
     const KArg(GateArgs)* ka = (const KArg(GateArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
     int bidx;
     const KArg(GateTower)& T = ka->tw[gate_tower(ka, bidx)];
     float* g1s = lds;  // fp32 G1, or (X) its three bf16 planes
     unsigned char* img = reinterpret_cast<unsigned char*>(lds);
-    float* g2s = X ? reinterpret_cast<float*>(img + C::X1_BYTES) : g1s + HG * C::F_LD1;
-    float* c1s = g2s + D * C::F_LD2;
+    float* g2s = X ? reinterpret_cast<float*>(img + C::X1_BYTES) : g1s + HG * C::F_LD1;  // (!GG)
+    float* c1s = C::GG ? g2s : g2s + D * C::F_LD2;
     float* c2s = c1s + HG;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
-    float* scr = lds + C::F_LDS + wave * kSlabScratch;  // (!X)
+    float* scr = lds + C::F_LDS + wave * C::SCR;  // (!X)
     const int64_t R = T.R;
     const int64_t nslab = (R + 15) / 16;
-    const int64_t stride = (int64_t)T.blocks * kGateWaves;
-    int64_t s = (int64_t)bidx * kGateWaves + wave;
+    const int64_t stride = (int64_t)T.blocks * NW;
+    int64_t s = (int64_t)bidx * NW + wave;
     // the first slab's rows are in flight while the block stages the gate matrices
     f4v ef[C::TE];
     int64_t arow = 0;  // the slab row's mimic-table row
@@ -251,7 +292,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_fwd_kernel(GateArgs) {
     }
     constexpr int N1 = HG * (2 * D / 4), N2 = D * (HG / 4);
 #pragma unroll
-    for (int e0 = 0; e0 < N1; e0 += kGateThreads) {
+    for (int e0 = 0; e0 < N1; e0 += NT) {
         const int e = e0 + (int)threadIdx.x;
         if (e < N1) {
             const int i = e / (2 * D / 4), c = 4 * (e % (2 * D / 4));
@@ -265,15 +306,17 @@ __global__ __launch_bounds__(kGateThreads) void gate_fwd_kernel(GateArgs) {
             }
         }
     }
+    if constexpr (!C::GG) {
 #pragma unroll
-    for (int e0 = 0; e0 < N2; e0 += kGateThreads) {
-        const int e = e0 + (int)threadIdx.x;
-        if (e < N2) {
-            const int i = e / (HG / 4), c = 4 * (e % (HG / 4));
-            *reinterpret_cast<f4v*>(g2s + i * C::F_LD2 + c) = ldg4(T.G2 + (int64_t)i * HG + c);
+        for (int e0 = 0; e0 < N2; e0 += NT) {
+            const int e = e0 + (int)threadIdx.x;
+            if (e < N2) {
+                const int i = e / (HG / 4), c = 4 * (e % (HG / 4));
+                *reinterpret_cast<f4v*>(g2s + i * C::F_LD2 + c) = ldg4(T.G2 + (int64_t)i * HG + c);
+            }
         }
     }
-    for (int e = threadIdx.x; e < HG + D; e += kGateThreads) c1s[e] = e < HG ? T.c1[e] : T.c2[e - HG];
+    for (int e = threadIdx.x; e < HG + D; e += NT) c1s[e] = e < HG ? T.c1[e] : T.c2[e - HG];
     __syncthreads();
     for (; s < nslab; s += stride) {
         const int64_t row = s * 16 + li;
@@ -284,11 +327,12 @@ __global__ __launch_bounds__(kGateThreads) void gate_fwd_kernel(GateArgs) {
         zero(z);
         if constexpr (X) tile_gemm_x<C::TH, NX, HG>(img, 0, ef, z, li, q);  // z^T = G1 . ef^T
         else tile_gemm<C::TH, C::TE, C::F_LD1>(g1s, 0, ef, z, li, q);
-        // the next slab's rows, in flight during the rest of this one
-        f4v nx[C::TE];
+        // the next slab's rows, in flight during the rest of this one (GG: a wave rarely has a
+        // second slab, and the registers hold the global G2 fragments instead)
+        f4v nx[C::GG ? 1 : C::TE];
         int64_t arow_n = 0;
         const int64_t sn = s + stride;
-        if (sn < nslab) {
+        if (!C::GG && sn < nslab) {
             const int64_t rn = sn * 16 + li < R ? sn * 16 + li : R - 1;
             load_row(nx, T.ef, 2 * D, rn, q);
             if (T.table) arow_n = T.idx[rn];
@@ -306,7 +350,8 @@ __global__ __launch_bounds__(kGateThreads) void gate_fwd_kernel(GateArgs) {
         if (!(X || ka->direct) && !ka->ablate) store_slab<C::TH>(scr, z, T.z, HG, s * 16, R, lane);
         f4v x[C::TD];
         zero(x);
-        tile_gemm<C::TD, C::TH, C::F_LD2>(g2s, 0, z, x, li, q);  // (pre-sigmoid)^T = G2 . z^T
+        if constexpr (C::GG) tile_gemm_g<C::TD, C::TH, HG>(T.G2, 0, z, x, li, q);  // (pre-sigmoid)^T = G2 . z^T
+        else tile_gemm<C::TD, C::TH, C::F_LD2>(g2s, 0, z, x, li, q);
         if (!(X || ka->direct) && !ka->ablate) {
             // g, then t = g e + (1 - g) f in place, a, then aug = t + a in place: one live array
 #pragma unroll
@@ -355,7 +400,13 @@ __global__ __launch_bounds__(kGateThreads) void gate_fwd_kernel(GateArgs) {
                 if (T.aug) stg4(T.aug + row * D + col, aug);
             }
         }
-        if (sn < nslab) {
+        if constexpr (C::GG) {
+            if (sn < nslab) {
+                const int64_t rn = sn * 16 + li < R ? sn * 16 + li : R - 1;
+                load_row(ef, T.ef, 2 * D, rn, q);
+                if (T.table) arow = T.idx[rn];
+            }
+        } else if (sn < nslab) {
 #pragma unroll
             for (int t = 0; t < C::TE; ++t) ef[t] = nx[t];
             arow = arow_n;
@@ -364,35 +415,109 @@ __global__ __launch_bounds__(kGateThreads) void gate_fwd_kernel(GateArgs) {
 }
 
 template <int D, int HG, bool X>
-__global__ __launch_bounds__(kGateThreads) void gate_bwd_kernel(GateArgs) {
+__global__ __launch_bounds__(GateWaves<D>::THREADS) void gate_bwd_kernel(GateArgs) {
     using C = GateCfg<D, HG>;
+    constexpr int NW = C::NW, NT = 64 * NW;
     constexpr int NX = HG / 32;  // split: k-steps of the dEF GEMM
-    __shared__ __attribute__((aligned(16))) float lds[X ? C::XB_BYTES / 4 : C::B_LDS + kGateWaves * kSlabScratch];
+    __shared__ __attribute__((aligned(16))) float lds[X ? C::XB_BYTES / 4 : C::B_LDS + NW * C::SCR];
     const KArg(GateArgs)* ka = (const KArg(GateArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
     int bidx;
     const KArg(GateTower)& T = ka->tw[gate_tower(ka, bidx)];
     unsigned char* img = reinterpret_cast<unsigned char*>(lds);  // (X) G1^T as three bf16 planes
     float* g2t = X ? reinterpret_cast<float*>(img + C::X1_BYTES) : lds;  // G2^T [HG][D]
-    float* g1t = lds + HG * C::B_LD1;                                    // G1^T [2D][HG]
+    float* g1t = lds + C::B_G1T;  // G1^T [2D][HG] (GG: over G2^T, staged after it)
+    float* scr = lds + C::B_LDS + (threadIdx.x >> 6) * C::SCR;          // (!X)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int li = lane & 15, q = lane >> 4;
     const int64_t R = T.R;
     const int64_t nslab = (R + 15) / 16;
-    const int64_t stride = (int64_t)T.blocks * kGateWaves;
+    const int64_t stride = (int64_t)T.blocks * NW;
     // transposed staging: float4 reads along a row, four scalar LDS writes down a column
     constexpr int N2 = D * (HG / 4), N1 = HG * (2 * D / 4);
+    auto stage_g2t = [&]() {
 #pragma unroll
-    for (int e0 = 0; e0 < N2; e0 += kGateThreads) {
-        const int e = e0 + (int)threadIdx.x;
-        if (e < N2) {
-            const int d = e / (HG / 4), j = 4 * (e % (HG / 4));  // G2 [D][HG]
-            const f4v v = ldg4(T.G2 + (int64_t)d * HG + j);
+        for (int e0 = 0; e0 < N2; e0 += NT) {
+            const int e = e0 + (int)threadIdx.x;
+            if (e < N2) {
+                const int d = e / (HG / 4), j = 4 * (e % (HG / 4));  // G2 [D][HG]
+                const f4v v = ldg4(T.G2 + (int64_t)d * HG + j);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) g2t[(j + i) * C::B_LD1 + d] = v[i];
+                for (int i = 0; i < 4; ++i) g2t[(j + i) * C::B_LD1 + d] = v[i];
+            }
         }
-    }
+    };
+    if constexpr (C::GG) {
+        // the two matrices do not fit together: per round of NW slabs the block stages G2^T, every
+        // wave forms its slab's dq and dz, then G1^T over it and every wave forms dEF (every wave
+        // passes every barrier; one round at C4, where R / 16 <= blocks x NW)
+        for (int64_t s0 = (int64_t)bidx * NW; s0 < nslab; s0 += stride) {
+            const int64_t s = s0 + wave;
+            const bool has = s < nslab;
+            const int64_t row = s * 16 + li;
+            const bool ok = has && row < R;
+            const int64_t rr = ok ? row : R - 1;
+            f4v d[C::TD], g[C::TD], dz[C::TH];
+            {
+                f4v ef[C::TE];
+                load_row(d, T.dT, T.ld_dT, rr, q);
+                load_row(ef, T.ef, 2 * D, rr, q);
+                load_row(g, T.g, D, rr, q);
+                stage_g2t();
+                __syncthreads();
+                if (has) {
+                    f4v dq[C::TD];  // dq = (dT e - dT f) (1 - g) g
 #pragma unroll
-    for (int e0 = 0; e0 < N1; e0 += kGateThreads) {
+                    for (int t = 0; t < C::TD; ++t)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float dg = d[t][r] * ef[t][r] - d[t][r] * ef[C::TD + t][r];
+                            dq[t][r] = dg * (1.0f - g[t][r]) * g[t][r];
+                        }
+                    if (!ka->ablate) store_slab<C::TD>(scr, dq, T.dq, D, s * 16, R, lane);
+                    f4v zr[C::TH];
+                    load_row(zr, T.z, HG, rr, q);
+                    zero(dz);
+                    tile_gemm<C::TH, C::TD, C::B_LD1>(g2t, 0, dq, dz, li, q);  // dz^T = G2^T . dq^T
+#pragma unroll
+                    for (int ob = 0; ob < C::TH; ++ob)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) dz[ob][r] = zr[ob][r] > 0.f ? dz[ob][r] : 0.f;
+                    if (!ka->ablate) store_slab<C::TH>(scr, dz, T.dz, HG, s * 16, R, lane);
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int e0 = 0; e0 < N1; e0 += NT) {
+                const int e = e0 + (int)threadIdx.x;
+                if (e < N1) {
+                    const int j = e / (2 * D / 4), c = 4 * (e % (2 * D / 4));  // G1 [HG][2D]
+                    const f4v v = ldg4(T.G1 + (int64_t)j * 2 * D + c);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) g1t[(c + i) * C::B_LD2 + j] = v[i];
+                }
+            }
+            __syncthreads();
+            if (has) {
+#pragma unroll 1
+                for (int half = 0; half < 2; ++half) {  // dEF^T = G1^T . dz^T + [dT g | dT (1 - g)]
+                    f4v de[C::TD];
+                    zero(de);
+                    tile_gemm<C::TD, C::TH, C::B_LD2>(g1t, half * C::TD, dz, de, li, q);
+#pragma unroll
+                    for (int ob = 0; ob < C::TD; ++ob)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            de[ob][r] += half == 0 ? d[ob][r] * g[ob][r] : d[ob][r] * (1.0f - g[ob][r]);
+                    if (!ka->ablate) store_slab<C::TD>(scr, de, T.dEF + half * D, 2 * D, s * 16, R, lane);
+                }
+            }
+            __syncthreads();  // the next round's G2^T overwrites G1^T
+        }
+        return;
+    }
+    stage_g2t();
+#pragma unroll
+    for (int e0 = 0; e0 < N1; e0 += NT) {
         const int e = e0 + (int)threadIdx.x;
         if (e < N1) {
             const int j = e / (2 * D / 4), c = 4 * (e % (2 * D / 4));  // G1 [HG][2D]
@@ -420,7 +545,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_bwd_kernel(GateArgs) {
         }
     }
     __syncthreads();
-    for (int64_t s = (int64_t)bidx * kGateWaves + wave; s < nslab; s += stride) {
+    for (int64_t s = (int64_t)bidx * NW + wave; s < nslab; s += stride) {
         const int64_t row = s * 16 + li;
         const bool ok = row < R;
         const int64_t rr = ok ? row : R - 1;
@@ -443,7 +568,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_bwd_kernel(GateArgs) {
                 if ((X || ka->direct) && ok && !ka->ablate) stg4(T.dq + row * D + 16 * t + 4 * q, dq[t]);
             }
             if (!(X || ka->direct) && !ka->ablate)
-                store_slab<C::TD>(lds + C::B_LDS + wave * kSlabScratch, dq, T.dq, D, s * 16, R, lane);
+                store_slab<C::TD>(scr, dq, T.dq, D, s * 16, R, lane);
             zero(dz);
             tile_gemm<C::TH, C::TD, C::B_LD1>(g2t, 0, dq, dz, li, q);  // dz^T = G2^T . dq^T
         }
@@ -454,7 +579,7 @@ __global__ __launch_bounds__(kGateThreads) void gate_bwd_kernel(GateArgs) {
             if ((X || ka->direct) && ok && !ka->ablate) stg4(T.dz + row * HG + 16 * ob + 4 * q, dz[ob]);
         }
         if (!(X || ka->direct) && !ka->ablate)
-            store_slab<C::TH>(lds + C::B_LDS + wave * kSlabScratch, dz, T.dz, HG, s * 16, R, lane);
+            store_slab<C::TH>(scr, dz, T.dz, HG, s * 16, R, lane);
         // dEF^T = G1^T . dz^T + [dT g | dT (1 - g)], in two halves (e part, f part)
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
@@ -472,13 +597,13 @@ __global__ __launch_bounds__(kGateThreads) void gate_bwd_kernel(GateArgs) {
                 for (int ob = 0; ob < C::TD; ++ob) stg4(T.dEF + row * 2 * D + half * D + 16 * ob + 4 * q, de[ob]);
             }
             if (!(X || ka->direct) && !ka->ablate)
-                store_slab<C::TD>(lds + C::B_LDS + wave * kSlabScratch, de, T.dEF + half * D, 2 * D, s * 16, R, lane);
+                store_slab<C::TD>(scr, de, T.dEF + half * D, 2 * D, s * 16, R, lane);
         }
     }
 }
 
 // persistent grid: about one block per CU, split between the towers by row count
-int gate_blocks(GateArgs& a) {
+int gate_blocks(GateArgs& a, int waves) {
     static int cus = 0;
     if (cus == 0) {
         int dev = 0, n = 0;
@@ -491,7 +616,7 @@ int gate_blocks(GateArgs& a) {
     for (int i = 0; i < a.count; ++i) total += a.tw[i].R;
     int sum = 0;
     for (int i = 0; i < a.count; ++i) {
-        const int64_t need = ceil_div(ceil_div(a.tw[i].R, 16), kGateWaves);  // blocks with a slab per wave
+        const int64_t need = ceil_div(ceil_div(a.tw[i].R, 16), waves);  // blocks with a slab per wave
         int64_t share = (cus * a.tw[i].R + total - 1) / total;
         if (share > need) share = need;
         a.tw[i].blocks = (int)(share < 1 ? 1 : share);
@@ -502,7 +627,8 @@ int gate_blocks(GateArgs& a) {
 
 template <int D, int HG>
 int launch_gate_t(GateArgs& a, bool backward, hipStream_t s) {
-    const int blocks = gate_blocks(a);
+    const int blocks = gate_blocks(a, GateWaves<D>::NW);
+    constexpr int kGateThreads = GateWaves<D>::THREADS;
     // TTAMM_GATE_SPLIT=1: the 2D-wide GEMM on split-bf16 MFMA.  Measured at C2 (D = 96): forward
     // 64 -> 62 us, backward 67 -> 79 us, step 0.726 -> 0.758 ms (profiles/r03_c2_gate_split_s17.txt):
     // the kernels are not MFMA-bound (SQ: ~31 % MFMA busy, profiles/r03_c2_pmc_sq_s13.json) and the
@@ -523,7 +649,7 @@ int launch_gate_t(GateArgs& a, bool backward, hipStream_t s) {
 
 }  // namespace
 
-bool gate_fused_supported(int D, int HG) { return D == HG && (D == 32 || D == 64 || D == 96); }
+bool gate_fused_supported(int D, int HG) { return D == HG && (D == 32 || D == 64 || D == 96 || D == 128); }
 
 int launch_gate(GateArgs& a, bool backward, hipStream_t s) {
     static const bool ablate = std::getenv("TTAMM_GATE_ABLATE") != nullptr;
@@ -535,7 +661,8 @@ int launch_gate(GateArgs& a, bool backward, hipStream_t s) {
     switch (a.D) {
         case 32: return launch_gate_t<32, 32>(a, backward, s);
         case 64: return launch_gate_t<64, 64>(a, backward, s);
-        default: return launch_gate_t<96, 96>(a, backward, s);
+        case 96: return launch_gate_t<96, 96>(a, backward, s);
+        default: return launch_gate_t<128, 128>(a, backward, s);
     }
 }
 

@@ -680,7 +680,22 @@ int launch_sample_negatives(const int64_t* users, int64_t batch, int num_neg, in
 // The step's prologue in one launch: staging (StageArgs), the negative sampler (when num_neg > 0;
 // as launch_sample_negatives, users = the RAW batch ids, range-checked against user_rows) and,
 // by the last block, launch_step_begin's work.  done: a uint32 in the zeroed workspace.
+// the first feature layer's weight in the layout its GEMM reads (rows padded to 16 B, or rounded
+// to bf16 and padded to a multiple of 8), formed in the step prologue's launch (it changes every
+// step: the dense optimizer), not in launches of their own ahead of the GEMM
+struct WeightPrep {
+    const float* src;
+    int64_t rows;
+    int cols;
+    int64_t ld_src;
+    void* dst;       // float (bf16 == 0) or uint16 (bf16 == 1)
+    int64_t ld_dst;  // elements
+    int bf16;
+};
+constexpr int kMaxWeightPrep = 2;
 struct PrologueArgs {
+    WeightPrep prep[kMaxWeightPrep];
+    int n_prep;
     const int64_t* users;
     int64_t user_rows;
     int64_t batch;

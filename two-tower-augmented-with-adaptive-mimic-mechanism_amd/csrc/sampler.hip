@@ -95,6 +95,17 @@ __global__ void step_prologue_kernel(StepPrologue) {
         }
         if (st->status && __ballot(bad) != 0ull && (threadIdx.x & 63) == 0)
             atomicOr(st->status, TTAMM_STATUS_INDEX_OUT_OF_RANGE);
+    } else if (y >= st->count + (pa->num_neg > 0 ? 1 : 0)) {
+        // weight prep segment: the first feature layer's weight padded / rounded to bf16
+        const KArg(WeightPrep)& W = pa->prep[y - st->count - (pa->num_neg > 0 ? 1 : 0)];
+        const int64_t total = W.rows * W.ld_dst;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+            const int64_t r = i / W.ld_dst;
+            const int c = (int)(i - r * W.ld_dst);
+            const float v = c < W.cols ? W.src[r * W.ld_src + c] : 0.f;
+            if (W.bf16) static_cast<uint16_t*>(W.dst)[i] = __builtin_bit_cast(uint16_t, (__bf16)v);  // RNE
+            else static_cast<float*>(W.dst)[i] = v;
+        }
     } else {
         const int64_t slots = pa->batch * pa->num_neg;
         for (int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; slot < slots;
@@ -141,7 +152,14 @@ int launch_step_prologue(const StageArgs& st, const PrologueArgs& pa, hipStream_
     int64_t gx = ceil_div(most, 256);
     if (gx > 64) gx = 64;
     if (gx < 1) gx = 1;
-    const unsigned gy = (unsigned)st.count + (pa.num_neg > 0 ? 1u : 0u);
+    TTAMM_REQUIRE(pa.n_prep >= 0 && pa.n_prep <= kMaxWeightPrep, "step prologue: weight prep segments");
+    for (int i = 0; i < pa.n_prep; ++i) {
+        const WeightPrep& w = pa.prep[i];
+        TTAMM_REQUIRE(w.src && w.dst && w.rows > 0 && w.cols > 0 && w.ld_dst >= w.cols && w.ld_src >= w.cols,
+                      "step prologue: bad weight prep segment");
+        most = w.rows * w.ld_dst > most ? w.rows * w.ld_dst : most;
+    }
+    const unsigned gy = (unsigned)st.count + (pa.num_neg > 0 ? 1u : 0u) + (unsigned)pa.n_prep;
     TTAMM_REQUIRE(gy >= 1 && gx * gy < (int64_t(1) << 31), "step prologue: grid too large");
     hipLaunchKernelGGL(step_prologue_kernel, dim3((unsigned)gx, gy), dim3(256), 0, s, StepPrologue{st, pa});
     TTAMM_LAUNCH_CHECK();

@@ -83,6 +83,9 @@ struct TowerWs {
     float* piece_a = nullptr;
     float* wpad = nullptr;  // first feature layer weight, in_features padded to a multiple of 4
     uint16_t* w16 = nullptr;  // bf16 towers with bf16 feature rows: the weight rounded, padded to % 8
+    // wpad / w16 formed by this step's prologue launch (ttamm_train_step; the standalone tower
+    // entry points form them themselves)
+    bool weight_prepped = false;
     int wgrad_rps[kWgradClasses] = {512, 512, 512, 512};  // split-K rows of the weight gradients, per tile class
 };
 
@@ -601,15 +604,17 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
                 p.ldb = L.in_features;
                 if (l == 0 && w.w16) {  // bf16 operands in memory (C5 layer 1)
                     const int kp = round8(L.in_features);
-                    if ((rc = launch_to_bf16(L.weight, L.out_features, L.in_features, L.in_features, w.w16, kp, s)))
+                    if (!w.weight_prepped &&
+                        (rc = launch_to_bf16(L.weight, L.out_features, L.in_features, L.in_features, w.w16, kp, s)))
                         return rc;
                     p.A16 = t.features_bf16;
                     p.lda = t.feat_bf16_ld;
                     p.B16 = w.w16;
                     p.ldb = kp;
                 } else if (l == 0 && w.wpad) {
-                    pads.seg[pads.count++] = PadSeg{L.weight, L.out_features, L.in_features, L.in_features, w.wpad,
-                                                    round4(L.in_features)};
+                    if (!w.weight_prepped)
+                        pads.seg[pads.count++] = PadSeg{L.weight, L.out_features, L.in_features, L.in_features, w.wpad,
+                                                        round4(L.in_features)};
                     p.B = w.wpad;
                     p.ldb = round4(L.in_features);
                 }
@@ -1655,6 +1660,11 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     if (!shard) I.renorm_split = B;
     const ttamm_tower* T[2] = {&A.user, &A.item};
     TowerWs* W[2] = {&U, &I};
+    // the SAMPLE phase's prologue forms the first-layer weights (every step runs it first)
+    {
+        const char* e = std::getenv("TTAMM_PROLOGUE_PREP");  // "0": separate pad / bf16 launches (A/B)
+        U.weight_prepped = I.weight_prepped = !(e && e[0] == '0');
+    }
     const ttamm_hparams& hp = A.hp;
     AdamConsts ad = hp.dense_optimizer == TTAMM_DENSE_SGD
                         ? make_sgd_consts(hp.lr, hp.weight_decay, hp.momentum, hp.dampening, hp.nesterov,
@@ -1711,6 +1721,20 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
             pa.out2 = (!shard && A.b.neg_items != neg) ? A.b.neg_items : nullptr;
         }
         pa.done = ws.prologue_done;
+        // the first feature layer's weight in its GEMM's layout, in this launch (both towers; every
+        // later phase of the step reads it: tower_forward skips its own pad / bf16 launches)
+        for (int k = 0; k < 2; ++k) {
+            const ttamm_tower& t = *T[k];
+            TowerWs& w = *W[k];
+            if (t.fusion == TTAMM_FUSION_IDENTITY || t.n_linear == 0 || !w.weight_prepped) continue;
+            const ttamm_linear& L = t.linear[0];
+            if (w.w16)
+                pa.prep[pa.n_prep++] = WeightPrep{L.weight, L.out_features, L.in_features, L.in_features, w.w16,
+                                                  round8(L.in_features), 1};
+            else if (w.wpad)
+                pa.prep[pa.n_prep++] = WeightPrep{L.weight, L.out_features, L.in_features, L.in_features, w.wpad,
+                                                  round4(L.in_features), 0};
+        }
         pa.applied = A.steps_applied;
         pa.hist = df.on ? df.hist : nullptr;
         pa.cap = df.on ? df.cap : 2;
