@@ -1660,10 +1660,13 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     if (!shard) I.renorm_split = B;
     const ttamm_tower* T[2] = {&A.user, &A.item};
     TowerWs* W[2] = {&U, &I};
-    // the SAMPLE phase's prologue forms the first-layer weights (every step runs it first)
+    // TTAMM_PROLOGUE_PREP=1: the SAMPLE phase's prologue forms the first-layer weights (every step
+    // runs it first) instead of the pad / bf16 launches before the first GEMM.  Measured slower at
+    // C2 (0.660 vs 0.648 ms/step, two A/B pairs on one box; C5 unchanged at 1.413 ms,
+    // profiles/r05_s9_prologue_prep.txt): the first GEMM waits for the whole prologue grid
     {
-        const char* e = std::getenv("TTAMM_PROLOGUE_PREP");  // "0": separate pad / bf16 launches (A/B)
-        U.weight_prepped = I.weight_prepped = !(e && e[0] == '0');
+        const char* e = std::getenv("TTAMM_PROLOGUE_PREP");
+        U.weight_prepped = I.weight_prepped = e && e[0] == '1';
     }
     const ttamm_hparams& hp = A.hp;
     AdamConsts ad = hp.dense_optimizer == TTAMM_DENSE_SGD
