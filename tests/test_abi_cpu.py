@@ -119,3 +119,22 @@ def test_train_step_validation_rejects_bad_descriptors():
     with pytest.raises(ValueError, match="% 4"):
         _lib.check(lib.ttamm_train_step(ctypes.byref(args), None))
     assert lib.ttamm_train_step_workspace_size(ctypes.byref(args)) > 0
+
+
+@pytest.mark.parametrize("row_base", [-1, 5])
+def test_inbatch_bce_rejects_row_base_outside_the_columns(row_base):
+    """ttamm_inbatch_bce checks row_base itself (not only the Python wrapper): the B users' label
+    diagonal must lie inside the Bc positive columns.  The check runs before any device work, so
+    it is exercised here with host buffers that are never touched."""
+    from ttamm import _lib
+
+    lib = _lib.load()
+    B, Bc, D = 4, 8, 16
+    buf = (ctypes.c_float * 64)()
+    loss = ctypes.c_double(0.0)
+    ws = (ctypes.c_char * 16)()
+    p = ctypes.cast(buf, ctypes.c_void_p)
+    rc = lib.ttamm_inbatch_bce(p, B, D, p, Bc, D, D, row_base, 1.0, p, D, p, D, ctypes.byref(loss),
+                               ctypes.cast(ws, ctypes.c_void_p), 16, None)
+    assert rc != 0
+    assert b"row_base" in lib.ttamm_last_error()

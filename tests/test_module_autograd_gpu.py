@@ -218,3 +218,42 @@ def test_tower_forward_with_mimic_rows_under_autograd():
     want = torch.zeros_like(table).index_add_(0, pos.cuda(), w)
     assert rel_err(table.grad, want) <= 1e-6
     assert model.item_encoder.embedding.weight.grad is not None
+
+
+@pytest.mark.parametrize("D", [128, 256])
+def test_bf16_tower_fused_gate_matches_generic_gate(D, monkeypatch):
+    """The module path (ttamm_tower_forward / _backward) of a bf16 gated tower at D == Hg in
+    {128, 256}: the fused bf16 gate (gate16.hip, its weight images formed in each call) against the
+    generic two-GEMM gate (TTAMM_GENERIC_GATE=1) on the same rows and output gradient, at the bf16
+    tolerance of the step tests (2e-3 max-norm, 2e-5 mean, per tensor)."""
+    import copy
+
+    shape = Shape(U=900, I=900, F=40, H=D, D=D, hidden_dims=(D,), matmul_dtype="bf16", dropout=0.0)
+    torch.manual_seed(7)
+    enc0 = ttamm.build_tower_encoder(shape.tower_cfg(), num_embeddings=900, feature_dim=40, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(7)
+    R = 1300  # 11 blocks of 128 rows, the last one partial
+    idx = torch.randint(0, 900, (R,), device="cuda", generator=g)
+    feats = torch.randn((R, 40), device="cuda", generator=g)
+    dT = torch.randn((R, D), device="cuda", generator=g)
+    res = {}
+    for mode in ("fused", "generic"):
+        if mode == "generic":
+            monkeypatch.setenv("TTAMM_GENERIC_GATE", "1")
+        else:
+            monkeypatch.delenv("TTAMM_GENERIC_GATE", raising=False)
+        enc = copy.deepcopy(enc0)
+        out = enc({"indices": idx, "features": feats})
+        out.backward(dT)
+        torch.cuda.synchronize()
+        grads = {n: (p.grad.to_dense() if p.grad.is_sparse else p.grad).clone()
+                 for n, p in enc.named_parameters() if p.grad is not None}
+        res[mode] = (out.detach().clone(), grads)
+    (of, gf), (og, gg) = res["fused"], res["generic"]
+    assert rel_err(of, og) <= 2e-3
+    assert set(gf) == set(gg) and gf
+    for n in gg:
+        err = rel_err(gf[n], gg[n])
+        mean = ((gf[n].double() - gg[n].double()).abs().mean() / gg[n].double().abs().max().clamp_min(1e-30)).item()
+        assert err <= 2e-3, f"{n}: rel err {err:.3e}"
+        assert mean <= 2e-5, f"{n}: mean rel err {mean:.3e}"

@@ -110,20 +110,29 @@ def test_three_steps_match_oracle(shape):
 # fp32 accumulation).  Both sides round the SAME definition, but an fp32 activation that differs
 # by one ulp (summation order) can round to the neighbouring bf16 value, so the tolerance is the
 # bf16 one: max-norm relative 2e-3 per tensor, and the mean error stays at fp32 level.
+# D == Hg in {128, 256} runs the fused bf16 gate (gate16.hip) unless TTAMM_GENERIC_GATE=1 ("generic").
 BF16_TOL = 2e-3
 
 
+@pytest.mark.parametrize("generic", [False, True], ids=["fused", "generic"])
 @pytest.mark.parametrize(
     "shape",
     [
         Shape(matmul_dtype="bf16"),
         Shape(U=50, I=300, F=37, H=24, D=12, B=40, N=3, gate_hidden=20, hidden_dims=(24,), matmul_dtype="bf16"),
         Shape(U=96, I=768, F=605, H=512, D=256, B=48, N=5, hidden_dims=(512,), matmul_dtype="bf16"),
+        Shape(U=3000, I=20000, F=64, H=128, D=128, B=1500, N=3, hidden_dims=(128,), matmul_dtype="bf16"),
+        Shape(U=2000, I=8000, F=605, H=512, D=256, B=300, N=3, hidden_dims=(512,), matmul_dtype="bf16", mimic=False),
     ],
-    ids=["tiny", "odd", "c5-dims"],
+    ids=["tiny", "odd", "c5-dims", "d128-rows", "d256-nomimic"],
 )
-def test_bf16_step_gradients_match_bf16_oracle(shape):
+def test_bf16_step_gradients_match_bf16_oracle(shape, generic, monkeypatch):
     from gpu_helpers import run_ttamm
+
+    if generic:
+        monkeypatch.setenv("TTAMM_GENERIC_GATE", "1")
+    else:
+        monkeypatch.delenv("TTAMM_GENERIC_GATE", raising=False)
 
     prob = make_problem(shape, steps=1)
     om, oo, ores = run_oracle(prob, lr=0.0, betas=(0.0, 0.999))

@@ -56,7 +56,7 @@ def hazards_in_listing(lines) -> list[tuple[str, str]]:
 
 # library objects that hold kernels: finding no gfx950 code in one of them means the section or
 # bundle naming changed under a toolchain update and the scan would check nothing -> fail
-KERNEL_OBJECTS = {"rows.o", "optim.o", "cal.o", "gemm.o", "gate.o", "inbatch.o", "retrieval.o",
+KERNEL_OBJECTS = {"rows.o", "optim.o", "cal.o", "gemm.o", "gate.o", "gate16.o", "inbatch.o", "retrieval.o",
                   "sampler.o", "data.o", "route.o"}
 
 

@@ -652,6 +652,11 @@ int launch_gate_t(GateArgs& a, bool backward, hipStream_t s) {
 bool gate_fused_supported(int D, int HG) { return D == HG && (D == 32 || D == 64 || D == 96 || D == 128); }
 
 int launch_gate(GateArgs& a, bool backward, hipStream_t s) {
+    if (a.bf16) {
+        int rc;
+        if ((rc = launch_gate16_prep(a, s))) return rc;
+        return launch_gate16(a, backward, s);
+    }
     static const bool ablate = std::getenv("TTAMM_GATE_ABLATE") != nullptr;
     static const bool direct = std::getenv("TTAMM_GATE_DIRECT_STORES") != nullptr;
     a.ablate = ablate ? 1 : 0;

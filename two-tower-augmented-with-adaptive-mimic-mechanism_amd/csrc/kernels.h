@@ -181,17 +181,25 @@ struct GateTower {
     float* dq;           // [R, D]
     float* dz;           // [R, Hg]
     float* dEF;          // [R, 2D]
+    uint16_t* w16;       // bf16 towers: the weight images (gate16.hip, gate16_image_elems)
     int blocks;          // filled by the launcher
 };
 struct GateArgs {
     GateTower tw[2];
     int count;
     int D, HG;
+    int bf16;  // bf16 towers: gate16.hip (operands rounded to bf16, fp32 accumulation)
     int ablate;  // developer timing ablation (TTAMM_GATE_ABLATE=1: no output stores); set by launch_gate
     int direct;  // TTAMM_GATE_DIRECT_STORES=1: stores from the MFMA layout (16 rows x 64 B each); set by launch_gate
 };
 bool gate_fused_supported(int D, int HG);
 int launch_gate(GateArgs& a, bool backward, hipStream_t s);
+// bf16 towers (gate16.hip): D == Hg in {128, 256}; the per-tower bf16 weight images are formed by
+// launch_gate16_prep (launch_gate runs it before each direction when a.bf16)
+bool gate16_supported(int D, int HG);
+int64_t gate16_image_elems(int D, int HG);
+int launch_gate16_prep(GateArgs& a, hipStream_t s);
+int launch_gate16(GateArgs& a, bool backward, hipStream_t s);
 
 // ------------------------------------------------------------------------------------
 // Row kernels (rows.hip)

@@ -83,6 +83,7 @@ struct TowerWs {
     float* piece_a = nullptr;
     float* wpad = nullptr;  // first feature layer weight, in_features padded to a multiple of 4
     uint16_t* w16 = nullptr;  // bf16 towers with bf16 feature rows: the weight rounded, padded to % 8
+    uint16_t* gw16 = nullptr;  // bf16 gated towers (D == Hg in {128, 256}): the fused gate's weight images
     // wpad / w16 formed by this step's prologue launch (ttamm_train_step; the standalone tower
     // entry points form them themselves)
     bool weight_prepped = false;
@@ -315,6 +316,7 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
             w.dz = ar.take<float>((size_t)R * Hg);
             w.g = ar.take<float>((size_t)R * D);
             w.dq = ar.take<float>((size_t)R * D);
+            if (T.matmul_bf16 && gate16_supported(D, Hg)) w.gw16 = ar.take<uint16_t>((size_t)gate16_image_elems(D, Hg));
         } else if (!uses_ef(T)) {
             w.e = ar.take<float>((size_t)R * D);
             if (T.fusion == TTAMM_FUSION_SUM) w.f = ar.take<float>((size_t)R * D);
@@ -472,9 +474,9 @@ void set_keys(GemmProblem& p, const TowerWs& w) {
 }
 
 // ---- fused gate (gate.hip) ------------------------------------------------------------------
-// Used when every gated tower of a grouped launch is fp32 with a supported D == Hg; any other
-// configuration (bf16 towers, other widths) runs the generic GEMM path.  TTAMM_GENERIC_GATE=1
-// forces the generic path (the tests run both).
+// Used when every gated tower of a grouped launch has a supported D == Hg: fp32 towers gate.hip
+// (D in {32, 64, 96, 128}), bf16 towers gate16.hip (D in {128, 256}); any other configuration runs
+// the generic GEMM path.  TTAMM_GENERIC_GATE=1 forces the generic path (the tests run both).
 bool generic_gate_forced() {
     const char* v = std::getenv("TTAMM_GENERIC_GATE");
     return v && v[0] == '1';
@@ -483,15 +485,19 @@ bool generic_gate_forced() {
 bool gate_group(const ttamm_tower* const* T, TowerWs* const* W, int ntowers, int D, bool mimic, GateArgs& ga) {
     std::memset(&ga, 0, sizeof(ga));
     if (generic_gate_forced()) return false;
-    int hg = -1;
+    int hg = -1, b16 = -1;
     for (int k = 0; k < ntowers; ++k) {
         const ttamm_tower& t = *T[k];
         if (t.fusion != TTAMM_FUSION_GATED) continue;
         const int h = t.gate[0].out_features;
-        if (t.matmul_bf16 || !gate_fused_supported(D, h) || (hg >= 0 && h != hg)) return false;
+        const int tb = t.matmul_bf16 ? 1 : 0;
+        if ((hg >= 0 && h != hg) || (b16 >= 0 && tb != b16)) return false;
+        if (tb ? !(gate16_supported(D, h) && W[k]->gw16) : !gate_fused_supported(D, h)) return false;
         hg = h;
+        b16 = tb;
     }
     if (hg < 0) return false;
+    ga.bf16 = b16;
     for (int k = 0; k < ntowers; ++k) {
         const ttamm_tower& t = *T[k];
         const TowerWs& w = *W[k];
@@ -516,6 +522,7 @@ bool gate_group(const ttamm_tower* const* T, TowerWs* const* W, int ntowers, int
         g.dq = w.dq;
         g.dz = w.dz;
         g.dEF = w.dEF;
+        g.w16 = w.gw16;
     }
     ga.D = D;
     ga.HG = hg;
@@ -2140,6 +2147,7 @@ void plan_tower_train(Arena& ar, const ttamm_tower& T, int64_t n, TowerWs& w) {
         w.dz = ar.take<float>((size_t)n * Hg);
         w.g = ar.take<float>((size_t)n * D);
         w.dq = ar.take<float>((size_t)n * D);
+        if (T.matmul_bf16 && gate16_supported(D, Hg)) w.gw16 = ar.take<uint16_t>((size_t)gate16_image_elems(D, Hg));
     }
     WgradShape shapes[TTAMM_MAX_LINEAR + 2];
     const int ns = wgrad_shapes(T, n, shapes);
