@@ -654,7 +654,7 @@ bool gate_fused_supported(int D, int HG) { return D == HG && (D == 32 || D == 64
 int launch_gate(GateArgs& a, bool backward, hipStream_t s) {
     if (a.bf16) {
         int rc;
-        if ((rc = launch_gate16_prep(a, s))) return rc;
+        if (!a.images_ready && (rc = launch_gate16_prep(a, s))) return rc;
         return launch_gate16(a, backward, s);
     }
     static const bool ablate = std::getenv("TTAMM_GATE_ABLATE") != nullptr;

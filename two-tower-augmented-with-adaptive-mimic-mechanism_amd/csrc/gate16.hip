@@ -281,30 +281,41 @@ __global__ __launch_bounds__(kG16Threads) void gate16_fwd_kernel(GateArgs) {
     acc_to_rows<D>(xs, acc, r, h);
     const int lr = lane / (D / 4), f0 = 4 * (lane % (D / 4));
     const f4v c2 = *reinterpret_cast<const f4v*>(cb + HG + f0);
-#pragma unroll 4
-    for (int it = 0; it < 32 / RPI; ++it) {
-        const int rl = it * RPI + lr;
-        const int64_t grow_ = wrow0 + rl;
-        if (grow_ >= R) continue;
-        const f4v x = *reinterpret_cast<const f4v*>(xs + rl * L::XROW + f0);
-        const float* er = T.ef + grow_ * K1;
-        const f4v e4 = ld4(er + f0), fv = ld4(er + D + f0);
-        f4v gg, tt;
+    // batches of RB rows: every load of a batch issued before its stores (the stores may alias
+    // the loads as far as the compiler knows, so it would not hoist them itself)
+    constexpr int RB = 8;
+    for (int it0 = 0; it0 < 32 / RPI; it0 += RB) {
+        f4v e4[RB], fv[RB], a4[RB];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            gg[i] = __builtin_amdgcn_rcpf(1.0f + __expf(-(x[i] + c2[i])));
-            tt[i] = gg[i] * e4[i] + (1.0f - gg[i]) * fv[i];
+        for (int j = 0; j < RB; ++j) {
+            const int64_t g0 = wrow0 + (it0 + j) * RPI + lr;
+            const int64_t gr = g0 < R ? g0 : R - 1;
+            e4[j] = ld4(T.ef + gr * K1 + f0);
+            fv[j] = ld4(T.ef + gr * K1 + D + f0);
+            if (T.table) a4[j] = ld4(T.table + T.idx[gr] * (int64_t)D + f0);
         }
-        st4(T.g + grow_ * D + f0, gg);
-        st4(T.t + grow_ * T.ld_t + f0, tt);
-        f4v aug = tt;
-        if (T.table) {
-            const f4v a4 = ld4(T.table + T.idx[grow_] * (int64_t)D + f0);
-            st4(T.a + grow_ * T.ld_t + f0, a4);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) aug[i] = tt[i] + a4[i];
+        for (int j = 0; j < RB; ++j) {
+            const int rl = (it0 + j) * RPI + lr;
+            const int64_t grow_ = wrow0 + rl;
+            if (grow_ >= R) continue;
+            const f4v x = *reinterpret_cast<const f4v*>(xs + rl * L::XROW + f0);
+            f4v gg, tt;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                gg[i] = __builtin_amdgcn_rcpf(1.0f + __expf(-(x[i] + c2[i])));
+                tt[i] = gg[i] * e4[j][i] + (1.0f - gg[i]) * fv[j][i];
+            }
+            st4(T.g + grow_ * D + f0, gg);
+            st4(T.t + grow_ * T.ld_t + f0, tt);
+            f4v aug = tt;
+            if (T.table) {
+                st4(T.a + grow_ * T.ld_t + f0, a4[j]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) aug[i] = tt[i] + a4[j][i];
+            }
+            if (T.aug) st4(T.aug + grow_ * D + f0, aug);
         }
-        if (T.aug) st4(T.aug + grow_ * D + f0, aug);
     }
 }
 
@@ -335,22 +346,32 @@ __global__ __launch_bounds__(kG16Threads) void gate16_bwd_kernel(GateArgs) {
     // dq = (dT e - dT f)(1 - g) g over whole rows (stored; as bf16 into the wave's dq rows, the B
     // operand of the dz product: k = feature)
     uint16_t* qs = lds + 2 * L::QS + wave * 32 * L::QROW;
-#pragma unroll 4
-    for (int it = 0; it < 32 / RPI; ++it) {
-        const int rl = it * RPI + lr;
-        const int64_t grow_ = wrow0 + rl < R ? wrow0 + rl : R - 1;
-        const float* er = T.ef + grow_ * K1;
-        const f4v d4 = ld4(T.dT + grow_ * T.ld_dT + f0), e4 = ld4(er + f0), fv = ld4(er + D + f0),
-                  g4 = ld4(T.g + grow_ * D + f0);
-        f4v q;
+    constexpr int RB = 8, RQ = 4;  // rows per batch: every load of a batch issued before its stores
+    for (int it0 = 0; it0 < 32 / RPI; it0 += RQ) {
+        f4v d4[RQ], e4[RQ], fv[RQ], g4[RQ];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float dg = d4[i] * e4[i] - d4[i] * fv[i];
-            q[i] = dg * (1.0f - g4[i]) * g4[i];
+        for (int j = 0; j < RQ; ++j) {
+            const int64_t g0 = wrow0 + (it0 + j) * RPI + lr;
+            const int64_t gr = g0 < R ? g0 : R - 1;
+            d4[j] = ld4(T.dT + gr * T.ld_dT + f0);
+            e4[j] = ld4(T.ef + gr * K1 + f0);
+            fv[j] = ld4(T.ef + gr * K1 + D + f0);
+            g4[j] = ld4(T.g + gr * D + f0);
         }
-        if (wrow0 + rl < R) st4(T.dq + grow_ * D + f0, q);
-        typedef __bf16 g16_bf16x4 __attribute__((ext_vector_type(4)));
-        *reinterpret_cast<g16_bf16x4*>(qs + rl * L::QROW + f0) = __builtin_convertvector(q, g16_bf16x4);
+#pragma unroll
+        for (int j = 0; j < RQ; ++j) {
+            const int rl = (it0 + j) * RPI + lr;
+            const int64_t grow_ = wrow0 + rl;
+            f4v q;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float dg = d4[j][i] * e4[j][i] - d4[j][i] * fv[j][i];
+                q[i] = dg * (1.0f - g4[j][i]) * g4[j][i];
+            }
+            if (grow_ < R) st4(T.dq + grow_ * D + f0, q);
+            typedef __bf16 g16_bf16x4 __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<g16_bf16x4*>(qs + rl * L::QROW + f0) = __builtin_convertvector(q, g16_bf16x4);
+        }
     }
     // z (the ReLU mask) of the first half of the unit tiles in flight during the dz product
     f4v zp[NT / 2][4];
@@ -429,17 +450,27 @@ __global__ __launch_bounds__(kG16Threads) void gate16_bwd_kernel(GateArgs) {
             buf ^= 1;
         }
         acc_to_rows<D>(xs, acc, r, h);
-#pragma unroll 4
-        for (int it = 0; it < 32 / RPI; ++it) {
-            const int rl = it * RPI + lr;
-            const int64_t grow_ = wrow0 + rl;
-            if (grow_ >= R) continue;
-            const f4v x = *reinterpret_cast<const f4v*>(xs + rl * L::XROW + f0);
-            const f4v d4 = ld4(T.dT + grow_ * T.ld_dT + f0), g4 = ld4(T.g + grow_ * D + f0);
-            f4v de;
+        for (int it0 = 0; it0 < 32 / RPI; it0 += RB) {
+            f4v d4[RB], g4[RB];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) de[i] = x[i] + (pass == 0 ? d4[i] * g4[i] : d4[i] * (1.0f - g4[i]));
-            st4(T.dEF + grow_ * K1 + pass * D + f0, de);
+            for (int j = 0; j < RB; ++j) {
+                const int64_t g0 = wrow0 + (it0 + j) * RPI + lr;
+                const int64_t gr = g0 < R ? g0 : R - 1;
+                d4[j] = ld4(T.dT + gr * T.ld_dT + f0);
+                g4[j] = ld4(T.g + gr * D + f0);
+            }
+#pragma unroll
+            for (int j = 0; j < RB; ++j) {
+                const int rl = (it0 + j) * RPI + lr;
+                const int64_t grow_ = wrow0 + rl;
+                if (grow_ >= R) continue;
+                const f4v x = *reinterpret_cast<const f4v*>(xs + rl * L::XROW + f0);
+                f4v de;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    de[i] = x[i] + (pass == 0 ? d4[j][i] * g4[j][i] : d4[j][i] * (1.0f - g4[j][i]));
+                st4(T.dEF + grow_ * K1 + pass * D + f0, de);
+            }
         }
         __syncthreads();  // every wave is done with its rows before the next pass stages over them
     }

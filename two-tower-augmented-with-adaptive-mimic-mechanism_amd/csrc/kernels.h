@@ -189,6 +189,7 @@ struct GateArgs {
     int count;
     int D, HG;
     int bf16;  // bf16 towers: gate16.hip (operands rounded to bf16, fp32 accumulation)
+    int images_ready;  // bf16: the towers' weight images were formed earlier in this step (no prep)
     int ablate;  // developer timing ablation (TTAMM_GATE_ABLATE=1: no output stores); set by launch_gate
     int direct;  // TTAMM_GATE_DIRECT_STORES=1: stores from the MFMA layout (16 rows x 64 B each); set by launch_gate
 };

@@ -84,6 +84,7 @@ struct TowerWs {
     float* wpad = nullptr;  // first feature layer weight, in_features padded to a multiple of 4
     uint16_t* w16 = nullptr;  // bf16 towers with bf16 feature rows: the weight rounded, padded to % 8
     uint16_t* gw16 = nullptr;  // bf16 gated towers (D == Hg in {128, 256}): the fused gate's weight images
+    bool gw16_ready = false;   // formed by this call's forward (the weights do not change before its backward)
     // wpad / w16 formed by this step's prologue launch (ttamm_train_step; the standalone tower
     // entry points form them themselves)
     bool weight_prepped = false;
@@ -498,6 +499,7 @@ bool gate_group(const ttamm_tower* const* T, TowerWs* const* W, int ntowers, int
     }
     if (hg < 0) return false;
     ga.bf16 = b16;
+    ga.images_ready = 1;
     for (int k = 0; k < ntowers; ++k) {
         const ttamm_tower& t = *T[k];
         const TowerWs& w = *W[k];
@@ -523,6 +525,7 @@ bool gate_group(const ttamm_tower* const* T, TowerWs* const* W, int ntowers, int
         g.dz = w.dz;
         g.dEF = w.dEF;
         g.w16 = w.gw16;
+        if (!w.gw16_ready) ga.images_ready = 0;
     }
     ga.D = D;
     ga.HG = hg;
@@ -677,8 +680,10 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
     // fusion
     GateArgs ga;
     const bool fused_gate = gate_group(T, W, ntowers, D, mimic, ga);
-    if (fused_gate && ga.count > 0)
+    if (fused_gate && ga.count > 0) {
         if ((rc = launch_gate(ga, false, s))) return rc;
+        for (int k = 0; k < ntowers; ++k) W[k]->gw16_ready = W[k]->gw16 != nullptr;
+    }
     Batcher g1, g2, gc;
     for (int k = 0; k < ntowers; ++k) {
         const ttamm_tower& t = *T[k];
