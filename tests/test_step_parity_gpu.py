@@ -177,12 +177,24 @@ GATE_SHAPES = [
 @pytest.mark.parametrize("shape", GATE_SHAPES,
                          ids=["d32", "d64", "d96-c2dims", "d32-nomimic", "d32-dense-id", "d128", "d128-rounds"])
 def test_gate_paths_match_oracle(shape, generic, monkeypatch):
-    from gpu_helpers import run_ttamm
-
     if generic:
         monkeypatch.setenv("TTAMM_GENERIC_GATE", "1")
     else:
         monkeypatch.delenv("TTAMM_GENERIC_GATE", raising=False)
+    _gate_case(shape)
+
+
+def test_gate16_split_form_matches_oracle_at_d96(monkeypatch):
+    """fp32 towers at D = 96 on gate16.hip's split-bf16 form (TTAMM_GATE16_SPLIT=1, opt-in: measured
+    slower than gate.hip at C2), at the fp32 tolerance."""
+    monkeypatch.setenv("TTAMM_GATE16_SPLIT", "1")
+    monkeypatch.delenv("TTAMM_GENERIC_GATE", raising=False)
+    _gate_case(GATE_SHAPES[2])
+
+
+def _gate_case(shape):
+    from gpu_helpers import run_ttamm
+
     prob = make_problem(shape, steps=1)
     om, oo, ores = run_oracle(prob, lr=0.0, betas=(0.0, 0.999))
     tm, to, tres = run_ttamm(prob, lr=0.0, betas=(0.0, 0.999))

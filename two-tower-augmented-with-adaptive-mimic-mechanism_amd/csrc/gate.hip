@@ -652,7 +652,7 @@ int launch_gate_t(GateArgs& a, bool backward, hipStream_t s) {
 bool gate_fused_supported(int D, int HG) { return D == HG && (D == 32 || D == 64 || D == 96 || D == 128); }
 
 int launch_gate(GateArgs& a, bool backward, hipStream_t s) {
-    if (a.bf16) {
+    if (a.planes) {
         int rc;
         if (!a.images_ready && (rc = launch_gate16_prep(a, s))) return rc;
         return launch_gate16(a, backward, s);

@@ -188,17 +188,20 @@ struct GateArgs {
     GateTower tw[2];
     int count;
     int D, HG;
-    int bf16;  // bf16 towers: gate16.hip (operands rounded to bf16, fp32 accumulation)
-    int images_ready;  // bf16: the towers' weight images were formed earlier in this step (no prep)
+    // gate16.hip operand planes: 1 = bf16 towers (operands rounded to bf16), 3 = fp32 towers
+    // (split-bf16, fp32-accurate); 0 = gate.hip (fp32 MFMA)
+    int planes;
+    int images_ready;  // gate16: the towers' weight images were formed earlier in this step (no prep)
     int ablate;  // developer timing ablation (TTAMM_GATE_ABLATE=1: no output stores); set by launch_gate
     int direct;  // TTAMM_GATE_DIRECT_STORES=1: stores from the MFMA layout (16 rows x 64 B each); set by launch_gate
 };
 bool gate_fused_supported(int D, int HG);
 int launch_gate(GateArgs& a, bool backward, hipStream_t s);
-// bf16 towers (gate16.hip): D == Hg in {128, 256}; the per-tower bf16 weight images are formed by
-// launch_gate16_prep (launch_gate runs it before each direction when a.bf16)
-bool gate16_supported(int D, int HG);
-int64_t gate16_image_elems(int D, int HG);
+// gate16.hip: bf16 towers at D == Hg in {128, 256} (planes 1), fp32 towers at D == Hg == 96
+// (planes 3); the per-tower bf16 weight images are formed by launch_gate16_prep (launch_gate runs
+// it unless a.images_ready)
+bool gate16_supported(int D, int HG, int planes);
+int64_t gate16_image_elems(int D, int HG, int planes);
 int launch_gate16_prep(GateArgs& a, hipStream_t s);
 int launch_gate16(GateArgs& a, bool backward, hipStream_t s);
 

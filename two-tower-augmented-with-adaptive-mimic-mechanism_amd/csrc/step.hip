@@ -317,7 +317,8 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
             w.dz = ar.take<float>((size_t)R * Hg);
             w.g = ar.take<float>((size_t)R * D);
             w.dq = ar.take<float>((size_t)R * D);
-            if (T.matmul_bf16 && gate16_supported(D, Hg)) w.gw16 = ar.take<uint16_t>((size_t)gate16_image_elems(D, Hg));
+            const int np = T.matmul_bf16 ? 1 : 3;
+            if (gate16_supported(D, Hg, np)) w.gw16 = ar.take<uint16_t>((size_t)gate16_image_elems(D, Hg, np));
         } else if (!uses_ef(T)) {
             w.e = ar.take<float>((size_t)R * D);
             if (T.fusion == TTAMM_FUSION_SUM) w.f = ar.take<float>((size_t)R * D);
@@ -486,19 +487,33 @@ bool generic_gate_forced() {
 bool gate_group(const ttamm_tower* const* T, TowerWs* const* W, int ntowers, int D, bool mimic, GateArgs& ga) {
     std::memset(&ga, 0, sizeof(ga));
     if (generic_gate_forced()) return false;
-    int hg = -1, b16 = -1;
+    // TTAMM_GATE16_SPLIT=1: fp32 towers at D = 96 on gate16.hip's split-bf16 form instead of gate.hip
+    // (fp32 MFMA).  Measured slower at C2 (forward 71 vs 61 us, backward 72 vs 70, step 0.695 vs
+    // 0.655 ms, profiles/r05_s20_gate16_split.txt): the kernels are latency-bound, not MFMA-bound
+    const char* e16 = std::getenv("TTAMM_GATE16_SPLIT");
+    const bool split16 = e16 && e16[0] == '1';
+    int hg = -1, planes = -1;
     for (int k = 0; k < ntowers; ++k) {
         const ttamm_tower& t = *T[k];
         if (t.fusion != TTAMM_FUSION_GATED) continue;
         const int h = t.gate[0].out_features;
-        const int tb = t.matmul_bf16 ? 1 : 0;
-        if ((hg >= 0 && h != hg) || (b16 >= 0 && tb != b16)) return false;
-        if (tb ? !(gate16_supported(D, h) && W[k]->gw16) : !gate_fused_supported(D, h)) return false;
+        int np;
+        if (t.matmul_bf16) {
+            if (!(gate16_supported(D, h, 1) && W[k]->gw16)) return false;
+            np = 1;
+        } else if (split16 && gate16_supported(D, h, 3) && W[k]->gw16) {
+            np = 3;
+        } else if (gate_fused_supported(D, h)) {
+            np = 0;
+        } else {
+            return false;
+        }
+        if ((hg >= 0 && h != hg) || (planes >= 0 && np != planes)) return false;
         hg = h;
-        b16 = tb;
+        planes = np;
     }
     if (hg < 0) return false;
-    ga.bf16 = b16;
+    ga.planes = planes;
     ga.images_ready = 1;
     for (int k = 0; k < ntowers; ++k) {
         const ttamm_tower& t = *T[k];
@@ -2152,7 +2167,8 @@ void plan_tower_train(Arena& ar, const ttamm_tower& T, int64_t n, TowerWs& w) {
         w.dz = ar.take<float>((size_t)n * Hg);
         w.g = ar.take<float>((size_t)n * D);
         w.dq = ar.take<float>((size_t)n * D);
-        if (T.matmul_bf16 && gate16_supported(D, Hg)) w.gw16 = ar.take<uint16_t>((size_t)gate16_image_elems(D, Hg));
+        const int np = T.matmul_bf16 ? 1 : 3;
+        if (gate16_supported(D, Hg, np)) w.gw16 = ar.take<uint16_t>((size_t)gate16_image_elems(D, Hg, np));
     }
     WgradShape shapes[TTAMM_MAX_LINEAR + 2];
     const int ns = wgrad_shapes(T, n, shapes);
