@@ -466,6 +466,7 @@ def main() -> None:
     eng.flush()
     marks[2].record()
     torch.cuda.synchronize()
+    rows1 = getattr(eng, "item_rows_seen", 0)  # the timed steps' owner rows (before the exact sub-line)
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -535,7 +536,7 @@ def main() -> None:
     if not sharded:
         item_rows = B * (1 + N)
     else:
-        item_rows = (getattr(eng, "item_rows_seen", 0) - rows0) / args.steps
+        item_rows = (rows1 - rows0) / args.steps
     rows = {"user": B, "item": item_rows}
     if bf16:
         impl = "bf16 operands, v_mfma_f32_32x32x16_bf16"
