@@ -681,6 +681,9 @@ struct XCfg {
     static constexpr bool APL = APL_;
     static constexpr int RB = KT * 2;  // MN-major row bytes
     static constexpr int TM = BM / WAVES_M, TN = BN / WAVES_N, I = TM / 32, J = TN / 32;
+    // blocks per CU the register budget is planned for: wave tiles of 8 or more accumulator tiles
+    // (128 registers and up) run one wave per SIMD with the whole register file
+    static constexpr int MINB = I * J >= 8 ? 1 : 2;
     static constexpr int A_F4 = APL ? BM * KT * 6 / 16 : BM * KT / 4, B_F4 = BN * KT / 4;
     static_assert(!APL || KT == 16, "A planes: 16-k tiles (one 96-byte chunk per row and k-tile)");
     static constexpr int A_LOADS = (A_F4 + kThreads - 1) / kThreads;
@@ -778,7 +781,7 @@ __device__ __forceinline__ int xcd_remap(int b, int n) {  // bijective: consecut
 }
 
 template <class CX, int E, int PL>
-__global__ __launch_bounds__(kThreads, 2) void gemm_x_kernel(GemmBatch batch) {
+__global__ __launch_bounds__(kThreads, CX::MINB) void gemm_x_kernel(GemmBatch batch) {
     constexpr int BM = CX::BM, BN = CX::BN, TM = CX::TM, TN = CX::TN, I = CX::I, J = CX::J, KT = CX::KT;
     constexpr bool AK = CX::A_KMAJ, BKM = CX::B_KMAJ;
     __shared__ __attribute__((aligned(16))) unsigned char lds[CX::lds_bytes(PL)];
@@ -1733,6 +1736,11 @@ using WgradWideX32 = XCfg<128, 192, 2, 2, true, true, 32>;
 using WgradNarrowX32 = XCfg<128, 96, 4, 1, true, true, 32>;
 using Wgrad128X = XCfg<128, 128, 2, 2, true, true>;
 using Wgrad128X32 = XCfg<128, 128, 2, 2, true, true, 32>;
+// bf16 weight gradients on 256 x 128 tiles (each wave 128 x 64, 8 accumulator tiles): with one
+// plane the 128 x 128 tile (4 per wave) issued ~4 LDS instructions per MFMA (two transposed reads
+// per fragment + the staging writes), so the LDS, not the MFMA, set its pace (C5,
+// profiles/r05_s21_c5_gemm_sq.txt); 256 x 256 (16 per wave) spilled 444 B per thread
+using Wgrad256X32 = XCfg<256, 128, 2, 2, true, true, 32>;
 // X pre-split into planes (the first feature layer's weight gradient, fp32 towers)
 using WgradNarrowXP = XCfg<128, 96, 4, 1, true, true, 16, 2, true>;
 using WgradWideXP = XCfg<128, 192, 2, 2, true, true, 16, 2, true>;
@@ -1841,8 +1849,12 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
     std::memset(gp, 0, sizeof(gp));
     const bool bf = wb.count > 0 && wb.p[0].bf16;
     const bool exact = exact_mfma();
+    // TTAMM_BF16_WGRAD256=1: bf16 weight gradients of the 128-wide classes on 256 x 256 tiles (cfg 3)
+    const char* e256 = std::getenv("TTAMM_BF16_WGRAD256");
+    const bool w256 = e256 && e256[0] == '1';
     auto cfg_of = [&](int cls) {
         if (exact) return cls == 0 ? 0 : 1;  // the fp32-MFMA kernels: narrow / wide
+        if (bf && w256 && cls >= 2) return 3;
         return cls == 3 ? 2 : cls;
     };
     auto flush = [&](GemmBatch& b, int cfg, bool planes = false) -> int {
@@ -1858,6 +1870,7 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
         } else if (bf) {
             rc = cfg == 0   ? launch_one_x<WgradNarrowX32, EPI_STORE, 1>(b, s)
                  : cfg == 1 ? launch_one_x<WgradWideX32, EPI_STORE, 1>(b, s)
+                 : cfg == 3 ? launch_one_x<Wgrad256X32, EPI_STORE, 1>(b, s)
                             : launch_one_x<Wgrad128X32, EPI_STORE, 1>(b, s);
         } else {
             rc = cfg == 0   ? (wgrad_a3() ? launch_one_x<WgradNarrowXA3, EPI_STORE, 3>(b, s)
