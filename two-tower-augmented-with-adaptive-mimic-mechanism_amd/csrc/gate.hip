@@ -225,10 +225,10 @@ __device__ __forceinline__ void store_slab(float* scr, const f4v (&v)[NO], float
     }
 }
 
-template <int D, int HG>
+template <int D, int HG, int NW_ = GateWaves<D>::NW>
 struct GateCfg {
     static constexpr int TD = D / 16, TH = HG / 16, TE = 2 * D / 16;  // 16-feature tiles
-    static constexpr int NW = GateWaves<D>::NW;
+    static constexpr int NW = NW_;
     // GG: G2 (forward) / G2^T (backward) read from global memory instead of LDS
     static constexpr bool GG = D >= 128;
     static constexpr int SCR = slab_scratch<(D > HG ? D : HG)>();  // floats of slab scratch per wave
@@ -260,10 +260,10 @@ __device__ __forceinline__ int gate_tower(const KArg(GateArgs) * ka, int& bidx) 
     return 0;
 }
 
-template <int D, int HG, bool X>
-__global__ __launch_bounds__(GateWaves<D>::THREADS) void gate_fwd_kernel(GateArgs) {
-    using C = GateCfg<D, HG>;
-    constexpr int NW = C::NW, NT = 64 * NW;
+template <int D, int HG, bool X, int NW>
+__global__ __launch_bounds__(64 * NW) void gate_fwd_kernel(GateArgs) {
+    using C = GateCfg<D, HG, NW>;
+    constexpr int NT = 64 * NW;
     constexpr int NX = (2 * D) / 32;  // split: k-steps of the first GEMM
     // !X: each wave's slab-store scratch after the matrices (store_slab)
     __shared__ __attribute__((aligned(16))) float lds[X ? C::XF_BYTES / 4 : C::F_LDS + NW * C::SCR];
@@ -414,10 +414,10 @@ __global__ __launch_bounds__(GateWaves<D>::THREADS) void gate_fwd_kernel(GateArg
     }
 }
 
-template <int D, int HG, bool X>
-__global__ __launch_bounds__(GateWaves<D>::THREADS) void gate_bwd_kernel(GateArgs) {
-    using C = GateCfg<D, HG>;
-    constexpr int NW = C::NW, NT = 64 * NW;
+template <int D, int HG, bool X, int NW>
+__global__ __launch_bounds__(64 * NW) void gate_bwd_kernel(GateArgs) {
+    using C = GateCfg<D, HG, NW>;
+    constexpr int NT = 64 * NW;
     constexpr int NX = HG / 32;  // split: k-steps of the dEF GEMM
     __shared__ __attribute__((aligned(16))) float lds[X ? C::XB_BYTES / 4 : C::B_LDS + NW * C::SCR];
     const KArg(GateArgs)* ka = (const KArg(GateArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
@@ -625,26 +625,39 @@ int gate_blocks(GateArgs& a, int waves) {
     return sum;
 }
 
-template <int D, int HG>
-int launch_gate_t(GateArgs& a, bool backward, hipStream_t s) {
-    const int blocks = gate_blocks(a, GateWaves<D>::NW);
-    constexpr int kGateThreads = GateWaves<D>::THREADS;
+template <int D, int HG, int NW>
+int launch_gate_nw(GateArgs& a, bool backward, hipStream_t s) {
+    const int blocks = gate_blocks(a, NW);
     // TTAMM_GATE_SPLIT=1: the 2D-wide GEMM on split-bf16 MFMA.  Measured at C2 (D = 96): forward
     // 64 -> 62 us, backward 67 -> 79 us, step 0.726 -> 0.758 ms (profiles/r03_c2_gate_split_s17.txt):
     // the kernels are not MFMA-bound (SQ: ~31 % MFMA busy, profiles/r03_c2_pmc_sq_s13.json) and the
     // split variant runs at the 256-VGPR limit, so both GEMMs stay on v_mfma_f32_16x16x4_f32
     static const bool split = std::getenv("TTAMM_GATE_SPLIT") != nullptr;
-    constexpr bool XOK = GateCfg<D, HG>::X_OK;
+    constexpr bool XOK = GateCfg<D, HG, NW>::X_OK;
     if (XOK && split) {
-        if (backward) hipLaunchKernelGGL((gate_bwd_kernel<D, HG, XOK>), dim3(blocks), dim3(kGateThreads), 0, s, a);
-        else hipLaunchKernelGGL((gate_fwd_kernel<D, HG, XOK>), dim3(blocks), dim3(kGateThreads), 0, s, a);
+        if (backward) hipLaunchKernelGGL((gate_bwd_kernel<D, HG, XOK, NW>), dim3(blocks), dim3(64 * NW), 0, s, a);
+        else hipLaunchKernelGGL((gate_fwd_kernel<D, HG, XOK, NW>), dim3(blocks), dim3(64 * NW), 0, s, a);
         TTAMM_LAUNCH_CHECK();
         return TTAMM_OK;
     }
-    if (backward) hipLaunchKernelGGL((gate_bwd_kernel<D, HG, false>), dim3(blocks), dim3(kGateThreads), 0, s, a);
-    else hipLaunchKernelGGL((gate_fwd_kernel<D, HG, false>), dim3(blocks), dim3(kGateThreads), 0, s, a);
+    if (backward) hipLaunchKernelGGL((gate_bwd_kernel<D, HG, false, NW>), dim3(blocks), dim3(64 * NW), 0, s, a);
+    else hipLaunchKernelGGL((gate_fwd_kernel<D, HG, false, NW>), dim3(blocks), dim3(64 * NW), 0, s, a);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
+}
+
+template <int D, int HG>
+int launch_gate_t(GateArgs& a, bool backward, hipStream_t s) {
+    // TTAMM_GATE_4W=1 (D = 96): 4-wave blocks, one wave per SIMD with the whole register file (the
+    // split variant then has room: TTAMM_GATE_SPLIT=1)
+    if constexpr (D == 96) {
+        static const bool w4 = [] {
+            const char* e = std::getenv("TTAMM_GATE_4W");
+            return e && e[0] == '1';
+        }();
+        if (w4) return launch_gate_nw<D, HG, 4>(a, backward, s);
+    }
+    return launch_gate_nw<D, HG, GateWaves<D>::NW>(a, backward, s);
 }
 
 }  // namespace
