@@ -144,6 +144,32 @@ def test_deferred_c2_equals_eager():
     assert sums[0][3] == sums[1][3]
 
 
+def test_deferred_c2_fast_overlap_repeatable():
+    """The bench's configuration (C2, fast g = 0 arithmetic, replay slices on the aux stream beside
+    the MLP GEMMs) run twice from the same seed: bit-identical tables and moments (the regression
+    check for the packed-operand hazard of round 4, tools/diag/deferred_c2.py: a race or hazard that
+    comes back shows as run-to-run differences even if tools/check_pk_operands.py finds nothing)."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    c2 = bench.CONFIGS["c2"]
+    runs = []
+    for _ in range(2):
+        w = bench.Workload(c2, torch.device("cuda"), seed=11, deferred=True, table_math="fast")
+        for _ in range(5):
+            w.engine.step(*w.batch())
+        w.engine.finish()
+        mm = w.model.adaptive_mimic
+        st = w.opts[0].state[mm.item_augmented.weight]
+        su = w.opts[0].state[mm.user_augmented.weight]
+        runs.append([mm.item_augmented.weight.detach().clone(), st["exp_avg"].clone(), st["exp_avg_sq"].clone(),
+                     mm.user_augmented.weight.detach().clone(), su["exp_avg"].clone(), su["exp_avg_sq"].clone()])
+        del w
+        torch.cuda.empty_cache()
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+
+
 def test_fast_g0_math_close_to_exact():
     """table_adamw_math="fast" (v_sqrt / v_rcp for the g = 0 updates) against the IEEE path over
     17 steps with lagging rows: every parameter and moment within 1e-6 of the tensor's largest

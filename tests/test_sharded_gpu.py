@@ -123,6 +123,9 @@ def _run(batches, g, ranks, W):
     (8, Shape(U=800, I=4000, F=40, H=64, D=128, B=256, N=0, hidden_dims=(64,)), True, True),
     # 8 ranks, sampled negatives (the C2 topology at W = 8), both schedules
     (8, Shape(U=800, I=4000, B=64, N=3), False, True),
+    # 8 ranks at C2's widths (605 -> 192 -> 96, the fused D = 96 gate, N = 5), 512 interactions per
+    # rank: the production kernels of the rank-of-8 step (3,072 owner rows per rank on average)
+    (8, Shape(U=4000, I=40000, F=605, H=192, D=96, B=512, N=5, hidden_dims=(192,)), False, True),
     (8, Shape(U=800, I=4000, B=64, N=3), False, False),
 ])
 def test_sharded_gradients_match_global_step(W, shape, in_batch, group):
