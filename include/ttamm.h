@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 23
+#define TTAMM_ABI_VERSION 24
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -359,6 +359,21 @@ typedef struct ttamm_step_args {
     /* element stride of item_rows and item_row_keys (0 = 1): the (local row, key) pairs of an
      * owner's request all-to-all are read in place (stride 2), the step stages contiguous copies */
     int64_t item_rows_ld;
+    /* ---- compact exchange rows (sharded, mimic on; ttamm_exchange_compact_supported) -----------
+     * NULL: every exchange row is 2*dim wide ((t | a) forward, (dT | dA) backward).  Otherwise a
+     * negative request's row is dim wide — t + a forward, dT backward (its dA is dT: negatives go
+     * through augment_items only, with no mimic loss, training.py:772-787) — and a positive's stays
+     * (t | a) / (dT | dA): the buffers are sequences of dim-float units, a positive taking two.
+     * exchange_counts = the count all-to-all's rows [2 * exchange_world, exchange_counts_ld]:
+     * rows [0, world) what this rank sent to each owner, rows [world, 2 world) what it received from
+     * each requester; column 0 the requests, column 2 how many of them are positives (the leading
+     * ones: ttamm_route_rows with counts_ld >= 3).  Requester buffers are owner-grouped as
+     * item_slot orders them, the owner's requester-grouped as item_rows arrive; each group is
+     * [positives | negatives], so the all-to-alls move dim * (requests + positives) floats per
+     * peer, unpermuted.  ITEM_FWD forms both unit maps; later phases reuse them. */
+    const int64_t* exchange_counts;
+    int64_t exchange_counts_ld;
+    int32_t exchange_world;
 } ttamm_step_args;
 
 #define TTAMM_G0_EXACT 0
@@ -376,6 +391,10 @@ const char* ttamm_last_error(void);
  * AdamW (dense group incl. the full mimic tables) and SparseAdam (ID tables). */
 size_t ttamm_train_step_workspace_size(const ttamm_step_args* args);
 int ttamm_train_step(const ttamm_step_args* args, void* stream);
+/* 1 when a row-sharded step with these towers may set exchange_counts (compact exchange rows):
+ * mimic on and the item tower's gate on the fused kernels (gate.hip / gate16.hip), alone and
+ * grouped with the user tower; 0 otherwise (the 2*dim-wide rows).  Host-only, no device work. */
+int ttamm_exchange_compact_supported(const ttamm_step_args* args);
 
 /* Size (floats) of the replicated-weight gradient arena of a sharded step: both towers'
  * feature-encoder and gate weight+bias gradients, contiguous (the all-reduce buffer). */
@@ -454,7 +473,9 @@ int ttamm_epoch_batch(const int64_t* users, const int64_t* items, int64_t n, uin
  * (torch.argsort(owner, stable=True), ttamm/sharded.py).  1 <= world <= 1024; every id >= 0;
  * scratch: device memory of ttamm_route_scratch_bytes(n0 + n1, world) bytes.  counts[o * counts_ld]
  * (counts_ld >= 1); with status != NULL and counts_ld >= 2, counts[o * counts_ld + 1] = *status —
- * the (count, status word) rows of the sharded step's count all-to-all, written in the same launch. */
+ * the (count, status word) rows of the sharded step's count all-to-all, written in the same launch;
+ * with counts_ld >= 3, counts[o * counts_ld + 2] = how many of owner o's ids came from id0 (the
+ * positives of a step's requests: ttamm_step_args.exchange_counts). */
 size_t ttamm_route_scratch_bytes(int64_t n, int32_t world);
 int ttamm_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_t n1, const int64_t* payload,
                      int64_t key0, int64_t key1, int32_t world, int64_t* packed, int64_t* slot, int64_t* counts,

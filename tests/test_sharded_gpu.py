@@ -129,7 +129,13 @@ def _run(batches, g, ranks, W):
     (8, Shape(U=800, I=4000, B=64, N=3), False, False),
 ])
 def test_sharded_gradients_match_global_step(W, shape, in_batch, group):
+    _one_step_check(W, shape, in_batch, group)
+
+
+def _one_step_check(W, shape, in_batch, group, compact=None):
     prob, batches, g, ranks = _setup(shape, W, lr=0.0, betas=(0.0, 0.999), steps=1, in_batch=in_batch, group=group)
+    if compact is not None:
+        assert all(eng.compact == compact for (_, _, _, eng) in ranks)
     glosses, rlosses, negs, gavg, ravg = _run(batches, g, ranks, W)
     B, N = shape.B, shape.N
     gneg, rneg = negs[0]
@@ -151,6 +157,56 @@ def test_sharded_gradients_match_global_step(W, shape, in_batch, group):
             assert rel_err(st["exp_avg"], want) <= 1e-5, (own.rank, name)
 
 
+# Compact exchange rows (ttamm.h ttamm_step_args.exchange_counts): with mimic on and the item gate
+# on the fused kernels a negative request moves D floats each way (t + a, dT) instead of 2 D.  The
+# shapes above mostly run the generic gate (D = 8) and so the 2 D-wide rows; these run the fused
+# gate widths (D = Hg = 32 on gate.hip, D = Hg = 128 bf16 on gate16.hip, C2's D = 96).
+C32 = dict(D=32, H=32, hidden_dims=(32,))
+COMPACT_CASES = [
+    (2, Shape(**C32), False, True),
+    (2, Shape(**C32), False, False),
+    (3, Shape(N=2, **C32), True, False),
+    (1, Shape(**C32), False, True),
+    (1, Shape(N=2, **C32), True, True),
+    (3, Shape(U=300, I=900, N=0, B=70, **C32), True, True),
+    (2, Shape(dropout=0.0, **C32), False, True),
+    (2, Shape(U=200, I=900, F=37, H=128, D=128, B=40, N=3, hidden_dims=(128,), matmul_dtype="bf16"), False, True),
+    (8, Shape(U=800, I=4000, B=64, N=3, **C32), False, False),
+    (8, Shape(U=4000, I=40000, F=605, H=192, D=96, B=512, N=5, hidden_dims=(192,)), False, True),
+]
+COMPACT_IDS = ["w2", "w2-overlapped", "w3-in-batch-overlapped", "w1", "w1-in-batch", "w3-in-batch-n0", "w2-nodrop",
+               "w2-bf16-d128", "w8-overlapped", "w8-c2-widths"]
+
+
+@pytest.mark.parametrize("W,shape,in_batch,group", COMPACT_CASES, ids=COMPACT_IDS)
+def test_compact_exchange_matches_global_step(W, shape, in_batch, group):
+    _one_step_check(W, shape, in_batch, group, compact=True)
+
+
+@pytest.mark.parametrize("W,shape,in_batch,group", [COMPACT_CASES[i] for i in (0, 2, 7, 8)],
+                         ids=[COMPACT_IDS[i] for i in (0, 2, 7, 8)])
+def test_wide_exchange_matches_global_step(W, shape, in_batch, group, monkeypatch):
+    """TTAMM_WIDE_EXCHANGE=1 keeps the 2 D-wide rows on the same shapes."""
+    monkeypatch.setenv("TTAMM_WIDE_EXCHANGE", "1")
+    _one_step_check(W, shape, in_batch, group, compact=False)
+
+
+def test_compact_exchange_payload():
+    """The rank-of-8 exchange at C2's widths: each rank's (dT | dA) send is D (B (1 + N) + B) floats
+    — its B positives two units, its B N negatives one — against the wide rows' 2 D B (1 + N), a
+    (2 + N) / (2 + 2 N) share (C2, B = 8192, N = 5, D = 96: 37.7 -> 22.0 MB per rank per direction);
+    the owners' (t | a) sends add up to the same total."""
+    W, shape = 8, COMPACT_CASES[-1][1]
+    prob, batches, g, ranks = _setup(shape, W, lr=0.0, betas=(0.0, 0.999), steps=1)
+    _run(batches, g, ranks, W)
+    B, N, D = shape.B, shape.N, shape.D
+    sends = [eng.exchange_floats for (_, _, _, eng) in ranks]
+    assert all(eng.compact for (_, _, _, eng) in ranks)
+    assert all(bwd == D * (B * (1 + N) + B) for _, bwd in sends)
+    assert sum(fwd for fwd, _ in sends) == sum(bwd for _, bwd in sends)
+    assert sends[0][1] * (2 + 2 * N) == 2 * D * B * (1 + N) * (2 + N)
+
+
 @pytest.mark.parametrize("group", [True, False], ids=["grouped", "overlapped"])
 @pytest.mark.parametrize("in_batch", [False, True], ids=["sampled", "in-batch"])
 def test_sharded_three_steps_match_global_step(in_batch, group):
@@ -168,16 +224,20 @@ def test_sharded_three_steps_match_global_step(in_batch, group):
             assert d <= 5e-5, f"rank {own.rank} {k}: {d:.2e}"
 
 
-@pytest.mark.parametrize("W,in_batch,group", [(2, False, True), (3, True, True), (2, False, False), (8, False, True)],
-                         ids=["w2", "w3-in-batch", "w2-overlapped", "w8"])
-def test_look_ahead_routing_matches_global_step(W, in_batch, group):
+@pytest.mark.parametrize("W,in_batch,group,d32", [(2, False, True, False), (3, True, True, False),
+                                                 (2, False, False, False), (8, False, True, False),
+                                                 (2, False, True, True), (3, True, False, True), (8, False, True, True)],
+                         ids=["w2", "w3-in-batch", "w2-overlapped", "w8", "w2-compact", "w3-in-batch-overlapped-compact",
+                              "w8-compact"])
+def test_look_ahead_routing_matches_global_step(W, in_batch, group, d32):
     """program(next_batch=...): each step draws the next step's negatives, groups its requests
     and exchanges its counts after the forward exchange (look-ahead routing).  Three steps
     against the one-process step over the global batches: the same losses and final state as
     test_sharded_three_steps_match_global_step, and the look-ahead's draws are the ones the
     one-process sampler makes (Philox keyed by global slot and step)."""
-    shape = Shape(N=2) if in_batch else Shape()
+    shape = Shape(N=2, **(C32 if d32 else {})) if in_batch else Shape(**(C32 if d32 else {}))
     prob, batches, g, ranks = _setup(shape, W, lr=1e-3, betas=(0.9, 0.999), steps=3, in_batch=in_batch, group=group)
+    assert all(eng.compact == d32 for (_, _, _, eng) in ranks)  # (the look-ahead's count rows carry positives)
     gm, gopts, geng = g
     dev = [[((u // W).cuda(), p.cuda()) for (u, p) in per_rank] for per_rank in batches]
     for s, per_rank in enumerate(batches):

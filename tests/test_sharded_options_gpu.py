@@ -62,6 +62,7 @@ def _shard_cfg(shape: Shape, own: RowOwnership) -> dict:
 
 
 CAL_WEIGHTS = {**LOSS_WEIGHTS, "category_alignment": 2.0}
+C32 = dict(D=32, H=32, hidden_dims=(32,))  # D = Hg = 32: the fused gate, compact exchange rows
 
 
 def _categories(I: int, C: int = 4, major_share: float = 0.4, seed: int = 9) -> torch.Tensor:
@@ -132,14 +133,22 @@ CASES = [
     (3, Shape(N=3), None, True),
     (3, Shape(sparse=False, max_norm=0.05, padding_idx=6), 0.05, True),
     (2, Shape(fusion="concat", feature_out=12, concat_out=20), None, True),
+    # the fused gate widths: compact exchange rows (ttamm.h exchange_counts) under every option
+    (2, Shape(padding_idx=5, **C32), None, False),
+    (3, Shape(sparse=False, max_norm=0.05, N=3, **C32), None, False),
+    (2, Shape(sparse=False, **C32), 0.05, False),
+    (3, Shape(N=3, **C32), None, True),
+    (3, Shape(sparse=False, max_norm=0.05, padding_idx=6, **C32), 0.05, True),
 ]
 IDS = ["padding-w2", "dense-padding-w3", "max-norm-w2", "max-norm-w3", "clip-w2", "noclip-w3", "all-w2",
-       "cal-w2", "cal-w3", "cal-all-w3", "concat-out20-cal-w2"]
+       "cal-w2", "cal-w3", "cal-all-w3", "concat-out20-cal-w2", "padding-w2-compact", "max-norm-w3-compact",
+       "clip-w2-compact", "cal-w3-compact", "cal-all-w3-compact"]
 
 
 @pytest.mark.parametrize("W,shape,clip,cal", CASES, ids=IDS)
 def test_sharded_options_gradients_match_global_step(W, shape, clip, cal):
     (gm, gopts), ranks, gl, rl = _run(shape, W, lr=0.0, betas=(0.0, 0.999), steps=1, clip=clip, cal=cal)
+    assert all(eng.compact == (shape.D == 32) for (_, _, _, eng) in ranks)
     if cal:
         assert gl[0]["category_alignment"] > 0
     for key in ("total", "bce", "mimic_user", "mimic_item", "category_alignment"):
@@ -159,8 +168,10 @@ def test_sharded_options_gradients_match_global_step(W, shape, clip, cal):
                 assert rel_err(m.state_dict()[k], gsd[k][own.rank:: W]) <= 1e-6, (own.rank, k)
 
 
-@pytest.mark.parametrize("W,shape,clip,cal", [CASES[0], CASES[3], CASES[4], CASES[6], CASES[8], CASES[9]],
-                         ids=["padding-w2", "max-norm-w3", "clip-w2", "all-w2", "cal-w3", "cal-all-w3"])
+@pytest.mark.parametrize("W,shape,clip,cal", [CASES[0], CASES[3], CASES[4], CASES[6], CASES[8], CASES[9], CASES[14],
+                                              CASES[15]],
+                         ids=["padding-w2", "max-norm-w3", "clip-w2", "all-w2", "cal-w3", "cal-all-w3", "cal-w3-compact",
+                              "cal-all-w3-compact"])
 def test_sharded_options_three_steps_match_global_step(W, shape, clip, cal):
     (gm, _), ranks, gl, rl = _run(shape, W, lr=1e-3, betas=(0.9, 0.999), steps=3, clip=clip, cal=cal)
     for s in range(3):

@@ -22,6 +22,7 @@ int fail(int code, const std::string& msg) {
 size_t train_step_workspace_size(const ttamm_step_args& A);
 int train_step(const ttamm_step_args& A, hipStream_t s);
 int64_t dense_grad_floats(const ttamm_step_args& A);
+int exchange_compact_supported(const ttamm_step_args& A);
 int flush_tables(const ttamm_step_args& A, hipStream_t s);
 size_t tower_forward_workspace_size(const ttamm_tower& T, int64_t n);
 int tower_forward_eval(const ttamm_tower& T, const int64_t* idx, const int64_t* fidx, int64_t n, int augment,
@@ -53,6 +54,10 @@ TTAMM_API size_t ttamm_train_step_workspace_size(const ttamm_step_args* args) {
 TTAMM_API int64_t ttamm_dense_grad_floats(const ttamm_step_args* args) {
     if (!args) return 0;
     return dense_grad_floats(*args);
+}
+
+TTAMM_API int ttamm_exchange_compact_supported(const ttamm_step_args* args) {
+    return args ? exchange_compact_supported(*args) : 0;
 }
 
 TTAMM_API size_t ttamm_adam_history_entry_bytes(void) { return sizeof(AdamConsts); }

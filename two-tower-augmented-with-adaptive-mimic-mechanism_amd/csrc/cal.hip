@@ -100,8 +100,9 @@ __device__ __forceinline__ int64_t buf_row(const CalArgs& A, int64_t j) { return
 
 // element col of sorted row k: x (+ xa, the mimic rows of the sharded exchange buffer)
 __device__ __forceinline__ float row_val(const CalArgs& A, int k, int col) {
-    const int64_t o = buf_row(A, A.co.vals_out[k]) * A.ld_x + col;
-    return A.xa ? A.x[o] + A.xa[o] : A.x[o];
+    const int64_t j = A.co.vals_out[k];
+    const int64_t o = buf_row(A, j) * A.ld_x + col;
+    return A.xa && j < A.xa_rows ? A.x[o] + A.xa[o] : A.x[o];
 }
 
 // psum[p][d] = sum of the piece's rows (row order)

@@ -225,6 +225,49 @@ __device__ __forceinline__ void store_slab(float* scr, const f4v (&v)[NO], float
     }
 }
 
+// store_slab into compact exchange rows (GateTower::xu): slab row grow goes to out + u * 16 NO for
+// u = xu[grow] (a positive) or ~xu[grow] (a negative; left out when pos_only)
+template <int NO>
+__device__ __forceinline__ void store_slab_xu(float* scr, const f4v (&v)[NO], float* out, const int64_t* xu,
+                                              bool pos_only, int64_t row0, int64_t R, int lane) {
+    constexpr int W = 16 * NO, LDW = W + 4, C4 = W / 4, PER = 8 * C4 / 64;
+    static_assert((8 * C4) % 64 == 0, "slab scratch");
+    const int li = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        if ((li >> 3) == half) {
+#pragma unroll
+            for (int ob = 0; ob < NO; ++ob) *reinterpret_cast<f4v*>(scr + (li & 7) * LDW + 16 * ob + 4 * q) = v[ob];
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int idx = lane + 64 * k, r = idx / C4, c = idx - r * C4;
+            const f4v val = *reinterpret_cast<const f4v*>(scr + r * LDW + 4 * c);
+            const int64_t grow = row0 + 8 * half + r;
+            if (grow < R) {
+                const int64_t u = xu[grow];
+                if (u >= 0 || !pos_only) stg4(out + (u >= 0 ? u : ~u) * W + 4 * c, val);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// lane (li, q)'s part of a dT row: row `row` at ld, or its compact exchange unit (GateTower::xu)
+template <int N>
+__device__ __forceinline__ void load_dt_row(f4v (&v)[N], const float* base, int64_t ld, const int64_t* xu, int D,
+                                            int64_t row, int q) {
+    if (xu) {
+        const int64_t u = xu[row];
+        load_row(v, base, D, u >= 0 ? u : ~u, q);
+    } else {
+        load_row(v, base, ld, row, q);
+    }
+}
+
 template <int D, int HG, int NW_ = GateWaves<D>::NW>
 struct GateCfg {
     static constexpr int TD = D / 16, TH = HG / 16, TE = 2 * D / 16;  // 16-feature tiles
@@ -367,17 +410,32 @@ __global__ __launch_bounds__(64 * NW) void gate_fwd_kernel(GateArgs) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) x[ob][r] = x[ob][r] * e[r] + (1.0f - x[ob][r]) * f[r];
             }
-            store_slab<C::TD>(scr, x, T.t, T.ld_t, s * 16, R, lane);
-            if (T.table) {
-                store_slab<C::TD>(scr, a, T.a, T.ld_t, s * 16, R, lane);
+            if (T.xu) {  // compact exchange rows: (t | a) of a positive, t + a of a negative
+                store_slab_xu<C::TD>(scr, a, T.a, T.xu, true, s * 16, R, lane);
+                const bool neg = ok && T.xu[row] < 0;
 #pragma unroll
                 for (int ob = 0; ob < C::TD; ++ob)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) x[ob][r] = x[ob][r] + a[ob][r];
+                    for (int r = 0; r < 4; ++r) x[ob][r] = neg ? x[ob][r] + a[ob][r] : x[ob][r];
+                store_slab_xu<C::TD>(scr, x, T.t, T.xu, false, s * 16, R, lane);
+            } else {
+                store_slab<C::TD>(scr, x, T.t, T.ld_t, s * 16, R, lane);
+                if (T.table) {
+                    store_slab<C::TD>(scr, a, T.a, T.ld_t, s * 16, R, lane);
+#pragma unroll
+                    for (int ob = 0; ob < C::TD; ++ob)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) x[ob][r] = x[ob][r] + a[ob][r];
+                }
+                if (T.aug) store_slab<C::TD>(scr, x, T.aug, D, s * 16, R, lane);
             }
-            if (T.aug) store_slab<C::TD>(scr, x, T.aug, D, s * 16, R, lane);
         }
         if ((X || ka->direct) && ok && !ka->ablate) {
+            // compact exchange rows (T.xu): a positive's t and a at its unit, a negative's t + a
+            int64_t xu = 0;
+            if (T.xu) xu = T.xu[row];
+            float* tdst = T.xu ? T.t + (xu >= 0 ? xu : ~xu) * D : T.t + row * T.ld_t;
+            float* adst = T.xu ? (xu >= 0 ? T.a + xu * D : nullptr) : (T.table ? T.a + row * T.ld_t : nullptr);
 #pragma unroll
             for (int ob = 0; ob < C::TD; ++ob) {
                 const int col = 16 * ob + 4 * q;
@@ -390,13 +448,13 @@ __global__ __launch_bounds__(64 * NW) void gate_fwd_kernel(GateArgs) {
                     tt[r] = g[r] * e[r] + (1.0f - g[r]) * f[r];
                 }
                 stg4(T.g + row * D + col, g);
-                stg4(T.t + row * T.ld_t + col, tt);
                 f4v aug = tt;
                 if (T.table) {
-                    stg4(T.a + row * T.ld_t + col, a[ob]);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) aug[r] = tt[r] + a[ob][r];
                 }
+                stg4(tdst + col, T.xu && xu < 0 ? aug : tt);
+                if (adst) stg4(adst + col, a[ob]);
                 if (T.aug) stg4(T.aug + row * D + col, aug);
             }
         }
@@ -459,7 +517,7 @@ __global__ __launch_bounds__(64 * NW) void gate_bwd_kernel(GateArgs) {
             f4v d[C::TD], g[C::TD], dz[C::TH];
             {
                 f4v ef[C::TE];
-                load_row(d, T.dT, T.ld_dT, rr, q);
+                load_dt_row(d, T.dT, T.ld_dT, T.xu, D, rr, q);
                 load_row(ef, T.ef, 2 * D, rr, q);
                 load_row(g, T.g, D, rr, q);
                 stage_g2t();
@@ -551,7 +609,7 @@ __global__ __launch_bounds__(64 * NW) void gate_bwd_kernel(GateArgs) {
         const int64_t rr = ok ? row : R - 1;
         // every operand of the slab requested at once
         f4v d[C::TD], ef[C::TE], g[C::TD], zr[C::TH];
-        load_row(d, T.dT, T.ld_dT, rr, q);
+        load_dt_row(d, T.dT, T.ld_dT, T.xu, D, rr, q);
         load_row(ef, T.ef, 2 * D, rr, q);
         load_row(g, T.g, D, rr, q);
         load_row(zr, T.z, HG, rr, q);

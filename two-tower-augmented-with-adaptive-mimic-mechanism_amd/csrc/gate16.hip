@@ -377,16 +377,33 @@ __global__ __launch_bounds__(kG16Threads) void gate16_fwd_kernel(GateArgs) {
                 tt[i] = gg[i] * e4[j][i] + (1.0f - gg[i]) * fv[j][i];
             }
             st4(T.g + grow_ * D + f0, gg);
-            st4(T.t + grow_ * T.ld_t + f0, tt);
             f4v aug = tt;
             if (T.table) {
-                st4(T.a + grow_ * T.ld_t + f0, a4[j]);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) aug[i] = tt[i] + a4[j][i];
+            }
+            if (T.xu) {  // compact exchange rows: (t | a) of a positive, t + a of a negative
+                const int64_t u = T.xu[grow_];
+                if (u >= 0) {
+                    st4(T.t + u * D + f0, tt);
+                    st4(T.a + u * D + f0, a4[j]);
+                } else {
+                    st4(T.t + (~u) * D + f0, aug);
+                }
+            } else {
+                st4(T.t + grow_ * T.ld_t + f0, tt);
+                if (T.table) st4(T.a + grow_ * T.ld_t + f0, a4[j]);
             }
             if (T.aug) st4(T.aug + grow_ * D + f0, aug);
         }
     }
+}
+
+// row gr's dT: at gr * ld_dT, or its compact exchange unit (GateTower::xu)
+__device__ __forceinline__ const float* dt_row(const KArg(GateTower) & T, int64_t gr, int D) {
+    if (!T.xu) return T.dT + gr * T.ld_dT;
+    const int64_t u = T.xu[gr];
+    return T.dT + (u >= 0 ? u : ~u) * D;
 }
 
 template <int D, int NP>
@@ -424,7 +441,7 @@ __global__ __launch_bounds__(kG16Threads) void gate16_bwd_kernel(GateArgs) {
             const int q = (it0 + j) * 64 + lane, rl = q / RI::F4, f0 = 4 * (q - rl * RI::F4);
             const int64_t g0 = wrow0 + rl;
             const int64_t gr = g0 < R ? g0 : R - 1;
-            d4[j] = ld4(T.dT + gr * T.ld_dT + f0);
+            d4[j] = ld4(dt_row(T, gr, D) + f0);
             e4[j] = ld4(T.ef + gr * K1 + f0);
             fv[j] = ld4(T.ef + gr * K1 + D + f0);
             g4[j] = ld4(T.g + gr * D + f0);
@@ -540,7 +557,7 @@ __global__ __launch_bounds__(kG16Threads) void gate16_bwd_kernel(GateArgs) {
                 const int q = (it0 + j) * 64 + lane, rl = q / RI::F4, f0 = 4 * (q - rl * RI::F4);
                 const int64_t g0 = wrow0 + rl;
                 const int64_t gr = g0 < R ? g0 : R - 1;
-                d4[j] = ld4(T.dT + gr * T.ld_dT + f0);
+                d4[j] = ld4(dt_row(T, gr, D) + f0);
                 g4[j] = ld4(T.g + gr * D + f0);
             }
 #pragma unroll

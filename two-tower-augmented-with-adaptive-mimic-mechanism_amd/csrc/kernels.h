@@ -104,6 +104,9 @@ size_t route_scratch_bytes(int64_t n, int world);
 int launch_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_t n1, const int64_t* payload,
                       int64_t key0, int64_t key1, int world, int64_t* packed, int64_t* slot, int64_t* counts,
                       int64_t counts_ld, const uint32_t* status, void* scratch, size_t scratch_bytes, hipStream_t s);
+// compact exchange: the first unit of each of n rows (route.hip exchange_units_kernel)
+int launch_exchange_units(const int64_t* counts, int64_t ld, int W, const int64_t* slot, int64_t n, int mark_neg,
+                          int64_t* out, hipStream_t s);
 void epoch_round_keys(uint64_t seed, int64_t epoch, uint32_t keys[4]);
 int launch_epoch_batch(const int64_t* users, const int64_t* items, int64_t n, uint64_t seed, int64_t epoch,
                        int shuffle, int64_t start, int64_t count, int64_t* out_users, int64_t* out_items,
@@ -178,6 +181,10 @@ struct GateTower {
     float* aug;          // [R, D] or null (sharded item owner)
     const float* dT;     // backward: [R, ld_dT]
     int64_t ld_dT;
+    // compact exchange (sharded item owner): row r's t / dT at t / dT + u D and its a at a + u D
+    // for u = xu[r] >= 0 (a positive); u < 0: a negative, whose one unit ~u holds t + a (forward)
+    // and dT (backward).  Null: row r at r * ld_t / r * ld_dT.
+    const int64_t* xu;
     float* dq;           // [R, D]
     float* dz;           // [R, Hg]
     float* dEF;          // [R, 2D]
@@ -314,6 +321,7 @@ struct ScoreArgs {
     float* dA_user;   // [B, D]  (mimic)
     float* dA_item;   // (mimic) [B, ld_dti] positives only, or all B(1+N) rows when dA_all
     int dA_all;
+    int neg_aug;      // compact exchange: negative request rows hold t + a in t_item (no a_item read)
     int64_t ld_dti;
     const int64_t* item_slot;  // or null: item request r's rows (t_item .. dA_item) are at item_slot[r]
     float* partials;  // [blocks, 3]
@@ -432,6 +440,7 @@ struct CalArgs {
     const float* x;             // augmented item rows [R, ld_x] = cat[positives; negatives]
     int64_t ld_x;
     const float* xa;            // sharded: the mimic rows (row value = x + xa); null: x is t + a
+    int64_t xa_rows;            // request rows >= xa_rows read x alone (compact exchange negatives)
     const int64_t* slot;        // sharded: exchange-buffer row of request row r; null: row r
     const int64_t* idx;         // item id of row r
     const int64_t* idx1;        // sharded: item ids of rows [split, R) (the negatives); null: idx
@@ -524,6 +533,9 @@ struct RowUpdateArgs {
     const float* dA_hi;
     int64_t ld_dA;
     int64_t split_row;
+    // compact exchange (sharded item owner, GateTower::xu): row r's mimic gradient at
+    // dA_lo + xu[r] ld_dA for a positive (xu >= 0), at dA_hi + ~xu[r] ld_dA (its dT) for a negative
+    const int64_t* xu;
     ttamm_table mimic;
     // per-position partial sums of the segmented reduction [n, dim]
     float* piece_e;

@@ -406,6 +406,10 @@ constexpr int kPiece = kCoalescePiece;
 constexpr int kRowWaves = 4;
 
 __device__ __forceinline__ const float* dA_row(const RowUpdateArgs& A, int64_t r) {
+    if (A.xu) {
+        const int64_t u = A.xu[r];
+        return u >= 0 ? A.dA_lo + u * A.ld_dA : A.dA_hi + (~u) * A.ld_dA;
+    }
     return (r < A.split_row ? A.dA_lo : A.dA_hi) + r * A.ld_dA;
 }
 

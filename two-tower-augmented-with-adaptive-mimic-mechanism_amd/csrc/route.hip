@@ -34,30 +34,44 @@ __device__ __forceinline__ uint64_t id_at(const RouteIn& a, int64_t j) {
     return (uint64_t)(j < a.n0 ? a.id0[j] : a.id1[j - a.n0]);
 }
 
-__global__ __launch_bounds__(kRouteThreads) void route_count_kernel(RouteIn a, int32_t* __restrict__ blk) {
+// blk[b][o]: ids of block b owned by o; blk0[b][o] (when given): of them from id0
+__global__ __launch_bounds__(kRouteThreads) void route_count_kernel(RouteIn a, int32_t* __restrict__ blk,
+                                                                    int32_t* __restrict__ blk0) {
     extern __shared__ int32_t hist[];
     const int W = (int)a.world;
-    for (int o = threadIdx.x; o < W; o += kRouteThreads) hist[o] = 0;
+    int32_t* hist0 = hist + W;
+    for (int o = threadIdx.x; o < 2 * W; o += kRouteThreads) hist[o] = 0;
     __syncthreads();
     const int64_t lo = (int64_t)blockIdx.x * kRouteSpan;
     for (int r = 0; r < kRouteRounds; ++r) {
         const int64_t j = lo + r * kRouteThreads + threadIdx.x;
-        if (j < a.n) atomicAdd(&hist[id_at(a, j) % a.world], 1);
+        if (j < a.n) {
+            const int o = (int)(id_at(a, j) % a.world);
+            atomicAdd(&hist[o], 1);
+            if (blk0 && j < a.n0) atomicAdd(&hist0[o], 1);
+        }
     }
     __syncthreads();
-    for (int o = threadIdx.x; o < W; o += kRouteThreads) blk[(int64_t)blockIdx.x * W + o] = hist[o];
+    for (int o = threadIdx.x; o < W; o += kRouteThreads) {
+        blk[(int64_t)blockIdx.x * W + o] = hist[o];
+        if (blk0) blk0[(int64_t)blockIdx.x * W + o] = hist0[o];
+    }
 }
 
 __global__ __launch_bounds__(kRouteThreads) void route_scan_kernel(int32_t* __restrict__ blk, int nb, int W,
                                                                    int64_t* __restrict__ counts, int64_t ld,
-                                                                   const uint32_t* __restrict__ status) {
+                                                                   const uint32_t* __restrict__ status,
+                                                                   const int32_t* __restrict__ blk0) {
     extern __shared__ int64_t tot[];
     for (int o = threadIdx.x; o < W; o += kRouteThreads) {
-        int64_t t = 0;
+        int64_t t = 0, t0 = 0;
         for (int b = 0; b < nb; ++b) t += blk[(int64_t)b * W + o];
+        if (ld >= 3)
+            for (int b = 0; b < nb && blk0; ++b) t0 += blk0[(int64_t)b * W + o];
         tot[o] = t;
         counts[o * ld] = t;
         if (status) counts[o * ld + 1] = (int64_t)*status;
+        if (ld >= 3) counts[o * ld + 2] = t0;  // of them from id0 (a step's positives)
     }
     __syncthreads();
     if (threadIdx.x == 0) {  // exclusive scan over owners (W <= 1024)
@@ -128,11 +142,62 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(RouteIn a,
     }
 }
 
+// Compact exchange units (ttamm.h ttamm_step_args.exchange_counts): groups o = 0 .. W-1 of
+// counts[o * ld] rows each, the first counts[o * ld + 2] of them positives (two units) and the
+// rest negatives (one unit).  Row s (s = slot[i] when slot is given, else i) starts at unit
+//   s + (positives of the groups before o) + min(s - start(o), positives of o);
+// mark_neg stores ~unit for a negative row (the owner's row maps carry the row class).
+constexpr int kUnitThreads = 256;
+__global__ __launch_bounds__(kUnitThreads) void exchange_units_kernel(const int64_t* __restrict__ counts, int64_t ld,
+                                                                     int W, const int64_t* __restrict__ slot,
+                                                                     int64_t n, int mark_neg, int64_t* __restrict__ out) {
+    extern __shared__ int64_t tab[];  // start[W], pcum[W], pos[W]
+    int64_t* start = tab;
+    int64_t* pcum = tab + W;
+    int64_t* pos = tab + 2 * W;
+    if (threadIdx.x == 0) {
+        int64_t r = 0, p = 0;
+        for (int o = 0; o < W; ++o) {
+            const int64_t c = counts[o * ld], q = counts[o * ld + 2];
+            start[o] = r;
+            pcum[o] = p;
+            pos[o] = q;
+            r += c;
+            p += q;
+        }
+    }
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * kUnitThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kUnitThreads) {
+        const int64_t s = slot ? slot[i] : i;
+        int lo = 0, hi = W - 1;  // the last group starting at or before s (empty groups share starts)
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (start[mid] <= s) lo = mid;
+            else hi = mid - 1;
+        }
+        const int64_t r = s - start[lo], p = pos[lo];
+        const int64_t unit = s + pcum[lo] + (r < p ? r : p);
+        out[i] = (mark_neg && r >= p) ? ~unit : unit;
+    }
+}
+
 }  // namespace
+
+int launch_exchange_units(const int64_t* counts, int64_t ld, int W, const int64_t* slot, int64_t n, int mark_neg,
+                          int64_t* out, hipStream_t s) {
+    TTAMM_REQUIRE(W >= 1 && W <= 1024 && ld >= 3 && counts, "exchange units: bad count rows");
+    if (n <= 0) return TTAMM_OK;
+    TTAMM_REQUIRE(out != nullptr, "exchange units: null output");
+    const int64_t blocks = std::min<int64_t>(ceil_div(n, kUnitThreads), 4096);
+    hipLaunchKernelGGL(exchange_units_kernel, dim3((unsigned)blocks), dim3(kUnitThreads), 3 * sizeof(int64_t) * W, s,
+                       counts, ld, W, slot, n, mark_neg, out);
+    TTAMM_LAUNCH_CHECK();
+    return TTAMM_OK;
+}
 
 size_t route_scratch_bytes(int64_t n, int world) {
     const int64_t nb = n > 0 ? ceil_div(n, kRouteSpan) : 0;
-    return (size_t)(nb * (world > 0 ? world : 0)) * sizeof(int32_t);
+    return (size_t)(2 * nb * (world > 0 ? world : 0)) * sizeof(int32_t);  // blk, blk0
 }
 
 int launch_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_t n1, const int64_t* payload,
@@ -145,7 +210,8 @@ int launch_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_
     const int64_t n = n0 + n1;
     if (n == 0) {  // zero counts (and the status column): the scan over no blocks
         hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(kRouteThreads), sizeof(int64_t) * world, s,
-                           static_cast<int32_t*>(nullptr), 0, world, counts, counts_ld, status);
+                           static_cast<int32_t*>(nullptr), 0, world, counts, counts_ld, status,
+                           static_cast<const int32_t*>(nullptr));
         TTAMM_LAUNCH_CHECK();
         return TTAMM_OK;
     }
@@ -156,10 +222,12 @@ int launch_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_
     int bits = 0;
     while ((1 << bits) < world) ++bits;
     int32_t* blk = static_cast<int32_t*>(scratch);
-    hipLaunchKernelGGL(route_count_kernel, dim3(nb), dim3(kRouteThreads), sizeof(int32_t) * world, s, a, blk);
+    int32_t* blk0 = counts_ld >= 3 ? blk + (int64_t)nb * world : nullptr;
+    hipLaunchKernelGGL(route_count_kernel, dim3(nb), dim3(kRouteThreads), 2 * sizeof(int32_t) * world, s, a, blk,
+                       blk0);
     TTAMM_LAUNCH_CHECK();
     hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(kRouteThreads), sizeof(int64_t) * world, s, blk, nb, world,
-                       counts, counts_ld, status);
+                       counts, counts_ld, status, static_cast<const int32_t*>(blk0));
     TTAMM_LAUNCH_CHECK();
     hipLaunchKernelGGL(route_scatter_kernel, dim3(nb), dim3(kRouteThreads),
                        sizeof(int32_t) * world * (1 + kRouteWaves), s, a, blk, bits, packed, slot);

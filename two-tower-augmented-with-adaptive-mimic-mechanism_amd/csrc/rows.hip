@@ -220,10 +220,11 @@ constexpr int kMaxDChunks = 8;  // D <= 512
 constexpr int kMaxNeg = 64;
 
 // r: the row in the item buffers (item_slot already applied)
-__device__ __forceinline__ float item_aug_at(const ScoreArgs& A, int64_t r, int d) {
+// (neg: a negative request's row, which holds t + a already under A.neg_aug)
+__device__ __forceinline__ float item_aug_at(const ScoreArgs& A, int64_t r, int d, bool neg = false) {
     if (A.item_aug) return A.item_aug[r * A.ld_item + d];
     const float t = A.t_item[r * A.ld_item + d];
-    return A.a_item ? t + A.a_item[r * A.ld_item + d] : t;
+    return A.a_item && !(neg && A.neg_aug) ? t + A.a_item[r * A.ld_item + d] : t;
 }
 
 // NCH = ceil(D / 64) chunks per lane.  Every row the wave reads is requested before the first
@@ -302,7 +303,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_kernel(ScoreArgs 
                     nr[jj] = A.item_slot ? A.item_slot[q] : q;
                 }
 #pragma unroll
-                for (int c = 0; c < NCH; ++c) nv[jj][c] = (jj < ng && ok[c]) ? item_aug_at(A, nr[jj], c * 64 + lane) : 0.f;
+                for (int c = 0; c < NCH; ++c) nv[jj][c] = (jj < ng && ok[c]) ? item_aug_at(A, nr[jj], c * 64 + lane, true) : 0.f;
             }
             float sn[kScoreNG];
 #pragma unroll
@@ -394,10 +395,10 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_v_kernel(ScoreArg
     float bce = 0.f, mse_u = 0.f, mse_i = 0.f;
     if (b < B) {
         const int64_t pb = A.item_slot ? A.item_slot[b] : b;
-        auto item_row = [&](int64_t r, int c) {
+        auto item_row = [&](int64_t r, int c, bool neg) {
             if (A.item_aug) return ld4(A.item_aug + r * ldt + c);
             const float4 t = ld4(A.t_item + r * ldt + c);
-            return A.a_item ? addf4(t, ld4(A.a_item + r * ldt + c)) : t;
+            return A.a_item && !(neg && A.neg_aug) ? addf4(t, ld4(A.a_item + r * ldt + c)) : t;
         };
         const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
         float4 u[NV], p[NV], au[NV], tp[NV], ap[NV], tu[NV], ibp[NV], ibu[NV];
@@ -405,7 +406,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_v_kernel(ScoreArg
         for (int i = 0; i < NV; ++i) {
             const int c = 4 * (s + G * i);
             u[i] = ld4(A.user_aug + b * D + c);
-            p[i] = item_row(pb, c);
+            p[i] = item_row(pb, c, false);
             au[i] = tp[i] = ap[i] = tu[i] = ibp[i] = ibu[i] = z4;
             if (A.mimic) {
                 au[i] = ld4(A.a_user + b * D + c);
@@ -446,7 +447,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void score_loss_v_kernel(ScoreArg
                     nr[jj] = A.item_slot ? A.item_slot[q] : q;
                 }
 #pragma unroll
-                for (int i = 0; i < NV; ++i) nv[jj][i] = jj < ng ? item_row(nr[jj], 4 * (s + G * i)) : z4;
+                for (int i = 0; i < NV; ++i) nv[jj][i] = jj < ng ? item_row(nr[jj], 4 * (s + G * i), true) : z4;
             }
             float sn[NG];
 #pragma unroll

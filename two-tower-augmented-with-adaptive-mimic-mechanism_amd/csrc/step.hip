@@ -68,6 +68,7 @@ struct TowerWs {
     float* dA_own = nullptr;
     int64_t dA_ld = 0;
     int64_t dA_split = 0;       // rows < dA_split read dA, the rest read dT
+    const int64_t* xu = nullptr;  // sharded owner, compact exchange rows: row units (GateTower::xu)
     float* dq = nullptr;
     float* dEF = nullptr;  // [R, 2D]
     float* gw[TTAMM_MAX_LINEAR] = {};
@@ -96,6 +97,10 @@ struct StepWs {
     float* partials = nullptr;
     uint32_t* prologue_done = nullptr;  // completion counter of step_prologue_kernel (zero between calls)
     int64_t* keys_own = nullptr;        // sharded owner: staged request keys [item_rows_capacity]
+    // compact exchange rows (ttamm_step_args.exchange_counts), formed by ITEM_FWD: the first unit
+    // of each request (requester, [B (1 + N)]) and of each owned row (owner, ~unit for a negative)
+    int64_t* req_units = nullptr;
+    int64_t* own_units = nullptr;
     int score_blocks = 0;
     // in-batch negatives (ttamm_step_args.in_batch)
     bool ib_on = false;
@@ -209,6 +214,8 @@ int validate_tower(const ttamm_tower& T, const char* name, int D, bool training)
 }
 
 bool sharded(const ttamm_step_args& A) { return A.phase != TTAMM_PHASE_ALL; }
+// compact exchange rows (ttamm.h ttamm_step_args.exchange_counts)
+bool compact_exchange(const ttamm_step_args& A) { return sharded(A) && A.exchange_counts != nullptr; }
 int64_t global_batch(const ttamm_step_args& A) { return A.global_batch > 0 ? A.global_batch : A.b.batch; }
 
 // The replicated-weight gradient arena: per tower (user, item) the feature-encoder layers'
@@ -369,6 +376,8 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
     if (shard) {
         tower(A.item, ws.item, A.item_rows_capacity, true, 0);
         ws.keys_own = ar.take<int64_t>(A.item_rows_capacity);
+        ws.own_units = ar.take<int64_t>(A.item_rows_capacity);
+        ws.req_units = ar.take<int64_t>(B * (1 + N));
     }
     else
         tower(A.item, ws.item, B * (1 + N), false, B);
@@ -539,12 +548,22 @@ bool gate_group(const ttamm_tower* const* T, TowerWs* const* W, int ntowers, int
         g.dq = w.dq;
         g.dz = w.dz;
         g.dEF = w.dEF;
+        g.xu = w.xu;
         g.w16 = w.gw16;
         if (!w.gw16_ready) ga.images_ready = 0;
     }
     ga.D = D;
     ga.HG = hg;
     return true;
+}
+
+// compact exchange rows (TowerWs::xu) are addressed by the fused gate kernels only
+int require_fused_for_units(const ttamm_tower* const* T, TowerWs* const* W, int ntowers, bool fused_gate) {
+    for (int k = 0; k < ntowers; ++k)
+        TTAMM_REQUIRE(!W[k]->xu || (T[k]->fusion == TTAMM_FUSION_GATED && fused_gate),
+                      "compact exchange rows (exchange_counts) need the item tower on the fused gate kernels "
+                      "(ttamm_exchange_compact_supported)");
+    return TTAMM_OK;
 }
 
 // ---- forward -------------------------------------------------------------------------------
@@ -695,6 +714,7 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
     // fusion
     GateArgs ga;
     const bool fused_gate = gate_group(T, W, ntowers, D, mimic, ga);
+    if ((rc = require_fused_for_units(T, W, ntowers, fused_gate))) return rc;
     if (fused_gate && ga.count > 0) {
         if ((rc = launch_gate(ga, false, s))) return rc;
         for (int k = 0; k < ntowers; ++k) W[k]->gw16_ready = W[k]->gw16 != nullptr;
@@ -808,6 +828,7 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
     // gate: dq, dz, dEF
     GateArgs ga;
     const bool fused_gate = gate_group(T, W, ntowers, D, false, ga);
+    if ((rc = require_fused_for_units(T, W, ntowers, fused_gate))) return rc;
     if (fused_gate && ga.count > 0)
         if ((rc = launch_gate(ga, true, s))) return rc;
     Batcher b1, b2;
@@ -1321,6 +1342,7 @@ RowUpdateArgs row_update_args(const ttamm_tower& t, TowerWs& w, int D, bool mimi
         ru.dA_hi = w.dT;
         ru.ld_dA = w.dA_ld;
         ru.split_row = w.dA_split;
+        ru.xu = w.xu;
     }
     ru.side_id = w.side_id;
     ru.side_mimic = w.side_mimic;
@@ -1532,11 +1554,17 @@ int deferred_of(const ttamm_step_args& A, Deferred& df) {
 // [positives; negatives]; sharded requester, its requests' (t | a) exchange rows and global ids
 CalArgs& bind_cal(const ttamm_step_args& A, StepWs& ws, const TowerWs& I, int64_t B, int D, bool mimic) {
     CalArgs& c = ws.cal;
+    c.xa_rows = INT64_MAX;
     if (sharded(A)) {
         c.x = A.item_fwd_in;
         c.xa = mimic ? A.item_fwd_in + D : nullptr;
         c.ld_x = 2 * D;
         c.slot = A.item_slot;
+        if (compact_exchange(A)) {  // units of D floats; a negative's row is t + a already
+            c.ld_x = D;
+            c.slot = ws.req_units;
+            c.xa_rows = B;
+        }
         c.idx = A.b.pos_items;
         c.idx1 = A.b.neg_items;
         c.split = B;
@@ -1622,6 +1650,14 @@ int validate_step(const ttamm_step_args& A) {
                   "n_item_rows exceeds item_rows_capacity");
     if (ph & TTAMM_PHASE_SAMPLE)
         TTAMM_REQUIRE(!A.b.sample_negatives || A.b.neg_items, "sharded SAMPLE phase needs b.neg_items for the exchange");
+    if (A.exchange_counts) {
+        TTAMM_REQUIRE(A.mimic_enabled && A.item.fusion == TTAMM_FUSION_GATED,
+                      "compact exchange rows (exchange_counts) need mimic on and a gated item tower");
+        TTAMM_REQUIRE(A.exchange_world >= 1 && A.exchange_world <= 1024 && A.exchange_counts_ld >= 3,
+                      "exchange_counts needs exchange_world in [1, 1024] and exchange_counts_ld >= 3");
+        TTAMM_REQUIRE(!(ph & TTAMM_PHASE_ITEM_FWD) || A.b.batch * (1 + A.b.num_neg) == 0 || A.item_slot,
+                      "compact exchange rows need item_slot");
+    }
     if ((ph & (TTAMM_PHASE_ITEM_FWD | TTAMM_PHASE_ITEM_BWD)) && A.n_item_rows > 0)
         TTAMM_REQUIRE(A.item_rows && A.item_row_keys, "item_rows / item_row_keys missing");
     if (ph & TTAMM_PHASE_ITEM_FWD) TTAMM_REQUIRE(A.item_fwd_out || A.n_item_rows == 0, "item_fwd_out missing");
@@ -1672,6 +1708,10 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         I.dA = A.item_bwd_in ? A.item_bwd_in + D : nullptr;
         I.dA_ld = 2 * D;
         I.dA_split = I.R;  // every row's mimic gradient is shipped in (dT | dA)
+        if (compact_exchange(A)) {  // D-float units: (t | a) of a positive, t + a of a negative
+            I.t_ld = I.dT_ld = I.dA_ld = D;
+            I.xu = ws.own_units;
+        }
         I.renorm_key_split = Bg;  // request keys: positives [0, Bg), negatives from Bg on
         neg = A.b.neg_items;
     } else {
@@ -1772,6 +1812,16 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         pa.c = ad;
         if ((rc = launch_step_prologue(st, pa, s))) return rc;
     }
+    if (compact_exchange(A) && (ph & TTAMM_PHASE_ITEM_FWD)) {
+        // the units of this rank's requests (owner-grouped by item_slot, [positives | negatives] per
+        // owner) and of the rows it owns (requester-grouped as they arrived, likewise split)
+        const int64_t ld = A.exchange_counts_ld;
+        const int Wd = A.exchange_world;
+        if ((rc = launch_exchange_units(A.exchange_counts, ld, Wd, A.item_slot, B * (1 + N), 0, ws.req_units, s)))
+            return rc;
+        if ((rc = launch_exchange_units(A.exchange_counts + (int64_t)Wd * ld, ld, Wd, nullptr, I.R, 1, ws.own_units, s)))
+            return rc;
+    }
     if (shard && (ph & TTAMM_PHASE_ITEM_FWD) && I.R > 0) {
         // owner: stage the requested local rows (range-checked) and their keys, contiguous
         StageArgs st;
@@ -1814,8 +1864,9 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     const int64_t ib_cols = ws.ib_on ? (shard ? Bg : B) : 0;  // positives every user is scored against
     if (ws.ib_on && shard && (ph & TTAMM_PHASE_INBATCH_SRC)) {
         TTAMM_REQUIRE(A.item_fwd_in && A.inbatch_local, "INBATCH_SRC needs item_fwd_in and inbatch_local");
-        if ((rc = launch_add_rows(A.item_fwd_in, 2 * D, mimic ? A.item_fwd_in + D : nullptr, 2 * D, B, D,
-                                  A.inbatch_local, D, s, A.item_slot)))
+        const bool cx = compact_exchange(A);  // positives keep (t | a) in either layout
+        if ((rc = launch_add_rows(A.item_fwd_in, cx ? D : 2 * D, mimic ? A.item_fwd_in + D : nullptr, cx ? D : 2 * D,
+                                  B, D, A.inbatch_local, D, s, cx ? ws.req_units : A.item_slot)))
             return rc;
     }
     if (ws.ib_on && (ph & (shard ? TTAMM_PHASE_INBATCH : TTAMM_PHASE_USER))) {
@@ -1875,6 +1926,12 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
             sa.dA_all = 1;
             sa.ld_dti = 2 * D;
             sa.item_slot = A.item_slot;
+            if (compact_exchange(A)) {  // D-float units; negatives: t + a in, dT out (their dA is dT)
+                sa.ld_item = sa.ld_dti = D;
+                sa.dA_all = 0;
+                sa.neg_aug = 1;
+                sa.item_slot = ws.req_units;
+            }
         } else {
             sa.item_aug = I.aug;
             sa.t_item = I.t;
@@ -1902,6 +1959,10 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
                 c.dA = mimic ? A.item_bwd_out + D : nullptr;
                 c.ld_d = 2 * D;
                 c.dA_rows = c.R;  // every request ships its own dA
+                if (compact_exchange(A)) {  // only the positives ship a dA
+                    c.ld_d = D;
+                    c.dA_rows = B;
+                }
                 if ((rc = launch_cal_finish(c, s))) return rc;
             } else {
                 c.dT = I.dT_own;
@@ -2013,6 +2074,28 @@ size_t train_step_workspace_size(const ttamm_step_args& A) {
     StepWs ws;
     plan(ar, A, ws);
     return ar.off + 256;
+}
+
+int exchange_compact_supported(const ttamm_step_args& A) {
+    if (!A.mimic_enabled || A.item.fusion != TTAMM_FUSION_GATED) return 0;
+    const int D = out_dim(A.user);
+    // gate_group's choice as the step makes it: a gated tower has gate16 weight images exactly when
+    // plan() gives it some (a stand-in pointer here; gate_group only tests it)
+    static uint16_t stand_in;
+    TowerWs u, it;
+    const ttamm_tower* T2[2] = {&A.user, &A.item};
+    TowerWs* W2[2] = {&u, &it};
+    for (int k = 0; k < 2; ++k) {
+        W2[k]->R = 1;
+        const ttamm_tower& t = *T2[k];
+        if (t.fusion == TTAMM_FUSION_GATED && gate16_supported(D, t.gate[0].out_features, t.matmul_bf16 ? 1 : 3))
+            W2[k]->gw16 = &stand_in;
+    }
+    GateArgs ga;
+    const ttamm_tower* Ti[2] = {&A.item, nullptr};
+    TowerWs* Wi[2] = {&it, nullptr};
+    if (!gate_group(Ti, Wi, 1, D, true, ga)) return 0;
+    return gate_group(T2, W2, 2, D, true, ga) ? 1 : 0;
 }
 
 int64_t dense_grad_floats(const ttamm_step_args& A) {

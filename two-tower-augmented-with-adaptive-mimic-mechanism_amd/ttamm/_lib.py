@@ -177,10 +177,14 @@ class StepArgs(ctypes.Structure):
         ("cal_stats", c_vp),
         ("cal_scatter", c_vp),
         ("item_rows_ld", c_i64),
+        # compact exchange rows (ttamm_exchange_compact_supported)
+        ("exchange_counts", c_vp),
+        ("exchange_counts_ld", c_i64),
+        ("exchange_world", c_i32),
     ]
 
 
-ABI_VERSION = 23  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 24  # ttamm.h TTAMM_ABI_VERSION
 G0_EXACT = 0  # ttamm.h TTAMM_G0_EXACT
 DENSE_ADAM = 0  # ttamm.h TTAMM_DENSE_ADAM
 DENSE_SGD = 1  # ttamm.h TTAMM_DENSE_SGD
@@ -211,6 +215,7 @@ SIGNATURES = {
     "ttamm_train_step_workspace_size": (ctypes.c_size_t, [ctypes.POINTER(StepArgs)]),
     "ttamm_train_step": (ctypes.c_int, [ctypes.POINTER(StepArgs), c_vp]),
     "ttamm_dense_grad_floats": (c_i64, [ctypes.POINTER(StepArgs)]),
+    "ttamm_exchange_compact_supported": (ctypes.c_int, [ctypes.POINTER(StepArgs)]),
     "ttamm_adam_history_entry_bytes": (ctypes.c_size_t, []),
     "ttamm_retrieval_topk_workspace_size": (ctypes.c_size_t, [c_i64, c_i64, c_i32, c_i32]),
     "ttamm_normalize_rows": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i64, c_vp]),

@@ -38,7 +38,8 @@ from __future__ import annotations
 
 import ctypes
 import functools
-from dataclasses import dataclass
+import os
+from dataclasses import dataclass, field
 from typing import Any, Callable, Generator, Mapping, Sequence
 
 import torch
@@ -318,6 +319,11 @@ class Route:
     keys: torch.Tensor  # owner side: global request positions [n_recv]
     own_status: int = 0  # this rank's status word after SAMPLE (when piggybacked)
     peer_status: int = 0  # OR of the other ranks' status words
+    # compact exchange rows (count rows with a positives column): of send_counts / recv_counts,
+    # the leading positives; sr = the device count rows [2W, ld] (ttamm_step_args.exchange_counts)
+    send_pos: list[int] = field(default_factory=list)
+    recv_pos: list[int] = field(default_factory=list)
+    sr: torch.Tensor | None = None
 
 
 def device_route(lib: Any, world: int, id0: torch.Tensor, id1: torch.Tensor | None = None,
@@ -355,25 +361,29 @@ class PendingRoute:
     packed: torch.Tensor
     slot: torch.Tensor
     n: int
-    sr: torch.Tensor  # [2W, 2] (count, status) rows sent, then received
+    sr: torch.Tensor  # [2W, ld] (count, status[, positives]) rows sent, then received
     host: torch.Tensor | None  # pinned copy of sr (None: read sr itself)
     event: Any  # torch.cuda.Event after the copy, or None
 
 
 def route_start(own: RowOwnership, router: Router, pos: torch.Tensor, negs: torch.Tensor, key0: int, key1: int,
-                status: torch.Tensor | None = None, host: torch.Tensor | None = None) -> Program:
+                status: torch.Tensor | None = None, host: torch.Tensor | None = None, ld: int = 2) -> Program:
     """Program: group the requests [pos; negs] by owner (keys key0 + j for positives, key1 + j for
-    negatives) and exchange the per-owner counts with the rank's status word.  With a pinned
-    ``host`` buffer the counts are copied to it asynchronously (no host synchronisation here:
-    route_finish waits, so a look-ahead can start the copy a step early)."""
+    negatives) and exchange the per-owner counts with the rank's status word (``ld`` = 3: and how
+    many of them are positives, for the compact exchange rows).  With a pinned ``host`` buffer the
+    counts are copied to it asynchronously (no host synchronisation here: route_finish waits, so a
+    look-ahead can start the copy a step early)."""
     W = own.world_size
     n = pos.numel() + negs.numel()
-    # rows 0..W-1: what this rank sends (count to owner d, its status word); rows W..2W-1: received
-    sr = torch.empty((2 * W, 2), dtype=torch.long, device=pos.device)
+    # rows 0..W-1: what this rank sends (count to owner d, its status word[, positives]); rows
+    # W..2W-1: received
+    sr = torch.empty((2 * W, ld), dtype=torch.long, device=pos.device)
     if status is None:
         sr[:W, 1] = 0
     packed, slot, _ = router(W, pos, negs, None, key0, key1, counts_out=sr[:W], status=status)
     event = None
+    if W == 1 and ld >= 3:  # the owner's rows are this rank's own requests
+        sr[1:].copy_(sr[:1])
     if W > 1:
         yield AllToAll(sr[:W], [1] * W, [1] * W, out=sr[W:])
         if host is not None and sr.device.type == "cuda":
@@ -391,20 +401,25 @@ def route_finish(own: RowOwnership, pend: PendingRoute) -> Program:
     Returns a Route.  The status words that rode with the counts tell every rank whether any rank's
     step is poisoned (Route.peer_status) before any of them writes state."""
     W = own.world_size
+    ld = pend.sr.shape[1]
     if W == 1:  # (local row, key) columns read in place by the step (ttamm_step_args.item_rows_ld)
-        return Route(pend.slot, [pend.n], [pend.n], pend.packed[:, 0], pend.packed[:, 1])
+        # (no exchange: the positives' count stays on the device, in sr, for the step's unit maps)
+        return Route(pend.slot, [pend.n], [pend.n], pend.packed[:, 0], pend.packed[:, 1], sr=pend.sr)
     if pend.host is not None:
         pend.event.synchronize()
         c = pend.host.reshape(-1).tolist()
     else:
         c = pend.sr.reshape(-1).tolist()
-    sent, got_c = c[0:2 * W:2], c[2 * W::2]
+    sent, got_c = c[0:ld * W:ld], c[ld * W::ld]
     peers = 0
-    for r, st in enumerate(c[2 * W + 1::2]):
+    for r, st in enumerate(c[ld * W + 1::ld]):
         if r != own.rank:
             peers |= int(st)
     got = yield AllToAll(pend.packed, sent, got_c)
-    return Route(pend.slot, sent, got_c, got[:, 0], got[:, 1], int(c[1]), peers)
+    route = Route(pend.slot, sent, got_c, got[:, 0], got[:, 1], int(c[1]), peers, sr=pend.sr)
+    if ld >= 3:
+        route.send_pos, route.recv_pos = c[2:ld * W:ld], c[ld * W + 2::ld]
+    return route
 
 
 def route_requests(own: RowOwnership, router: Router, pos: torch.Tensor, negs: torch.Tensor, key0: int,
@@ -509,6 +524,13 @@ class ShardedTrainStep(FusedTrainStep):
             args.cal_scatter = self.cal_scatter.data_ptr()
         self.fwd_in = torch.empty((R, 2 * D), dtype=torch.float32, device=self.device)
         self.bwd_out = torch.empty((R, 2 * D), dtype=torch.float32, device=self.device)
+        # compact exchange rows (ttamm.h ttamm_step_args.exchange_counts): a negative request moves D
+        # floats each way instead of 2 D (t + a forward, dT backward); TTAMM_WIDE_EXCHANGE=1 keeps the
+        # 2 D-wide rows.  The buffers above stay sized for the wide rows (the compact ones fit).
+        self.compact = (bool(self.lib.ttamm_exchange_compact_supported(ctypes.byref(args)))
+                        and os.environ.get("TTAMM_WIDE_EXCHANGE") != "1")
+        self.count_ld = 3 if self.compact else 2
+        self.exchange_floats = [0, 0]  # this rank's last (t | a) send, (dT | dA) send, in floats
 
     def _phase(self, bits: int) -> None:
         self.args.phase = bits
@@ -575,7 +597,7 @@ class ShardedTrainStep(FusedTrainStep):
             pend = ahead.pending
         else:
             pend = yield from route_start(self.own, self.router, pos_items.reshape(-1), negs, base, Bg + base * N,
-                                          status=self.status)
+                                          status=self.status, ld=self.count_ld)
         route = yield from route_finish(self.own, pend)
         if route.peer_status and not route.own_status:
             # another rank's step is poisoned (an id outside its table, sampler exhaustion):
@@ -596,6 +618,23 @@ class ShardedTrainStep(FusedTrainStep):
         a.item_slot = route.slot.data_ptr()  # exchange buffers stay in owner-grouped order
         a.item_fwd_out = self.fwd_out.data_ptr()
         R = B * (1 + N)
+        if self.compact:
+            # D-float units, a positive taking two: per peer D (requests + positives) floats each way
+            a.exchange_counts = route.sr.data_ptr()
+            a.exchange_counts_ld = route.sr.stride(0)
+            a.exchange_world = W
+            if W > 1:
+                to_req = [D * (c + p) for c, p in zip(route.recv_counts, route.recv_pos)]
+                to_own = [D * (c + p) for c, p in zip(route.send_counts, route.send_pos)]
+                fwd_src = self.fwd_out.view(-1)[:sum(to_req)]
+                fwd_dst = self.fwd_in.view(-1)[:sum(to_own)]
+                bwd_src = self.bwd_out.view(-1)[:sum(to_own)]
+        else:
+            a.exchange_counts = None
+            a.exchange_counts_ld = 0
+            a.exchange_world = 0
+            to_req, to_own = route.recv_counts, route.send_counts
+            fwd_src, fwd_dst, bwd_src = self.fwd_out[:n], self.fwd_in[:R], self.bwd_out[:R]
         for i in (2, 3, 8, 9, 10, 11):  # first-layer GEMM, catch-up replays
             a.timing_events[i] = ev[i]
         if W == 1:  # no exchange: the requester's buffers are the owner's
@@ -605,11 +644,12 @@ class ShardedTrainStep(FusedTrainStep):
             back = self.fwd_out[:n]
         elif self.group_towers:
             self._phase(_lib.PHASE_ITEM_FWD | _lib.PHASE_USER_FWD)
-            back = yield AllToAll(self.fwd_out[:n], route.recv_counts, route.send_counts, out=self.fwd_in[:R])
+            self.exchange_floats[0] = fwd_src.numel()
+            back = yield AllToAll(fwd_src, to_req, to_own, out=fwd_dst)
         else:  # (t | a) back to the requesters, the user tower meanwhile
             self._phase(_lib.PHASE_ITEM_FWD)
-            h = yield AllToAll(self.fwd_out[:n], route.recv_counts, route.send_counts, async_op=True,
-                               out=self.fwd_in[:R])
+            self.exchange_floats[0] = fwd_src.numel()
+            h = yield AllToAll(fwd_src, to_req, to_own, async_op=True, out=fwd_dst)
             self._phase(_lib.PHASE_USER_FWD)
             back = yield Wait(h)
         for i in (2, 3, 8, 9, 10, 11):
@@ -645,7 +685,8 @@ class ShardedTrainStep(FusedTrainStep):
         if W == 1:
             bwd_in = self.bwd_out[:R]
         else:
-            bwd_in = yield AllToAll(self.bwd_out[:R], route.send_counts, route.recv_counts)
+            self.exchange_floats[1] = bwd_src.numel()
+            bwd_in = yield AllToAll(bwd_src, to_own, to_req)
         a.item_bwd_in = bwd_in.data_ptr()
         for i in (0, 1, 6, 7):  # table maintenance, wide weight-gradient GEMM
             a.timing_events[i] = ev[i]
@@ -684,7 +725,7 @@ class ShardedTrainStep(FusedTrainStep):
         if self._ahead_bufs is None:
             self._ahead_bufs = [torch.empty(self.max_batch * N, dtype=torch.long, device=dev) for _ in range(2)]
             self._ahead_status = [torch.zeros(1, dtype=torch.int32, device=dev) for _ in range(2)]
-            self._ahead_host = (torch.empty((2 * W, 2), dtype=torch.long, pin_memory=True)
+            self._ahead_host = (torch.empty((2 * W, self.count_ld), dtype=torch.long, pin_memory=True)
                                 if dev.type == "cuda" and W > 1 else None)
         k = self._ahead_flip
         self._ahead_flip ^= 1
@@ -701,7 +742,7 @@ class ShardedTrainStep(FusedTrainStep):
                 self.csr.num_users, self.args.b.seed, self.steps_done + 1, base * N, negs.data_ptr(),
                 status.data_ptr(), stream))
         pend = yield from route_start(self.own, self.router, pos, negs, base, Bg + base * N, status=status,
-                                      host=self._ahead_host)
+                                      host=self._ahead_host, ld=self.count_ld)
         return _Ahead(users0, pos0, negs, status, pend)
 
     def step(self, users, pos_items, neg_items=None, *, keep_masks=None, timing_events=None,
