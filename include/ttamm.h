@@ -370,7 +370,8 @@ typedef struct ttamm_step_args {
      * ones: ttamm_route_rows with counts_ld >= 3).  Requester buffers are owner-grouped as
      * item_slot orders them, the owner's requester-grouped as item_rows arrive; each group is
      * [positives | negatives], so the all-to-alls move dim * (requests + positives) floats per
-     * peer, unpermuted.  ITEM_FWD forms both unit maps; later phases reuse them. */
+     * peer, unpermuted.  item_slot then holds each request's first unit (ttamm_route_rows with
+     * counts_ld >= 3 writes them); ITEM_FWD forms the owner's with its staging. */
     const int64_t* exchange_counts;
     int64_t exchange_counts_ld;
     int32_t exchange_world;
@@ -475,7 +476,9 @@ int ttamm_epoch_batch(const int64_t* users, const int64_t* items, int64_t n, uin
  * (counts_ld >= 1); with status != NULL and counts_ld >= 2, counts[o * counts_ld + 1] = *status —
  * the (count, status word) rows of the sharded step's count all-to-all, written in the same launch;
  * with counts_ld >= 3, counts[o * counts_ld + 2] = how many of owner o's ids came from id0 (the
- * positives of a step's requests: ttamm_step_args.exchange_counts). */
+ * positives of a step's requests: ttamm_step_args.exchange_counts), and slot[j] is then position
+ * j's first unit of the compact exchange layout instead of its grouped row: the owner groups in
+ * order, each [its id0 ids, two units each | its id1 ids, one unit each]. */
 size_t ttamm_route_scratch_bytes(int64_t n, int32_t world);
 int ttamm_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_t n1, const int64_t* payload,
                      int64_t key0, int64_t key1, int32_t world, int64_t* packed, int64_t* slot, int64_t* counts,

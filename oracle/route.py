@@ -17,7 +17,10 @@ def route_rows(world: int, id0: torch.Tensor, id1: torch.Tensor | None = None, p
                key0: int = 0, key1: int = 0, counts_out: torch.Tensor | None = None,
                status: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """(packed [n, 2], slot [n], counts [world]) as ttamm_route_rows defines them; a [world, 2]
-    ``counts_out`` gets the counts in column 0 and, with ``status``, the status word in column 1."""
+    ``counts_out`` gets the counts in column 0 and, with ``status``, the status word in column 1; a
+    [world, >= 3] one also the count of id0 ids per owner in column 2, and slot then holds each
+    request's first unit of the compact exchange layout (ttamm.h exchange_counts): the groups in
+    owner order, each [its id0 ids, two units each | its id1 ids, one unit each]."""
     ids = id0.reshape(-1).cpu() if id1 is None else torch.cat([id0.reshape(-1).cpu(), id1.reshape(-1).cpu()])
     n0 = id0.numel()
     n = ids.numel()
@@ -35,6 +38,11 @@ def route_rows(world: int, id0: torch.Tensor, id1: torch.Tensor | None = None, p
             counts_out[:, 0].copy_(counts)
             if status is not None:
                 counts_out[:, 1] = int(status.reshape(-1)[0])
+            if counts_out.shape[1] >= 3:
+                first = torch.bincount(owner[:n0], minlength=world)
+                counts_out[:, 2].copy_(first)
+                start, pcum = torch.cumsum(counts, 0) - counts, torch.cumsum(first, 0) - first
+                slot = slot + pcum[owner] + torch.minimum(slot - start[owner], first[owner])
         else:
             counts_out.copy_(counts)
         counts = counts_out

@@ -74,7 +74,8 @@ def test_route_empty_and_bad_world():
 @pytest.mark.parametrize("n", [0, 2049, 49152])
 def test_route_positive_counts_column(world, n):
     """counts_ld >= 3 (the compact exchange's count rows): column 2 = how many of each owner's
-    ids came from id0 (the positives), beside the counts and the status word."""
+    ids came from id0 (the positives), beside the counts and the status word, and slot = each
+    request's first unit of the compact exchange layout (oracle/route.py)."""
     lib = _lib.load()
     g = torch.Generator().manual_seed(world + n)
     ids = torch.randint(0, 1 << 40, (n,), generator=g).cuda()
@@ -83,9 +84,12 @@ def test_route_positive_counts_column(world, n):
     status = torch.tensor([5], dtype=torch.int32, device="cuda")
     packed, slot, _ = device_route(lib, world, ids[:n0], ids[n0:], None, 7, 9, counts_out=counts, status=status)
     torch.cuda.synchronize()
-    want = route_rows(world, ids[:n0].cpu(), ids[n0:].cpu(), None, 7, 9)
+    wc = torch.zeros((world, 3), dtype=torch.long)
+    want = route_rows(world, ids[:n0].cpu(), ids[n0:].cpu(), None, 7, 9, counts_out=wc,
+                      status=torch.tensor([5], dtype=torch.int32))
     assert torch.equal(packed.cpu(), want[0].cpu()) and torch.equal(slot.cpu(), want[1].cpu())
     c = counts.cpu()
-    assert torch.equal(c[:, 0], want[2].cpu())
+    assert torch.equal(c, wc)
+    assert torch.equal(c[:, 0], torch.bincount(ids.cpu() % world, minlength=world))
     assert c[:, 1].tolist() == [5] * world
     assert torch.equal(c[:, 2], torch.bincount(ids[:n0].cpu() % world, minlength=world))

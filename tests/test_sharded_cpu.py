@@ -172,3 +172,21 @@ def test_route_pairs_to_user_owners(W):
         want_i = torch.cat([si[su % W == r] for su, si in streams])
         assert torch.equal(u, want_u // W) and torch.equal(i, want_i)  # local user rows
         assert sizes == [sum(int((su % W == d).sum()) for su, _ in streams) for d in range(W)]
+
+
+def test_route_oracle_compact_units_tile_the_exchange_buffer():
+    """oracle/route.py with [world, 3] count rows (the compact exchange layout, ttamm.h
+    exchange_counts): the units of a rank's requests tile [0, requests + positives) exactly, each
+    owner's group starting where the previous one ends, positives two units apart."""
+    g = torch.Generator().manual_seed(3)
+    for world in (1, 3, 8):
+        ids = torch.randint(0, 10 ** 6, (600,), generator=g)
+        counts = torch.zeros((world, 3), dtype=torch.long)
+        _, units, _ = route_rows(world, ids[:100], ids[100:], None, 0, 0, counts_out=counts)
+        width = torch.ones(600, dtype=torch.long)
+        width[:100] = 2
+        cover = torch.zeros(600 + 100, dtype=torch.long)
+        for u, w in zip(units.tolist(), width.tolist()):
+            cover[u:u + w] += 1
+        assert torch.equal(cover, torch.ones_like(cover))
+        assert counts[:, 2].sum() == 100 and counts[:, 0].sum() == 600

@@ -168,19 +168,25 @@ COMPACT_CASES = [
     (3, Shape(N=2, **C32), True, False),
     (1, Shape(**C32), False, True),
     (1, Shape(N=2, **C32), True, True),
-    (3, Shape(U=300, I=900, N=0, B=70, **C32), True, True),
+    (3, Shape(U=300, I=900, N=1, B=70, **C32), True, True),
     (2, Shape(dropout=0.0, **C32), False, True),
     (2, Shape(U=200, I=900, F=37, H=128, D=128, B=40, N=3, hidden_dims=(128,), matmul_dtype="bf16"), False, True),
     (8, Shape(U=800, I=4000, B=64, N=3, **C32), False, False),
     (8, Shape(U=4000, I=40000, F=605, H=192, D=96, B=512, N=5, hidden_dims=(192,)), False, True),
 ]
-COMPACT_IDS = ["w2", "w2-overlapped", "w3-in-batch-overlapped", "w1", "w1-in-batch", "w3-in-batch-n0", "w2-nodrop",
+COMPACT_IDS = ["w2", "w2-overlapped", "w3-in-batch-overlapped", "w1", "w1-in-batch", "w3-in-batch-n1", "w2-nodrop",
                "w2-bf16-d128", "w8-overlapped", "w8-c2-widths"]
 
 
 @pytest.mark.parametrize("W,shape,in_batch,group", COMPACT_CASES, ids=COMPACT_IDS)
 def test_compact_exchange_matches_global_step(W, shape, in_batch, group):
     _one_step_check(W, shape, in_batch, group, compact=True)
+
+
+def test_no_negatives_keeps_wide_exchange():
+    """In-batch only (num_neg = 0): every request is a positive, both layouts move the same bytes,
+    and the step keeps the wide rows (no unit maps)."""
+    _one_step_check(2, Shape(U=300, I=900, N=0, B=70, **C32), True, True, compact=False)
 
 
 @pytest.mark.parametrize("W,shape,in_batch,group", [COMPACT_CASES[i] for i in (0, 2, 7, 8)],

@@ -226,9 +226,10 @@ __device__ __forceinline__ void store_slab(float* scr, const f4v (&v)[NO], float
 }
 
 // store_slab into compact exchange rows (GateTower::xu): slab row grow goes to out + u * 16 NO for
-// u = xu[grow] (a positive) or ~xu[grow] (a negative; left out when pos_only)
+// u = xu[grow] (a positive) or ~xu[grow] (a negative; left out when pos_only).  xu_li: this lane's
+// row's xu[row0 + (lane & 15)], loaded ahead by the caller (a store's row takes it by shuffle)
 template <int NO>
-__device__ __forceinline__ void store_slab_xu(float* scr, const f4v (&v)[NO], float* out, const int64_t* xu,
+__device__ __forceinline__ void store_slab_xu(float* scr, const f4v (&v)[NO], float* out, int xu_li,
                                               bool pos_only, int64_t row0, int64_t R, int lane) {
     constexpr int W = 16 * NO, LDW = W + 4, C4 = W / 4, PER = 8 * C4 / 64;
     static_assert((8 * C4) % 64 == 0, "slab scratch");
@@ -246,10 +247,8 @@ __device__ __forceinline__ void store_slab_xu(float* scr, const f4v (&v)[NO], fl
             const int idx = lane + 64 * k, r = idx / C4, c = idx - r * C4;
             const f4v val = *reinterpret_cast<const f4v*>(scr + r * LDW + 4 * c);
             const int64_t grow = row0 + 8 * half + r;
-            if (grow < R) {
-                const int64_t u = xu[grow];
-                if (u >= 0 || !pos_only) stg4(out + (u >= 0 ? u : ~u) * W + 4 * c, val);
-            }
+            const int u = __shfl(xu_li, 8 * half + r, 64);
+            if (grow < R && (u >= 0 || !pos_only)) stg4(out + (int64_t)(u >= 0 ? u : ~u) * W + 4 * c, val);
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
@@ -366,6 +365,7 @@ __global__ __launch_bounds__(64 * NW) void gate_fwd_kernel(GateArgs) {
         const bool ok = row < R;
         f4v a[C::TD];  // mimic rows for the epilogue, requested before the MFMA chain
         if (T.table) load_row(a, T.table, D, arow, q);
+        const int xu_li = T.xu && ok ? (int)T.xu[row] : 0;  // compact exchange unit (int: < 2^31 units)
         f4v z[C::TH];
         zero(z);
         if constexpr (X) tile_gemm_x<C::TH, NX, HG>(img, 0, ef, z, li, q);  // z^T = G1 . ef^T
@@ -411,13 +411,13 @@ __global__ __launch_bounds__(64 * NW) void gate_fwd_kernel(GateArgs) {
                 for (int r = 0; r < 4; ++r) x[ob][r] = x[ob][r] * e[r] + (1.0f - x[ob][r]) * f[r];
             }
             if (T.xu) {  // compact exchange rows: (t | a) of a positive, t + a of a negative
-                store_slab_xu<C::TD>(scr, a, T.a, T.xu, true, s * 16, R, lane);
-                const bool neg = ok && T.xu[row] < 0;
+                store_slab_xu<C::TD>(scr, a, T.a, xu_li, true, s * 16, R, lane);
+                const bool neg = xu_li < 0;
 #pragma unroll
                 for (int ob = 0; ob < C::TD; ++ob)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) x[ob][r] = neg ? x[ob][r] + a[ob][r] : x[ob][r];
-                store_slab_xu<C::TD>(scr, x, T.t, T.xu, false, s * 16, R, lane);
+                store_slab_xu<C::TD>(scr, x, T.t, xu_li, false, s * 16, R, lane);
             } else {
                 store_slab<C::TD>(scr, x, T.t, T.ld_t, s * 16, R, lane);
                 if (T.table) {
@@ -432,8 +432,7 @@ __global__ __launch_bounds__(64 * NW) void gate_fwd_kernel(GateArgs) {
         }
         if ((X || ka->direct) && ok && !ka->ablate) {
             // compact exchange rows (T.xu): a positive's t and a at its unit, a negative's t + a
-            int64_t xu = 0;
-            if (T.xu) xu = T.xu[row];
+            const int64_t xu = xu_li;
             float* tdst = T.xu ? T.t + (xu >= 0 ? xu : ~xu) * D : T.t + row * T.ld_t;
             float* adst = T.xu ? (xu >= 0 ? T.a + xu * D : nullptr) : (T.table ? T.a + row * T.ld_t : nullptr);
 #pragma unroll

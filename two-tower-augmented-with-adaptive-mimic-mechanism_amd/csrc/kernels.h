@@ -104,9 +104,6 @@ size_t route_scratch_bytes(int64_t n, int world);
 int launch_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_t n1, const int64_t* payload,
                       int64_t key0, int64_t key1, int world, int64_t* packed, int64_t* slot, int64_t* counts,
                       int64_t counts_ld, const uint32_t* status, void* scratch, size_t scratch_bytes, hipStream_t s);
-// compact exchange: the first unit of each of n rows (route.hip exchange_units_kernel)
-int launch_exchange_units(const int64_t* counts, int64_t ld, int W, const int64_t* slot, int64_t n, int mark_neg,
-                          int64_t* out, hipStream_t s);
 void epoch_round_keys(uint64_t seed, int64_t epoch, uint32_t keys[4]);
 int launch_epoch_batch(const int64_t* users, const int64_t* items, int64_t n, uint64_t seed, int64_t epoch,
                        int shuffle, int64_t start, int64_t count, int64_t* out_users, int64_t* out_items,
@@ -241,6 +238,15 @@ struct StageArgs {
     StageSeg seg[kMaxStageSegs];
     int count;
     uint32_t* status;
+    // compact exchange rows (ttamm.h exchange_counts), stage_rows_kernel only: the first unit of
+    // each of unit_n owner rows, grouped by requester as they arrived (unit_groups groups of
+    // unit_counts[g * unit_ld] rows, the first unit_counts[g * unit_ld + 2] of them positives:
+    // two units each); ~unit for a negative row.  unit_out null = none.
+    const int64_t* unit_counts;
+    int64_t unit_ld;
+    int unit_groups;
+    int64_t unit_n;
+    int64_t* unit_out;
 };
 int launch_stage_rows(const StageArgs& a, hipStream_t s);
 // out = x (+ y) over [n, dim] rows (y may be null): an augmented row t + a (adaptive_mimic.py:88-95);

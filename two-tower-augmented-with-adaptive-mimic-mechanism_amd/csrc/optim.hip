@@ -415,6 +415,7 @@ __device__ __forceinline__ const float* dA_row(const RowUpdateArgs& A, int64_t r
 
 __global__ __launch_bounds__(64 * kRowWaves) void piece_sum_kernel(RowUpdateArgs A) {
     __shared__ int64_t srows[kRowWaves][kPiece];
+    __shared__ const float* sda[kRowWaves][kPiece];  // each position's dA row (resolved once: GateTower::xu)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t chunk = (int64_t)blockIdx.x * kRowWaves + w;
     const int64_t k0 = chunk * kPiece;
@@ -432,10 +433,13 @@ __global__ __launch_bounds__(64 * kRowWaves) void piece_sum_kernel(RowUpdateArgs
     const int next_key = __shfl_down(my_key, 1, 64);
     if (lane + 1 < cnt) my_last = next_key != my_key;
     const uint64_t last_mask = __ballot(lane < cnt && my_last);
-    if (lane < kPiece) srows[w][lane] = my_row;  // read back uniformly inside the d loop
+    const bool mimic = A.mimic.weight != nullptr;
+    if (lane < kPiece) {  // read back uniformly inside the d loop
+        srows[w][lane] = my_row;
+        sda[w][lane] = mimic && lane < cnt ? dA_row(A, my_row) : nullptr;
+    }
     __builtin_amdgcn_wave_barrier();
     const int D = A.dim;
-    const bool mimic = A.mimic.weight != nullptr;
     const bool idt = A.id.weight != nullptr;  // (a mimic-only pass leaves the ID table out)
     for (int d = lane; d < D; d += 64) {
         float ve[kPiece], va[kPiece];
@@ -443,7 +447,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void piece_sum_kernel(RowUpdateArgs
         for (int p = 0; p < kPiece; ++p) {  // issue every load of the chunk before adding
             const int64_t r = srows[w][p];
             ve[p] = (idt && p < cnt) ? A.dE[r * A.ld_dE + d] : 0.f;
-            va[p] = (mimic && p < cnt) ? dA_row(A, r)[d] : 0.f;
+            va[p] = (mimic && p < cnt) ? sda[w][p][d] : 0.f;
         }
         float ge = 0.f, ga = 0.f;
         int start = 0;

@@ -61,25 +61,34 @@ __global__ __launch_bounds__(kRouteThreads) void route_count_kernel(RouteIn a, i
 __global__ __launch_bounds__(kRouteThreads) void route_scan_kernel(int32_t* __restrict__ blk, int nb, int W,
                                                                    int64_t* __restrict__ counts, int64_t ld,
                                                                    const uint32_t* __restrict__ status,
-                                                                   const int32_t* __restrict__ blk0) {
-    extern __shared__ int64_t tot[];
+                                                                   const int32_t* __restrict__ blk0,
+                                                                   int64_t* __restrict__ grp) {
+    extern __shared__ int64_t tot[];  // [W] totals, then their exclusive scan
+    int64_t* tot0 = tot + W;          // (blk0) [W] id0 totals
     for (int o = threadIdx.x; o < W; o += kRouteThreads) {
         int64_t t = 0, t0 = 0;
         for (int b = 0; b < nb; ++b) t += blk[(int64_t)b * W + o];
         if (ld >= 3)
             for (int b = 0; b < nb && blk0; ++b) t0 += blk0[(int64_t)b * W + o];
         tot[o] = t;
+        if (blk0) tot0[o] = t0;
         counts[o * ld] = t;
         if (status) counts[o * ld + 1] = (int64_t)*status;
         if (ld >= 3) counts[o * ld + 2] = t0;  // of them from id0 (a step's positives)
     }
     __syncthreads();
     if (threadIdx.x == 0) {  // exclusive scan over owners (W <= 1024)
-        int64_t run = 0;
+        int64_t run = 0, run0 = 0;
         for (int o = 0; o < W; ++o) {
             const int64_t t = tot[o];
             tot[o] = run;
             run += t;
+            if (grp) {  // the compact exchange units of owner o's group: (first row, id0 rows before, id0 rows)
+                grp[3 * o] = tot[o];
+                grp[3 * o + 1] = run0;
+                grp[3 * o + 2] = tot0[o];
+                run0 += tot0[o];
+            }
         }
     }
     __syncthreads();
@@ -93,15 +102,20 @@ __global__ __launch_bounds__(kRouteThreads) void route_scan_kernel(int32_t* __re
     }
 }
 
+// grp (compact exchange units, counts_ld >= 3): slot[j] = the request's first unit instead of its row
 __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(RouteIn a, const int32_t* __restrict__ blk,
                                                                       int owner_bits, int64_t* __restrict__ packed,
-                                                                      int64_t* __restrict__ slot) {
+                                                                      int64_t* __restrict__ slot,
+                                                                      const int64_t* __restrict__ grp) {
     extern __shared__ int32_t lds[];
     const int W = (int)a.world;
     int32_t* off = lds;       // [W] next slot of each owner in this block
     int32_t* wc = lds + W;    // [kRouteWaves][W] this round's per-wave counts
+    int64_t* gt = reinterpret_cast<int64_t*>(lds + W * (1 + kRouteWaves + ((1 + kRouteWaves) & 1)));  // [3W]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (int o = threadIdx.x; o < W; o += kRouteThreads) off[o] = blk[(int64_t)blockIdx.x * W + o];
+    if (grp)
+        for (int e = threadIdx.x; e < 3 * W; e += kRouteThreads) gt[e] = grp[e];
     const int64_t lo = (int64_t)blockIdx.x * kRouteSpan;
     const uint64_t below = (1ull << lane) - 1ull;
     for (int r = 0; r < kRouteRounds; ++r) {
@@ -127,7 +141,12 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(RouteIn a,
         if (valid) {
             int32_t s = off[o] + rank;
             for (int q = 0; q < w; ++q) s += wc[q * W + o];
-            slot[j] = s;
+            if (grp) {
+                const int64_t r = s - gt[3 * o], p = gt[3 * o + 2];
+                slot[j] = s + gt[3 * o + 1] + (r < p ? r : p);
+            } else {
+                slot[j] = s;
+            }
             packed[2 * (int64_t)s] = (int64_t)(id / a.world);
             packed[2 * (int64_t)s + 1] = a.payload ? a.payload[j] : (j < a.n0 ? a.key0 + j : a.key1 + (j - a.n0));
         }
@@ -142,62 +161,12 @@ __global__ __launch_bounds__(kRouteThreads) void route_scatter_kernel(RouteIn a,
     }
 }
 
-// Compact exchange units (ttamm.h ttamm_step_args.exchange_counts): groups o = 0 .. W-1 of
-// counts[o * ld] rows each, the first counts[o * ld + 2] of them positives (two units) and the
-// rest negatives (one unit).  Row s (s = slot[i] when slot is given, else i) starts at unit
-//   s + (positives of the groups before o) + min(s - start(o), positives of o);
-// mark_neg stores ~unit for a negative row (the owner's row maps carry the row class).
-constexpr int kUnitThreads = 256;
-__global__ __launch_bounds__(kUnitThreads) void exchange_units_kernel(const int64_t* __restrict__ counts, int64_t ld,
-                                                                     int W, const int64_t* __restrict__ slot,
-                                                                     int64_t n, int mark_neg, int64_t* __restrict__ out) {
-    extern __shared__ int64_t tab[];  // start[W], pcum[W], pos[W]
-    int64_t* start = tab;
-    int64_t* pcum = tab + W;
-    int64_t* pos = tab + 2 * W;
-    if (threadIdx.x == 0) {
-        int64_t r = 0, p = 0;
-        for (int o = 0; o < W; ++o) {
-            const int64_t c = counts[o * ld], q = counts[o * ld + 2];
-            start[o] = r;
-            pcum[o] = p;
-            pos[o] = q;
-            r += c;
-            p += q;
-        }
-    }
-    __syncthreads();
-    for (int64_t i = (int64_t)blockIdx.x * kUnitThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kUnitThreads) {
-        const int64_t s = slot ? slot[i] : i;
-        int lo = 0, hi = W - 1;  // the last group starting at or before s (empty groups share starts)
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (start[mid] <= s) lo = mid;
-            else hi = mid - 1;
-        }
-        const int64_t r = s - start[lo], p = pos[lo];
-        const int64_t unit = s + pcum[lo] + (r < p ? r : p);
-        out[i] = (mark_neg && r >= p) ? ~unit : unit;
-    }
-}
-
 }  // namespace
-
-int launch_exchange_units(const int64_t* counts, int64_t ld, int W, const int64_t* slot, int64_t n, int mark_neg,
-                          int64_t* out, hipStream_t s) {
-    TTAMM_REQUIRE(W >= 1 && W <= 1024 && ld >= 3 && counts, "exchange units: bad count rows");
-    if (n <= 0) return TTAMM_OK;
-    TTAMM_REQUIRE(out != nullptr, "exchange units: null output");
-    const int64_t blocks = std::min<int64_t>(ceil_div(n, kUnitThreads), 4096);
-    hipLaunchKernelGGL(exchange_units_kernel, dim3((unsigned)blocks), dim3(kUnitThreads), 3 * sizeof(int64_t) * W, s,
-                       counts, ld, W, slot, n, mark_neg, out);
-    TTAMM_LAUNCH_CHECK();
-    return TTAMM_OK;
-}
 
 size_t route_scratch_bytes(int64_t n, int world) {
     const int64_t nb = n > 0 ? ceil_div(n, kRouteSpan) : 0;
-    return (size_t)(2 * nb * (world > 0 ? world : 0)) * sizeof(int32_t);  // blk, blk0
+    const int64_t w = world > 0 ? world : 0;
+    return (size_t)(2 * nb * w) * sizeof(int32_t) + 8 + (size_t)(3 * w) * sizeof(int64_t);  // blk, blk0, grp
 }
 
 int launch_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_t n1, const int64_t* payload,
@@ -209,9 +178,9 @@ int launch_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_
     TTAMM_REQUIRE(counts_ld >= 1 && (status == nullptr || counts_ld >= 2), "route: counts_ld must be >= 1 (>= 2 with status)");
     const int64_t n = n0 + n1;
     if (n == 0) {  // zero counts (and the status column): the scan over no blocks
-        hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(kRouteThreads), sizeof(int64_t) * world, s,
+        hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(kRouteThreads), 2 * sizeof(int64_t) * world, s,
                            static_cast<int32_t*>(nullptr), 0, world, counts, counts_ld, status,
-                           static_cast<const int32_t*>(nullptr));
+                           static_cast<const int32_t*>(nullptr), static_cast<int64_t*>(nullptr));
         TTAMM_LAUNCH_CHECK();
         return TTAMM_OK;
     }
@@ -223,14 +192,19 @@ int launch_route_rows(const int64_t* id0, int64_t n0, const int64_t* id1, int64_
     while ((1 << bits) < world) ++bits;
     int32_t* blk = static_cast<int32_t*>(scratch);
     int32_t* blk0 = counts_ld >= 3 ? blk + (int64_t)nb * world : nullptr;
+    int64_t* grp = nullptr;  // [3 world], 8-B aligned after blk, blk0
+    if (blk0) grp = reinterpret_cast<int64_t*>(align_up(reinterpret_cast<uintptr_t>(blk + 2 * (int64_t)nb * world), 8));
     hipLaunchKernelGGL(route_count_kernel, dim3(nb), dim3(kRouteThreads), 2 * sizeof(int32_t) * world, s, a, blk,
                        blk0);
     TTAMM_LAUNCH_CHECK();
-    hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(kRouteThreads), sizeof(int64_t) * world, s, blk, nb, world,
-                       counts, counts_ld, status, static_cast<const int32_t*>(blk0));
+    hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(kRouteThreads), 2 * sizeof(int64_t) * world, s, blk, nb, world,
+                       counts, counts_ld, status, static_cast<const int32_t*>(blk0), grp);
     TTAMM_LAUNCH_CHECK();
+    // LDS: off [W], wc [waves][W] (int32, padded to 8 B), then grp's copy [3W] (int64)
+    const size_t lds_i32 = (size_t)world * (1 + kRouteWaves + ((1 + kRouteWaves) & 1));
     hipLaunchKernelGGL(route_scatter_kernel, dim3(nb), dim3(kRouteThreads),
-                       sizeof(int32_t) * world * (1 + kRouteWaves), s, a, blk, bits, packed, slot);
+                       sizeof(int32_t) * lds_i32 + (grp ? sizeof(int64_t) * 3 * world : 0), s, a, blk, bits, packed,
+                       slot, static_cast<const int64_t*>(grp));
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

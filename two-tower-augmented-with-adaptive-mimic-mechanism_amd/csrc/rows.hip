@@ -119,9 +119,39 @@ __global__ void gather_rows_scalar(const float* __restrict__ table, int64_t rows
     }
 }
 
-// Index staging of a training step (kernels.h StageArgs); blockIdx.y = segment.
+// Index staging of a training step (kernels.h StageArgs); blockIdx.y = segment, y == count: the
+// owner's compact exchange units (StageArgs::unit_out)
 __global__ void stage_rows_kernel(StageArgs) {
     const KArg(StageArgs)* ka = (const KArg(StageArgs)*)(__builtin_amdgcn_kernarg_segment_ptr());
+    if ((int)blockIdx.y == ka->count) {
+        extern __shared__ int64_t tab[];  // per group: first row, positive rows before, positive rows
+        const int G = ka->unit_groups;
+        if (threadIdx.x == 0) {
+            int64_t r = 0, p = 0;
+            for (int g = 0; g < G; ++g) {
+                const int64_t c = ka->unit_counts[g * ka->unit_ld], q = ka->unit_counts[g * ka->unit_ld + 2];
+                tab[3 * g] = r;
+                tab[3 * g + 1] = p;
+                tab[3 * g + 2] = q;
+                r += c;
+                p += q;
+            }
+        }
+        __syncthreads();
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ka->unit_n;
+             i += (int64_t)gridDim.x * blockDim.x) {
+            int lo = 0, hi = G - 1;  // the last group starting at or before row i (empty groups share starts)
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (tab[3 * mid] <= i) lo = mid;
+                else hi = mid - 1;
+            }
+            const int64_t r = i - tab[3 * lo], p = tab[3 * lo + 2];
+            const int64_t unit = i + tab[3 * lo + 1] + (r < p ? r : p);
+            ka->unit_out[i] = r < p ? unit : ~unit;
+        }
+        return;
+    }
     const KArg(StageSeg)& S = ka->seg[blockIdx.y];
     const int64_t n = S.n, rows = S.rows;
     bool bad = false;
@@ -903,8 +933,13 @@ int launch_stage_rows(const StageArgs& a, hipStream_t s) {
     TTAMM_REQUIRE(a.count >= 0 && a.count <= kMaxStageSegs, "stage_rows: bad arguments");
     int64_t most = 0;
     for (int i = 0; i < a.count; ++i) most = a.seg[i].n > most ? a.seg[i].n : most;
+    const bool units = a.unit_out != nullptr && a.unit_n > 0;
+    TTAMM_REQUIRE(!units || (a.unit_counts && a.unit_ld >= 3 && a.unit_groups >= 1 && a.unit_groups <= 1024),
+                  "stage_rows: bad unit-map arguments");
+    if (units) most = a.unit_n > most ? a.unit_n : most;
     if (most == 0) return TTAMM_OK;
-    hipLaunchKernelGGL(stage_rows_kernel, dim3(grid_for(most), a.count), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(stage_rows_kernel, dim3(grid_for(most), a.count + (units ? 1 : 0)), dim3(256),
+                       units ? 3 * sizeof(int64_t) * a.unit_groups : 0, s, a);
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }

@@ -97,9 +97,8 @@ struct StepWs {
     float* partials = nullptr;
     uint32_t* prologue_done = nullptr;  // completion counter of step_prologue_kernel (zero between calls)
     int64_t* keys_own = nullptr;        // sharded owner: staged request keys [item_rows_capacity]
-    // compact exchange rows (ttamm_step_args.exchange_counts), formed by ITEM_FWD: the first unit
-    // of each request (requester, [B (1 + N)]) and of each owned row (owner, ~unit for a negative)
-    int64_t* req_units = nullptr;
+    // compact exchange rows (ttamm_step_args.exchange_counts): the first unit of each owned row
+    // (~unit for a negative), formed with the ITEM_FWD staging
     int64_t* own_units = nullptr;
     int score_blocks = 0;
     // in-batch negatives (ttamm_step_args.in_batch)
@@ -377,7 +376,6 @@ int plan(Arena& ar, const ttamm_step_args& A, StepWs& ws) {
         tower(A.item, ws.item, A.item_rows_capacity, true, 0);
         ws.keys_own = ar.take<int64_t>(A.item_rows_capacity);
         ws.own_units = ar.take<int64_t>(A.item_rows_capacity);
-        ws.req_units = ar.take<int64_t>(B * (1 + N));
     }
     else
         tower(A.item, ws.item, B * (1 + N), false, B);
@@ -1562,7 +1560,7 @@ CalArgs& bind_cal(const ttamm_step_args& A, StepWs& ws, const TowerWs& I, int64_
         c.slot = A.item_slot;
         if (compact_exchange(A)) {  // units of D floats; a negative's row is t + a already
             c.ld_x = D;
-            c.slot = ws.req_units;
+            c.slot = A.item_slot;  // units (ttamm_route_rows with counts_ld >= 3)
             c.xa_rows = B;
         }
         c.idx = A.b.pos_items;
@@ -1655,8 +1653,7 @@ int validate_step(const ttamm_step_args& A) {
                       "compact exchange rows (exchange_counts) need mimic on and a gated item tower");
         TTAMM_REQUIRE(A.exchange_world >= 1 && A.exchange_world <= 1024 && A.exchange_counts_ld >= 3,
                       "exchange_counts needs exchange_world in [1, 1024] and exchange_counts_ld >= 3");
-        TTAMM_REQUIRE(!(ph & TTAMM_PHASE_ITEM_FWD) || A.b.batch * (1 + A.b.num_neg) == 0 || A.item_slot,
-                      "compact exchange rows need item_slot");
+        TTAMM_REQUIRE(A.item_slot, "compact exchange rows need item_slot (the requests' units)");
     }
     if ((ph & (TTAMM_PHASE_ITEM_FWD | TTAMM_PHASE_ITEM_BWD)) && A.n_item_rows > 0)
         TTAMM_REQUIRE(A.item_rows && A.item_row_keys, "item_rows / item_row_keys missing");
@@ -1812,16 +1809,6 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         pa.c = ad;
         if ((rc = launch_step_prologue(st, pa, s))) return rc;
     }
-    if (compact_exchange(A) && (ph & TTAMM_PHASE_ITEM_FWD)) {
-        // the units of this rank's requests (owner-grouped by item_slot, [positives | negatives] per
-        // owner) and of the rows it owns (requester-grouped as they arrived, likewise split)
-        const int64_t ld = A.exchange_counts_ld;
-        const int Wd = A.exchange_world;
-        if ((rc = launch_exchange_units(A.exchange_counts, ld, Wd, A.item_slot, B * (1 + N), 0, ws.req_units, s)))
-            return rc;
-        if ((rc = launch_exchange_units(A.exchange_counts + (int64_t)Wd * ld, ld, Wd, nullptr, I.R, 1, ws.own_units, s)))
-            return rc;
-    }
     if (shard && (ph & TTAMM_PHASE_ITEM_FWD) && I.R > 0) {
         // owner: stage the requested local rows (range-checked) and their keys, contiguous
         StageArgs st;
@@ -1829,6 +1816,13 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         st.status = A.status;
         st.seg[st.count++] = StageSeg{A.item_rows, I.idx_own, I.R, A.item.id.rows, A.item_rows_ld};
         st.seg[st.count++] = StageSeg{A.item_row_keys, ws.keys_own, I.R, INT64_MAX, A.item_rows_ld};
+        if (compact_exchange(A)) {  // ... and their exchange units (requester groups as they arrived)
+            st.unit_counts = A.exchange_counts + (int64_t)A.exchange_world * A.exchange_counts_ld;
+            st.unit_ld = A.exchange_counts_ld;
+            st.unit_groups = A.exchange_world;
+            st.unit_n = I.R;
+            st.unit_out = ws.own_units;
+        }
         if ((rc = launch_stage_rows(st, s))) return rc;
     }
     // ---- forward ----------------------------------------------------------------------------
@@ -1866,7 +1860,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         TTAMM_REQUIRE(A.item_fwd_in && A.inbatch_local, "INBATCH_SRC needs item_fwd_in and inbatch_local");
         const bool cx = compact_exchange(A);  // positives keep (t | a) in either layout
         if ((rc = launch_add_rows(A.item_fwd_in, cx ? D : 2 * D, mimic ? A.item_fwd_in + D : nullptr, cx ? D : 2 * D,
-                                  B, D, A.inbatch_local, D, s, cx ? ws.req_units : A.item_slot)))
+                                  B, D, A.inbatch_local, D, s, A.item_slot)))
             return rc;
     }
     if (ws.ib_on && (ph & (shard ? TTAMM_PHASE_INBATCH : TTAMM_PHASE_USER))) {
@@ -1930,7 +1924,6 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
                 sa.ld_item = sa.ld_dti = D;
                 sa.dA_all = 0;
                 sa.neg_aug = 1;
-                sa.item_slot = ws.req_units;
             }
         } else {
             sa.item_aug = I.aug;

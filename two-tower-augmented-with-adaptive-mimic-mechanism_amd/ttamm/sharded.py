@@ -526,8 +526,10 @@ class ShardedTrainStep(FusedTrainStep):
         self.bwd_out = torch.empty((R, 2 * D), dtype=torch.float32, device=self.device)
         # compact exchange rows (ttamm.h ttamm_step_args.exchange_counts): a negative request moves D
         # floats each way instead of 2 D (t + a forward, dT backward); TTAMM_WIDE_EXCHANGE=1 keeps the
-        # 2 D-wide rows.  The buffers above stay sized for the wide rows (the compact ones fit).
-        self.compact = (bool(self.lib.ttamm_exchange_compact_supported(ctypes.byref(args)))
+        # 2 D-wide rows.  The buffers above stay sized for the wide rows (the compact ones fit).  Without
+        # sampled negatives (in-batch only, num_neg = 0) every request is a positive and the layouts
+        # move the same bytes: the wide one is kept (no unit maps).
+        self.compact = (self.num_neg > 0 and bool(self.lib.ttamm_exchange_compact_supported(ctypes.byref(args)))
                         and os.environ.get("TTAMM_WIDE_EXCHANGE") != "1")
         self.count_ld = 3 if self.compact else 2
         self.exchange_floats = [0, 0]  # this rank's last (t | a) send, (dT | dA) send, in floats
