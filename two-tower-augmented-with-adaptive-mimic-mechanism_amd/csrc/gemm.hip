@@ -670,7 +670,7 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmBatch batch) {
 //                     two ds_read_b64_tr_b16 (hardware transpose: lane i of a 16-lane group gets
 //                     column i of a 4 x 16 block), conflict-free per 32-lane half.
 template <int BM_, int BN_, int WAVES_M_, int WAVES_N_, bool A_KMAJ_, bool B_KMAJ_, int KT_ = 16, int AD_ = 2,
-          bool APL_ = false>
+          bool APL_ = false, bool A16_ = false>
 struct XCfg {
     static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_;
     static constexpr bool A_KMAJ = A_KMAJ_, B_KMAJ = B_KMAJ_;
@@ -679,12 +679,16 @@ struct XCfg {
     // A pre-split in memory (GemmProblem::A3p: [row][k / 16][hi, mid, lo][16] bf16, the feature rows
     // split once): staged as 16-B pieces of the three planes, no split arithmetic in the loop
     static constexpr bool APL = APL_;
+    // A16: K-major A already bf16 in memory (GemmProblem::A16 / lda16, rows gathered by a_idx; the bf16
+    // towers' feature copy): 16-B pieces of 8 columns straight into the plane, no conversion
+    static constexpr bool A16 = A16_;
+    static_assert(!A16 || (A_KMAJ_ && KT_ == 32 && !APL_), "bf16 A: K-major, one plane (32-k tiles)");
     static constexpr int RB = KT * 2;  // MN-major row bytes
     static constexpr int TM = BM / WAVES_M, TN = BN / WAVES_N, I = TM / 32, J = TN / 32;
     // blocks per CU the register budget is planned for: wave tiles of 8 or more accumulator tiles
     // (128 registers and up) run one wave per SIMD with the whole register file
     static constexpr int MINB = I * J >= 8 ? 1 : 2;
-    static constexpr int A_F4 = APL ? BM * KT * 6 / 16 : BM * KT / 4, B_F4 = BN * KT / 4;
+    static constexpr int A_F4 = APL ? BM * KT * 6 / 16 : (A16 ? BM * KT / 8 : BM * KT / 4), B_F4 = BN * KT / 4;
     static_assert(!APL || KT == 16, "A planes: 16-k tiles (one 96-byte chunk per row and k-tile)");
     static constexpr int A_LOADS = (A_F4 + kThreads - 1) / kThreads;
     static constexpr int B_LOADS = (B_F4 + kThreads - 1) / kThreads;
@@ -841,6 +845,11 @@ __global__ __launch_bounds__(kThreads, CX::MINB) void gemm_x_kernel(GemmBatch ba
                 ap_lds[it] = pl * CX::A_PLANE + a_r[it] * CX::SA + (ch * 16 + hf * 8) * 2;
             }
             a_rp[it] = nullptr;
+        } else if constexpr (CX::A16) {  // k row lin / (BM / 8), columns 8 (lin % (BM / 8)) .. + 7
+            a_r[it] = lin / (BM / 8);
+            a_c[it] = (lin % (BM / 8)) * 8;
+            a_ok[it] = m0 + a_c[it] < P.a_cols;  // the copy is zero from a_cols to its row end
+            a_rp[it] = nullptr;
         } else if (!AK) {
             a_r[it] = lin / (KT / 4);
             a_c[it] = (lin % (KT / 4)) * 4;
@@ -914,6 +923,12 @@ __global__ __launch_bounds__(kThreads, CX::MINB) void gemm_x_kernel(GemmBatch ba
                     }
                     continue;
                 }
+                if constexpr (CX::A16) {
+                    const int k = FAST ? k0 + a_r[it] : min(k0 + a_r[it], k_end - 1);
+                    const uint16_t* rp = P.A16 + kidx[k - k_begin] * P.lda16 + m0 + a_c[it];
+                    ra[R][it] = (FAST || a_ok[it]) ? *reinterpret_cast<const float4*>(rp) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    continue;
+                }
                 if (!AK) {
                     ra[R][it] = FAST ? *reinterpret_cast<const float4*>(a_rp[it] + k0 + a_c[it])
                                      : raw4(a_rp[it], k0 + a_c[it], P.lda);
@@ -968,6 +983,13 @@ __global__ __launch_bounds__(kThreads, CX::MINB) void gemm_x_kernel(GemmBatch ba
                     const float4 r = ra[RA][it];
                     const float4 v = make_float4(ok ? r.x : 0.f, ok ? r.y : 0.f, ok ? r.z : 0.f, ok ? r.w : 0.f);
                     *reinterpret_cast<float4*>(Ap2 + ap_lds[it]) = v;
+                    return;
+                }
+                if constexpr (CX::A16) {  // eight bf16 columns of k row a_r (zero past the split's rows)
+                    const bool ok = FAST || k0 + a_r[it] < k_end;
+                    const float4 r = ra[RA][it];
+                    const float4 v = make_float4(ok ? r.x : 0.f, ok ? r.y : 0.f, ok ? r.z : 0.f, ok ? r.w : 0.f);
+                    *reinterpret_cast<float4*>(Ap + a_r[it] * CX::SA + a_c[it] * 2) = v;
                     return;
                 }
                 if (!AK) {
@@ -1741,6 +1763,9 @@ using Wgrad128X32 = XCfg<128, 128, 2, 2, true, true, 32>;
 // per fragment + the staging writes), so the LDS, not the MFMA, set its pace (C5,
 // profiles/r05_s21_c5_gemm_sq.txt); 256 x 256 (16 per wave) spilled 444 B per thread
 using Wgrad256X32 = XCfg<256, 128, 2, 2, true, true, 32>;
+// bf16 X read from the towers' bf16 feature copy (WgradProblem::X16)
+using Wgrad128X32A16 = XCfg<128, 128, 2, 2, true, true, 32, 2, false, true>;
+using WgradWideX32A16 = XCfg<128, 192, 2, 2, true, true, 32, 2, false, true>;
 // X pre-split into planes (the first feature layer's weight gradient, fp32 towers)
 using WgradNarrowXP = XCfg<128, 96, 4, 1, true, true, 16, 2, true>;
 using WgradWideXP = XCfg<128, 192, 2, 2, true, true, 16, 2, true>;
@@ -1844,7 +1869,7 @@ static bool wgrad_a3() {
 int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
     // one launch per tile configuration: class 0 (128 x 96), 1 (128 x 192), 2 and 3 (128 x 128; a
     // 128 x 256 bf16 tile spilled 132 B of scratch per thread)
-    GemmBatch g[kWgradClasses], gp[kWgradClasses];  // gp: X pre-split into planes
+    GemmBatch g[kWgradClasses], gp[kWgradClasses];  // gp: X pre-split into planes, or (bf16) X in bf16
     std::memset(g, 0, sizeof(g));
     std::memset(gp, 0, sizeof(gp));
     const bool bf = wb.count > 0 && wb.p[0].bf16;
@@ -1860,7 +1885,10 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
     auto flush = [&](GemmBatch& b, int cfg, bool planes = false) -> int {
         if (b.count == 0) return TTAMM_OK;
         int rc;
-        if (planes) {
+        if (planes && bf) {  // X16 (cfg 1 / 2 only)
+            rc = cfg == 1 ? launch_one_x<WgradWideX32A16, EPI_STORE, 1>(b, s)
+                          : launch_one_x<Wgrad128X32A16, EPI_STORE, 1>(b, s);
+        } else if (planes) {
             rc = cfg == 0   ? launch_one_x<WgradNarrowXP, EPI_STORE, 3>(b, s)
                  : cfg == 1 ? launch_one_x<WgradWideXP, EPI_STORE, 3>(b, s)
                             : launch_one_x<Wgrad128XP, EPI_STORE, 3>(b, s);
@@ -1921,11 +1949,17 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
         p.inv_keep = 1.f;
         p.bf16 = w.bf16;
         const int cfg = cfg_of(wgrad_class(w.M));
-        const bool planes = w.X3p != nullptr && !exact && !bf && w.ld_x3 % 8 == 0 && (uintptr_t)w.X3p % 16 == 0 &&
-                            w.ld_x3 >= 48 * ceil_div(w.N, 16);
+        bool planes = w.X3p != nullptr && !exact && !bf && w.ld_x3 % 8 == 0 && (uintptr_t)w.X3p % 16 == 0 &&
+                      w.ld_x3 >= 48 * ceil_div(w.N, 16);
         if (planes) {
             p.A3p = w.X3p;
             p.lda3 = w.ld_x3;
+        }
+        if (bf && w.X16 && (cfg == 1 || cfg == 2) && w.ld_x16 % 8 == 0 && w.ld_x16 >= 8 * ceil_div(w.N, 8) &&
+            (uintptr_t)w.X16 % 16 == 0) {
+            planes = true;  // (the gp group: X from its bf16 copy)
+            p.A16 = w.X16;
+            p.lda16 = w.ld_x16;
         }
         GemmBatch& gb = planes ? gp[cfg] : g[cfg];
         if (gb.count == kMaxGemmProblems) {

@@ -75,6 +75,9 @@ struct GemmProblem {
     // (multiples of 8), K a multiple of 8.  Same epilogues as the fp32 kernel.
     const uint16_t* A16;
     const uint16_t* B16;
+    // weight gradients of bf16 towers (split kernel, K-major A, XCfg::A16): A16 = the bf16 copy of X,
+    // rows gathered by a_idx, lda16 elements per row (% 8 == 0, zero from a_cols on)
+    int64_t lda16;
     // A pre-split into bf16 planes (split kernel, fp32 towers): row r's k-tile t (16 k) is the 96 B
     // at A3p + r * lda3 + 48 t: hi[16], mid[16], lo[16] with hi + mid + lo == the fp32 value; A keeps
     // pointing at the fp32 rows (the exact-MFMA path reads those).  lda3 in uint16 elements.
@@ -125,6 +128,8 @@ struct WgradProblem {
     int64_t ld_x;
     const uint16_t* X3p;   // X pre-split into bf16 planes (GemmProblem::A3p layout) or null
     int64_t ld_x3;
+    const uint16_t* X16;   // bf16 problems: X already rounded to bf16 (ld_x16 elements, % 8) or null
+    int64_t ld_x16;
     int R, M, N;           // rows, out features, in features
     float* grad_w;         // [M, N]
     float* grad_b;         // [M] (may be null)

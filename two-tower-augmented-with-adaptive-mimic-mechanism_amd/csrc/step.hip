@@ -814,6 +814,12 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
     return TTAMM_OK;
 }
 
+// TTAMM_WGRAD_X16=1: the bf16 towers' first-layer weight gradient reads X from the bf16 feature copy
+bool wgrad_x16() {
+    const char* e = std::getenv("TTAMM_WGRAD_X16");
+    return e && e[0] == '1';
+}
+
 // ---- backward ------------------------------------------------------------------------------
 // wg_events (optional, 2 events): around the wide weight-gradient GEMM launch (bench)
 // part BWD_GATE: the fusion's backward (dEF, the ID rows' gradient with it); BWD_MLP: the feature
@@ -1008,6 +1014,10 @@ int tower_backward(const ttamm_tower* T[2], TowerWs* W[2], int D, hipStream_t s,
                 p.X = t.features;
                 p.x_idx = w.fidx;
                 p.ld_x = t.feat_ld;
+                if (uses_w16(t) && wgrad_x16()) {  // the same bf16 values, from the tower's bf16 copy
+                    p.X16 = t.features_bf16;
+                    p.ld_x16 = t.feat_bf16_ld;
+                }
                 if (t.features_planes && !t.matmul_bf16) {
                     p.X3p = t.features_planes;
                     p.ld_x3 = t.feat_planes_ld;
