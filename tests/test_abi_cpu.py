@@ -138,3 +138,34 @@ def test_inbatch_bce_rejects_row_base_outside_the_columns(row_base):
                                ctypes.cast(ws, ctypes.c_void_p), 16, None)
     assert rc != 0
     assert b"row_base" in lib.ttamm_last_error()
+
+
+@pytest.mark.parametrize("case,want", [
+    ("fp32-d96", 1), ("fp32-d32", 1), ("fp32-d8-generic", 0), ("no-mimic", 0), ("bf16-d128", 1),
+    ("bf16-d64", 0), ("user-hg-differs", 0), ("item-sum-fusion", 0),
+])
+def test_exchange_compact_supported_is_host_logic(case, want):
+    """ttamm_exchange_compact_supported (host only, no device call): compact exchange rows need
+    mimic, a gated item tower, and the fused gate kernels for it alone and grouped with the user
+    tower — gate.hip at D = Hg in {32, 64, 96, 128} (fp32), gate16.hip at D = Hg in {128, 256}
+    (bf16); anything else keeps the 2D-wide rows."""
+    from ttamm import _lib
+
+    lib = _lib.load()
+    a = _lib.StepArgs()
+    D = {"fp32-d32": 32, "fp32-d8-generic": 8, "bf16-d128": 128, "bf16-d64": 64}.get(case, 96)
+    bf = 1 if case.startswith("bf16") else 0
+    for t in (a.user, a.item):
+        t.id.dim = D
+        t.fusion = 2  # TTAMM_FUSION_GATED
+        t.gate[0].out_features = D
+        t.gate[0].in_features = 2 * D
+        t.gate[1].out_features = D
+        t.gate[1].in_features = D
+        t.matmul_bf16 = bf
+    a.mimic_enabled = 0 if case == "no-mimic" else 1
+    if case == "user-hg-differs":
+        a.user.gate[0].out_features = 64
+    if case == "item-sum-fusion":
+        a.item.fusion = 1  # TTAMM_FUSION_SUM
+    assert lib.ttamm_exchange_compact_supported(ctypes.byref(a)) == want
