@@ -1975,14 +1975,24 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
                 if ((rc = launch_category_alignment(c, s))) return rc;
             }
         }
-        if (A.loss_out) {
-            if ((rc = launch_loss_finalize(ws.partials, ws.score_blocks, ws.ib_on ? ws.ib.loss_part : nullptr,
-                                           ws.ib_on ? ws.ib_parts : 0, bce_count, B, Bg, D, sa.lambda_u, sa.lambda_i,
-                                           sa.mimic, ws.cal_on && A.row_base == 0 ? ws.cal.out : nullptr,
-                                           (float)A.hp.lambda_category_alignment, A.loss_out, A.loss_accum, A.status,
-                                           s)))
-                return rc;
-        }
+        auto finalize = [&](hipStream_t st) {
+            return A.loss_out ? launch_loss_finalize(ws.partials, ws.score_blocks, ws.ib_on ? ws.ib.loss_part : nullptr,
+                                                     ws.ib_on ? ws.ib_parts : 0, bce_count, B, Bg, D, sa.lambda_u,
+                                                     sa.lambda_i, sa.mimic,
+                                                     ws.cal_on && A.row_base == 0 ? ws.cal.out : nullptr,
+                                                     (float)A.hp.lambda_category_alignment, A.loss_out, A.loss_accum,
+                                                     A.status, st)
+                              : TTAMM_OK;
+        };
+        // one process with the touched-row updates on the aux stream: the loss reduction (nothing in
+        // the backward reads it) goes there too, ahead of them, instead of between the scores and the
+        // fusion backward on the main stream.  TTAMM_ROWS_MAIN=1 / TTAMM_FINALIZE_MAIN=1: main stream.
+        static const bool rows_main = std::getenv("TTAMM_ROWS_MAIN") != nullptr;
+        static const bool fin_main = std::getenv("TTAMM_FINALIZE_MAIN") != nullptr;
+        const bool rows_aux = !shard && !ws.clip_on && !rows_main && aux != nullptr && aux != s &&
+                              overlapped(T, 2, df, s, aux);
+        const bool fin_aux = rows_aux && !fin_main;
+        if (!fin_aux && (rc = finalize(s))) return rc;
         if (!shard) {
             // ---- the whole backward + optimizers in one process --------------------------------
             // With the aux stream (no clipping: the table updates would wait for the global norm)
@@ -1990,8 +2000,6 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
             // mimic rows' gradients, beside the MLP's dgrad chain and weight gradients (memory-
             // bound row traffic under MFMA-bound GEMMs); the step's end joins them, so the next
             // step's ID-row gather reads the updated rows.  TTAMM_ROWS_MAIN=1: on the main stream.
-            static const bool rows_main = std::getenv("TTAMM_ROWS_MAIN") != nullptr;
-            const bool rows_aux = !ws.clip_on && !rows_main && aux != nullptr && aux != s && overlapped(T, 2, df, s, aux);
             if (!rows_aux) {
                 if ((rc = tower_backward(T, W, D, s, 2, A.timing_events + 6))) return rc;
                 if (ws.clip_on && (rc = clip_coefficient(T, W, D, mimic, sp, ad, df, A, ws, s, aux))) return rc;
@@ -2004,6 +2012,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
             if ((rc = tower_backward(T, W, D, s, 2, nullptr, BWD_GATE))) return rc;
             TTAMM_HIP(hipEventRecord(ev[4], s));
             TTAMM_HIP(hipStreamWaitEvent(aux, ev[4], 0));
+            if (fin_aux && (rc = finalize(aux))) return rc;
             // on the aux stream: the grouping before it there already, so no join
             if ((rc = table_updates(T, W, 2, D, mimic, sp, ad, df, A.timing_events, aux, aux))) return rc;
             TTAMM_HIP(hipEventRecord(ev[5], aux));
