@@ -413,6 +413,9 @@ __device__ __forceinline__ const float* dA_row(const RowUpdateArgs& A, int64_t r
     return (r < A.split_row ? A.dA_lo : A.dA_hi) + r * A.ld_dA;
 }
 
+// SDA: each position's dA row resolved once into LDS (compact exchange unit maps: their dependent
+// load); otherwise per column from its row (TTAMM_PIECE_SDA=1 forces SDA)
+template <bool SDA>
 __global__ __launch_bounds__(64 * kRowWaves) void piece_sum_kernel(RowUpdateArgs A) {
     __shared__ int64_t srows[kRowWaves][kPiece];
     __shared__ const float* sda[kRowWaves][kPiece];  // each position's dA row (resolved once: GateTower::xu)
@@ -436,7 +439,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void piece_sum_kernel(RowUpdateArgs
     const bool mimic = A.mimic.weight != nullptr;
     if (lane < kPiece) {  // read back uniformly inside the d loop
         srows[w][lane] = my_row;
-        sda[w][lane] = mimic && lane < cnt ? dA_row(A, my_row) : nullptr;
+        if (SDA) sda[w][lane] = mimic && lane < cnt ? dA_row(A, my_row) : nullptr;
     }
     __builtin_amdgcn_wave_barrier();
     const int D = A.dim;
@@ -447,7 +450,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void piece_sum_kernel(RowUpdateArgs
         for (int p = 0; p < kPiece; ++p) {  // issue every load of the chunk before adding
             const int64_t r = srows[w][p];
             ve[p] = (idt && p < cnt) ? A.dE[r * A.ld_dE + d] : 0.f;
-            va[p] = (mimic && p < cnt) ? sda[w][p][d] : 0.f;
+            va[p] = (mimic && p < cnt) ? (SDA ? sda[w][p][d] : dA_row(A, r)[d]) : 0.f;
         }
         float ge = 0.f, ga = 0.f;
         int start = 0;
@@ -1392,7 +1395,13 @@ int launch_row_update(const RowUpdateArgs& args, hipStream_t s) {
                   "row update: dim and gradient leading dims must be multiples of 4");
     a.lanes_per_row = 1;
     while (a.lanes_per_row < a.dim / 4 && a.lanes_per_row < 64) a.lanes_per_row *= 2;
-    hipLaunchKernelGGL(piece_sum_kernel, dim3((unsigned)ceil_div(ceil_div(a.n, kPiece), kRowWaves)),
+    // per-column dA rows unless the unit maps are on (their dependent load): the LDS-resolved form
+    // cost the one-process C2 step 7 us (0.6616 vs 0.6545 ms, profiles/r05_s42_piece_sum.txt)
+    static const bool sda_env = [] { const char* e = std::getenv("TTAMM_PIECE_SDA"); return e && e[0] == '1'; }();
+    const bool sda = sda_env || a.xu != nullptr;
+    if (sda) hipLaunchKernelGGL(piece_sum_kernel<true>, dim3((unsigned)ceil_div(ceil_div(a.n, kPiece), kRowWaves)),
+                       dim3(64 * kRowWaves), 0, s, a);
+    else hipLaunchKernelGGL(piece_sum_kernel<false>, dim3((unsigned)ceil_div(ceil_div(a.n, kPiece), kRowWaves)),
                        dim3(64 * kRowWaves), 0, s, a);
     TTAMM_LAUNCH_CHECK();
     const int64_t rows_per_block = (int64_t)kRowWaves * (64 / a.lanes_per_row);
