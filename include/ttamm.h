@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define TTAMM_ABI_VERSION 24
+#define TTAMM_ABI_VERSION 25
 
 #define TTAMM_OK 0
 #define TTAMM_E_INVALID 1 /* bad shape / config / dtype  -> ValueError   */
@@ -386,6 +386,10 @@ typedef struct ttamm_step_args {
 
 int ttamm_abi_version(void);
 const char* ttamm_last_error(void);
+/* 1 for a developer build (make DEV=1), which also honours the A/B, ablation and measured-slower
+ * environment switches; 0 for the default library, which reads only the documented knobs
+ * (INTEGRATION.md "Environment").  No reference counterpart (build introspection for tests). */
+int ttamm_developer_build(void);
 
 /* Replaces one iteration of `_train_one_epoch` (training.py:726-831): negative sampling,
  * both tower forwards, mimic augmentation + losses, dot-product scoring, BCE, backward,

@@ -169,3 +169,33 @@ def test_exchange_compact_supported_is_host_logic(case, want):
     if case == "item-sum-fusion":
         a.item.fusion = 1  # TTAMM_FUSION_SUM
     assert lib.ttamm_exchange_compact_supported(ctypes.byref(a)) == want
+
+
+# The documented environment knobs (INTEGRATION.md "Environment"); every other TTAMM_* switch in
+# the sources is a developer A/B / ablation / measured-slower variant read only by a `make DEV=1`
+# library (csrc/common.h dev_env).  TTAMM_DENSE_* / TTAMM_G0_* are enum names in error messages.
+DOCUMENTED_ENV = {"TTAMM_FP32_MFMA", "TTAMM_RETRIEVAL_FP32", "TTAMM_GENERIC_GATE"}
+ENUM_NAMES = {"TTAMM_DENSE_ADAM", "TTAMM_DENSE_SGD", "TTAMM_G0_EXACT", "TTAMM_G0_FAST"}
+DEV_SWITCHES = ("TTAMM_GATE_ABLATE", "TTAMM_RETRIEVAL_ABLATE", "TTAMM_BF16_WGRAD256", "TTAMM_PROLOGUE_PREP",
+                "TTAMM_SLICE_LATE", "TTAMM_GATE16_SPLIT", "TTAMM_WGRAD_ROWS_PER_SPLIT", "TTAMM_FEATURE_PLANES")
+
+
+def test_default_library_reads_only_documented_env_knobs():
+    """the default build names no developer switch at all — the getenv calls
+    behind them are compiled out (dev_env returns nullptr), so a stray ablation variable in a
+    user's environment cannot change what the drop-in library computes."""
+    from ttamm import _lib
+
+    lib = _lib.load()
+    assert lib.ttamm_developer_build() == 0
+    blob = _lib.library_path().read_bytes()
+    names = {m.decode() for m in re.findall(rb"TTAMM_[A-Z0-9_]+", blob)}
+    assert names - ENUM_NAMES <= DOCUMENTED_ENV, sorted(names - ENUM_NAMES - DOCUMENTED_ENV)
+    for name in DEV_SWITCHES:
+        assert name not in names
+    # the Python host reads only TTAMM_WIDE_EXCHANGE (documented) and TTAMM_LIBRARY (the loader)
+    pkg = ROOT / "two-tower-augmented-with-adaptive-mimic-mechanism_amd" / "ttamm"
+    env_reads = set()
+    for f in pkg.glob("*.py"):
+        env_reads |= set(re.findall(r"os\.environ(?:\.get)?\(?\[?\"(TTAMM_[A-Z0-9_]+)", f.read_text()))
+    assert env_reads <= {"TTAMM_WIDE_EXCHANGE", "TTAMM_LIBRARY"}, env_reads

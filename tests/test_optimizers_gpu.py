@@ -123,3 +123,35 @@ def test_sgd_deferred_creates_momentum_buffers():
                                                                     "item": [x.cuda() for x in im]})
     assert opts[0].state[tm.adaptive_mimic.item_augmented.weight]["momentum_buffer"].shape == (prob.shape.I, 8)
     eng.finish()
+
+
+@pytest.mark.parametrize("m0,m1", [(0.9, 0.0), (0.0, 0.9)], ids=["momentum-off", "momentum-on"])
+def test_sgd_momentum_switch_between_zero_and_nonzero_rejected(m0, m1):
+    """what the kernels' moment slots alias (momentum buffer or parameter) and whether
+    g = 0 table rows are deferred are fixed when the step is built, so a later switch of SGD
+    momentum between zero and non-zero raises ValueError before any state is written (torch would
+    leave the buffers alone; the replay would overwrite them)."""
+    import ttamm
+    from gpu_helpers import ttamm_model_from, ttamm_optimizers
+    from helpers import LOSS_WEIGHTS
+
+    prob = make_problem(Shape(), steps=2)
+    model = ttamm_model_from(prob)
+    opts = ttamm_optimizers(model, lr=0.5, weight_decay=0.01, optimizer="sgd", momentum=m0)
+    eng = ttamm.FusedTrainStep(model, opts, negatives_per_positive=prob.shape.N, positives=prob.positives,
+                               user_features=prob.user_features.cuda(), item_features=prob.item_features.cuda(),
+                               loss_weights=LOSS_WEIGHTS, max_batch=prob.shape.B)
+    users, pos, neg, um, im = prob.batches[0]
+    kw = dict(keep_masks={"user": [m.cuda() for m in um], "item": [m.cuda() for m in im]})
+    eng.step(users.cuda(), pos.cuda(), neg.cuda().reshape(-1), **kw)
+    before = {k: v.clone() for k, v in model.state_dict().items()}
+    opts[0].param_groups[0]["momentum"] = m1
+    users, pos, neg, um, im = prob.batches[1]
+    with pytest.raises(ValueError, match="momentum"):
+        eng.step(users.cuda(), pos.cuda(), neg.cuda().reshape(-1),
+                 keep_masks={"user": [m.cuda() for m in um], "item": [m.cuda() for m in im]})
+    opts[0].param_groups[0]["momentum"] = m0
+    eng.finish()
+    for k, v in model.state_dict().items():
+        if "augmented" not in k:  # the mimic tables' deferred g = 0 rows move at finish
+            assert torch.equal(v, before[k]), k

@@ -582,3 +582,23 @@ def test_look_ahead_rejects_bad_next_batch_before_any_collective():
     prog = eng.program(u, p, next_batch=(u.to(torch.int32), p))
     with pytest.raises(ValueError, match="next_batch"):
         next(prog)
+
+
+def test_look_ahead_checks_next_batch_after_a_prepared_look_ahead_replaces_row_base():
+    """a step that consumes a prepared look-ahead runs at default positions whatever
+    row_base / global_batch the call passes, so its own look-ahead runs too — and its next_batch
+    must be validated on that effective condition.  An oversized next_batch passed together with
+    row_base raises ValueError before the step's first collective (never a B x N draw into the
+    max_batch x N look-ahead buffers)."""
+    W, shape = 2, Shape()
+    prob, ranks = _ranks_only(shape, W, max_batch=shape.B)
+    steps = _owned_batches(prob, shape, W, 2)
+    run_loopback([eng.program(u, p, next_batch=steps[1][r])
+                  for r, ((_, _, _, eng), (u, p)) in enumerate(zip(ranks, steps[0]))])
+    eng = ranks[0][3]
+    u, p = steps[1][0]
+    big_u = torch.cat([u, u])[: shape.B + 1]
+    big_p = torch.cat([p, p])[: shape.B + 1]
+    prog = eng.program(u, p, row_base=0, next_batch=(big_u, big_p))
+    with pytest.raises(ValueError, match="next_batch"):
+        next(prog)

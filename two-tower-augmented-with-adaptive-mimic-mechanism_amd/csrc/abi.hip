@@ -46,6 +46,8 @@ TTAMM_API int ttamm_abi_version(void) { return TTAMM_ABI_VERSION; }
 
 TTAMM_API const char* ttamm_last_error(void) { return g_last_error.c_str(); }
 
+TTAMM_API int ttamm_developer_build(void) { return kDevKnobs ? 1 : 0; }
+
 TTAMM_API size_t ttamm_train_step_workspace_size(const ttamm_step_args* args) {
     if (!args) return 0;
     return train_step_workspace_size(*args);

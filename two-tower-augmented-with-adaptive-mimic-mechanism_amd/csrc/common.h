@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <cstdlib>
 #include <string>
 
 #include "../../include/ttamm.h"
@@ -41,6 +43,20 @@ int fail(int code, const std::string& msg);
 
 static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 static inline size_t align_up(size_t a, size_t b) { return (a + b - 1) / b * b; }
+
+// ---- environment switches -----------------------------------------------------------------
+// product_env: the documented knobs (INTEGRATION.md "Environment"): TTAMM_FP32_MFMA,
+// TTAMM_RETRIEVAL_FP32, TTAMM_GENERIC_GATE.  dev_env: A/B variants, ablations and measured-slower
+// opt-ins, honoured only by a developer build (make DEV=1 defines TTAMM_DEV_KNOBS); the default
+// library never reads them, so a stray variable cannot change what it computes.
+static inline const char* product_env(const char* name) { return std::getenv(name); }
+#ifdef TTAMM_DEV_KNOBS
+constexpr bool kDevKnobs = true;
+static inline const char* dev_env(const char* name) { return std::getenv(name); }
+#else
+constexpr bool kDevKnobs = false;  // timing ablations inside kernels are compiled out
+static inline const char* dev_env(const char*) { return nullptr; }
+#endif
 
 // ---- workspace bump allocator (host side) -----------------------------------------------
 struct Arena {

@@ -388,14 +388,14 @@ __global__ __launch_bounds__(64 * NW) void gate_fwd_kernel(GateArgs) {
                 const float v = z[ob][r] + c1[r];
                 z[ob][r] = v > 0.f ? v : 0.f;
             }
-            if ((X || ka->direct) && ok && !ka->ablate) stg4(T.z + row * HG + 16 * ob + 4 * q, z[ob]);
+            if ((X || (kDevKnobs && ka->direct)) && ok && !(kDevKnobs && ka->ablate)) stg4(T.z + row * HG + 16 * ob + 4 * q, z[ob]);
         }
-        if (!(X || ka->direct) && !ka->ablate) store_slab<C::TH>(scr, z, T.z, HG, s * 16, R, lane);
+        if (!(X || (kDevKnobs && ka->direct)) && !(kDevKnobs && ka->ablate)) store_slab<C::TH>(scr, z, T.z, HG, s * 16, R, lane);
         f4v x[C::TD];
         zero(x);
         if constexpr (C::GG) tile_gemm_g<C::TD, C::TH, HG>(T.G2, 0, z, x, li, q);  // (pre-sigmoid)^T = G2 . z^T
         else tile_gemm<C::TD, C::TH, C::F_LD2>(g2s, 0, z, x, li, q);
-        if (!(X || ka->direct) && !ka->ablate) {
+        if (!(X || (kDevKnobs && ka->direct)) && !(kDevKnobs && ka->ablate)) {
             // g, then t = g e + (1 - g) f in place, a, then aug = t + a in place: one live array
 #pragma unroll
             for (int ob = 0; ob < C::TD; ++ob) {
@@ -430,7 +430,7 @@ __global__ __launch_bounds__(64 * NW) void gate_fwd_kernel(GateArgs) {
                 if (T.aug) store_slab<C::TD>(scr, x, T.aug, D, s * 16, R, lane);
             }
         }
-        if ((X || ka->direct) && ok && !ka->ablate) {
+        if ((X || (kDevKnobs && ka->direct)) && ok && !(kDevKnobs && ka->ablate)) {
             // compact exchange rows (T.xu): a positive's t and a at its unit, a negative's t + a
             const int64_t xu = xu_li;
             float* tdst = T.xu ? T.t + (xu >= 0 ? xu : ~xu) * D : T.t + row * T.ld_t;
@@ -530,7 +530,7 @@ __global__ __launch_bounds__(64 * NW) void gate_bwd_kernel(GateArgs) {
                             const float dg = d[t][r] * ef[t][r] - d[t][r] * ef[C::TD + t][r];
                             dq[t][r] = dg * (1.0f - g[t][r]) * g[t][r];
                         }
-                    if (!ka->ablate) store_slab<C::TD>(scr, dq, T.dq, D, s * 16, R, lane);
+                    if (!(kDevKnobs && ka->ablate)) store_slab<C::TD>(scr, dq, T.dq, D, s * 16, R, lane);
                     f4v zr[C::TH];
                     load_row(zr, T.z, HG, rr, q);
                     zero(dz);
@@ -539,7 +539,7 @@ __global__ __launch_bounds__(64 * NW) void gate_bwd_kernel(GateArgs) {
                     for (int ob = 0; ob < C::TH; ++ob)
 #pragma unroll
                         for (int r = 0; r < 4; ++r) dz[ob][r] = zr[ob][r] > 0.f ? dz[ob][r] : 0.f;
-                    if (!ka->ablate) store_slab<C::TH>(scr, dz, T.dz, HG, s * 16, R, lane);
+                    if (!(kDevKnobs && ka->ablate)) store_slab<C::TH>(scr, dz, T.dz, HG, s * 16, R, lane);
                 }
             }
             __syncthreads();
@@ -565,7 +565,7 @@ __global__ __launch_bounds__(64 * NW) void gate_bwd_kernel(GateArgs) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r)
                             de[ob][r] += half == 0 ? d[ob][r] * g[ob][r] : d[ob][r] * (1.0f - g[ob][r]);
-                    if (!ka->ablate) store_slab<C::TD>(scr, de, T.dEF + half * D, 2 * D, s * 16, R, lane);
+                    if (!(kDevKnobs && ka->ablate)) store_slab<C::TD>(scr, de, T.dEF + half * D, 2 * D, s * 16, R, lane);
                 }
             }
             __syncthreads();  // the next round's G2^T overwrites G1^T
@@ -622,9 +622,9 @@ __global__ __launch_bounds__(64 * NW) void gate_bwd_kernel(GateArgs) {
                     const float dg = d[t][r] * ef[t][r] - d[t][r] * ef[C::TD + t][r];
                     dq[t][r] = dg * (1.0f - g[t][r]) * g[t][r];
                 }
-                if ((X || ka->direct) && ok && !ka->ablate) stg4(T.dq + row * D + 16 * t + 4 * q, dq[t]);
+                if ((X || (kDevKnobs && ka->direct)) && ok && !(kDevKnobs && ka->ablate)) stg4(T.dq + row * D + 16 * t + 4 * q, dq[t]);
             }
-            if (!(X || ka->direct) && !ka->ablate)
+            if (!(X || (kDevKnobs && ka->direct)) && !(kDevKnobs && ka->ablate))
                 store_slab<C::TD>(scr, dq, T.dq, D, s * 16, R, lane);
             zero(dz);
             tile_gemm<C::TH, C::TD, C::B_LD1>(g2t, 0, dq, dz, li, q);  // dz^T = G2^T . dq^T
@@ -633,9 +633,9 @@ __global__ __launch_bounds__(64 * NW) void gate_bwd_kernel(GateArgs) {
         for (int ob = 0; ob < C::TH; ++ob) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) dz[ob][r] = zr[ob][r] > 0.f ? dz[ob][r] : 0.f;
-            if ((X || ka->direct) && ok && !ka->ablate) stg4(T.dz + row * HG + 16 * ob + 4 * q, dz[ob]);
+            if ((X || (kDevKnobs && ka->direct)) && ok && !(kDevKnobs && ka->ablate)) stg4(T.dz + row * HG + 16 * ob + 4 * q, dz[ob]);
         }
-        if (!(X || ka->direct) && !ka->ablate)
+        if (!(X || (kDevKnobs && ka->direct)) && !(kDevKnobs && ka->ablate))
             store_slab<C::TH>(scr, dz, T.dz, HG, s * 16, R, lane);
         // dEF^T = G1^T . dz^T + [dT g | dT (1 - g)], in two halves (e part, f part)
 #pragma unroll
@@ -649,11 +649,11 @@ __global__ __launch_bounds__(64 * NW) void gate_bwd_kernel(GateArgs) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                     de[ob][r] += half == 0 ? d[ob][r] * g[ob][r] : d[ob][r] * (1.0f - g[ob][r]);
-            if ((X || ka->direct) && ok && !ka->ablate) {
+            if ((X || (kDevKnobs && ka->direct)) && ok && !(kDevKnobs && ka->ablate)) {
 #pragma unroll
                 for (int ob = 0; ob < C::TD; ++ob) stg4(T.dEF + row * 2 * D + half * D + 16 * ob + 4 * q, de[ob]);
             }
-            if (!(X || ka->direct) && !ka->ablate)
+            if (!(X || (kDevKnobs && ka->direct)) && !(kDevKnobs && ka->ablate))
                 store_slab<C::TD>(scr, de, T.dEF + half * D, 2 * D, s * 16, R, lane);
         }
     }
@@ -689,7 +689,7 @@ int launch_gate_nw(GateArgs& a, bool backward, hipStream_t s) {
     // 64 -> 62 us, backward 67 -> 79 us, step 0.726 -> 0.758 ms (profiles/r03_c2_gate_split_s17.txt):
     // the kernels are not MFMA-bound (SQ: ~31 % MFMA busy, profiles/r03_c2_pmc_sq_s13.json) and the
     // split variant runs at the 256-VGPR limit, so both GEMMs stay on v_mfma_f32_16x16x4_f32
-    static const bool split = std::getenv("TTAMM_GATE_SPLIT") != nullptr;
+    static const bool split = dev_env("TTAMM_GATE_SPLIT") != nullptr;
     constexpr bool XOK = GateCfg<D, HG, NW>::X_OK;
     if (XOK && split) {
         if (backward) hipLaunchKernelGGL((gate_bwd_kernel<D, HG, XOK, NW>), dim3(blocks), dim3(64 * NW), 0, s, a);
@@ -709,7 +709,7 @@ int launch_gate_t(GateArgs& a, bool backward, hipStream_t s) {
     // split variant then has room: TTAMM_GATE_SPLIT=1)
     if constexpr (D == 96) {
         static const bool w4 = [] {
-            const char* e = std::getenv("TTAMM_GATE_4W");
+            const char* e = dev_env("TTAMM_GATE_4W");
             return e && e[0] == '1';
         }();
         if (w4) return launch_gate_nw<D, HG, 4>(a, backward, s);
@@ -727,8 +727,8 @@ int launch_gate(GateArgs& a, bool backward, hipStream_t s) {
         if (!a.images_ready && (rc = launch_gate16_prep(a, s))) return rc;
         return launch_gate16(a, backward, s);
     }
-    static const bool ablate = std::getenv("TTAMM_GATE_ABLATE") != nullptr;
-    static const bool direct = std::getenv("TTAMM_GATE_DIRECT_STORES") != nullptr;
+    static const bool ablate = dev_env("TTAMM_GATE_ABLATE") != nullptr;
+    static const bool direct = dev_env("TTAMM_GATE_DIRECT_STORES") != nullptr;
     a.ablate = ablate ? 1 : 0;
     a.direct = direct ? 1 : 0;
     TTAMM_REQUIRE(a.count >= 1 && a.count <= 2 && gate_fused_supported(a.D, a.HG), "fused gate: unsupported shape");

@@ -1559,7 +1559,7 @@ int dispatch_epi_x(GemmBatch& b, hipStream_t s) {
 template <int BM, int BN, int WM, int WN, bool AK, bool BK>
 int dispatch_x(GemmBatch& b, hipStream_t s) {
     static const bool adeep2 = [] {
-        const char* e = std::getenv("TTAMM_GEMM_ADEEP");
+        const char* e = dev_env("TTAMM_GEMM_ADEEP");
         return e && e[0] == '2';
     }();
     if (b.p[0].bf16) return dispatch_epi_x<XCfg<BM, BN, WM, WN, AK, BK, 32>, 1>(b, s);
@@ -1572,7 +1572,7 @@ int dispatch_x(GemmBatch& b, hipStream_t s) {
 // bound launches (dgrad, or few 128-row tiles) take the narrow set, which keeps more blocks.
 int pick_tile_n(const GemmBatch& b, bool narrow, bool bf16) {
     static const bool legacy = [] {
-        const char* e = std::getenv("TTAMM_GEMM_TILES");
+        const char* e = dev_env("TTAMM_GEMM_TILES");
         return e && std::strcmp(e, "legacy") == 0;
     }();
     int maxN = 0;
@@ -1600,7 +1600,7 @@ int pick_tile_n(const GemmBatch& b, bool narrow, bool bf16) {
 // TTAMM_FP32_MFMA=exact the v_mfma_f32_32x32x2_f32 kernel (exact fp32 products; bf16 towers
 // round in registers) — a developer switch, read per launch so tests can compare the two.
 bool exact_mfma() {
-    const char* e = std::getenv("TTAMM_FP32_MFMA");
+    const char* e = product_env("TTAMM_FP32_MFMA");
     return e && std::strcmp(e, "exact") == 0;
 }
 
@@ -1711,7 +1711,7 @@ int launch_gemm(GemmBatch& b, hipStream_t s) {
     for (int i = 0; i < b.count; ++i) wide_tiles += ceil_div(b.p[i].M, 128) * ceil_div(b.p[i].N, 192);
     // dgrad (K-major weights, K = one layer's width: six k-tiles at C2) is latency-bound: twice the
     // blocks on 128 x 96 tiles hide more of it (C2 0.638 -> 0.630-0.635 ms, profiles/r04_dgrad_tiles_s31.txt)
-    const bool narrow_tiles = (wide_tiles < 300 || bkn) && std::getenv("TTAMM_GEMM_WIDE_TILES") == nullptr;
+    const bool narrow_tiles = (wide_tiles < 300 || bkn) && dev_env("TTAMM_GEMM_WIDE_TILES") == nullptr;
     bool planes = b.p[0].A3p != nullptr && !exact_mfma() && !b.p[0].bf16 && !bkn;
     for (int i = 0; i < b.count; ++i) {
         const GemmProblem& p = b.p[i];
@@ -1799,7 +1799,7 @@ constexpr int kWgradTileN[kWgradClasses] = {96, 192, 128, 128};
 // many short splits; wide ones fill the chip with few.
 void wgrad_rows_per_split(const WgradShape* shapes, int n, int rps[kWgradClasses]) {
     // developer / test override (tests/test_step_parity_gpu.py covers splits past 512 rows)
-    if (const char* e = std::getenv("TTAMM_WGRAD_ROWS_PER_SPLIT")) {
+    if (const char* e = dev_env("TTAMM_WGRAD_ROWS_PER_SPLIT")) {
         const int v = std::atoi(e);
         if (v >= BK && v <= kWgradMaxRowsPerSplit && v % BK == 0) {
             for (int c = 0; c < kWgradClasses; ++c) rps[c] = v;
@@ -1840,9 +1840,9 @@ size_t wgrad_slab_floats(int R, int M, int N, int rps) {
 }
 
 int wgrad_class(int m_out) {
-    static const bool all_narrow = std::getenv("TTAMM_WGRAD_ALL_NARROW") != nullptr;
+    static const bool all_narrow = dev_env("TTAMM_WGRAD_ALL_NARROW") != nullptr;
     static const bool legacy = [] {
-        const char* e = std::getenv("TTAMM_GEMM_TILES");
+        const char* e = dev_env("TTAMM_GEMM_TILES");
         return e && std::strcmp(e, "legacy") == 0;
     }();
     if (all_narrow || m_out <= 96) return 0;
@@ -1858,7 +1858,7 @@ int wgrad_class(int m_out) {
 // TTAMM_WGRAD_ADEEP=3: the narrow weight-gradient launch's X operand two k-tiles ahead
 static bool wgrad_a3() {
     static const bool on = [] {
-        const char* e = std::getenv("TTAMM_WGRAD_ADEEP");
+        const char* e = dev_env("TTAMM_WGRAD_ADEEP");
         return e && e[0] == '3';
     }();
     return on;
@@ -1875,7 +1875,7 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
     const bool bf = wb.count > 0 && wb.p[0].bf16;
     const bool exact = exact_mfma();
     // TTAMM_BF16_WGRAD256=1: bf16 weight gradients of the 128-wide classes on 256 x 256 tiles (cfg 3)
-    const char* e256 = std::getenv("TTAMM_BF16_WGRAD256");
+    const char* e256 = dev_env("TTAMM_BF16_WGRAD256");
     const bool w256 = e256 && e256[0] == '1';
     auto cfg_of = [&](int cls) {
         if (exact) return cls == 0 ? 0 : 1;  // the fp32-MFMA kernels: narrow / wide
@@ -1976,7 +1976,7 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
     // which the aux stream's memory-bound row updates then run beside: C2 0.660 -> 0.652 ms,
     // the emulated 8-rank C2 0.804 -> 0.769 ms (profiles/r04_wgrad_order_s22.txt).
     // TTAMM_WGRAD_WIDE_FIRST=1: the old order.
-    static const bool narrow_first = std::getenv("TTAMM_WGRAD_WIDE_FIRST") == nullptr;
+    static const bool narrow_first = dev_env("TTAMM_WGRAD_WIDE_FIRST") == nullptr;
     if (narrow_first && ((rc = flush(g[0], 0)) || (rc = flush(gp[0], 0, true)))) return rc;
     if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)ev[0], s));
     for (int c = 1; c < kWgradClasses; ++c)

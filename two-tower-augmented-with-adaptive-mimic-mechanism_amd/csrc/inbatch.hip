@@ -809,18 +809,18 @@ __global__ void ib_loss_sum_kernel(const float* __restrict__ parts, int n, doubl
 // 3.15 ms at the C4 rank shape, profiles/r04_inbatch_variants.txt); the fp32-MFMA kernel
 // (TTAMM_FP32_MFMA=exact) always uses 4.
 int inbatch_waves() {
-    const char* mf = std::getenv("TTAMM_FP32_MFMA");
+    const char* mf = product_env("TTAMM_FP32_MFMA");
     if (mf && std::strcmp(mf, "exact") == 0) return 4;
-    const char* env = std::getenv("TTAMM_IB_WAVES");
+    const char* env = dev_env("TTAMM_IB_WAVES");
     return (env && std::atoi(env) == 8) ? 8 : 4;
 }
 
 // TTAMM_IB_KERNEL=p: the software-pipelined one-wave-per-SIMD kernel (inbatch_p_kernel), one
 // launch per role
 bool inbatch_pipelined() {
-    const char* mf = std::getenv("TTAMM_FP32_MFMA");
+    const char* mf = product_env("TTAMM_FP32_MFMA");
     if (mf && std::strcmp(mf, "exact") == 0) return false;
-    const char* env = std::getenv("TTAMM_IB_KERNEL");
+    const char* env = dev_env("TTAMM_IB_KERNEL");
     return env && std::strcmp(env, "p") == 0;
 }
 
@@ -833,7 +833,7 @@ void inbatch_plan(int64_t B, int64_t Bc, InBatchArgs& a) {
     // the C4 rank-of-8 shape unchanged, profiles/r04_s43_inbatch_blocks.txt); developer knob
     // TTAMM_IB_BLOCKS = blocks per role
     static const int64_t want_env = [] {
-        const char* e = std::getenv("TTAMM_IB_BLOCKS");
+        const char* e = dev_env("TTAMM_IB_BLOCKS");
         return e ? (int64_t)std::atoi(e) : (int64_t)0;
     }();
     // (the all-gathered columns of a sharded step, Bc > 2B, keep 512: 3.63 vs 3.74 ms per step at
@@ -865,7 +865,7 @@ int launch_inbatch(InBatchArgs& a, hipStream_t s) {
     const unsigned blocks = (unsigned)(a.rblk_u * a.splits_u + a.rblk_p * a.splits_p);
     const int dp = (a.D + 31) / 32 * 32;
     // TTAMM_FP32_MFMA=exact: the v_mfma_f32_32x32x2_f32 kernel (as gemm.hip's developer switch)
-    const char* env = std::getenv("TTAMM_FP32_MFMA");
+    const char* env = product_env("TTAMM_FP32_MFMA");
     if (env && std::strcmp(env, "exact") == 0) {
         switch (dp) {
             case 32: hipLaunchKernelGGL(inbatch_kernel<32>, dim3(blocks), dim3(256), 0, s, a); break;

@@ -706,10 +706,15 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
         // unchanged for every p — so its replay is p *= decay, v *= b2 per step, bit for bit what
         // the full update computes, without the two transcendentals.  Most rows of a large table
         // are cold for many steps (C4: the in-batch positives touch ~8 K of 6.25 M rows a step).
-        uint32_t mbits = 0u;
+        uint32_t mbits = 0u, vbits = 0u;
 #pragma unroll
-        for (int i = 0; i < V; ++i)
+        for (int i = 0; i < V; ++i) {
             mbits |= __float_as_uint(m[i].x) | __float_as_uint(m[i].y) | __float_as_uint(m[i].z) | __float_as_uint(m[i].w);
+            vbits |= __float_as_uint(v[i].x) | __float_as_uint(v[i].y) | __float_as_uint(v[i].z) | __float_as_uint(v[i].w);
+        }
+        // a cold row's m is unchanged (+0.0), and a virgin row's v too (+0.0 * b2 = +0.0): their
+        // stores are skipped (the flush after a short run is mostly such rows: 24 -> 16 B per element)
+        const bool keep_m = DECOUPLED && mbits == 0u, keep_v = keep_m && vbits == 0u;
         if (DECOUPLED && mbits == 0u) {
             for (; hc != hend; ++hc) {
                 const float decay = lo_of(hc->decay), b2 = lo_of(hc->b2);
@@ -768,8 +773,8 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
         for (int i = 0; i < V; ++i) {
             const int64_t oi = o + (int64_t)(4 * per_row) * i;
             *reinterpret_cast<float4*>(S.p + oi) = p[i];
-            *reinterpret_cast<float4*>(S.m + oi) = m[i];
-            *reinterpret_cast<float4*>(S.v + oi) = v[i];
+            if (!keep_m) *reinterpret_cast<float4*>(S.m + oi) = m[i];
+            if (!keep_v) *reinterpret_cast<float4*>(S.v + oi) = v[i];
         }
     }
 }
@@ -1397,7 +1402,7 @@ int launch_row_update(const RowUpdateArgs& args, hipStream_t s) {
     while (a.lanes_per_row < a.dim / 4 && a.lanes_per_row < 64) a.lanes_per_row *= 2;
     // per-column dA rows unless the unit maps are on (their dependent load): the LDS-resolved form
     // cost the one-process C2 step 7 us (0.6616 vs 0.6545 ms, profiles/r05_s42_piece_sum.txt)
-    static const bool sda_env = [] { const char* e = std::getenv("TTAMM_PIECE_SDA"); return e && e[0] == '1'; }();
+    static const bool sda_env = [] { const char* e = dev_env("TTAMM_PIECE_SDA"); return e && e[0] == '1'; }();
     const bool sda = sda_env || a.xu != nullptr;
     if (sda) hipLaunchKernelGGL(piece_sum_kernel<true>, dim3((unsigned)ceil_div(ceil_div(a.n, kPiece), kRowWaves)),
                        dim3(64 * kRowWaves), 0, s, a);
@@ -1439,7 +1444,7 @@ static void launch_replay_v(const ReplayArgs& a, dim3 grid, size_t lds, hipStrea
     // TTAMM_REPLAY_SCALAR=1: constants in scalar registers (replay_s_kernel); default: the
     // history ring staged in LDS per block (replay_kernel)
     static const bool scalar = [] {
-        const char* e = getenv("TTAMM_REPLAY_SCALAR");
+        const char* e = dev_env("TTAMM_REPLAY_SCALAR");
         return e && e[0] == '1';
     }();
     if (a.sgd) {

@@ -243,7 +243,7 @@ __global__ __launch_bounds__(256) void retrieval_partial_kernel(RetrievalArgs A)
     }
     for (int64_t t0 = i_begin; t0 < i_end; t0 += IT) {
         __syncthreads();  // tile t0 is in LDS; thresholds and counts are current
-        if (t0 + IT < i_end && !(A.ablate & 4)) load_tile(t0 + IT);
+        if (t0 + IT < i_end && !(kDevKnobs && (A.ablate & 4))) load_tile(t0 + IT);
         const float my_tau = tau[myq];
         f32x16 acc[MT];
 #pragma unroll
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(kXThreads) void retrieval_x_kernel(RetrievalArgs A)
     }
     for (int64_t t0 = i_begin; t0 < i_end; t0 += IT) {
         __syncthreads();  // tile t0 is in LDS buffer `buf`; thresholds and counts are current
-        if (t0 + IT < i_end && !(A.ablate & 4)) load_tile(t0 + IT);
+        if (t0 + IT < i_end && !(kDevKnobs && (A.ablate & 4))) load_tile(t0 + IT);
         const float my_tau = tau[myq];
         const unsigned char* base = lds + buf * BUF;
         f32x16 acc[MT];
@@ -427,7 +427,7 @@ __global__ __launch_bounds__(kXThreads) void retrieval_x_kernel(RetrievalArgs A)
             for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-            if (A.ablate & 2) break;
+            if (kDevKnobs && (A.ablate & 2)) break;
 #pragma unroll
             for (int m = 0; m < MT; ++m) {
                 bf16x8r af[3];
@@ -454,7 +454,7 @@ __global__ __launch_bounds__(kXThreads) void retrieval_x_kernel(RetrievalArgs A)
             for (int r = 1; r < 16; ++r) mm[m] = fmaxf(mm[m], acc[m][r]);
         }
         const bool full = t0 + IT <= i_end;
-        if (!(A.ablate & 1) && qvalid) {
+        if (!(kDevKnobs && (A.ablate & 1)) && qvalid) {
 #pragma unroll
             for (int m = 0; m < MT; ++m) {
                 if (mm[m] >= my_tau) {
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(kXThreads) void retrieval_x_kernel(RetrievalArgs A)
                               __shfl(bhi, j, 64));
             }
         }
-        if (t0 + IT < i_end && !(A.ablate & 4)) store_tile(buf ^ 1);
+        if (t0 + IT < i_end && !(kDevKnobs && (A.ablate & 4))) store_tile(buf ^ 1);
         buf ^= 1;
     }
     __syncthreads();  // an empty partition skips the loop: counts and thresholds were set by waves 0-3
@@ -535,7 +535,7 @@ int pick_parts(int64_t nq, int64_t ni, int k, int qb = kRQ) {
     // k ln(items / (parts k)) candidate insertions and their compactions
     const int64_t target = qb == kXQ ? 256 : 2048;
     int64_t parts = (target + qtiles - 1) / qtiles;
-    if (const char* e = std::getenv("TTAMM_RETRIEVAL_PARTS")) parts = std::atoi(e);  // sweeps only
+    if (const char* e = dev_env("TTAMM_RETRIEVAL_PARTS")) parts = std::atoi(e);  // sweeps only
     const int64_t by_items = (ni + 4 * kRI - 1) / (4 * kRI);  // >= 4 tiles per partition
     if (parts > by_items) parts = by_items;
     const int64_t by_merge = (64 * kMergeJ) / k;
@@ -756,7 +756,7 @@ int launch_x_ks(const RetrievalArgs& A, dim3 grid, bool wide, hipStream_t s) {
 }
 
 // the split-bf16 kernel's query block (dim <= 128), else the fp32 kernel's
-bool retrieval_split(int dim) { return dim <= 128 && std::getenv("TTAMM_RETRIEVAL_FP32") == nullptr; }
+bool retrieval_split(int dim) { return dim <= 128 && product_env("TTAMM_RETRIEVAL_FP32") == nullptr; }
 int retrieval_qb(int dim) { return retrieval_split(dim) ? kXQ : kRQ; }
 
 size_t retrieval_workspace_bytes(int64_t nq, int64_t ni, int dim, int k) {
@@ -794,7 +794,7 @@ int launch_retrieval_topk(const float* Q, int64_t nq, int64_t ldq, const float* 
     A.boff = boff;
     A.bval = bval;
     A.k = k;
-    if (const char* e = std::getenv("TTAMM_RETRIEVAL_ABLATE")) A.ablate = std::atoi(e);
+    if (const char* e = dev_env("TTAMM_RETRIEVAL_ABLATE")) A.ablate = std::atoi(e);
     const int qb = retrieval_qb(dim);
     A.parts = pick_parts(nq, ni, k, qb);
     A.items_per_part = ni > 0 ? ((ni + A.parts - 1) / A.parts + 127) / 128 * 128 : 0;

@@ -487,7 +487,7 @@ void set_keys(GemmProblem& p, const TowerWs& w) {
 // (D in {32, 64, 96, 128}), bf16 towers gate16.hip (D in {128, 256}); any other configuration runs
 // the generic GEMM path.  TTAMM_GENERIC_GATE=1 forces the generic path (the tests run both).
 bool generic_gate_forced() {
-    const char* v = std::getenv("TTAMM_GENERIC_GATE");
+    const char* v = product_env("TTAMM_GENERIC_GATE");
     return v && v[0] == '1';
 }
 
@@ -497,7 +497,7 @@ bool gate_group(const ttamm_tower* const* T, TowerWs* const* W, int ntowers, int
     // TTAMM_GATE16_SPLIT=1: fp32 towers at D = 96 on gate16.hip's split-bf16 form instead of gate.hip
     // (fp32 MFMA).  Measured slower at C2 (forward 71 vs 61 us, backward 72 vs 70, step 0.695 vs
     // 0.655 ms, profiles/r05_s20_gate16_split.txt): the kernels are latency-bound, not MFMA-bound
-    const char* e16 = std::getenv("TTAMM_GATE16_SPLIT");
+    const char* e16 = dev_env("TTAMM_GATE16_SPLIT");
     const bool split16 = e16 && e16[0] == '1';
     int hg = -1, planes = -1;
     for (int k = 0; k < ntowers; ++k) {
@@ -570,7 +570,7 @@ int require_fused_for_units(const ttamm_tower* const* T, TowerWs* const* W, int 
 // TTAMM_GATE_OUT_EPILOGUE=1: the generic gate's sigmoid mix / mimic augment in the second gate
 // GEMM's epilogue (EPI_GATE_OUT) instead of gate_mix_kernel after an EPI_STORE launch
 bool gate_out_epilogue() {
-    static const bool on = std::getenv("TTAMM_GATE_OUT_EPILOGUE") != nullptr;
+    static const bool on = dev_env("TTAMM_GATE_OUT_EPILOGUE") != nullptr;
     return on;
 }
 enum { FWD_GATHER = 1, FWD_FUSION = 2, FWD_FEAT = 4, FWD_MLP = FWD_GATHER | FWD_FEAT, FWD_ALL = 7 };
@@ -816,7 +816,7 @@ int tower_forward(const ttamm_tower* T[2], TowerWs* W[2], const ttamm_batch& bt,
 
 // TTAMM_WGRAD_X16=1: the bf16 towers' first-layer weight gradient reads X from the bf16 feature copy
 bool wgrad_x16() {
-    const char* e = std::getenv("TTAMM_WGRAD_X16");
+    const char* e = dev_env("TTAMM_WGRAD_X16");
     return e && e[0] == '1';
 }
 
@@ -1284,10 +1284,10 @@ int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_b
     if ((rc = aux_events(ev, aux))) return rc;
     // bf16 towers: the prologue starts after the first layer's GEMM (its one-block-per-CU tiles
     // otherwise wait for CUs behind the catch-up replay); fp32 towers: at once
-    const bool late_fork = T[0]->matmul_bf16 && std::getenv("TTAMM_EARLY_FORK") == nullptr;
+    const bool late_fork = T[0]->matmul_bf16 && dev_env("TTAMM_EARLY_FORK") == nullptr;
     // fp32 towers: the ID-row gather also runs on the aux stream (ahead of the catch-up), beside the
     // first-layer GEMM, which reads only the feature rows; the fusion joins it with the catch-up
-    static const bool gather_main = std::getenv("TTAMM_GATHER_MAIN") != nullptr;
+    static const bool gather_main = dev_env("TTAMM_GATHER_MAIN") != nullptr;
     const bool gather_aux = !late_fork && !gather_main;
     if (!late_fork) TTAMM_HIP(hipEventRecord(ev[0], s));
     if ((rc = tower_forward(T, W, bt, D, mimic, s, n, l0_events, gather_aux ? FWD_FEAT : FWD_MLP,
@@ -1739,7 +1739,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     // C2 (0.660 vs 0.648 ms/step, two A/B pairs on one box; C5 unchanged at 1.413 ms,
     // profiles/r05_s9_prologue_prep.txt): the first GEMM waits for the whole prologue grid
     {
-        const char* e = std::getenv("TTAMM_PROLOGUE_PREP");
+        const char* e = dev_env("TTAMM_PROLOGUE_PREP");
         U.weight_prepped = I.weight_prepped = e && e[0] == '1';
     }
     const ttamm_hparams& hp = A.hp;
@@ -1838,8 +1838,8 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     // ---- forward ----------------------------------------------------------------------------
     hipStream_t aux = static_cast<hipStream_t>(A.aux_stream);
     if (!shard) {
-        df.slice_on_aux = df.on && overlapped(T, 2, df, s, aux) && !std::getenv("TTAMM_SLICE_MAIN");
-        df.slice_late = df.slice_on_aux && std::getenv("TTAMM_SLICE_LATE") != nullptr;
+        df.slice_on_aux = df.on && overlapped(T, 2, df, s, aux) && !dev_env("TTAMM_SLICE_MAIN");
+        df.slice_late = df.slice_on_aux && dev_env("TTAMM_SLICE_LATE") != nullptr;
         if ((rc = prepare_forward(T, W, 2, A.b, D, mimic, df, s, aux, A.timing_events + 2, A.timing_events,
                                   A.timing_events + 8)))
             return rc;
@@ -1987,8 +1987,8 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         // one process with the touched-row updates on the aux stream: the loss reduction (nothing in
         // the backward reads it) goes there too, ahead of them, instead of between the scores and the
         // fusion backward on the main stream.  TTAMM_ROWS_MAIN=1 / TTAMM_FINALIZE_MAIN=1: main stream.
-        static const bool rows_main = std::getenv("TTAMM_ROWS_MAIN") != nullptr;
-        static const bool fin_main = std::getenv("TTAMM_FINALIZE_MAIN") != nullptr;
+        static const bool rows_main = dev_env("TTAMM_ROWS_MAIN") != nullptr;
+        static const bool fin_main = dev_env("TTAMM_FINALIZE_MAIN") != nullptr;
         const bool rows_aux = !shard && !ws.clip_on && !rows_main && aux != nullptr && aux != s &&
                               overlapped(T, 2, df, s, aux);
         const bool fin_aux = rows_aux && !fin_main;
@@ -2028,7 +2028,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     }
     // ---- grouped: both towers' backward and table updates ------------------------------------
     if (ph & TTAMM_PHASE_TOWERS_BWD) {
-        static const bool rows_main = std::getenv("TTAMM_ROWS_MAIN") != nullptr;
+        static const bool rows_main = dev_env("TTAMM_ROWS_MAIN") != nullptr;
         if (I.R > 0 && !ws.clip_on && !rows_main && aux != nullptr && aux != s && overlapped(T, 2, df, s, aux)) {
             // as in one process: the touched-row updates on the aux stream beside the MLP backward,
             // joined before this phase ends (the caller's all-reduce and DENSE follow)

@@ -184,7 +184,7 @@ class StepArgs(ctypes.Structure):
     ]
 
 
-ABI_VERSION = 24  # ttamm.h TTAMM_ABI_VERSION
+ABI_VERSION = 25  # ttamm.h TTAMM_ABI_VERSION
 G0_EXACT = 0  # ttamm.h TTAMM_G0_EXACT
 DENSE_ADAM = 0  # ttamm.h TTAMM_DENSE_ADAM
 DENSE_SGD = 1  # ttamm.h TTAMM_DENSE_SGD
@@ -212,6 +212,7 @@ PHASE_CAL_SCATTER = 4096
 SIGNATURES = {
     "ttamm_abi_version": (ctypes.c_int, []),
     "ttamm_last_error": (ctypes.c_char_p, []),
+    "ttamm_developer_build": (ctypes.c_int, []),
     "ttamm_train_step_workspace_size": (ctypes.c_size_t, [ctypes.POINTER(StepArgs)]),
     "ttamm_train_step": (ctypes.c_int, [ctypes.POINTER(StepArgs), c_vp]),
     "ttamm_dense_grad_floats": (c_i64, [ctypes.POINTER(StepArgs)]),

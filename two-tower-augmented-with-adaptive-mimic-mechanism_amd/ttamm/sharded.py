@@ -556,8 +556,6 @@ class ShardedTrainStep(FusedTrainStep):
         routing; the draws and ids are the ones that step would make itself)."""
         ahead = self._ahead
         self._ahead = None
-        if next_batch is not None and row_base is None and global_batch is None:
-            self._check_next_batch(*next_batch)  # before this step's first collective
         mismatch = False
         if ahead is not None:
             # A prepared look-ahead already exchanged this step's request counts on EVERY rank, so
@@ -570,6 +568,13 @@ class ShardedTrainStep(FusedTrainStep):
             mismatch = not same or neg_items is not None or row_base is not None or global_batch is not None
             users, pos_items, neg_items, row_base, global_batch = ahead.users, ahead.pos, None, None, None
         use_ahead = ahead is not None
+        # the look-ahead runs at default positions only, decided on the EFFECTIVE row_base /
+        # global_batch (after a prepared look-ahead replaced the caller's); its batch is validated
+        # here, before this step's first collective, so a bad next_batch raises on this rank before
+        # any other rank can wait on it
+        look_ahead = next_batch is not None and row_base is None and global_batch is None
+        if look_ahead:
+            self._check_next_batch(*next_batch)
         if not self._bind_batch(users, pos_items, ahead.negs if use_ahead else neg_items, keep_masks):
             raise ValueError("ttamm: empty batch in a sharded step (every rank must step)")
         a = self.args
@@ -658,7 +663,7 @@ class ShardedTrainStep(FusedTrainStep):
             a.timing_events[i] = None
         a.item_fwd_in = back.data_ptr()
         a.item_bwd_out = self.bwd_out.data_ptr()
-        if next_batch is not None and row_base is None and global_batch is None:
+        if look_ahead:
             self._ahead = yield from self._look_ahead(*next_batch)
         ib = ()
         if self.in_batch:
@@ -721,6 +726,11 @@ class ShardedTrainStep(FusedTrainStep):
         validated before the step's first collective (_check_next_batch)."""
         W, rank = self.own.world_size, self.own.rank
         B, N = users.numel(), self.num_neg
+        # cheap guards on the buffers the draws below write (the full check ran before the step's
+        # first collective): never write past _ahead_bufs' max_batch x N slots
+        if not (0 < B <= self.max_batch) or users.dtype != torch.long or pos.dtype != torch.long or \
+                pos.numel() != B or (N > 0 and self.csr is None):
+            raise RuntimeError("ttamm: look-ahead batch failed validation (internal error)")
         users0, pos0 = users, pos  # the next step's program finds its batch by identity
         users, pos = users.reshape(-1), pos.reshape(-1)
         dev = self.device

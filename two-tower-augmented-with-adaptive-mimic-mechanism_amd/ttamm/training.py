@@ -108,17 +108,6 @@ def _dense_params(opt: torch.optim.Optimizer) -> list[torch.Tensor]:
     return [p for g in opt.param_groups for p in g["params"]]
 
 
-def feature_planes_enabled() -> bool:
-    """TTAMM_FEATURE_PLANES=1: fp32 towers keep their feature rows pre-split into bf16 planes
-    (1.5x the fp32 rows' bytes in HBM) for the first layer's forward and weight gradient, instead
-    of splitting them inside the GEMMs (same results, bit for bit).  Off by default: measured at C2
-    the forward GEMM reads 1.5x the gathered bytes and ran 126 -> 135 us, the weight gradient
-    103 -> 99 us, the step 0.656 -> 0.664 ms (profiles/r05_s7_feature_planes.txt)."""
-    import os
-
-    return os.environ.get("TTAMM_FEATURE_PLANES", "0") == "1"
-
-
 class FusedTrainStep:
     """Owns the native step descriptor and workspace for one (model, optimizers) pair."""
 
@@ -144,7 +133,13 @@ class FusedTrainStep:
         major_category_id: int | None = None,
         in_batch_negatives: bool = False,
         gradient_clip_norm: float | None = None,
+        feature_planes: bool = False,
     ) -> None:
+        # feature_planes (developer option, off by default): fp32 towers keep their feature rows
+        # pre-split into bf16 hi / mid / lo planes (1.5x the fp32 rows' bytes in HBM) for the first
+        # layer's forward and weight gradient instead of splitting them inside the GEMMs (same
+        # results, bit for bit).  Measured slower at C2: the forward GEMM reads 1.5x the gathered
+        # bytes, 126 -> 135 us, the step 0.656 -> 0.664 ms (profiles/r05_s7_feature_planes.txt).
         # in_batch_negatives: ttamm's in-batch mode (ttamm.h ttamm_step_args.in_batch; not the
         # reference's behaviour): every user is also scored against every positive of the batch
         self.in_batch = bool(in_batch_negatives)
@@ -179,6 +174,9 @@ class FusedTrainStep:
         self.dense_opt, self.sparse_opt = dense_opt, sparse_opt
         # the dense group's optimizer (training.py:1311-1333): Adam / AdamW, or SGD with momentum
         self.sgd = isinstance(dense_opt, torch.optim.SGD)
+        # SGD with / without momentum decides, once, what the kernels' moment slots alias (the
+        # momentum buffer, or the parameter itself) and whether the tables' g = 0 rows are deferred
+        self._sgd_momentum_on = self.sgd and float(dense_opt.param_groups[0]["momentum"]) != 0.0
         self._sgd_buffers: list[tuple[torch.Tensor, torch.Tensor]] = []  # (param, buffer) not yet in state
         dense_ids = {id(p) for g in (dense_opt.param_groups if dense_opt else []) for p in g["params"]}
         sparse_ids = {id(p) for g in (sparse_opt.param_groups if sparse_opt else []) for p in g["params"]}
@@ -273,7 +271,7 @@ class FusedTrainStep:
                 f16 = self._bf16_copy(feats)
                 desc.features_bf16 = f16.data_ptr()
                 desc.feat_bf16_ld = f16.stride(0)
-            elif feats is not None and feature_planes_enabled():
+            elif feats is not None and feature_planes:
                 # fp32 towers: the feature rows split once into their bf16 hi / mid / lo planes (the
                 # split every split-bf16 GEMM of the step forms), so the first layer's forward and
                 # weight gradient stage them instead of splitting in every k-tile (same bits)
@@ -441,6 +439,11 @@ class FusedTrainStep:
             hp.lr = float(g["lr"])
             hp.weight_decay = float(g["weight_decay"])
             hp.momentum = float(g["momentum"])
+            if (hp.momentum != 0.0) != self._sgd_momentum_on:
+                # the moment slots alias the parameter without momentum and a momentum buffer with it
+                # (and the deferred replay would overwrite lagging rows' buffers): not switchable
+                raise ValueError("ttamm: SGD momentum changed between zero and non-zero after the step was "
+                                 "built; build a new FusedTrainStep for the new setting")
             hp.dampening = float(g["dampening"])
             hp.nesterov = 1 if g["nesterov"] else 0
             # torch creates a momentum buffer at its parameter's first step (buf = grad.clone()),
