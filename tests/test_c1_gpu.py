@@ -158,9 +158,10 @@ def test_c1_large_recall_at_20_within_oracle_band():
     ttamm.train_one_epoch exactly like the oracle runs committed in
     tests/golden/c1_large/oracle_recall.json (make_c1_large_oracle.py: the CPU restatement with 8
     threads = the reference value, with 1 thread, and with the first layer's K reduction split in
-    two — summation-order-only variants whose Recall@20 spread is recorded there).  ttamm's
-    Recall@20 (CPU evaluation of its weights, the same restated _evaluate_model) must lie within
-    0.002 of the reference value."""
+    two — summation-order-only variants whose Recall@20 spread is recorded there — and in float64).
+    ttamm's Recall@20 (CPU evaluation of its weights, the same restated _evaluate_model) must lie
+    within 0.002 of the reference value, and its epoch means as close to the float64 trajectory as
+    the fp32 reference runs are (below)."""
     import json
     from pathlib import Path
 
@@ -187,8 +188,24 @@ def test_c1_large_recall_at_20_within_oracle_band():
     print(f"\nC1-large Recall@20: ttamm {r_ttamm:.5f}  oracle {variants}  oracle spread "
           f"{doc['oracle_spread_recall20']:.5f}  |ttamm - oracle| {abs(r_ttamm - ref20):.5f}")
     print(f"epoch means ttamm {means} oracle {doc['variants']['threads8']['epoch_means']}")
-    # epoch-1 mean loss: 433 steps per epoch let summation-order rounding compound (Adam turns it
-    # into lr-sized steps); the oracle's own variants differ by 2-3e-5 from the reference run, ttamm
-    # by 1.1e-4 (first box run), so 5e-4 — the Recall gate below is the parity claim
-    assert abs(means[0] - doc["variants"]["threads8"]["epoch_means"][0]) <= 5e-4 * means[0]
+    # Epoch means against the float64 trajectory (the "float64" variant: the same run, same streams,
+    # in float64 — the arithmetic every fp32 run approximates).  Rounding compounds over 433 steps
+    # per epoch (Adam turns it into lr-sized steps), and where it lands depends on the KIND of
+    # rounding, not only its size: the fp32 CPU runs (threads8 = the reference value, threads1,
+    # splitk2) all sit ABOVE the float64 mean of epoch 1 by 4.0-6.8e-5, ttamm's split-bf16 GEMMs
+    # (exact bf16 products, MFMA sums rounded once per 16 k) sit BELOW it by 4.0e-5, and ttamm
+    # with the fp32-MFMA kernels (TTAMM_FP32_MFMA=exact, fp32 fma chains like the CPU) above it
+    # by 5.1e-5.  So ttamm vs threads8 (1.1e-4) is the two sides of the
+    # exact trajectory, not a larger error: measured against float64, ttamm is as close as the
+    # fp32 reference itself.  Bounds: epoch 1 within 5e-5 of float64; every epoch within twice the
+    # fp32 reference runs' own largest distance from float64.
+    f64 = doc["variants"]["float64"]["epoch_means"]
+    fp32_runs = [doc["variants"][v]["epoch_means"] for v in ("threads8", "threads1", "splitk2")]
+    dist = [abs(means[e] - f64[e]) / f64[e] for e in range(EPOCHS)]
+    own = [max(abs(v[e] - f64[e]) for v in fp32_runs) / f64[e] for e in range(EPOCHS)]
+    print(f"epoch means vs float64: ttamm {['%.2e' % d for d in dist]}  fp32 oracle runs up to "
+          f"{['%.2e' % o for o in own]}")
+    assert dist[0] <= 5e-5, dist
+    for e in range(EPOCHS):
+        assert dist[e] <= 2 * own[e], (e, dist[e], own[e])
     assert abs(r_ttamm - ref20) <= 0.002

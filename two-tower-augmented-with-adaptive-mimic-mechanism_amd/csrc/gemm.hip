@@ -705,7 +705,9 @@ struct XCfg {
     static constexpr int CLD = BN + 4;
     static constexpr int EPI_ROWS = WAVES_M >= 2 ? BM / 2 : (I > 1 ? (I + 1) / 2 * 32 : BM);
     static constexpr int EPI_PHASES = (BM + EPI_ROWS - 1) / EPI_ROWS;
-    static constexpr int KIDX_BYTES = A_KMAJ ? 8 * kWgradMaxRowsPerSplit : 0;
+    // K-major A: the split's (gathered) row ids as int32 (tables < 2^31 rows): 4 KB, so the
+    // 128 x 96 weight-gradient tile fits three blocks per CU (53,248 B of LDS each)
+    static constexpr int KIDX_BYTES = A_KMAJ ? 4 * kWgradMaxRowsPerSplit : 0;
     static constexpr int buf_bytes(int pl) { return pl * (A_PLANE + B_PLANE); }
     static constexpr int lds_bytes(int pl) {
         const int st = 2 * buf_bytes(pl) + KIDX_BYTES, ep = EPI_ROWS * CLD * 4;
@@ -725,6 +727,9 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 #ifndef TTAMM_X_ABLATE
 #define TTAMM_X_ABLATE 0
+#endif
+#ifndef TTAMM_SPLIT8
+#define TTAMM_SPLIT8 0
 #endif
 #ifndef TTAMM_BF16_DEEP
 #define TTAMM_BF16_DEEP 1
@@ -864,10 +869,10 @@ __global__ __launch_bounds__(kThreads, CX::MINB) void gemm_x_kernel(GemmBatch ba
             a_rp[it] = P.A;
         }
     }
-    int64_t* kidx = reinterpret_cast<int64_t*>(lds + 2 * CX::buf_bytes(PL));
+    int32_t* kidx = reinterpret_cast<int32_t*>(lds + 2 * CX::buf_bytes(PL));
     if (AK) {
         for (int k = tid; k < k_end - k_begin; k += kThreads)
-            kidx[k] = P.a_idx ? P.a_idx[k_begin + k] : (int64_t)(k_begin + k);
+            kidx[k] = (int32_t)(P.a_idx ? P.a_idx[k_begin + k] : (int64_t)(k_begin + k));
         __syncthreads();
     }
     const float* b_rp[CX::B_LOADS];
@@ -889,7 +894,10 @@ __global__ __launch_bounds__(kThreads, CX::MINB) void gemm_x_kernel(GemmBatch ba
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     // weight gradients with b_colsum: the blocks of M-tile 0 sum the dY values they stage (the
     // bias gradient, written to C row M after the main loop)
-    constexpr bool CSUM = AK && BKM;
+    // (bf16 towers and pre-split X planes only: the fp32 split kernels take the bias gradient as an
+    // implicit ones column of X — the column-sum registers pushed the 128 x 192 fp32 weight gradient
+    // to 256 VGPRs with scratch spills, C2 +6 us per step, profiles/r06_s2_bisect.txt)
+    constexpr bool CSUM = AK && BKM && (PL == 1 || CX::APL);
     const bool colsum = CSUM && P.b_colsum && tm == 0;
     float4 bsum[CSUM ? CX::B_LOADS : 1];
 #pragma unroll
@@ -918,14 +926,14 @@ __global__ __launch_bounds__(kThreads, CX::MINB) void gemm_x_kernel(GemmBatch ba
                         ra[R][it] = *reinterpret_cast<const float4*>(ap_rp[it] + (k0 >> 4) * 48 + a_c[it]);
                     } else {
                         const int k = FAST ? k0 + a_r[it] : min(k0 + a_r[it], k_end - 1);
-                        const uint16_t* rp = P.A3p + kidx[k - k_begin] * P.lda3 + (m0 >> 4) * 48;
+                        const uint16_t* rp = P.A3p + (int64_t)kidx[k - k_begin] * P.lda3 + (m0 >> 4) * 48;
                         ra[R][it] = *reinterpret_cast<const float4*>(rp + a_c[it]);
                     }
                     continue;
                 }
                 if constexpr (CX::A16) {
                     const int k = FAST ? k0 + a_r[it] : min(k0 + a_r[it], k_end - 1);
-                    const uint16_t* rp = P.A16 + kidx[k - k_begin] * P.lda16 + m0 + a_c[it];
+                    const uint16_t* rp = P.A16 + (int64_t)kidx[k - k_begin] * P.lda16 + m0 + a_c[it];
                     ra[R][it] = (FAST || a_ok[it]) ? *reinterpret_cast<const float4*>(rp) : make_float4(0.f, 0.f, 0.f, 0.f);
                     continue;
                 }
@@ -934,7 +942,7 @@ __global__ __launch_bounds__(kThreads, CX::MINB) void gemm_x_kernel(GemmBatch ba
                                      : raw4(a_rp[it], k0 + a_c[it], P.lda);
                 } else {
                     const int k = FAST ? k0 + a_r[it] : min(k0 + a_r[it], k_end - 1);
-                    const float* rp = P.A + kidx[k - k_begin] * P.lda;
+                    const float* rp = P.A + (int64_t)kidx[k - k_begin] * P.lda;
                     ra[R][it] = FAST ? *reinterpret_cast<const float4*>(rp + m0 + a_c[it]) : raw4(rp, m0 + a_c[it], P.lda);
                 }
             }
@@ -1062,6 +1070,10 @@ __global__ __launch_bounds__(kThreads, CX::MINB) void gemm_x_kernel(GemmBatch ba
 #pragma unroll
                 for (int pq = 0; pq < NP; ++pq) {
                     const int i = pq / J, j = pq % J;
+                    if constexpr (PL == 3 && TTAMM_SPLIT8) {  // developer: the 2^-24 terms ml, lm too
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][i], bf[2][j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2][i], bf[1][j], acc[i][j], 0, 0, 0);
+                    }
                     if constexpr (PL == 3 && TTAMM_X_ABLATE != 2) {  // small terms first (ablation 2: hh only)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][i], bf[1][j], acc[i][j], 0, 0, 0);
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2][i], bf[0][j], acc[i][j], 0, 0, 0);
@@ -1933,11 +1945,12 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
         p.B = w.dY;
         p.ldb = w.ld_dy;
         p.b_kn = 1;
-        // split kernels: the bias gradient as column sums of dY in the M-tile-0 blocks (b_colsum),
-        // so M = n_in; the fp32-MFMA kernels keep the implicit ones column (M = n_in + 1)
-        p.b_colsum = exact ? 0 : 1;
-        p.a_ones_col = exact ? w.N : -1;
-        p.M = exact ? w.N + 1 : w.N;
+        // bf16 / pre-split-plane kernels: the bias gradient as column sums of dY in the M-tile-0
+        // blocks (b_colsum), so M = n_in; the fp32 split and fp32-MFMA kernels: the implicit ones
+        // column (M = n_in + 1)
+        p.b_colsum = 0;
+        p.a_ones_col = w.N;
+        p.M = w.N + 1;
         p.N = w.M;
         p.K = w.R;
         p.k_split = w.rows_per_split;
@@ -1954,6 +1967,11 @@ int launch_wgrad(WgradBatch& wb, hipStream_t s, void* const* ev) {
         if (planes) {
             p.A3p = w.X3p;
             p.lda3 = w.ld_x3;
+        }
+        if (!exact && (bf || planes)) {  // (the column-sum kernels: see gemm_x_kernel CSUM)
+            p.b_colsum = 1;
+            p.a_ones_col = -1;
+            p.M = w.N;
         }
         if (bf && w.X16 && (cfg == 1 || cfg == 2) && w.ld_x16 % 8 == 0 && w.ld_x16 >= 8 * ceil_div(w.N, 8) &&
             (uintptr_t)w.X16 % 16 == 0) {
