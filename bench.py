@@ -363,8 +363,8 @@ def main() -> None:
                     help="IEEE sqrt / division for the g = 0 table AdamW updates (bit-identical to torch) "
                          "instead of v_sqrt / v_rcp")
     ap.add_argument("--no-exact-line", dest="exact_line", action="store_false",
-                    help="skip the exact_table_math sub-line (K more steps with the opt-in bit-exact g = 0 "
-                         "table arithmetic)")
+                    help="skip the exact_table_math sub-line (K more steps with the drop-in default's "
+                         "bit-exact g = 0 table arithmetic)")
     ap.add_argument("--kernel-events", choices=["every-step", "none"], default="every-step",
                     help="none: no per-kernel HIP event pairs in the timed steps (the roofline entries "
                          "then have no live launch durations; a measurement of the events' own cost)")
@@ -476,10 +476,10 @@ def main() -> None:
         elapsed = float(t.item())
     exact_line = None
     if args.exact_line and not args.eager_adamw and not args.exact_table_math and hasattr(eng, "args"):
-        # the bit-exact table arithmetic option (ttamm.FusedTrainStep(table_adamw_math="exact"),
-        # IEEE sqrt / division, bit-identical to torch's AdamW; the default is "fast", as timed above):
-        # the same step, K more steps + the flush, timed the same way.  Every row is current here
-        # (the flush above), so the switch applies from the next step on.
+        # the drop-in default's table arithmetic (ttamm.FusedTrainStep(table_adamw_math="exact"),
+        # IEEE sqrt / division, bit-identical to torch's AdamW): the same step, K more steps + the
+        # flush, timed the same way.  Every row is current here (the flush above), so the switch
+        # applies from the next step on.
         from ttamm import _lib as ttamm_lib
 
         eng.args.table_g0_math = ttamm_lib.G0_EXACT
@@ -501,8 +501,7 @@ def main() -> None:
         eng.args.table_g0_math = ttamm_lib.G0_FAST
         exact_line = {"value": round(args.steps * c["B"] * world / ex_elapsed, 1), "unit": "interactions/s",
                       "ms_per_step": round(ex_elapsed / args.steps * 1e3, 4), "steps": args.steps,
-                      "note": "table_adamw_math='exact' (the opt-in bit-exact option of ttamm.FusedTrainStep / "
-                              "train_one_epoch, whose default is the 'fast' arithmetic timed in the main line: IEEE "
+                      "note": "table_adamw_math='exact' (the ttamm.FusedTrainStep / train_one_epoch default: IEEE "
                               "sqrt and division in the g = 0 table AdamW, bit-identical to torch): the same "
                               "workload, K steps + the closing flush, right after the main timed region"}
     loss = eng.finish()
