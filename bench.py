@@ -260,6 +260,72 @@ def cpu_baseline(c: dict, steps: int, warmup: int, seed: int, in_batch: bool = F
     }
 
 
+def gather_bulk(device, rows: int = 50_000_000, dim: int = 128, n: int = 2_000_000, reps: int = 10) -> dict:
+    """north_star's "50M x 128 embedding gather" in bulk, after the timed
+    region: a 50M x 128 fp32 table (25.6 GB, N(0, 0.02)), 2M uniform row ids (every row a cold HBM
+    read).  `materialising`: the step's product gather (ttamm_gather_rows) copying the rows out —
+    it writes every byte it reads, so its read rate is at most half of HBM and `total_frac` prices
+    both directions; `read_only`: the product's consumer that reads the same rows by id and keeps
+    4 B per row (ttamm_candidate_topk, the sampled-candidate evaluation, 100 candidates per
+    query).  Every materialising launch is checked bit-exact against torch.index_select."""
+    from ttamm import _lib as L
+
+    lib = L.load()
+    gen = torch.Generator(device=device).manual_seed(4321)
+    table = torch.empty((rows, dim), dtype=torch.float32, device=device)
+    for lo in range(0, rows, 1 << 22):
+        table[lo:lo + (1 << 22)].normal_(0.0, 0.02, generator=gen)
+    idx = torch.randint(0, rows, (n,), generator=gen, device=device)
+    out = torch.empty((n, dim), dtype=torch.float32, device=device)
+    sp = torch.cuda.current_stream().cuda_stream
+
+    def launch():
+        L.check(lib.ttamm_gather_rows(table.data_ptr(), rows, dim, idx.data_ptr(), n, out.data_ptr(), dim, sp))
+
+    launch()
+    torch.cuda.synchronize()
+    exact = bool(torch.equal(out, torch.index_select(table, 0, idx)))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        launch()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    rd, tot = n * dim * 4, n * (2 * dim * 4 + 8)
+    mat = {"kernel": "gather_rows_wide (ttamm_gather_rows)", "rows_per_launch": n, "avg_launch_ms": round(ms, 4),
+           "read_GBps": round(rd / ms / 1e6, 1), "read_frac": round(rd / ms / 1e6 / HBM_PEAK_GBS, 4),
+           "total_GBps": round(tot / ms / 1e6, 1), "total_frac": round(tot / ms / 1e6 / HBM_PEAK_GBS, 4),
+           "bit_exact_vs_torch": exact}
+    del out
+    per_q, k = 100, 20
+    nq = n // per_q
+    q = torch.randn((nq, dim), generator=gen, device=device, dtype=torch.float32)
+    off = torch.arange(0, nq * per_q + 1, per_q, device=device, dtype=torch.long)
+    out_s = torch.empty((nq, k), dtype=torch.float32, device=device)
+    out_p = torch.empty((nq, k), dtype=torch.long, device=device)
+
+    def launch_c():
+        L.check(lib.ttamm_candidate_topk(q.data_ptr(), nq, dim, table.data_ptr(), rows, dim, dim, off.data_ptr(),
+                                         idx.data_ptr(), per_q, 0, k, out_s.data_ptr(), out_p.data_ptr(), sp))
+
+    launch_c()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        launch_c()
+    e1.record()
+    torch.cuda.synchronize()
+    ms_c = e0.elapsed_time(e1) / reps
+    ro = {"kernel": "candidate_topk_v_kernel (ttamm_candidate_topk)", "rows_per_launch": n,
+          "avg_launch_ms": round(ms_c, 4), "read_GBps": round(rd / ms_c / 1e6, 1),
+          "read_frac": round(rd / ms_c / 1e6 / HBM_PEAK_GBS, 4)}
+    del table
+    torch.cuda.empty_cache()
+    return {"table": f"{rows} x {dim} fp32", "indices": "uniform", "materialising": mat, "read_only": ro,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+
+
 def cpu_model() -> str:
     try:
         for line in Path("/proc/cpuinfo").read_text().splitlines():
@@ -365,6 +431,8 @@ def main() -> None:
     ap.add_argument("--no-exact-line", dest="exact_line", action="store_false",
                     help="skip the exact_table_math sub-line (K more steps with the drop-in default's "
                          "bit-exact g = 0 table arithmetic)")
+    ap.add_argument("--no-gather-bulk", dest="gather_bulk", action="store_false",
+                    help="--config c4: skip the 50M x 128 bulk gather sub-line (after the timed region)")
     ap.add_argument("--kernel-events", choices=["every-step", "none"], default="every-step",
                     help="none: no per-kernel HIP event pairs in the timed steps (the roofline entries "
                          "then have no live launch durations; a measurement of the events' own cost)")
@@ -440,8 +508,8 @@ def main() -> None:
     # per-step HIP event pairs (ttamm.h ttamm_step_args.timing_events), each recorded on the
     # stream its kernel runs on: [0,1] the deferred slice's replay kernel, [2,3] the grouped first
     # feature-layer forward GEMM, [4,5] the in-batch kernel, [6,7] the wide weight-gradient GEMM
-    # launch, [8,9] / [10,11] the user / item catch-up replay kernels
-    NEV = 12
+    # launch, [8,9] / [10,11] the user / item catch-up replay kernels, [12,13] the ID-row gather
+    NEV = 14
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(NEV)] for _ in range(args.steps)]
     for quad in evs:  # materialise the hipEvent_t handles
         for e in quad:
@@ -591,6 +659,23 @@ def main() -> None:
             ib_flops, pair_ms(4), split_ceiling, "inbatch_bytes_per_launch")
         ent["executed_flops_per_launch"] = 8.0 * B * Bg * D
         kernels.append(ent)
+    gather = None
+    g_ms = pair_ms(12)
+    if g_ms > 0 and not sharded:
+        # the step's ID-row gather (encoders.py:222-223: the user and item tables'
+        # rows of the batch, one grouped launch on the aux stream into the [e | f] rows): table-row
+        # bytes read against the HBM-read roofline (north_star's gather target), and every byte the
+        # copy moves (rows read + rows written + int64 ids)
+        g_rows = B + item_rows
+        rd = g_rows * D * 4
+        tot = g_rows * (2 * D * 4 + 8)
+        gather = {"kernel": "gather_rows_wide_seg (the step's user + item ID-row gather)", "bound": "hbm",
+                  "rows_per_launch": g_rows, "avg_launch_ms": round(g_ms, 4),
+                  "read_bytes_per_launch": rd, "read_GBps": round(rd / g_ms / 1e6, 1),
+                  "read_frac": round(rd / g_ms / 1e6 / HBM_PEAK_GBS, 4),
+                  "total_bytes_per_launch": tot, "total_GBps": round(tot / g_ms / 1e6, 1),
+                  "total_frac": round(tot / g_ms / 1e6 / HBM_PEAK_GBS, 4), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "traffic": traffic.get("gather_bytes_per_launch")}
     deferred = not args.eager_adamw
     slice_ms, cu_user_ms, cu_item_ms = pair_ms(0), pair_ms(8), pair_ms(10)
     if deferred:
@@ -684,6 +769,10 @@ def main() -> None:
     }
     if exact_line is not None:
         out["exact_table_math"] = exact_line
+    if gather is not None:
+        out["gather"] = gather
+    if args.config == "c4" and not emulate and world == 1 and args.gather_bulk:
+        out["gather"] = dict(gather or {}, bulk=gather_bulk(device))
     if emulate:
         out["emulated_world"] = shard_world
         out["config"]["parallelism"] = (f"EMULATED rank 0 of {shard_world}: row-sharded step with mirrored ranks "

@@ -168,6 +168,13 @@ typedef struct ttamm_table {
      * forward call — the user rows, then the positives', then the negatives' (training.py:
      * 748-775 calls the item encoder twice).  0 = off. */
     double max_norm;
+    /* Deferred dense-group tables (last_step != NULL) may also carry one byte per row: 0 = the
+     * row has never had a gradient, so exp_avg and exp_avg_sq are +0.0 in every column and its
+     * AdamW(g = 0) updates are p *= (1 - lr wd) alone (bit for bit: the update term is -0.0); the
+     * replay then moves only the parameter row (8 of its 24 bytes per element).  1 = anything
+     * else.  The step sets a row's byte when it gives the row a gradient; the caller initialises
+     * it (any nonzero exp_avg / exp_avg_sq in the row -> 1).  NULL = every row treated as 1. */
+    uint8_t* touched;
 } ttamm_table;
 
 /* One tower: TowerEncoder (encoders.py:171-255) + its half of AdaptiveMimicMechanism
@@ -273,14 +280,16 @@ typedef struct ttamm_step_args {
     uint32_t* status;     /* device status word (TTAMM_STATUS_* bits), OR-ed          */
     void* workspace;
     size_t workspace_bytes;
-    void* timing_events[12]; /* optional hipEvent_t pairs (bench roofline), NULL = off:
+    void* timing_events[14]; /* optional hipEvent_t pairs (bench roofline), NULL = off:
                                [0],[1] around the dense-group table maintenance (eager
                                AdamW(g=0) sweep, or the deferred slice's replay kernel);
                                [2],[3] around the grouped first feature-layer forward GEMM;
                                [4],[5] around the in-batch scoring kernel (in_batch);
                                [6],[7] around the wide weight-gradient GEMM launch;
                                [8],[9] / [10],[11] around the user / item tower's deferred
-                               catch-up replay kernel (on aux_stream when it is set)      */
+                               catch-up replay kernel (on aux_stream when it is set);
+                               [12],[13] around the grouped ID-row gather (one process,
+                               on aux_stream; round 6)                                    */
     /* ---- row-sharded multi-GPU step (phase != TTAMM_PHASE_ALL) ----------------------
      * The same workspace must be passed to every phase of a step.                        */
     int32_t phase;                /* TTAMM_PHASE_* bits                                      */

@@ -583,6 +583,7 @@ struct ReplaySeg {
     float* m;
     float* v;
     int32_t* last;
+    const uint8_t* touched;  // ttamm_table.touched: 0 = never given a gradient (m = v = +0), or null
     int dim;
     // rows [row_lo, row_hi), each from its own last[row] ...
     int64_t row_lo, row_hi;

@@ -450,7 +450,10 @@ __global__ __launch_bounds__(64 * kRowWaves) void piece_sum_kernel(RowUpdateArgs
         for (int p = 0; p < kPiece; ++p) {  // issue every load of the chunk before adding
             const int64_t r = srows[w][p];
             ve[p] = (idt && p < cnt) ? A.dE[r * A.ld_dE + d] : 0.f;
-            va[p] = (mimic && p < cnt) ? (SDA ? sda[w][p][d] : dA_row(A, r)[d]) : 0.f;
+            // (SDA = false only without unit maps, launch_row_update: the row's own dA row, no xu
+            // branch in this unrolled load batch — one there serialised the 32 loads, 24 -> 50 us
+            // per launch at C2, profiles/r06_s7_kernel_stats.txt)
+            va[p] = (mimic && p < cnt) ? (SDA ? sda[w][p][d] : (r < A.split_row ? A.dA_lo : A.dA_hi)[r * A.ld_dA + d]) : 0.f;
         }
         float ge = 0.f, ga = 0.f;
         int start = 0;
@@ -490,6 +493,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArg
     const bool mimic = A.mimic.weight != nullptr;
     const bool idt = A.id.weight != nullptr;  // (a mimic-only pass leaves the ID table out)
     const bool direct = k1 - k0 <= kPiece;
+    const bool pad_row = idt && A.id.has_padding_idx && key == A.id.padding_idx;
     auto each = [](float4& p, float4& m, float4& v, float4 g, auto&& f) {
         f(p.x, m.x, v.x, g.x);
         f(p.y, m.y, v.y, g.y);
@@ -574,8 +578,14 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArg
         }
     }
     if (sub == 0) {
-        if (idt && A.id.optimizer != TTAMM_OPT_SPARSE_ADAM && A.id.last_step) A.id.last_step[key] = A.dense_step;
-        if (mimic && A.mimic.last_step) A.mimic.last_step[key] = A.dense_step;
+        if (idt && A.id.optimizer != TTAMM_OPT_SPARSE_ADAM && A.id.last_step) {
+            A.id.last_step[key] = A.dense_step;
+            if (A.id.touched && !pad_row) A.id.touched[key] = 1;
+        }
+        if (mimic && A.mimic.last_step) {
+            A.mimic.last_step[key] = A.dense_step;
+            if (A.mimic.touched) A.mimic.touched[key] = 1;
+        }
     }
 }
 
@@ -691,6 +701,24 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
             if (l >= target) continue;
         }
         const int64_t o = row * dim + 4 * (int64_t)q;
+        const HC* hc = H2 + (l + 1) % cap;
+        const HC* const hend = hc + (target - l);
+        if (DECOUPLED && S.touched && S.touched[row] == 0) {
+            // a row never given a gradient: m = v = +0.0 stay so, and each step is p *= decay
+            // (the cold path below, bit for bit) — only the parameter row moves
+            float4 p[V];
+#pragma unroll
+            for (int i = 0; i < V; ++i) p[i] = *reinterpret_cast<const float4*>(S.p + o + (int64_t)(4 * per_row) * i);
+            for (; hc != hend; ++hc) {
+                const float decay = lo_of(hc->decay);
+#pragma unroll
+                for (int i = 0; i < V; ++i)
+                    p[i].x = p[i].x * decay, p[i].y = p[i].y * decay, p[i].z = p[i].z * decay, p[i].w = p[i].w * decay;
+            }
+#pragma unroll
+            for (int i = 0; i < V; ++i) *reinterpret_cast<float4*>(S.p + o + (int64_t)(4 * per_row) * i) = p[i];
+            continue;
+        }
         float4 p[V], m[V], v[V];
 #pragma unroll
         for (int i = 0; i < V; ++i) {
@@ -699,8 +727,6 @@ __global__ __launch_bounds__(256) void replay_kernel(ReplayArgs) {
             m[i] = *reinterpret_cast<const float4*>(S.m + oi);
             v[i] = *reinterpret_cast<const float4*>(S.v + oi);
         }
-        const HC* hc = H2 + (l + 1) % cap;
-        const HC* const hend = hc + (target - l);
         // A cold row (first moment +0.0: never given a gradient) stays cold under g = 0 (m = fma(w1,
         // -0, 0) = +0), and its update term neg_step * (0 * r) is -0.0, which leaves p * decay
         // unchanged for every p — so its replay is p *= decay, v *= b2 per step, bit for bit what

@@ -1079,6 +1079,7 @@ ReplaySeg replay_seg(const ttamm_table& tb) {
     g.m = tb.exp_avg;
     g.v = tb.exp_avg_sq;
     g.last = tb.last_step;
+    g.touched = tb.touched;
     g.dim = tb.dim;
     return g;
 }
@@ -1268,7 +1269,8 @@ bool overlapped(const ttamm_tower* const* T, int n, const Deferred& df, hipStrea
 // both towers' lists)
 int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_batch& bt, int D, bool mimic,
                     const Deferred& df, hipStream_t s, hipStream_t aux, void* const* l0_events,
-                    void* const* maint_events = nullptr, void* const* cu_events = nullptr) {
+                    void* const* maint_events = nullptr, void* const* cu_events = nullptr,
+                    void* const* gather_events = nullptr) {
     int rc;
     auto cu_ev = [&](int k) -> void* const* {
         return cu_events ? cu_events + (W[k]->role == ROLE_USER ? 0 : 2) : nullptr;
@@ -1294,7 +1296,12 @@ int prepare_forward(const ttamm_tower* T[2], TowerWs* W[2], int n, const ttamm_b
                             late_fork ? ev[0] : nullptr)))
         return rc;
     TTAMM_HIP(hipStreamWaitEvent(aux, ev[0], 0));
-    if (gather_aux && (rc = tower_forward(T, W, bt, D, mimic, aux, n, nullptr, FWD_GATHER))) return rc;
+    if (gather_aux) {
+        const bool timed = gather_events && gather_events[0] && gather_events[1];
+        if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)gather_events[0], aux));
+        if ((rc = tower_forward(T, W, bt, D, mimic, aux, n, nullptr, FWD_GATHER))) return rc;
+        if (timed) TTAMM_HIP(hipEventRecord((hipEvent_t)gather_events[1], aux));
+    }
     if ((rc = towers_prepare_a(T, W, n, mimic, df, aux, cu_ev(0)))) return rc;
     TTAMM_HIP(hipEventRecord(ev[1], aux));
     // the fusion is enqueued before the grouping's dozen launches: enqueued after them, the host
@@ -1841,7 +1848,7 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         df.slice_on_aux = df.on && overlapped(T, 2, df, s, aux) && !dev_env("TTAMM_SLICE_MAIN");
         df.slice_late = df.slice_on_aux && dev_env("TTAMM_SLICE_LATE") != nullptr;
         if ((rc = prepare_forward(T, W, 2, A.b, D, mimic, df, s, aux, A.timing_events + 2, A.timing_events,
-                                  A.timing_events + 8)))
+                                  A.timing_events + 8, A.timing_events + 12)))
             return rc;
     } else {
         const ttamm_tower* Ti[2] = {&A.item, nullptr};

@@ -63,6 +63,7 @@ class Table(ctypes.Structure):
         ("has_padding_idx", c_i32),
         ("padding_idx", c_i64),
         ("max_norm", c_d),
+        ("touched", c_vp),
     ]
 
 
@@ -142,7 +143,7 @@ class StepArgs(ctypes.Structure):
         ("status", c_vp),
         ("workspace", c_vp),
         ("workspace_bytes", ctypes.c_size_t),
-        ("timing_events", c_vp * 12),
+        ("timing_events", c_vp * 14),
         # row-sharded multi-GPU step (ttamm.h TTAMM_PHASE_*)
         ("phase", c_i32),
         ("row_base", c_i64),

@@ -357,13 +357,22 @@ class FusedTrainStep:
             for name in ("user", "item"):
                 desc = getattr(args, name)
                 if self.mimic is not None:
-                    tables.append(desc.mimic)
+                    tables.append((desc.mimic, self.mimic_tables[name]))
                 if desc.id.optimizer == _lib.OPT_DENSE:
-                    tables.append(desc.id)
-            for tb in tables:
+                    tables.append((desc.id, self.towers[name][0].embedding.weight))
+            for tb, param in tables:
                 last = torch.full((tb.rows,), self.dense_step0, dtype=torch.int32, device=self.device)
                 tb.last_step = last.data_ptr()
                 self._deferred.append(last)
+                if not self.sgd and self.decoupled:
+                    # rows never given a gradient (exp_avg = exp_avg_sq = +0.0 throughout: AdamW(g = 0)
+                    # moves only p) replay from the parameter row alone (ttamm.h ttamm_table.touched)
+                    st = state[id(param)]
+                    touched = ((st["exp_avg"].view(tb.rows, -1).view(torch.int32) != 0).any(dim=1)
+                               | (st["exp_avg_sq"].view(tb.rows, -1).view(torch.int32) != 0).any(dim=1))
+                    touched = touched.to(torch.uint8).contiguous()
+                    tb.touched = touched.data_ptr()
+                    self._deferred.append(touched)
             if tables:
                 cap = replay_slices + 2
                 self.adam_history = torch.zeros(cap * int(self.lib.ttamm_adam_history_entry_bytes()),
