@@ -528,7 +528,11 @@ def main() -> None:
         if args.kernel_events == "none":
             step()
         else:
-            step(timing_events=[e.cuda_event for e in evs[k]])
+            # the ID-row gather's pair [12, 13] only for --config c4 (SURVEY §8 g2's 50M x 128 gather):
+            # an event pair on the aux stream between its gather and catch-up launches is measured
+            # overhead in the C2 step under rocprofv3
+            n_ev = NEV if args.config == "c4" else 12
+            step(timing_events=[e.cuda_event for e in evs[k][:n_ev]])
     marks[1].record()
     # deferred AdamW: the g = 0 updates still owed to untouched rows are part of the K steps' work
     eng.flush()
@@ -660,7 +664,7 @@ def main() -> None:
         ent["executed_flops_per_launch"] = 8.0 * B * Bg * D
         kernels.append(ent)
     gather = None
-    g_ms = pair_ms(12)
+    g_ms = pair_ms(12) if args.config == "c4" else 0.0
     if g_ms > 0 and not sharded:
         # the step's ID-row gather (encoders.py:222-223: the user and item tables'
         # rows of the batch, one grouped launch on the aux stream into the [e | f] rows): table-row

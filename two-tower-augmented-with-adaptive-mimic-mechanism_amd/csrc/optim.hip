@@ -406,11 +406,17 @@ constexpr int kPiece = kCoalescePiece;
 constexpr int kRowWaves = 4;
 
 __device__ __forceinline__ const float* dA_row(const RowUpdateArgs& A, int64_t r) {
-    if (A.xu) {
-        const int64_t u = A.xu[r];
-        return u >= 0 ? A.dA_lo + u * A.ld_dA : A.dA_hi + (~u) * A.ld_dA;
+    // the fields as values first: a select between the two pointer FIELDS of the by-value kernel
+    // argument compiled to a select of their addresses, copying the argument to scratch (24 B per
+    // lane in row_update_kernel)
+    const float* const lo = A.dA_lo;
+    const float* const hi = A.dA_hi;
+    const int64_t ld = A.ld_dA;
+    if (const int64_t* xu = A.xu) {
+        const int64_t u = xu[r];
+        return u >= 0 ? lo + u * ld : hi + (~u) * ld;
     }
-    return (r < A.split_row ? A.dA_lo : A.dA_hi) + r * A.ld_dA;
+    return (r < A.split_row ? lo : hi) + r * ld;
 }
 
 // SDA: each position's dA row resolved once into LDS (compact exchange unit maps: their dependent
@@ -444,16 +450,33 @@ __global__ __launch_bounds__(64 * kRowWaves) void piece_sum_kernel(RowUpdateArgs
     __builtin_amdgcn_wave_barrier();
     const int D = A.dim;
     const bool idt = A.id.weight != nullptr;  // (a mimic-only pass leaves the ID table out)
+    // SDA = false (no unit maps, launch_row_update): buffer loads, the position's row offset in the
+    // scalar offset (the row is wave-uniform) and the column in one shared voffset — 64-bit
+    // addresses per load had held the kernel at 288 registers, one wave per SIMD
+    [[maybe_unused]] __amdgpu_buffer_rsrc_t rE, rAlo, rAhi;
+    if constexpr (!SDA) {
+        rE = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A.dE), 0, 0x7fffffff, 0x00020000);
+        rAlo = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A.dA_lo), 0, 0x7fffffff, 0x00020000);
+        rAhi = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A.dA_hi), 0, 0x7fffffff, 0x00020000);
+    }
     for (int d = lane; d < D; d += 64) {
         float ve[kPiece], va[kPiece];
 #pragma unroll
         for (int p = 0; p < kPiece; ++p) {  // issue every load of the chunk before adding
-            const int64_t r = srows[w][p];
-            ve[p] = (idt && p < cnt) ? A.dE[r * A.ld_dE + d] : 0.f;
-            // (SDA = false only without unit maps, launch_row_update: the row's own dA row, no xu
-            // branch in this unrolled load batch — one there serialised the 32 loads, 24 -> 50 us
-            // per launch at C2, profiles/r06_s7_kernel_stats.txt)
-            va[p] = (mimic && p < cnt) ? (SDA ? sda[w][p][d] : (r < A.split_row ? A.dA_lo : A.dA_hi)[r * A.ld_dA + d]) : 0.f;
+            if constexpr (SDA) {
+                const int64_t r = srows[w][p];
+                ve[p] = (idt && p < cnt) ? A.dE[r * A.ld_dE + d] : 0.f;
+                va[p] = (mimic && p < cnt) ? sda[w][p][d] : 0.f;
+            } else {
+                const int r = __builtin_amdgcn_readfirstlane((int)srows[w][p]);
+                ve[p] = (idt && p < cnt)
+                    ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rE, 4 * d, (int)(4 * r * A.ld_dE), 0))
+                    : 0.f;
+                va[p] = (mimic && p < cnt)
+                    ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r < A.split_row ? rAlo : rAhi, 4 * d,
+                                                                                     (int)(4 * r * A.ld_dA), 0))
+                    : 0.f;
+            }
         }
         float ge = 0.f, ga = 0.f;
         int start = 0;
@@ -479,9 +502,14 @@ __device__ __forceinline__ float4 ldf4(const float* p) { return *reinterpret_cas
 __device__ __forceinline__ void stf4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 __device__ __forceinline__ float4 addf4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
 
-// One unique row per `lanes_per_row` lanes (a power of two >= dim / 4, at most 64: two rows per
-// wave at D = 96 / 128), four consecutive elements per lane with 16-byte loads and stores.
+// One unique row per `lanes_per_row` lanes, NV float4 columns per lane (lanes_per_row = dim /
+// (4 NV), a power of two: D = 96 -> 8 lanes x 3 float4s, eight rows per wave, every lane busy),
+// all of a row's table and gradient loads issued before its arithmetic (developer variant, measured
+// slower: launch_row_update).  NV = 0 (default): any dim, lanes_per_row the power of two >= dim / 4
+// (at most 64), one float4 column per trip of a runtime loop.
+template <int NV>
 __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArgs A) {
+    constexpr int C = NV > 0 ? NV : 1;
     const int lane = threadIdx.x & 63;
     const int lpr = A.lanes_per_row, rpw = 64 / lpr;
     const int64_t u = ((int64_t)blockIdx.x * kRowWaves + (threadIdx.x >> 6)) * rpw + lane / lpr;
@@ -493,6 +521,8 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArg
     const bool mimic = A.mimic.weight != nullptr;
     const bool idt = A.id.weight != nullptr;  // (a mimic-only pass leaves the ID table out)
     const bool direct = k1 - k0 <= kPiece;
+    // nn.Embedding padding_idx: no gradient into that row (SparseAdam: not in the sparse gradient at
+    // all, so the row is left as it is; AdamW: a zero gradient row)
     const bool pad_row = idt && A.id.has_padding_idx && key == A.id.padding_idx;
     auto each = [](float4& p, float4& m, float4& v, float4 g, auto&& f) {
         f(p.x, m.x, v.x, g.x);
@@ -500,80 +530,99 @@ __global__ __launch_bounds__(64 * kRowWaves) void row_update_kernel(RowUpdateArg
         f(p.z, m.z, v.z, g.z);
         f(p.w, m.w, v.w, g.w);
     };
-    for (int d = 4 * sub; d < D; d += 4 * lpr) {
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int d0 = 4 * sub; d0 < D; d0 += 4 * lpr * C) {  // NV > 0: one trip
+        int dc[C];
+        float4 ip[C], im[C], iv[C], mp[C], mm[C], mv[C], ge[C], ga[C];
         // the table rows first: they do not depend on the gradient sums below
-        const int64_t o = key * D + d;
-        float4 ip = make_float4(0.f, 0.f, 0.f, 0.f), im = ip, iv = ip;
-        if (idt) {
-            ip = ldf4(A.id.weight + o);
-            im = ldf4(A.id.exp_avg + o);
-            iv = ldf4(A.id.exp_avg_sq + o);
+#pragma unroll
+        for (int i = 0; i < C; ++i) {
+            dc[i] = d0 + i * 4 * lpr;
+            const int64_t o = key * D + dc[i];
+            ip[i] = idt ? ldf4(A.id.weight + o) : z4;
+            im[i] = idt ? ldf4(A.id.exp_avg + o) : z4;
+            iv[i] = idt ? ldf4(A.id.exp_avg_sq + o) : z4;
+            mp[i] = mimic ? ldf4(A.mimic.weight + o) : z4;
+            mm[i] = mimic ? ldf4(A.mimic.exp_avg + o) : z4;
+            mv[i] = mimic ? ldf4(A.mimic.exp_avg_sq + o) : z4;
         }
-        float4 mp = make_float4(0.f, 0.f, 0.f, 0.f), mm = mp, mv = mp;
-        if (mimic) {
-            mp = ldf4(A.mimic.weight + o);
-            mm = ldf4(A.mimic.exp_avg + o);
-            mv = ldf4(A.mimic.exp_avg_sq + o);
-        }
-        float4 ge = make_float4(0.f, 0.f, 0.f, 0.f), ga = ge;
         if (direct) {  // the row's contributions in batch order
             const int64_t r0 = A.rows[k0];
-            if (idt) ge = ldf4(A.dE + r0 * A.ld_dE + d);
-            if (mimic) ga = ldf4(dA_row(A, r0) + d);
+            const float* e0 = A.dE + r0 * A.ld_dE;
+            const float* a0 = mimic ? dA_row(A, r0) : nullptr;
+#pragma unroll
+            for (int i = 0; i < C; ++i) {
+                ge[i] = idt ? ldf4(e0 + dc[i]) : z4;
+                ga[i] = mimic ? ldf4(a0 + dc[i]) : z4;
+            }
             for (int64_t k = k0 + 1; k < k1; ++k) {
                 const int64_t r = A.rows[k];
-                if (idt) ge = addf4(ge, ldf4(A.dE + r * A.ld_dE + d));
-                if (mimic) ga = addf4(ga, ldf4(dA_row(A, r) + d));
+                const float* er = A.dE + r * A.ld_dE;
+                const float* ar = mimic ? dA_row(A, r) : nullptr;
+#pragma unroll
+                for (int i = 0; i < C; ++i) {
+                    if (idt) ge[i] = addf4(ge[i], ldf4(er + dc[i]));
+                    if (mimic) ga[i] = addf4(ga[i], ldf4(ar + dc[i]));
+                }
             }
         } else {  // pieces (piece_sum_kernel), then the pieces in order
-            if (idt) ge = ldf4(A.piece_e + k0 * D + d);
-            if (mimic) ga = ldf4(A.piece_a + k0 * D + d);
+#pragma unroll
+            for (int i = 0; i < C; ++i) {
+                ge[i] = idt ? ldf4(A.piece_e + k0 * D + dc[i]) : z4;
+                ga[i] = mimic ? ldf4(A.piece_a + k0 * D + dc[i]) : z4;
+            }
             for (int64_t k = (k0 / kPiece + 1) * kPiece; k < k1; k += kPiece) {
-                if (idt) ge = addf4(ge, ldf4(A.piece_e + k * D + d));
-                if (mimic) ga = addf4(ga, ldf4(A.piece_a + k * D + d));
+#pragma unroll
+                for (int i = 0; i < C; ++i) {
+                    if (idt) ge[i] = addf4(ge[i], ldf4(A.piece_e + k * D + dc[i]));
+                    if (mimic) ga[i] = addf4(ga[i], ldf4(A.piece_a + k * D + dc[i]));
+                }
             }
         }
-        if (A.grad_scale) {  // clip_grad_norm_: g *= coef (training.py:824-825)
-            const float c = *A.grad_scale;
-            ge = make_float4(ge.x * c, ge.y * c, ge.z * c, ge.w * c);
-            ga = make_float4(ga.x * c, ga.y * c, ga.z * c, ga.w * c);
-        }
-        // nn.Embedding padding_idx: no gradient into that row (SparseAdam: not in the sparse
-        // gradient at all, so the row is left as it is; AdamW: a zero gradient row)
-        const bool pad = A.id.has_padding_idx && key == A.id.padding_idx;
-        if (pad) ge = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (!idt) {
-            // mimic-only pass
-        } else if (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM) {
-            if (!pad)
-                each(ip, im, iv, ge, [&](float& p, float& m, float& v, float g) { sparse_adam_elem(p, m, v, g, A.sp); });
-        } else {
-            each(ip, im, iv, ge, [&](float& p, float& m, float& v, float g) { adam_elem(p, m, v, g, A.ad); });
-        }
-        if (!idt || (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM && pad)) {
-            // untouched
-        } else if (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM || A.id.last_step) {
-            // SparseAdam, or deferred mode: the row was caught up before the forward
-            stf4(A.id.weight + o, ip);
-            stf4(A.id.exp_avg + o, im);
-            stf4(A.id.exp_avg_sq + o, iv);
-        } else {
-            float* sd = A.side_id + u * 3 * D;
-            stf4(sd + d, ip);
-            stf4(sd + D + d, im);
-            stf4(sd + 2 * D + d, iv);
-        }
-        if (mimic) {
-            each(mp, mm, mv, ga, [&](float& p, float& m, float& v, float g) { adam_elem(p, m, v, g, A.ad); });
-            if (A.mimic.last_step) {
-                stf4(A.mimic.weight + o, mp);
-                stf4(A.mimic.exp_avg + o, mm);
-                stf4(A.mimic.exp_avg_sq + o, mv);
+#pragma unroll
+        for (int i = 0; i < C; ++i) {
+            const int d = dc[i];
+            const int64_t o = key * D + d;
+            if (A.grad_scale) {  // clip_grad_norm_: g *= coef (training.py:824-825)
+                const float c = *A.grad_scale;
+                ge[i] = make_float4(ge[i].x * c, ge[i].y * c, ge[i].z * c, ge[i].w * c);
+                ga[i] = make_float4(ga[i].x * c, ga[i].y * c, ga[i].z * c, ga[i].w * c);
+            }
+            if (pad_row) ge[i] = z4;
+            if (!idt) {
+                // mimic-only pass
+            } else if (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM) {
+                if (!pad_row)
+                    each(ip[i], im[i], iv[i], ge[i],
+                         [&](float& p, float& m, float& v, float g) { sparse_adam_elem(p, m, v, g, A.sp); });
             } else {
-                float* sd = A.side_mimic + u * 3 * D;
-                stf4(sd + d, mp);
-                stf4(sd + D + d, mm);
-                stf4(sd + 2 * D + d, mv);
+                each(ip[i], im[i], iv[i], ge[i], [&](float& p, float& m, float& v, float g) { adam_elem(p, m, v, g, A.ad); });
+            }
+            if (!idt || (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM && pad_row)) {
+                // untouched
+            } else if (A.id.optimizer == TTAMM_OPT_SPARSE_ADAM || A.id.last_step) {
+                // SparseAdam, or deferred mode: the row was caught up before the forward
+                stf4(A.id.weight + o, ip[i]);
+                stf4(A.id.exp_avg + o, im[i]);
+                stf4(A.id.exp_avg_sq + o, iv[i]);
+            } else {
+                float* sd = A.side_id + u * 3 * D;
+                stf4(sd + d, ip[i]);
+                stf4(sd + D + d, im[i]);
+                stf4(sd + 2 * D + d, iv[i]);
+            }
+            if (mimic) {
+                each(mp[i], mm[i], mv[i], ga[i], [&](float& p, float& m, float& v, float g) { adam_elem(p, m, v, g, A.ad); });
+                if (A.mimic.last_step) {
+                    stf4(A.mimic.weight + o, mp[i]);
+                    stf4(A.mimic.exp_avg + o, mm[i]);
+                    stf4(A.mimic.exp_avg_sq + o, mv[i]);
+                } else {
+                    float* sd = A.side_mimic + u * 3 * D;
+                    stf4(sd + d, mp[i]);
+                    stf4(sd + D + d, mm[i]);
+                    stf4(sd + 2 * D + d, mv[i]);
+                }
             }
         }
     }
@@ -1424,20 +1473,42 @@ int launch_row_update(const RowUpdateArgs& args, hipStream_t s) {
     RowUpdateArgs a = args;
     TTAMM_REQUIRE(a.dim % 4 == 0 && (!a.id.weight || a.ld_dE % 4 == 0) && (!a.mimic.weight || a.ld_dA % 4 == 0),
                   "row update: dim and gradient leading dims must be multiples of 4");
-    a.lanes_per_row = 1;
-    while (a.lanes_per_row < a.dim / 4 && a.lanes_per_row < 64) a.lanes_per_row *= 2;
+    // NV float4 columns per lane when dim / (4 NV) is a power of two <= 64 (row_update_kernel<NV>):
+    // measured slower in the C2 step (the item launch 70 -> 91 us: eight rows per wave run the wave's
+    // longest Zipf segment, and 183 registers halve the waves per SIMD), so developer-only
+    // (TTAMM_ROW_UPDATE_NV=1); the default is one float4 per lane (NV = 0)
+    static const bool nv_env = [] { const char* e = dev_env("TTAMM_ROW_UPDATE_NV"); return e && e[0] == '1'; }();
+    int nv = 0;
+    for (int c = 4; c >= 1 && nv == 0 && nv_env; --c) {
+        const int q = a.dim / 4;
+        if (q % c == 0 && (q / c & (q / c - 1)) == 0 && q / c <= 64) nv = c;
+    }
+    if (nv) {
+        a.lanes_per_row = a.dim / (4 * nv);
+    } else {
+        a.lanes_per_row = 1;
+        while (a.lanes_per_row < a.dim / 4 && a.lanes_per_row < 64) a.lanes_per_row *= 2;
+    }
     // per-column dA rows unless the unit maps are on (their dependent load): the LDS-resolved form
     // cost the one-process C2 step 7 us (0.6616 vs 0.6545 ms, profiles/r05_s42_piece_sum.txt)
     static const bool sda_env = [] { const char* e = dev_env("TTAMM_PIECE_SDA"); return e && e[0] == '1'; }();
-    const bool sda = sda_env || a.xu != nullptr;
+    // (the buffer-load form takes 32-bit byte offsets of the gradient rows: positions index them)
+    const bool small = 4 * a.n * std::max<int64_t>(a.ld_dE, a.ld_dA) < (int64_t(1) << 31);
+    const bool sda = sda_env || a.xu != nullptr || !small;
     if (sda) hipLaunchKernelGGL(piece_sum_kernel<true>, dim3((unsigned)ceil_div(ceil_div(a.n, kPiece), kRowWaves)),
                        dim3(64 * kRowWaves), 0, s, a);
     else hipLaunchKernelGGL(piece_sum_kernel<false>, dim3((unsigned)ceil_div(ceil_div(a.n, kPiece), kRowWaves)),
                        dim3(64 * kRowWaves), 0, s, a);
     TTAMM_LAUNCH_CHECK();
     const int64_t rows_per_block = (int64_t)kRowWaves * (64 / a.lanes_per_row);
-    hipLaunchKernelGGL(row_update_kernel, dim3((unsigned)ceil_div(a.n, rows_per_block)), dim3(64 * kRowWaves), 0, s,
-                       a);
+    const dim3 grid((unsigned)ceil_div(a.n, rows_per_block));
+    switch (nv) {
+        case 4: hipLaunchKernelGGL(row_update_kernel<4>, grid, dim3(64 * kRowWaves), 0, s, a); break;
+        case 3: hipLaunchKernelGGL(row_update_kernel<3>, grid, dim3(64 * kRowWaves), 0, s, a); break;
+        case 2: hipLaunchKernelGGL(row_update_kernel<2>, grid, dim3(64 * kRowWaves), 0, s, a); break;
+        case 1: hipLaunchKernelGGL(row_update_kernel<1>, grid, dim3(64 * kRowWaves), 0, s, a); break;
+        default: hipLaunchKernelGGL(row_update_kernel<0>, grid, dim3(64 * kRowWaves), 0, s, a); break;
+    }
     TTAMM_LAUNCH_CHECK();
     return TTAMM_OK;
 }
