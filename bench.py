@@ -322,8 +322,13 @@ def gather_bulk(device, rows: int = 50_000_000, dim: int = 128, n: int = 2_000_0
           "read_frac": round(rd / ms_c / 1e6 / HBM_PEAK_GBS, 4)}
     del table
     torch.cuda.empty_cache()
+    pmc = load_traffic("c4_gather_bulk") or {}
+    mat["traffic"] = pmc.get("materialising_bytes_per_launch")
+    ro["traffic"] = pmc.get("read_only_bytes_per_launch")
     return {"table": f"{rows} x {dim} fp32", "indices": "uniform", "materialising": mat, "read_only": ro,
-            "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "note": "traffic: HBM bytes per launch from rocprofv3 FETCH_SIZE (x2, gfx950) / WRITE_SIZE passes "
+                    "(profiles/pmc_traffic.json c4_gather_bulk, profiles/r06_gather_bulk_*)"}
 
 
 def cpu_model() -> str:
