@@ -230,13 +230,22 @@ __device__ __forceinline__ void ibx_split(float4 v, uint2 out[3]) {
 __device__ __forceinline__ bf16x8_t ibx_cat(uint2 a, uint2 b) {
     return __builtin_bit_cast(bf16x8_t, uint4{a.x, a.y, b.x, b.y});
 }
+// bf16 partial products per fp32 product: 6 (hh, hm, mh, hl, lh, mm; the default).  Developer
+// measurement builds (-DTTAMM_IB_PRODUCTS=5: without mm, 4: hh hm mh mm, 3: hh hm mh) price the
+// dropped 2^-16-relative terms against the fp64 bounds
+#ifndef TTAMM_IB_PRODUCTS
+#define TTAMM_IB_PRODUCTS 6
+#endif
 __device__ __forceinline__ f32x16 ibx_mfma6(const bf16x8_t a[3], const bf16x8_t b[3], f32x16 c) {
     c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
+    if constexpr (TTAMM_IB_PRODUCTS == 6 || TTAMM_IB_PRODUCTS == 5) {
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
+    }
+    if constexpr (TTAMM_IB_PRODUCTS == 6 || TTAMM_IB_PRODUCTS == 4)
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
     return c;
 }
 
