@@ -230,11 +230,14 @@ __device__ __forceinline__ void ibx_split(float4 v, uint2 out[3]) {
 __device__ __forceinline__ bf16x8_t ibx_cat(uint2 a, uint2 b) {
     return __builtin_bit_cast(bf16x8_t, uint4{a.x, a.y, b.x, b.y});
 }
-// bf16 partial products per fp32 product: 6 (hh, hm, mh, hl, lh, mm; the default).  Developer
-// measurement builds (-DTTAMM_IB_PRODUCTS=5: without mm, 4: hh hm mh mm, 3: hh hm mh) price the
-// dropped 2^-16-relative terms against the fp64 bounds
+// bf16 partial products per fp32 product: 5 (hh, hm, mh, hl, lh; round 6, the default) or, in
+// developer measurement builds, 6 (+ mm), 4 (hh hm mh mm) or 3 (hh hm mh).  Measured against the
+// chunked float64 definition at the C4 rank-of-8 shape (profiles/r06_inbatch_products.txt):
+// 6: dU 9.8e-7, dP 2.9e-6, 3.24 ms; 5: 9.7e-7, 2.9e-6, 2.97 ms; 4: 5.6e-6, 7.3e-6, 2.27 ms;
+// 3: 5.7e-6, 7.0e-6, 2.00 ms (bound 1e-5) — mm (<= 2^-18 relative) is below the fp32 noise,
+// hl / lh (<= 2^-17 each) are not, so 5 keeps the 6-product accuracy
 #ifndef TTAMM_IB_PRODUCTS
-#define TTAMM_IB_PRODUCTS 6
+#define TTAMM_IB_PRODUCTS 5
 #endif
 __device__ __forceinline__ f32x16 ibx_mfma6(const bf16x8_t a[3], const bf16x8_t b[3], f32x16 c) {
     c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
