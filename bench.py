@@ -663,9 +663,12 @@ def main() -> None:
         # priced against the full split-bf16 ceiling: the kernel forms S twice (user and item roles,
         # 8 B Bg D executed flops), and that second formation is overhead of this kernel, not a lower roof
         ent = mfma_entry(
-            f"inbatch_x_kernel (S = U P^T [{B} x {Bg}] + BCE + dU + dP), {impl}" if not exact_mfma else
+            f"inbatch_x_kernel (S = U P^T [{B} x {Bg}] + BCE + dU + dP), {impl.replace('6 x', '5 x')}" if not exact_mfma else
             f"inbatch_kernel (S = U P^T [{B} x {Bg}] + BCE + dU + dP, fp32 MFMA 32x32x2)",
-            ib_flops, pair_ms(4), split_ceiling, "inbatch_bytes_per_launch")
+            ib_flops, pair_ms(4), MFMA_BF16_PEAK_TFLOPS / 5.0 if split_ceiling else None, "inbatch_bytes_per_launch")
+        if split_ceiling:  # five bf16 products per fp32 product in the in-batch kernel (round 6)
+            ent["peak_note"] = ("split-bf16 ceiling: v_mfma_f32_32x32x16_bf16 dense peak "
+                                f"{MFMA_BF16_PEAK_TFLOPS:.0f} TF/s / 5 bf16 MFMAs per fp32 product (hh, hm, mh, hl, lh)")
         ent["executed_flops_per_launch"] = 8.0 * B * Bg * D
         kernels.append(ent)
     gather = None
