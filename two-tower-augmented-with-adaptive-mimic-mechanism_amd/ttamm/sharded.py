@@ -575,6 +575,12 @@ class ShardedTrainStep(FusedTrainStep):
         look_ahead = next_batch is not None and row_base is None and global_batch is None
         if look_ahead:
             self._check_next_batch(*next_batch)
+        if self.compact and not self.lib.ttamm_exchange_compact_supported(ctypes.byref(self.args)):
+            # the compact layout was chosen at construction for the fused gate kernels; the gate
+            # path is read from TTAMM_GENERIC_GATE on every step: say so up front,
+            # before this step's first collective, instead of failing inside the step
+            raise ValueError("ttamm: the gate path changed (TTAMM_GENERIC_GATE) after this sharded step was built "
+                             "with compact exchange rows; build a new ShardedTrainStep")
         if not self._bind_batch(users, pos_items, ahead.negs if use_ahead else neg_items, keep_masks):
             raise ValueError("ttamm: empty batch in a sharded step (every rank must step)")
         a = self.args

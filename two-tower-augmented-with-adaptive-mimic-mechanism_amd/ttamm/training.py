@@ -567,7 +567,15 @@ class FusedTrainStep:
         if not self._deferred or self.steps_done == 0:
             return
         self.args.hp.dense_step = self.dense_step0 + self.steps_done
-        _lib.check(self.lib.ttamm_flush_tables(ctypes.byref(self.args), _lib.stream_handle(self.device)))
+        # the flush runs on the aux stream (beside the last step's weight-gradient tail) unless that
+        # stream is restricted to a CU subset (aux_cus): then on the caller's stream, on every CU
+        aux = self.args.aux_stream
+        if self._aux_handle:
+            self.args.aux_stream = None
+        try:
+            _lib.check(self.lib.ttamm_flush_tables(ctypes.byref(self.args), _lib.stream_handle(self.device)))
+        finally:
+            self.args.aux_stream = aux
 
     def _status_error(self) -> int:
         """Synchronise and return the device status bits.  After an error the device skipped
