@@ -88,6 +88,52 @@ CONFIGS = {
 }
 
 
+class HipTimingEvent:
+    """A timing hipEvent_t created with hipEventDisableSystemFence (device-scope release), the
+    interface bench.py uses of torch.cuda.Event (record / elapsed_time / cuda_event).  torch's
+    timing events take the default system-scope fence: each record between two kernels of a
+    stream held that stream idle ≈7 µs (an L2 writeback + invalidate), so the per-kernel pairs
+    inside the timed steps cost the step their own gaps (profiles/r06_s23_*).  The HIP entry
+    points come through libttamm.so's dependency on the process's one HIP runtime (torch's)."""
+
+    _hip = None
+
+    def __init__(self) -> None:
+        import ctypes
+
+        if HipTimingEvent._hip is None:
+            from ttamm import _lib
+
+            HipTimingEvent._hip = _lib.load()
+        self._c = ctypes
+        h = ctypes.c_void_p()
+        rc = self._hip.hipEventCreateWithFlags(ctypes.byref(h), ctypes.c_uint(0x20000000))
+        if rc != 0:  # a runtime without the flag: a default timing event
+            rc = self._hip.hipEventCreateWithFlags(ctypes.byref(h), ctypes.c_uint(0))
+        if rc != 0:
+            raise RuntimeError(f"hipEventCreateWithFlags failed ({rc})")
+        self.cuda_event = h.value
+        self._recorded = False
+
+    def record(self, stream=None) -> None:
+        s = (stream or torch.cuda.current_stream()).cuda_stream
+        rc = self._hip.hipEventRecord(self._c.c_void_p(self.cuda_event), self._c.c_void_p(s))
+        if rc != 0:
+            raise RuntimeError(f"hipEventRecord failed ({rc})")
+
+    def elapsed_time(self, end: "HipTimingEvent") -> float:
+        ms = self._c.c_float()
+        rc = self._hip.hipEventElapsedTime(self._c.byref(ms), self._c.c_void_p(self.cuda_event),
+                                           self._c.c_void_p(end.cuda_event))
+        if rc != 0:  # not recorded (e.g. a pair the step did not use)
+            raise RuntimeError(f"hipEventElapsedTime failed ({rc})")
+        return float(ms.value)
+
+    def __del__(self) -> None:
+        if self._hip is not None and getattr(self, "cuda_event", None):
+            self._hip.hipEventDestroy(self._c.c_void_p(self.cuda_event))
+
+
 def tower_cfg(c: dict) -> dict:
     return {
         "type": "tower",
@@ -441,6 +487,9 @@ def main() -> None:
     ap.add_argument("--kernel-events", choices=["every-step", "none"], default="every-step",
                     help="none: no per-kernel HIP event pairs in the timed steps (the roofline entries "
                          "then have no live launch durations; a measurement of the events' own cost)")
+    ap.add_argument("--event-kind", choices=["device", "torch"], default="device",
+                    help="device: timing events with a device-scope release (HipTimingEvent); torch: "
+                         "torch.cuda.Event (system-scope fence, ≈7 µs of stream idle per record)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the step's index-only prologue on the main stream (no aux stream)")
     ap.add_argument("--negatives", choices=["sampled", "in-batch"], default=None,
@@ -515,17 +564,21 @@ def main() -> None:
     # feature-layer forward GEMM, [4,5] the in-batch kernel, [6,7] the wide weight-gradient GEMM
     # launch, [8,9] / [10,11] the user / item catch-up replay kernels, [12,13] the ID-row gather
     NEV = 14
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(NEV)] for _ in range(args.steps)]
-    for quad in evs:  # materialise the hipEvent_t handles
-        for e in quad:
-            e.record()
+    if args.event_kind == "device":
+        new_event = HipTimingEvent
+    else:  # torch's (system-scope) timing events, for the A/B of their cost
+        def new_event():
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()  # materialise the hipEvent_t handle
+            return e
+    evs = [[new_event() for _ in range(NEV)] for _ in range(args.steps)]
     torch.cuda.synchronize()
     rows0 = getattr(eng, "item_rows_seen", 0)
 
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    marks = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    marks = [new_event() for _ in range(3)]
     t0 = time.perf_counter()
     marks[0].record()
     for k in range(args.steps):

@@ -1852,6 +1852,15 @@ void wgrad_rows_per_split(const WgradShape* shapes, int n, int rps[kWgradClasses
             }
         }
         rps[c] = best;
+        // developer: one class's rows per split (TTAMM_WGRAD_RPS0 narrow, 1 wide, 2 / 3 128-wide)
+        if constexpr (kDevKnobs) {
+            char name[] = "TTAMM_WGRAD_RPS0";
+            name[sizeof(name) - 2] = (char)('0' + c);
+            if (const char* e = dev_env(name)) {
+                const int v = std::atoi(e);
+                if (v >= BK && v <= kWgradMaxRowsPerSplit && v % BK == 0) rps[c] = v;
+            }
+        }
     }
 }
 

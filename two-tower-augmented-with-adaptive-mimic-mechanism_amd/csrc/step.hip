@@ -1229,6 +1229,17 @@ int tower_prepare(const ttamm_tower& t, TowerWs& w, bool mimic, const Deferred& 
 // (the late slice's start), [4] main stream after the fusion backward (the row updates' start
 // on the aux stream), [5] aux stream after the row updates (joined at the step's end).
 constexpr int kAuxEvents = 6;
+// Device-scope fork / join: both streams are on this device, so an agent-scope release / acquire
+// (what every kernel boundary already does) orders their memory.  The default system-scope fence
+// of an event record / wait added ≈2 µs of main-stream idle at each of the step's event
+// operations (an L2 writeback + invalidate per event, profiles/r06_s23_*).
+constexpr unsigned kSyncEventFlags = hipEventDisableTiming | hipEventDisableSystemFence;
+hipError_t create_sync_event(hipEvent_t* e) {
+    const hipError_t rc = hipEventCreateWithFlags(e, kSyncEventFlags);
+    if (rc != hipErrorInvalidValue) return rc;
+    (void)hipGetLastError();  // a runtime without the flag: the system-scope event
+    return hipEventCreateWithFlags(e, hipEventDisableTiming);
+}
 int aux_events(hipEvent_t ev[kAuxEvents], hipStream_t aux) {
     struct Set {
         int dev;
@@ -1246,7 +1257,7 @@ int aux_events(hipEvent_t ev[kAuxEvents], hipStream_t aux) {
     Set p;
     p.dev = dev;
     p.aux = aux;
-    for (int i = 0; i < kAuxEvents; ++i) TTAMM_HIP(hipEventCreateWithFlags(&p.e[i], hipEventDisableTiming));
+    for (int i = 0; i < kAuxEvents; ++i) TTAMM_HIP(create_sync_event(&p.e[i]));
     cache.push_back(p);
     for (int i = 0; i < kAuxEvents; ++i) ev[i] = p.e[i];
     return TTAMM_OK;
@@ -2156,7 +2167,7 @@ int flush_tables(const ttamm_step_args& A, hipStream_t s) {
     if ((rc = launch_replay(ra, run))) return rc;
     if (run != s) {
         hipEvent_t e;
-        TTAMM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        TTAMM_HIP(create_sync_event(&e));
         TTAMM_HIP(hipEventRecord(e, run));
         TTAMM_HIP(hipStreamWaitEvent(s, e, 0));
         TTAMM_HIP(hipEventDestroy(e));
