@@ -91,9 +91,10 @@ CONFIGS = {
 class HipTimingEvent:
     """A timing hipEvent_t created with hipEventDisableSystemFence (device-scope release), the
     interface bench.py uses of torch.cuda.Event (record / elapsed_time / cuda_event).  torch's
-    timing events take the default system-scope fence: each record between two kernels of a
-    stream held that stream idle ≈7 µs (an L2 writeback + invalidate), so the per-kernel pairs
-    inside the timed steps cost the step their own gaps (profiles/r06_s23_*).  The HIP entry
+    timing events take the default system-scope fence (an L2 writeback + invalidate): each record
+    between two kernels of a stream added ≈2 µs to the ≈5 µs of stream idle an event operation costs
+    there, so the per-kernel pairs inside the timed steps cost the step more than their own gaps
+    (C2 0.668 -> 0.659 ms/step, profiles/r06_s23_*).  The HIP entry
     points come through libttamm.so's dependency on the process's one HIP runtime (torch's)."""
 
     _hip = None
@@ -126,6 +127,7 @@ class HipTimingEvent:
         rc = self._hip.hipEventElapsedTime(self._c.byref(ms), self._c.c_void_p(self.cuda_event),
                                            self._c.c_void_p(end.cuda_event))
         if rc != 0:  # not recorded (e.g. a pair the step did not use)
+            self._hip.hipGetLastError()  # not left as the thread's error for torch's next check
             raise RuntimeError(f"hipEventElapsedTime failed ({rc})")
         return float(ms.value)
 
@@ -484,12 +486,15 @@ def main() -> None:
                          "bit-exact g = 0 table arithmetic)")
     ap.add_argument("--no-gather-bulk", dest="gather_bulk", action="store_false",
                     help="--config c4: skip the 50M x 128 bulk gather sub-line (after the timed region)")
-    ap.add_argument("--kernel-events", choices=["every-step", "none"], default="every-step",
-                    help="none: no per-kernel HIP event pairs in the timed steps (the roofline entries "
-                         "then have no live launch durations; a measurement of the events' own cost)")
+    ap.add_argument("--kernel-events", choices=["every-step", "roofline", "none"], default="every-step",
+                    help="every-step: every pair in the timed steps.  roofline: the timed steps carry the "
+                         "aux-stream replay pairs, the in-batch and c4 gather pairs only; the main-stream GEMM "
+                         "pairs (first layer, wide weight gradient) are timed in a detail pass of K more steps "
+                         "after it (C2 +0.6 %%, within noise: profiles/r06_s29_*).  none: no pairs (the "
+                         "roofline entries then have no live launch durations; the events' own cost)")
     ap.add_argument("--event-kind", choices=["device", "torch"], default="device",
                     help="device: timing events with a device-scope release (HipTimingEvent); torch: "
-                         "torch.cuda.Event (system-scope fence, ≈7 µs of stream idle per record)")
+                         "torch.cuda.Event (system-scope fence, ≈2 µs more stream idle per record)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the step's index-only prologue on the main stream (no aux stream)")
     ap.add_argument("--negatives", choices=["sampled", "in-batch"], default=None,
@@ -590,7 +595,13 @@ def main() -> None:
             # an event pair on the aux stream between its gather and catch-up launches is measured
             # overhead in the C2 step under rocprofv3
             n_ev = NEV if args.config == "c4" else 12
-            step(timing_events=[e.cuda_event for e in evs[k][:n_ev]])
+            handles = [e.cuda_event for e in evs[k][:n_ev]]
+            if args.kernel_events == "roofline":
+                # the main-stream GEMM pairs [2, 3] / [6, 7] are timed in the detail pass below: each
+                # event record on the main stream holds it idle a few µs (profiles/r06_s22_*)
+                for i in (2, 3, 6, 7):
+                    handles[i] = None
+            step(timing_events=handles)
     marks[1].record()
     # deferred AdamW: the g = 0 updates still owed to untouched rows are part of the K steps' work
     eng.flush()
@@ -634,13 +645,26 @@ def main() -> None:
                       "note": "table_adamw_math='exact' (the ttamm.FusedTrainStep / train_one_epoch default: IEEE "
                               "sqrt and division in the g = 0 table AdamW, bit-identical to torch): the same "
                               "workload, K steps + the closing flush, right after the main timed region"}
+    evs_detail = evs
+    if args.kernel_events == "roofline":
+        # detail pass: K more steps (+ the flush) carrying the main-stream GEMM pairs [2, 3] (first
+        # feature layer) and [6, 7] (wide weight gradient), for the kernels entries beside the roofline
+        evs_detail = [[new_event() for _ in range(NEV)] for _ in range(args.steps)]
+        torch.cuda.synchronize()
+        for k in range(args.steps):
+            handles = [None] * 12
+            for i in (2, 3, 6, 7):
+                handles[i] = evs_detail[k][i].cuda_event
+            step(timing_events=handles)
+        eng.flush()
+        torch.cuda.synchronize()
     loss = eng.finish()
     steps_only_ms = marks[0].elapsed_time(marks[1]) / args.steps
     flush_ms = marks[1].elapsed_time(marks[2])
 
     def pair_ms(i: int) -> float:  # mean over the timed steps of event pair (i, i + 1); 0 if unused
         tot = 0.0
-        for q in evs:
+        for q in (evs_detail if i in (2, 6) else evs):
             try:
                 tot += q[i].elapsed_time(q[i + 1])
             except RuntimeError:  # not recorded this step
@@ -710,6 +734,9 @@ def main() -> None:
             "wide weight-gradient GEMM launch (dW = dY^T X, split-K slabs; "
             + ", ".join(f"{M}x{Nn}" for _, M, Nn in wide[: len(wide) // 2]) + f" per tower), {impl}",
             sum(2.0 * R * M * Nn for R, M, Nn in wide), pair_ms(6), split_ceiling, "wgrad_wide_bytes_per_launch"))
+    if args.kernel_events == "roofline":
+        for e in kernels:
+            e["events"] = "detail pass: K steps after the timed region, the same step with these pairs recorded"
     if in_batch:
         Bg = B * shard_world if sharded else B
         ib_flops = 6.0 * B * Bg * D  # S = U P^T, dU = dS P, dP = dS^T U (S recomputed: not counted)
