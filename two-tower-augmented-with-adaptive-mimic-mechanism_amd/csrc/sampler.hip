@@ -41,6 +41,16 @@ __device__ __forceinline__ void sample_slot(int64_t slot, int64_t u, uint64_t nu
     int64_t cand = 0;
     bool ok = false;
     const int64_t key = slot_base + slot;  // global slot: a sharded batch draws what one process would
+    // a short positive list (the common case: ~20 per user) is loaded whole with independent loads
+    // and scanned in registers — one memory round trip instead of a binary search's log2(n)
+    // dependent ones on the step's critical path; longer lists keep the binary search
+    constexpr int kShort = 32;
+    const int64_t n = hi - lo;
+    int64_t pv[kShort];
+    if (n <= kShort) {
+#pragma unroll
+        for (int i = 0; i < kShort; ++i) pv[i] = i < n ? pos_values[lo + i] : -1;
+    }
     for (int attempt = 0; attempt < kMaxDraws && !ok; ++attempt) {
         const u32x4 r = philox4x32(
             u32x4{(uint32_t)key, (uint32_t)(key >> 32), (uint32_t)counter,
@@ -48,7 +58,14 @@ __device__ __forceinline__ void sample_slot(int64_t slot, int64_t u, uint64_t nu
             k0, k1);
         const uint64_t r64 = ((uint64_t)r.x << 32) | r.y;
         cand = (int64_t)__umul64hi(r64, num_items);  // uniform in [0, num_items), bias < 2^-40
-        ok = (hi == lo) || !is_positive(pos_values, lo, hi, cand);
+        if (n <= kShort) {
+            bool hit = false;
+#pragma unroll
+            for (int i = 0; i < kShort; ++i) hit |= pv[i] == cand;  // (-1 never equals a draw)
+            ok = !hit;
+        } else {
+            ok = !is_positive(pos_values, lo, hi, cand);
+        }
     }
     out[slot] = cand;
     if (out2) out2[slot] = cand;
@@ -116,7 +133,9 @@ __global__ void step_prologue_kernel(StepPrologue) {
                         pa->slot_base, pa->out, pa->out2, st->status);
         }
     }
-    // completion: the last block counts the step and publishes its AdamW constants
+    // completion: the last block counts the step and publishes its AdamW constants (done == null: the
+    // caller runs step_begin_kernel on its aux stream instead, off the critical path)
+    if (!pa->done) return;
     __syncthreads();
     if (threadIdx.x != 0) return;
     __threadfence();
@@ -142,7 +161,8 @@ __global__ void step_prologue_kernel(StepPrologue) {
 }  // namespace
 
 int launch_step_prologue(const StageArgs& st, const PrologueArgs& pa, hipStream_t s) {
-    TTAMM_REQUIRE(st.count >= 0 && st.count <= kMaxStageSegs && pa.done, "step prologue: bad arguments");
+    TTAMM_REQUIRE(st.count >= 0 && st.count <= kMaxStageSegs && (pa.done || (!pa.applied && !pa.hist)),
+                  "step prologue: bad arguments");
     TTAMM_REQUIRE(pa.num_neg == 0 || (pa.num_items > 1 && pa.users), "step prologue: sampler arguments");
     TTAMM_REQUIRE(!pa.hist || (pa.cap > 1 && pa.cap <= kMaxAdamHistory), "adam history: capacity must be in [2, 512]");
     int64_t most = pa.batch * pa.num_neg;

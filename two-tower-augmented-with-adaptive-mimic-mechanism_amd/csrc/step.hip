@@ -1774,6 +1774,11 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
     df.status = A.status;
 
     // ---- indices and negatives ---------------------------------------------------------------
+    // one process with the aux stream: the step's count / AdamW constants on the aux stream (below;
+    // not with the developer's slice on the main stream, which replays to this step's entry)
+    const bool begin_aux = !shard && (ph & TTAMM_PHASE_SAMPLE) &&
+                           overlapped(T, 2, df, s, static_cast<hipStream_t>(A.aux_stream)) &&
+                           !dev_env("TTAMM_SLICE_MAIN");
     if (ph & TTAMM_PHASE_SAMPLE) {
         // range-checked copies of the batch's ids (nn.Embedding raises IndexError,
         // encoders.py:222-223): an out-of-range id sets TTAMM_STATUS_INDEX_OUT_OF_RANGE, is
@@ -1835,6 +1840,17 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         pa.cap = df.on ? df.cap : 2;
         pa.step = df.step;
         pa.c = ad;
+        // one process with the aux stream: the step's count and AdamW constants are published by
+        // step_begin_kernel on the aux stream (after the fork, below) instead of by the prologue's
+        // last block — its completion counter (a release fence and an atomic per block) sat on the
+        // main stream's path to the first GEMM.  Nothing in this step reads this step's history
+        // entry (the catch-up and the rolling slice replay to step - 1); the next step's catch-up
+        // and the flush are ordered after it on the aux stream or after the step's join.
+        if (begin_aux) {
+            pa.applied = nullptr;
+            pa.hist = nullptr;
+            pa.done = nullptr;
+        }
         if ((rc = launch_step_prologue(st, pa, s))) return rc;
     }
     if (shard && (ph & TTAMM_PHASE_ITEM_FWD) && I.R > 0) {
@@ -1860,6 +1876,9 @@ int run_step(const ttamm_step_args& A, hipStream_t s) {
         df.slice_late = df.slice_on_aux && dev_env("TTAMM_SLICE_LATE") != nullptr;
         if ((rc = prepare_forward(T, W, 2, A.b, D, mimic, df, s, aux, A.timing_events + 2, A.timing_events,
                                   A.timing_events + 8, A.timing_events + 12)))
+            return rc;
+        if (begin_aux && (rc = launch_step_begin(A.status, A.steps_applied, df.on ? df.hist : nullptr,
+                                                 df.on ? df.cap : 2, df.step, ad, aux)))
             return rc;
     } else {
         const ttamm_tower* Ti[2] = {&A.item, nullptr};
