@@ -132,8 +132,14 @@ class HipTimingEvent:
         return float(ms.value)
 
     def __del__(self) -> None:
-        if self._hip is not None and getattr(self, "cuda_event", None):
+        # not at interpreter shutdown: the HIP runtime may already be torn down (the process's exit
+        # releases the events anyway)
+        if sys.is_finalizing() or self._hip is None or not getattr(self, "cuda_event", None):
+            return
+        try:
             self._hip.hipEventDestroy(self._c.c_void_p(self.cuda_event))
+        except Exception:
+            pass
 
 
 def tower_cfg(c: dict) -> dict:
